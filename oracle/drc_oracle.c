@@ -1,0 +1,1257 @@
+/*
+ * ORACLE / TEST INFRASTRUCTURE ONLY — see drc_oracle.h for what is restated
+ * and where.  Scalar, straightforward C: it is the checker and the CPU
+ * baseline, never the thing measured on the GPU.
+ */
+#include "drc_oracle.h"
+
+#include <math.h>
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define INFTY 1e30               /* OSQP_INFTY                               */
+#define MIN_SCALING 1e-4
+#define MAX_SCALING 1e4
+#define RHO_MIN 1e-6
+#define RHO_MAX 1e6
+#define RHO_TOL 1e-4
+#define RHO_EQ_OVER_RHO_INEQ 1e3
+#define DIVISION_TOL 1e-30
+
+/* ------------------------------------------------------------------------ */
+/* small dense helpers                                                      */
+/* ------------------------------------------------------------------------ */
+static inline double dot3(const double* a, const double* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+static inline void cross3(const double* a, const double* b, double* c) {
+    double x = a[1] * b[2] - a[2] * b[1], y = a[2] * b[0] - a[0] * b[2], z = a[0] * b[1] - a[1] * b[0];
+    c[0] = x; c[1] = y; c[2] = z;
+}
+static inline void sub3(const double* a, const double* b, double* c) { c[0] = a[0] - b[0]; c[1] = a[1] - b[1]; c[2] = a[2] - b[2]; }
+static inline double norm3(const double* a) { return sqrt(dot3(a, a)); }
+/* R (row-major) * v */
+static inline void matvec3(const double* R, const double* v, double* o) {
+    double x = R[0] * v[0] + R[1] * v[1] + R[2] * v[2];
+    double y = R[3] * v[0] + R[4] * v[1] + R[5] * v[2];
+    double z = R[6] * v[0] + R[7] * v[1] + R[8] * v[2];
+    o[0] = x; o[1] = y; o[2] = z;
+}
+static inline void matTvec3(const double* R, const double* v, double* o) {
+    double x = R[0] * v[0] + R[3] * v[1] + R[6] * v[2];
+    double y = R[1] * v[0] + R[4] * v[1] + R[7] * v[2];
+    double z = R[2] * v[0] + R[5] * v[1] + R[8] * v[2];
+    o[0] = x; o[1] = y; o[2] = z;
+}
+static inline void matmul3(const double* A, const double* B, double* C) {
+    double T[9];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) T[3 * i + j] = A[3 * i] * B[j] + A[3 * i + 1] * B[3 + j] + A[3 * i + 2] * B[6 + j];
+    memcpy(C, T, sizeof(T));
+}
+/* compose 12-vector transforms: out = a * b */
+static void tcompose(const double* a, const double* b, double* out) {
+    double R[9], p[3];
+    matmul3(a, b, R);
+    matvec3(a, b + 9, p);
+    p[0] += a[9]; p[1] += a[10]; p[2] += a[11];
+    memcpy(out, R, sizeof(R));
+    memcpy(out + 9, p, sizeof(p));
+}
+static void axis_rot(const double* ax, double q, double* R) {
+    double x = ax[0], y = ax[1], z = ax[2], c = cos(q), s = sin(q), C = 1 - c;
+    R[0] = c + x * x * C;     R[1] = x * y * C - z * s; R[2] = x * z * C + y * s;
+    R[3] = y * x * C + z * s; R[4] = c + y * y * C;     R[5] = y * z * C - x * s;
+    R[6] = z * x * C - y * s; R[7] = z * y * C + x * s; R[8] = c + z * z * C;
+}
+
+/* ------------------------------------------------------------------------ */
+/* kinematics  (robot_data.cpp:101-107 computeJointJacobians; :392-402)     */
+/* ------------------------------------------------------------------------ */
+typedef struct Kin {
+    double T[ORC_MAXJ + 1][12]; /* oMi */
+    double z[ORC_MAXJ + 1][3];  /* joint axis (world) */
+    double pe[3];               /* task frame origin */
+    double Te[12];
+} Kin;
+
+static void kin_fk(const OracleModel* m, const double* q, Kin* k) {
+    static const double I12[12] = {1, 0, 0, 0, 1, 0, 0, 0, 1, 0, 0, 0};
+    memcpy(k->T[0], I12, sizeof(I12));
+    for (int j = 1; j <= m->nv; ++j) {
+        double base[12], M[12];
+        tcompose(k->T[m->parent[j]], m->jplace[j], base);
+        memcpy(M, I12, sizeof(I12));
+        if (m->jtype[j] == 0) axis_rot(m->axis[j], q[j - 1], M);
+        else { M[9] = m->axis[j][0] * q[j - 1]; M[10] = m->axis[j][1] * q[j - 1]; M[11] = m->axis[j][2] * q[j - 1]; }
+        tcompose(base, M, k->T[j]);
+        matvec3(k->T[j], m->axis[j], k->z[j]);
+    }
+    tcompose(k->T[m->ee_joint], m->ee_place, k->Te);
+    memcpy(k->pe, k->Te + 9, 3 * sizeof(double));
+}
+
+static int is_ancestor(const OracleModel* m, int k, int j) { /* k supports j (k<=j on the path) */
+    while (j > 0) { if (j == k) return 1; j = m->parent[j]; }
+    return 0;
+}
+
+/* 6 x nv LWA Jacobian of a point attached to joint jid (row-major) */
+static void point_jacobian(const OracleModel* m, const Kin* k, int jid, const double* pt, double* J) {
+    int nv = m->nv;
+    memset(J, 0, 6 * nv * sizeof(double));
+    for (int a = jid; a > 0; a = m->parent[a]) {
+        double c[3];
+        if (m->jtype[a] == 0) {
+            double r[3];
+            sub3(pt, k->T[a] + 9, r);
+            cross3(k->z[a], r, c);
+            for (int i = 0; i < 3; ++i) { J[i * nv + a - 1] = c[i]; J[(3 + i) * nv + a - 1] = k->z[a][i]; }
+        } else {
+            for (int i = 0; i < 3; ++i) J[i * nv + a - 1] = k->z[a][i];
+        }
+    }
+}
+
+/* dJ/dq_kk of the task-frame LWA Jacobian: dJ[kk][6][nv] (getFrameJacobian-
+ * TimeVariation with qdot = e_k, robot_data.cpp:544-553) */
+static void frame_jacobian_dq(const OracleModel* m, const Kin* k, double* dJ /* nv*6*nv */) {
+    int nv = m->nv, je = m->ee_joint;
+    memset(dJ, 0, (size_t)nv * 6 * nv * sizeof(double));
+    for (int kk = je; kk > 0; kk = m->parent[kk]) {
+        double dpe[3] = {0, 0, 0};
+        if (m->jtype[kk] == 0) { double r[3]; sub3(k->pe, k->T[kk] + 9, r); cross3(k->z[kk], r, dpe); }
+        else memcpy(dpe, k->z[kk], sizeof(dpe));
+        double* D = dJ + (size_t)(kk - 1) * 6 * nv;
+        for (int i = je; i > 0; i = m->parent[i]) {
+            double dzi[3] = {0, 0, 0}, dpi[3] = {0, 0, 0};
+            int kk_moves_i = (kk != i) && is_ancestor(m, kk, i);
+            if (kk_moves_i && m->jtype[kk] == 0) cross3(k->z[kk], k->z[i], dzi);
+            if (kk_moves_i) {
+                if (m->jtype[kk] == 0) { double r[3]; sub3(k->T[i] + 9, k->T[kk] + 9, r); cross3(k->z[kk], r, dpi); }
+                else memcpy(dpi, k->z[kk], sizeof(dpi));
+            }
+            if (m->jtype[i] == 0) {
+                double r[3], a[3], b[3], dd[3];
+                sub3(k->pe, k->T[i] + 9, r);
+                cross3(dzi, r, a);
+                sub3(dpe, dpi, dd);
+                cross3(k->z[i], dd, b);
+                for (int c = 0; c < 3; ++c) { D[c * nv + i - 1] = a[c] + b[c]; D[(3 + c) * nv + i - 1] = dzi[c]; }
+            } else {
+                for (int c = 0; c < 3; ++c) D[c * nv + i - 1] = dzi[c];
+            }
+        }
+    }
+}
+
+/* ------------------------------------------------------------------------ */
+/* dense linear algebra                                                     */
+/* ------------------------------------------------------------------------ */
+/* LU determinant with partial pivoting (Eigen MatrixBase::determinant) */
+static double det_lu(const double* A, int n) {
+    double M[64];
+    memcpy(M, A, n * n * sizeof(double));
+    double det = 1;
+    for (int c = 0; c < n; ++c) {
+        int p = c;
+        for (int r = c + 1; r < n; ++r) if (fabs(M[r * n + c]) > fabs(M[p * n + c])) p = r;
+        if (M[p * n + c] == 0) return 0;
+        if (p != c) { for (int j = 0; j < n; ++j) { double t = M[c * n + j]; M[c * n + j] = M[p * n + j]; M[p * n + j] = t; } det = -det; }
+        det *= M[c * n + c];
+        for (int r = c + 1; r < n; ++r) {
+            double f = M[r * n + c] / M[c * n + c];
+            for (int j = c; j < n; ++j) M[r * n + j] -= f * M[c * n + j];
+        }
+    }
+    return det;
+}
+
+/* rank by column-pivoted Householder QR, |R_ii| > thr * max|R_ii| (Eigen COD) */
+static int rank_cpqr(const double* A, int n, double thr) {
+    double M[64], cn[8];
+    memcpy(M, A, n * n * sizeof(double));
+    double maxpiv = 0, piv[8];
+    for (int k = 0; k < n; ++k) {
+        for (int j = k; j < n; ++j) { double s = 0; for (int i = k; i < n; ++i) s += M[i * n + j] * M[i * n + j]; cn[j] = s; }
+        int p = k;
+        for (int j = k + 1; j < n; ++j) if (cn[j] > cn[p]) p = j;
+        if (p != k) for (int i = 0; i < n; ++i) { double t = M[i * n + k]; M[i * n + k] = M[i * n + p]; M[i * n + p] = t; }
+        double nrm = sqrt(cn[p]);
+        piv[k] = nrm;
+        if (nrm > maxpiv) maxpiv = nrm;
+        if (nrm == 0) { for (int r = k + 1; r < n; ++r) piv[r] = 0; break; }
+        double alpha = M[k * n + k] > 0 ? -nrm : nrm;
+        double v[8];
+        for (int i = k; i < n; ++i) v[i] = M[i * n + k];
+        v[k] -= alpha;
+        double vn = 0; for (int i = k; i < n; ++i) vn += v[i] * v[i];
+        if (vn > 0)
+            for (int j = k; j < n; ++j) {
+                double s = 0; for (int i = k; i < n; ++i) s += v[i] * M[i * n + j];
+                s = 2 * s / vn;
+                for (int i = k; i < n; ++i) M[i * n + j] -= s * v[i];
+            }
+    }
+    int r = 0;
+    for (int k = 0; k < n; ++k) if (piv[k] > thr * maxpiv) ++r;
+    return r;
+}
+
+/* symmetric Jacobi eigen-decomposition (for the rank-deficient pinv) */
+static void jacobi_eig(const double* A, int n, double* w, double* V) {
+    double M[64];
+    memcpy(M, A, n * n * sizeof(double));
+    for (int i = 0; i < n * n; ++i) V[i] = 0;
+    for (int i = 0; i < n; ++i) V[i * n + i] = 1;
+    for (int sweep = 0; sweep < 60; ++sweep) {
+        double off = 0;
+        for (int i = 0; i < n; ++i) for (int j = i + 1; j < n; ++j) off += M[i * n + j] * M[i * n + j];
+        if (off < 1e-300) break;
+        for (int p = 0; p < n; ++p)
+            for (int q = p + 1; q < n; ++q) {
+                if (fabs(M[p * n + q]) < 1e-300) continue;
+                double th = (M[q * n + q] - M[p * n + p]) / (2 * M[p * n + q]);
+                double t = (th >= 0 ? 1 : -1) / (fabs(th) + sqrt(th * th + 1));
+                double c = 1 / sqrt(t * t + 1), s = t * c;
+                for (int k = 0; k < n; ++k) {
+                    double mkp = M[k * n + p], mkq = M[k * n + q];
+                    M[k * n + p] = c * mkp - s * mkq; M[k * n + q] = s * mkp + c * mkq;
+                }
+                for (int k = 0; k < n; ++k) {
+                    double mpk = M[p * n + k], mqk = M[q * n + k];
+                    M[p * n + k] = c * mpk - s * mqk; M[q * n + k] = s * mpk + c * mqk;
+                }
+                for (int k = 0; k < n; ++k) {
+                    double vkp = V[k * n + p], vkq = V[k * n + q];
+                    V[k * n + p] = c * vkp - s * vkq; V[k * n + q] = s * vkp + c * vkq;
+                }
+            }
+    }
+    for (int i = 0; i < n; ++i) w[i] = M[i * n + i];
+}
+
+/* Cholesky LL^T in place (lower), returns 0 on failure */
+static int chol(double* A, int n) {
+    for (int j = 0; j < n; ++j) {
+        double s = A[j * n + j];
+        for (int k = 0; k < j; ++k) s -= A[j * n + k] * A[j * n + k];
+        if (!(s > 0)) return 0;
+        double d = sqrt(s);
+        A[j * n + j] = d;
+        for (int i = j + 1; i < n; ++i) {
+            double t = A[i * n + j];
+            for (int k = 0; k < j; ++k) t -= A[i * n + k] * A[j * n + k];
+            A[i * n + j] = t / d;
+        }
+    }
+    return 1;
+}
+static void chol_solve(const double* L, int n, double* b) {
+    for (int i = 0; i < n; ++i) { double t = b[i]; for (int k = 0; k < i; ++k) t -= L[i * n + k] * b[k]; b[i] = t / L[i * n + i]; }
+    for (int i = n - 1; i >= 0; --i) { double t = b[i]; for (int k = i + 1; k < n; ++k) t -= L[k * n + i] * b[k]; b[i] = t / L[i * n + i]; }
+}
+
+/* DyrosMath::PinvCOD for a symmetric PSD matrix (math_type_define.h:563) */
+static void pinv_cod_sym(const double* A, int n, double* X) {
+    int r = rank_cpqr(A, n, 1e-6);
+    if (r == n) {
+        double L[64];
+        memcpy(L, A, n * n * sizeof(double));
+        if (chol(L, n)) {
+            for (int c = 0; c < n; ++c) {
+                double e[8] = {0};
+                e[c] = 1;
+                chol_solve(L, n, e);
+                for (int i = 0; i < n; ++i) X[i * n + c] = e[i];
+            }
+            return;
+        }
+    }
+    double w[8], V[64];
+    int idx[8];
+    jacobi_eig(A, n, w, V);
+    for (int i = 0; i < n; ++i) idx[i] = i;
+    for (int i = 0; i < n; ++i) for (int j = i + 1; j < n; ++j) if (fabs(w[idx[j]]) > fabs(w[idx[i]])) { int t = idx[i]; idx[i] = idx[j]; idx[j] = t; }
+    memset(X, 0, n * n * sizeof(double));
+    for (int kk = 0; kk < r; ++kk) {
+        int e = idx[kk];
+        for (int i = 0; i < n; ++i) for (int j = 0; j < n; ++j) X[i * n + j] += V[i * n + e] * V[j * n + e] / w[e];
+    }
+}
+
+/* ------------------------------------------------------------------------ */
+/* manipulability  (robot_data.cpp:519-553; MoMa :439-475)                  */
+/* ------------------------------------------------------------------------ */
+static void manip(const OracleModel* m, const Kin* k, const double* J, int c0, int nc, double* man, double* grad) {
+    int nv = m->nv;
+    double Jr[6 * ORC_MAXJ], A[36], Ai[36], W[ORC_MAXJ * 6];
+    double* dJ = (double*)malloc((size_t)nv * 6 * nv * sizeof(double));
+    for (int i = 0; i < 6; ++i) for (int c = 0; c < nc; ++c) Jr[i * nc + c] = J[i * nv + c0 + c];
+    for (int i = 0; i < 6; ++i) for (int j = 0; j < 6; ++j) { double s = 0; for (int c = 0; c < nc; ++c) s += Jr[i * nc + c] * Jr[j * nc + c]; A[i * 6 + j] = s; }
+    double det = det_lu(A, 6);
+    *man = sqrt(det);
+    pinv_cod_sym(A, 6, Ai);
+    /* W = Jr^T Ai  (nc x 6) */
+    for (int c = 0; c < nc; ++c) for (int j = 0; j < 6; ++j) { double s = 0; for (int i = 0; i < 6; ++i) s += Jr[i * nc + c] * Ai[i * 6 + j]; W[c * 6 + j] = s; }
+    frame_jacobian_dq(m, k, dJ);
+    for (int kk = 0; kk < nc; ++kk) {
+        const double* D = dJ + (size_t)(c0 + kk) * 6 * nv;
+        double tr = 0;
+        for (int a = 0; a < 6; ++a) for (int c = 0; c < nc; ++c) tr += D[a * nv + c0 + c] * W[c * 6 + a];
+        grad[kk] = *man * tr;
+    }
+    free(dJ);
+}
+
+/* ------------------------------------------------------------------------ */
+/* narrow phase (hpp-fcl semantics, restated)                               */
+/* ------------------------------------------------------------------------ */
+typedef struct Shape { int type; double T[12]; double prm[3]; } Shape;
+
+static void support(const Shape* s, const double* d, double* out) {
+    if (s->type == 0) { memcpy(out, s->T + 9, 3 * sizeof(double)); return; }
+    double dl[3], loc[3];
+    matTvec3(s->T, d, dl);
+    if (s->type == 1) {
+        double r = s->prm[0], h = s->prm[1], rho = sqrt(dl[0] * dl[0] + dl[1] * dl[1]);
+        loc[0] = rho > 0 ? r * dl[0] / rho : 0;
+        loc[1] = rho > 0 ? r * dl[1] / rho : 0;
+        loc[2] = dl[2] > 0 ? h : -h;
+    } else {
+        for (int i = 0; i < 3; ++i) loc[i] = dl[i] > 0 ? s->prm[i] : -s->prm[i];
+    }
+    matvec3(s->T, loc, out);
+    out[0] += s->T[9]; out[1] += s->T[10]; out[2] += s->T[11];
+}
+
+typedef struct SV { double w[3], a[3], b[3]; } SV;
+
+static void sup_md(const Shape* A, const Shape* B, const double* d, SV* o) {
+    double nd[3] = {-d[0], -d[1], -d[2]};
+    support(A, d, o->a);
+    support(B, nd, o->b);
+    sub3(o->a, o->b, o->w);
+}
+
+/* closest point of conv(W) to the origin by exhaustive sub-simplex search */
+static int closest_simplex(SV* S, int n, double* v, double* lam_out) {
+    double best = INFINITY, bl[4] = {0};
+    int bmask = 0;
+    for (int mask = (1 << n) - 1; mask > 0; --mask) {
+        int idx[4], k = 0;
+        for (int i = 0; i < n; ++i) if (mask & (1 << i)) idx[k++] = i;
+        double lam[4];
+        if (k == 1) lam[0] = 1;
+        else {
+            double D[3][3], G[9], r[3];
+            for (int i = 1; i < k; ++i) sub3(S[idx[i]].w, S[idx[0]].w, D[i - 1]);
+            int d = k - 1;
+            for (int i = 0; i < d; ++i) { for (int j = 0; j < d; ++j) G[i * 3 + j] = dot3(D[i], D[j]); r[i] = -dot3(D[i], S[idx[0]].w); }
+            double mu[3];
+            if (d == 1) { if (G[0] <= 0) continue; mu[0] = r[0] / G[0]; }
+            else if (d == 2) {
+                double det = G[0] * G[4] - G[1] * G[3];
+                if (fabs(det) < 1e-300) continue;
+                mu[0] = (r[0] * G[4] - G[1] * r[1]) / det;
+                mu[1] = (G[0] * r[1] - r[0] * G[3]) / det;
+            } else {
+                double a = G[0], b = G[1], c = G[2], dd = G[3], e = G[4], f = G[5], g = G[6], h = G[7], ii = G[8];
+                double det = a * (e * ii - f * h) - b * (dd * ii - f * g) + c * (dd * h - e * g);
+                if (fabs(det) < 1e-300) continue;
+                mu[0] = (r[0] * (e * ii - f * h) - b * (r[1] * ii - f * r[2]) + c * (r[1] * h - e * r[2])) / det;
+                mu[1] = (a * (r[1] * ii - f * r[2]) - r[0] * (dd * ii - f * g) + c * (dd * r[2] - r[1] * g)) / det;
+                mu[2] = (a * (e * r[2] - r[1] * h) - b * (dd * r[2] - r[1] * g) + r[0] * (dd * h - e * g)) / det;
+            }
+            double s = 0;
+            for (int i = 0; i < d; ++i) s += mu[i];
+            lam[0] = 1 - s;
+            for (int i = 0; i < d; ++i) lam[i + 1] = mu[i];
+            int bad = 0;
+            for (int i = 0; i < k; ++i) if (lam[i] < -1e-14) bad = 1;
+            if (bad) continue;
+        }
+        double p[3] = {0, 0, 0};
+        for (int i = 0; i < k; ++i) for (int c = 0; c < 3; ++c) p[c] += lam[i] * S[idx[i]].w[c];
+        double dv = dot3(p, p);
+        if (bmask == 0 || dv < best - 1e-18) {
+            best = dv; bmask = mask;
+            memcpy(v, p, sizeof(p));
+            for (int i = 0; i < k; ++i) bl[i] = lam[i];
+        }
+    }
+    /* compact */
+    SV T[4];
+    int k = 0;
+    for (int i = 0; i < n; ++i) if (bmask & (1 << i)) T[k++] = S[i];
+    for (int i = 0; i < k; ++i) { S[i] = T[i]; lam_out[i] = bl[i]; }
+    return k;
+}
+
+/* GJK on the cores.  Returns 1 when the origin is enclosed (penetration). */
+static int gjk(const Shape* A, const Shape* B, SV* S, int* ns, double* lam, double* v) {
+    sub3(A->T + 9, B->T + 9, v);
+    if (dot3(v, v) < 1e-24) { v[0] = 1; v[1] = 0; v[2] = 0; }
+    int n = 0;
+    for (int it = 0; it < 128; ++it) {
+        double nv[3] = {-v[0], -v[1], -v[2]};
+        SV w;
+        sup_md(A, B, nv, &w);
+        double vv = dot3(v, v);
+        if (n > 0 && vv - dot3(v, w.w) <= 1e-12 * sqrt(vv)) break;
+        int dup = 0;
+        for (int i = 0; i < n; ++i) if (S[i].w[0] == w.w[0] && S[i].w[1] == w.w[1] && S[i].w[2] == w.w[2]) dup = 1;
+        if (dup) break;
+        S[n++] = w;
+        n = closest_simplex(S, n, v, lam);
+        if (n == 4 || dot3(v, v) < 1e-24) { *ns = n; return 1; }
+    }
+    *ns = n;
+    return 0;
+}
+
+#define EPA_MAXV 160
+#define EPA_MAXF 320
+static double epa(const Shape* A, const Shape* B, SV* S, int ns, double* pA, double* pB) {
+    static const double dirs[6][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}, {-1, 0, 0}, {0, -1, 0}, {0, 0, -1}};
+    SV V[EPA_MAXV];
+    int F[EPA_MAXF][3], nf = 0, nvx = ns;
+    for (int i = 0; i < ns; ++i) V[i] = S[i];
+    for (int di = 0; di < 6 && nvx < 4; ++di) {
+        SV w;
+        sup_md(A, B, dirs[di], &w);
+        int ok = 1;
+        for (int i = 0; i < nvx; ++i) { double d[3]; sub3(w.w, V[i].w, d); if (norm3(d) <= 1e-12) ok = 0; }
+        if (ok) V[nvx++] = w;
+    }
+    static const int tf[4][4] = {{0, 1, 2, 3}, {0, 3, 1, 2}, {0, 2, 3, 1}, {1, 3, 2, 0}};
+    for (int t = 0; t < 4; ++t) {
+        double e1[3], e2[3], nn[3], o[3];
+        sub3(V[tf[t][1]].w, V[tf[t][0]].w, e1);
+        sub3(V[tf[t][2]].w, V[tf[t][0]].w, e2);
+        cross3(e1, e2, nn);
+        sub3(V[tf[t][3]].w, V[tf[t][0]].w, o);
+        if (dot3(nn, o) <= 0) { F[nf][0] = tf[t][0]; F[nf][1] = tf[t][1]; F[nf][2] = tf[t][2]; }
+        else { F[nf][0] = tf[t][0]; F[nf][1] = tf[t][2]; F[nf][2] = tf[t][1]; }
+        ++nf;
+    }
+    double fn[EPA_MAXF][3], fdist[EPA_MAXF];
+    int best = 0;
+    for (int it = 0; it < 256; ++it) {
+        best = -1;
+        double bd = INFINITY;
+        for (int f = 0; f < nf; ++f) {
+            double e1[3], e2[3], nn[3];
+            sub3(V[F[f][1]].w, V[F[f][0]].w, e1);
+            sub3(V[F[f][2]].w, V[F[f][0]].w, e2);
+            cross3(e1, e2, nn);
+            double L = norm3(nn);
+            for (int c = 0; c < 3; ++c) fn[f][c] = nn[c] / L;
+            fdist[f] = dot3(fn[f], V[F[f][0]].w);
+            if (fdist[f] < bd) { bd = fdist[f]; best = f; }
+        }
+        SV w;
+        sup_md(A, B, fn[best], &w);
+        if (dot3(fn[best], w.w) - fdist[best] <= 1e-12 || nvx >= EPA_MAXV) break;
+        V[nvx] = w;
+        int vi = nvx++;
+        int E[EPA_MAXF][2], ne = 0, keep[EPA_MAXF][3], nk = 0;
+        for (int f = 0; f < nf; ++f) {
+            if (dot3(fn[f], w.w) - fdist[f] > 0) {
+                for (int e = 0; e < 3; ++e) {
+                    int a = F[f][e], b = F[f][(e + 1) % 3], found = -1;
+                    for (int x = 0; x < ne; ++x) if (E[x][0] == b && E[x][1] == a) { found = x; break; }
+                    if (found >= 0) { for (int x = found; x < ne - 1; ++x) { E[x][0] = E[x + 1][0]; E[x][1] = E[x + 1][1]; } --ne; }
+                    else { E[ne][0] = a; E[ne][1] = b; ++ne; }
+                }
+            } else { keep[nk][0] = F[f][0]; keep[nk][1] = F[f][1]; keep[nk][2] = F[f][2]; ++nk; }
+        }
+        if (nk + ne > EPA_MAXF) break;
+        nf = 0;
+        for (int f = 0; f < nk; ++f) { F[nf][0] = keep[f][0]; F[nf][1] = keep[f][1]; F[nf][2] = keep[f][2]; ++nf; }
+        for (int e = 0; e < ne; ++e) { F[nf][0] = E[e][0]; F[nf][1] = E[e][1]; F[nf][2] = vi; ++nf; }
+    }
+    /* recompute the closest face of the final polytope */
+    double bd = INFINITY;
+    for (int f = 0; f < nf; ++f) {
+        double e1[3], e2[3], nn[3];
+        sub3(V[F[f][1]].w, V[F[f][0]].w, e1);
+        sub3(V[F[f][2]].w, V[F[f][0]].w, e2);
+        cross3(e1, e2, nn);
+        double L = norm3(nn);
+        for (int c = 0; c < 3; ++c) fn[f][c] = nn[c] / L;
+        fdist[f] = dot3(fn[f], V[F[f][0]].w);
+        if (fdist[f] < bd) { bd = fdist[f]; best = f; }
+    }
+    const double *a = V[F[best][0]].w, *b = V[F[best][1]].w, *c = V[F[best][2]].w;
+    double p[3] = {fn[best][0] * bd, fn[best][1] * bd, fn[best][2] * bd};
+    double v0[3], v1[3], v2[3];
+    sub3(b, a, v0); sub3(c, a, v1); sub3(p, a, v2);
+    double d00 = dot3(v0, v0), d01 = dot3(v0, v1), d11 = dot3(v1, v1), d20 = dot3(v2, v0), d21 = dot3(v2, v1);
+    double den = d00 * d11 - d01 * d01;
+    double l1 = (d11 * d20 - d01 * d21) / den, l2 = (d00 * d21 - d01 * d20) / den, l0 = 1 - l1 - l2;
+    for (int k = 0; k < 3; ++k) {
+        pA[k] = l0 * V[F[best][0]].a[k] + l1 * V[F[best][1]].a[k] + l2 * V[F[best][2]].a[k];
+        pB[k] = l0 * V[F[best][0]].b[k] + l1 * V[F[best][1]].b[k] + l2 * V[F[best][2]].b[k];
+    }
+    return -bd;
+}
+
+/* signed distance and closest surface point of a solid cylinder / box */
+static double point_cylinder(const double* c, const Shape* s, double* qw) {
+    double d[3], loc[3], q[3];
+    sub3(c, s->T + 9, d);
+    matTvec3(s->T, d, loc);
+    double r = s->prm[0], h = s->prm[1], rho = sqrt(loc[0] * loc[0] + loc[1] * loc[1]), sd;
+    memcpy(q, loc, sizeof(q));
+    if (!(rho <= r && fabs(loc[2]) <= h)) {
+        if (rho > r) { q[0] = loc[0] * r / rho; q[1] = loc[1] * r / rho; }
+        q[2] = loc[2] < -h ? -h : (loc[2] > h ? h : loc[2]);
+        double dq[3] = {loc[0] - q[0], loc[1] - q[1], loc[2] - q[2]};
+        sd = norm3(dq);
+    } else {
+        double dside = r - rho, dtop = h - loc[2], dbot = h + loc[2];
+        if (dside <= dtop && dside <= dbot) {
+            if (rho > 0) { q[0] = loc[0] * r / rho; q[1] = loc[1] * r / rho; } else { q[0] = r; q[1] = 0; }
+            sd = -dside;
+        } else if (dtop <= dbot) { q[2] = h; sd = -dtop; }
+        else { q[2] = -h; sd = -dbot; }
+    }
+    matvec3(s->T, q, qw);
+    qw[0] += s->T[9]; qw[1] += s->T[10]; qw[2] += s->T[11];
+    return sd;
+}
+static double point_box(const double* c, const Shape* s, double* qw) {
+    double d[3], loc[3], q[3], sd;
+    sub3(c, s->T + 9, d);
+    matTvec3(s->T, d, loc);
+    int inside = 1;
+    for (int i = 0; i < 3; ++i) if (fabs(loc[i]) > s->prm[i]) inside = 0;
+    memcpy(q, loc, sizeof(q));
+    if (!inside) {
+        for (int i = 0; i < 3; ++i) q[i] = loc[i] < -s->prm[i] ? -s->prm[i] : (loc[i] > s->prm[i] ? s->prm[i] : loc[i]);
+        double dq[3] = {loc[0] - q[0], loc[1] - q[1], loc[2] - q[2]};
+        sd = norm3(dq);
+    } else {
+        int a = 0;
+        double g = s->prm[0] - fabs(loc[0]);
+        for (int i = 1; i < 3; ++i) { double gi = s->prm[i] - fabs(loc[i]); if (gi < g) { g = gi; a = i; } }
+        q[a] = loc[a] >= 0 ? s->prm[a] : -s->prm[a];
+        sd = -g;
+    }
+    matvec3(s->T, q, qw);
+    qw[0] += s->T[9]; qw[1] += s->T[10]; qw[2] += s->T[11];
+    return sd;
+}
+
+static double shape_distance(const Shape* A, const Shape* B, double* pA, double* pB) {
+    if (A->type == 0 && B->type == 0) {
+        double v[3];
+        sub3(B->T + 9, A->T + 9, v);
+        double L = norm3(v), n[3] = {1, 0, 0};
+        if (L > 0) { n[0] = v[0] / L; n[1] = v[1] / L; n[2] = v[2] / L; }
+        for (int i = 0; i < 3; ++i) { pA[i] = A->T[9 + i] + A->prm[0] * n[i]; pB[i] = B->T[9 + i] - B->prm[0] * n[i]; }
+        return L - A->prm[0] - B->prm[0];
+    }
+    if (A->type == 0 || B->type == 0) {
+        int flip = B->type == 0;
+        const Shape *s = flip ? B : A, *o = flip ? A : B;
+        const double* c = s->T + 9;
+        double q[3], sd = o->type == 1 ? point_cylinder(c, o, q) : point_box(c, o, q);
+        double u[3];
+        sub3(q, c, u);
+        double L = norm3(u), n[3] = {1, 0, 0};
+        if (L > 0) { n[0] = u[0] / L; n[1] = u[1] / L; n[2] = u[2] / L; }
+        if (sd < 0) { n[0] = -n[0]; n[1] = -n[1]; n[2] = -n[2]; }
+        double ps[3] = {c[0] + s->prm[0] * n[0], c[1] + s->prm[0] * n[1], c[2] + s->prm[0] * n[2]};
+        if (flip) { memcpy(pA, q, sizeof(q)); memcpy(pB, ps, sizeof(ps)); }
+        else { memcpy(pA, ps, sizeof(ps)); memcpy(pB, q, sizeof(q)); }
+        return sd - s->prm[0];
+    }
+    SV S[4];
+    int ns;
+    double lam[4], v[3];
+    if (gjk(A, B, S, &ns, lam, v)) return epa(A, B, S, ns, pA, pB);
+    for (int c = 0; c < 3; ++c) {
+        pA[c] = 0; pB[c] = 0;
+        for (int i = 0; i < ns; ++i) { pA[c] += lam[i] * S[i].a[c]; pB[c] += lam[i] * S[i].b[c]; }
+    }
+    double d[3];
+    sub3(pA, pB, d);
+    return norm3(d);
+}
+
+static void make_shape(const OracleModel* m, const Kin* k, int g, Shape* s) {
+    s->type = m->gtype[g];
+    tcompose(k->T[m->gparent[g]], m->gplace[g], s->T);
+    memcpy(s->prm, m->gparam[g], sizeof(s->prm));
+}
+
+/* RobotData::getMinDistance(true,false,false)  robot_data.cpp:424-494 */
+static void min_distance(const OracleModel* m, const Kin* k, double* dist, double* grad, int* pair_out) {
+    Shape sh[ORC_MAXG];
+    for (int g = 0; g < m->ngeom; ++g) make_shape(m, k, g, &sh[g]);
+    double best = 1.7976931348623157e308, bpA[3] = {0}, bpB[3] = {0};
+    int bi = -1;
+    for (int p = 0; p < m->npairs; ++p) {
+        double pA[3], pB[3];
+        double d = shape_distance(&sh[m->pair_a[p]], &sh[m->pair_b[p]], pA, pB);
+        if (d < best) { best = d; bi = p; memcpy(bpA, pA, sizeof(pA)); memcpy(bpB, pB, sizeof(pB)); }
+    }
+    *dist = best;
+    *pair_out = bi;
+    int nv = m->nv;
+    memset(grad, 0, nv * sizeof(double));
+    if (bi < 0) return;  /* reference indexes pair -1; we return zero gradient */
+    int jA = m->gparent[m->pair_a[bi]], jB = m->gparent[m->pair_b[bi]];
+    double n[3];
+    sub3(bpB, bpA, n);
+    double L = norm3(n);
+    n[0] /= L; n[1] /= L; n[2] /= L;
+    double JA[6 * ORC_MAXJ], JB[6 * ORC_MAXJ];
+    point_jacobian(m, k, jA, bpA, JA);
+    point_jacobian(m, k, jB, bpB, JB);
+    for (int c = 0; c < nv; ++c) {
+        double s = 0;
+        for (int i = 0; i < 3; ++i) s += n[i] * (JB[i * nv + c] - JA[i * nv + c]);
+        grad[c] = best < 0 ? -s : s;
+    }
+}
+
+/* ------------------------------------------------------------------------ */
+/* task-space helpers  (math_type_define.h)                                 */
+/* ------------------------------------------------------------------------ */
+static double cubic(double t, double t0, double tf, double x0, double xf, double xd0, double xdf) {
+    if (t < t0) return x0;
+    if (t > tf) return xf;
+    double e = t - t0, T = tf - t0, T2 = T * T, T3 = T2 * T, dx = xf - x0;
+    return x0 + xd0 * e + (3 * dx / T2 - 2 * xd0 / T - xdf / T) * e * e + (-2 * dx / T3 + (xd0 + xdf) / T2) * e * e * e;
+}
+static double cubic_dot(double t, double t0, double tf, double x0, double xf, double xd0, double xdf) {
+    if (t < t0) return xd0;
+    if (t > tf) return xdf;
+    double e = t - t0, T = tf - t0, T2 = T * T, T3 = T2 * T, dx = xf - x0;
+    return xd0 + 2 * (3 * dx / T2 - 2 * xd0 / T - xdf / T) * e + 3 * (-2 * dx / T3 + (xd0 + xdf) / T2) * e * e;
+}
+/* principal log of a rotation (row-major) as axis-angle vector */
+static void so3_log(const double* R, double* w) {
+    double c = (R[0] + R[4] + R[8] - 1) / 2;
+    c = c > 1 ? 1 : (c < -1 ? -1 : c);
+    double th = acos(c);
+    double v[3] = {R[7] - R[5], R[2] - R[6], R[3] - R[1]};
+    if (th < 1e-8) { w[0] = 0.5 * v[0]; w[1] = 0.5 * v[1]; w[2] = 0.5 * v[2]; return; }
+    if (M_PI - th < 1e-6) {
+        double B[9];
+        for (int i = 0; i < 9; ++i) B[i] = R[i] / 2;
+        B[0] += 0.5; B[4] += 0.5; B[8] += 0.5;
+        int kk = 0;
+        if (B[4] > B[kk * 4]) kk = 1;
+        if (B[8] > B[kk * 4]) kk = 2;
+        double s = sqrt(B[kk * 4]);
+        double a[3] = {B[0 * 3 + kk] / s, B[1 * 3 + kk] / s, B[2 * 3 + kk] / s};
+        if (dot3(a, v) < 0) { a[0] = -a[0]; a[1] = -a[1]; a[2] = -a[2]; }
+        w[0] = th * a[0]; w[1] = th * a[1]; w[2] = th * a[2];
+        return;
+    }
+    double f = th / (2 * sin(th));
+    w[0] = f * v[0]; w[1] = f * v[1]; w[2] = f * v[2];
+}
+static void so3_exp(const double* w, double* R) {
+    double th = norm3(w);
+    double K[9] = {0, -w[2], w[1], w[2], 0, -w[0], -w[1], w[0], 0}, K2[9];
+    matmul3(K, K, K2);
+    double a = th < 1e-12 ? 1 : sin(th) / th, b = th < 1e-12 ? 0 : (1 - cos(th)) / (th * th);
+    for (int i = 0; i < 9; ++i) R[i] = (i % 4 == 0 ? 1 : 0) + a * K[i] + b * K2[i];
+}
+/* 12-vector pose (R col-major 9, p 3) -> R row-major, p */
+static void pose_unpack(const double* x, double* R, double* p) {
+    for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) R[3 * r + c] = x[3 * c + r];
+    p[0] = x[9]; p[1] = x[10]; p[2] = x[11];
+}
+/* DyrosMath::getTaskSpaceCubic (math_type_define.h:647-687) */
+static void task_space_cubic(const double* xt, const double* xdt, const double* xi, const double* xdi,
+                             double t, double t0, double T, double* xd_out, double* xdd_out) {
+    double Rt[9], pt[3], Ri[9], pi_[3];
+    pose_unpack(xt, Rt, pt);
+    pose_unpack(xi, Ri, pi_);
+    double tf = t0 + T, Rd[9], pd[3];
+    for (int i = 0; i < 3; ++i) {
+        pd[i] = cubic(t, t0, tf, pi_[i], pt[i], xdi[i], xdt[i]);
+        xdd_out[i] = cubic_dot(t, t0, tf, pi_[i], pt[i], xdi[i], xdt[i]);
+    }
+    double RiT[9], M[9], r[3];
+    for (int a = 0; a < 3; ++a) for (int b = 0; b < 3; ++b) RiT[3 * a + b] = Ri[3 * b + a];
+    matmul3(RiT, Rt, M);
+    so3_log(M, r);
+    if (t >= tf) memcpy(Rd, Rt, sizeof(Rd));
+    else if (t < t0) memcpy(Rd, Ri, sizeof(Rd));
+    else {
+        double tau = cubic(t, t0, tf, 0, 1, 0, 0), wr[3] = {r[0] * tau, r[1] * tau, r[2] * tau}, E[9];
+        so3_exp(wr, E);
+        matmul3(Ri, E, Rd);
+    }
+    double rd[3];
+    for (int i = 0; i < 3; ++i) rd[i] = cubic_dot(t, t0, tf, 0, r[i], 0, 0);
+    double tau = (t - t0) / (tf - t0), o[3];
+    matvec3(Ri, rd, o);
+    if (tau < 0 || tau > 1) { o[0] = o[1] = o[2] = 0; }
+    xdd_out[3] = o[0]; xdd_out[4] = o[1]; xdd_out[5] = o[2];
+    for (int rr = 0; rr < 3; ++rr) for (int c = 0; c < 3; ++c) xd_out[3 * c + rr] = Rd[3 * rr + c];
+    xd_out[9] = pd[0]; xd_out[10] = pd[1]; xd_out[11] = pd[2];
+}
+
+/* ------------------------------------------------------------------------ */
+/* OSQP ADMM restatement (QP_base.h:100-180 -> OSQP)                        */
+/* ------------------------------------------------------------------------ */
+static double vnorm_inf(const double* v, int n) { double r = 0; for (int i = 0; i < n; ++i) if (fabs(v[i]) > r) r = fabs(v[i]); return r; }
+static void limit_scaling(double* v, int n) {
+    for (int i = 0; i < n; ++i) { if (v[i] < MIN_SCALING) v[i] = 1.0; else if (v[i] > MAX_SCALING) v[i] = MAX_SCALING; }
+}
+
+typedef struct QPW {
+    int n, m;
+    double P[ORC_MAXX * ORC_MAXX], q[ORC_MAXX], A[ORC_MAXC * ORC_MAXX], l[ORC_MAXC], u[ORC_MAXC];
+    double D[ORC_MAXX], E[ORC_MAXC], c;
+    double rho_vec[ORC_MAXC], rho;
+    int ctype[ORC_MAXC];  /* -1 loose, 0 ineq, 1 eq */
+    double L[ORC_MAXX * ORC_MAXX];
+    double x[ORC_MAXX], z[ORC_MAXC], y[ORC_MAXC], dy[ORC_MAXC];
+    double pri_res, dua_res, pri_res_s, dua_res_s;
+    double nAx_s, nz_s, nPx_s, nAty_s, nq_s;
+    double eps_pri, eps_dua;
+} QPW;
+
+static void qp_factor(QPW* w, double sigma) {
+    int n = w->n, m = w->m;
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < n; ++j) {
+            double s = w->P[i * n + j] + (i == j ? sigma : 0);
+            for (int k = 0; k < m; ++k) s += w->A[k * n + i] * w->rho_vec[k] * w->A[k * n + j];
+            w->L[i * n + j] = s;
+        }
+    chol(w->L, n);
+}
+
+static void set_rho_vec(QPW* w) {
+    for (int i = 0; i < w->m; ++i)
+        w->rho_vec[i] = w->ctype[i] < 0 ? RHO_MIN : (w->ctype[i] > 0 ? RHO_EQ_OVER_RHO_INEQ * w->rho : w->rho);
+}
+
+static void qp_scale(QPW* w, int iters) {
+    int n = w->n, m = w->m;
+    for (int i = 0; i < n; ++i) w->D[i] = 1;
+    for (int i = 0; i < m; ++i) w->E[i] = 1;
+    w->c = 1;
+    for (int it = 0; it < iters; ++it) {
+        double Dt[ORC_MAXX], Et[ORC_MAXC];
+        for (int j = 0; j < n; ++j) {
+            double s = 0;
+            for (int i = 0; i < n; ++i) s = fmax(s, fabs(w->P[i * n + j]));
+            for (int i = 0; i < m; ++i) s = fmax(s, fabs(w->A[i * n + j]));
+            Dt[j] = s;
+        }
+        for (int i = 0; i < m; ++i) { double s = 0; for (int j = 0; j < n; ++j) s = fmax(s, fabs(w->A[i * n + j])); Et[i] = s; }
+        limit_scaling(Dt, n);
+        limit_scaling(Et, m);
+        for (int j = 0; j < n; ++j) Dt[j] = 1.0 / sqrt(Dt[j]);
+        for (int i = 0; i < m; ++i) Et[i] = 1.0 / sqrt(Et[i]);
+        for (int i = 0; i < n; ++i) for (int j = 0; j < n; ++j) w->P[i * n + j] *= Dt[i] * Dt[j];
+        for (int i = 0; i < m; ++i) for (int j = 0; j < n; ++j) w->A[i * n + j] *= Et[i] * Dt[j];
+        for (int j = 0; j < n; ++j) { w->q[j] *= Dt[j]; w->D[j] *= Dt[j]; }
+        for (int i = 0; i < m; ++i) w->E[i] *= Et[i];
+        /* cost scaling */
+        double cm = 0;
+        for (int j = 0; j < n; ++j) { double s = 0; for (int i = 0; i < n; ++i) s = fmax(s, fabs(w->P[i * n + j])); cm += s; }
+        cm /= n;
+        double nq = vnorm_inf(w->q, n);
+        limit_scaling(&nq, 1);
+        double ct = fmax(cm, nq);
+        limit_scaling(&ct, 1);
+        ct = 1.0 / ct;
+        for (int i = 0; i < n * n; ++i) w->P[i] *= ct;
+        for (int j = 0; j < n; ++j) w->q[j] *= ct;
+        w->c *= ct;
+    }
+    for (int i = 0; i < m; ++i) {
+        w->l[i] *= w->E[i];
+        w->u[i] *= w->E[i];
+    }
+}
+
+/* residuals at the current iterate (scaled and unscaled) */
+static void qp_residuals(QPW* w, const double* x, const double* z, const double* y, double eps_abs, double eps_rel) {
+    int n = w->n, m = w->m;
+    double Ax[ORC_MAXC], Px[ORC_MAXX], Aty[ORC_MAXX];
+    for (int i = 0; i < m; ++i) { double s = 0; for (int j = 0; j < n; ++j) s += w->A[i * n + j] * x[j]; Ax[i] = s; }
+    for (int i = 0; i < n; ++i) { double s = 0, t = 0; for (int j = 0; j < n; ++j) s += w->P[i * n + j] * x[j]; for (int k = 0; k < m; ++k) t += w->A[k * n + i] * y[k]; Px[i] = s; Aty[i] = t; }
+    double pr = 0, prs = 0, nAx = 0, nz = 0, nAxs = 0, nzs = 0;
+    for (int i = 0; i < m; ++i) {
+        double r = Ax[i] - z[i];
+        prs = fmax(prs, fabs(r));
+        pr = fmax(pr, fabs(r / w->E[i]));
+        nAx = fmax(nAx, fabs(Ax[i] / w->E[i]));
+        nz = fmax(nz, fabs(z[i] / w->E[i]));
+        nAxs = fmax(nAxs, fabs(Ax[i]));
+        nzs = fmax(nzs, fabs(z[i]));
+    }
+    double dr = 0, drs = 0, nPx = 0, nAty = 0, nq = 0, nPxs = 0, nAtys = 0, nqs = 0;
+    for (int i = 0; i < n; ++i) {
+        double r = Px[i] + w->q[i] + Aty[i];
+        drs = fmax(drs, fabs(r));
+        dr = fmax(dr, fabs(r / w->D[i]));
+        nPx = fmax(nPx, fabs(Px[i] / w->D[i]));
+        nAty = fmax(nAty, fabs(Aty[i] / w->D[i]));
+        nq = fmax(nq, fabs(w->q[i] / w->D[i]));
+        nPxs = fmax(nPxs, fabs(Px[i]));
+        nAtys = fmax(nAtys, fabs(Aty[i]));
+        nqs = fmax(nqs, fabs(w->q[i]));
+    }
+    w->pri_res = pr;
+    w->dua_res = dr / w->c;
+    w->pri_res_s = prs;
+    w->dua_res_s = drs;
+    w->nAx_s = nAxs; w->nz_s = nzs; w->nPx_s = nPxs; w->nAty_s = nAtys; w->nq_s = nqs;
+    w->eps_pri = eps_abs + eps_rel * fmax(nAx, nz);
+    w->eps_dua = eps_abs + eps_rel * fmax(fmax(nPx, nAty), nq) / w->c;
+}
+
+static int qp_primal_infeasible(QPW* w, double eps) {
+    int n = w->n, m = w->m;
+    double dy[ORC_MAXC], nrm = 0;
+    for (int i = 0; i < m; ++i) {
+        double d = w->dy[i];
+        if (w->ctype[i] < 0) d = 0;
+        else if (w->u[i] > INFTY * MIN_SCALING) d = d < 0 ? d : 0;
+        else if (w->l[i] < -INFTY * MIN_SCALING) d = d > 0 ? d : 0;
+        dy[i] = d;
+        nrm = fmax(nrm, fabs(w->E[i] * d));
+    }
+    if (nrm <= DIVISION_TOL) return 0;
+    double lhs = 0;
+    for (int i = 0; i < m; ++i) {
+        if (dy[i] > 0) lhs += w->u[i] * dy[i];
+        else if (dy[i] < 0) lhs += w->l[i] * dy[i];
+    }
+    if (!(lhs < -eps * nrm)) return 0;
+    for (int j = 0; j < n; ++j) {
+        double s = 0;
+        for (int i = 0; i < m; ++i) s += w->A[i * n + j] * dy[i];
+        if (fabs(s / w->D[j]) >= eps * nrm) return 0;
+    }
+    return 1;
+}
+
+/* LDL^T of a quasi-definite dense matrix (no pivoting) */
+static int ldlt(double* K, int N, double* Dg) {
+    for (int j = 0; j < N; ++j) {
+        double d = K[j * N + j];
+        for (int k = 0; k < j; ++k) d -= K[j * N + k] * K[j * N + k] * Dg[k];
+        if (d == 0) return 0;
+        Dg[j] = d;
+        for (int i = j + 1; i < N; ++i) {
+            double t = K[i * N + j];
+            for (int k = 0; k < j; ++k) t -= K[i * N + k] * K[j * N + k] * Dg[k];
+            K[i * N + j] = t / d;
+        }
+    }
+    return 1;
+}
+static void ldlt_solve(const double* L, const double* Dg, int N, double* b) {
+    for (int i = 0; i < N; ++i) { double t = b[i]; for (int k = 0; k < i; ++k) t -= L[i * N + k] * b[k]; b[i] = t; }
+    for (int i = 0; i < N; ++i) b[i] /= Dg[i];
+    for (int i = N - 1; i >= 0; --i) { double t = b[i]; for (int k = i + 1; k < N; ++k) t -= L[k * N + i] * b[k]; b[i] = t; }
+}
+
+/* OSQP polish (polish.c) restated; on success writes x, z, y (scaled).
+ * strict != 0 additionally certifies KKT and dual signs. */
+static int qp_polish(QPW* w, const OracleSettings* s, int strict) {
+    int n = w->n, m = w->m;
+    int act[ORC_MAXC], nact = 0;
+    double b[ORC_MAXC];
+    for (int i = 0; i < m; ++i) {
+        if (w->z[i] - w->l[i] < -w->y[i]) { act[nact] = i; b[nact++] = w->l[i]; }
+        else if (w->u[i] - w->z[i] < w->y[i]) { act[nact] = i; b[nact++] = w->u[i]; }
+    }
+    int N = n + nact;
+    static __thread double K[(ORC_MAXX + ORC_MAXC) * (ORC_MAXX + ORC_MAXC)], K0[(ORC_MAXX + ORC_MAXC) * (ORC_MAXX + ORC_MAXC)];
+    double Dg[ORC_MAXX + ORC_MAXC], rhs[ORC_MAXX + ORC_MAXC], sol[ORC_MAXX + ORC_MAXC], r[ORC_MAXX + ORC_MAXC];
+    for (int i = 0; i < N * N; ++i) K0[i] = 0;
+    for (int i = 0; i < n; ++i) for (int j = 0; j < n; ++j) K0[i * N + j] = w->P[i * n + j];
+    for (int a = 0; a < nact; ++a)
+        for (int j = 0; j < n; ++j) { K0[(n + a) * N + j] = w->A[act[a] * n + j]; K0[j * N + n + a] = w->A[act[a] * n + j]; }
+    memcpy(K, K0, N * N * sizeof(double));
+    for (int i = 0; i < n; ++i) K[i * N + i] += s->delta;
+    for (int a = 0; a < nact; ++a) K[(n + a) * N + n + a] -= s->delta;
+    if (!ldlt(K, N, Dg)) return 0;
+    for (int i = 0; i < n; ++i) rhs[i] = -w->q[i];
+    for (int a = 0; a < nact; ++a) rhs[n + a] = b[a];
+    memcpy(sol, rhs, N * sizeof(double));
+    ldlt_solve(K, Dg, N, sol);
+    for (int it = 0; it < s->polish_refine_iter; ++it) {
+        for (int i = 0; i < N; ++i) { double t = rhs[i]; for (int j = 0; j < N; ++j) t -= K0[i * N + j] * sol[j]; r[i] = t; }
+        ldlt_solve(K, Dg, N, r);
+        for (int i = 0; i < N; ++i) sol[i] += r[i];
+    }
+    double xp[ORC_MAXX], yp[ORC_MAXC], zp[ORC_MAXC];
+    for (int i = 0; i < n; ++i) xp[i] = sol[i];
+    for (int i = 0; i < m; ++i) yp[i] = 0;
+    for (int a = 0; a < nact; ++a) yp[act[a]] = sol[n + a];
+    for (int i = 0; i < m; ++i) {
+        double t = 0;
+        for (int j = 0; j < n; ++j) t += w->A[i * n + j] * xp[j];
+        zp[i] = t < w->l[i] ? w->l[i] : (t > w->u[i] ? w->u[i] : t);
+    }
+    double pr0 = w->pri_res, dr0 = w->dua_res;
+    static __thread QPW tmp;  /* residuals of the polished point */
+    memcpy(&tmp, w, sizeof(QPW));
+    qp_residuals(&tmp, xp, zp, yp, s->eps_exact, s->eps_exact);
+    int ok = (tmp.pri_res < pr0 && tmp.dua_res < dr0) || (tmp.pri_res < pr0 && dr0 < 1e-10) || (tmp.dua_res < dr0 && pr0 < 1e-10);
+    if (strict) {
+        /* certified optimum: KKT residuals at eps_exact and dual signs that
+         * match the guessed active bounds (y<=0 at l, y>=0 at u) */
+        ok = tmp.pri_res <= tmp.eps_pri && tmp.dua_res <= tmp.eps_dua;
+        for (int a = 0; a < nact && ok; ++a) {
+            int i = act[a];
+            if (w->l[i] == w->u[i]) continue;
+            double yi = w->E[i] * yp[i] / w->c;
+            int lower = b[a] == w->l[i];
+            if (lower && yi > tmp.eps_dua) ok = 0;
+            if (!lower && yi < -tmp.eps_dua) ok = 0;
+        }
+    }
+    if (!ok) return 0;
+    memcpy(w->x, xp, n * sizeof(double));
+    memcpy(w->y, yp, m * sizeof(double));
+    memcpy(w->z, zp, m * sizeof(double));
+    w->pri_res = tmp.pri_res;
+    w->dua_res = tmp.dua_res;
+    return 1;
+}
+
+int oracle_solve_qp(int n, int m, const double* P, const double* qv, const double* A,
+                    const double* l, const double* u, const OracleSettings* s,
+                    double* x, double* y, int* iters, int* polished) {
+    static __thread QPW w;
+    w.n = n; w.m = m;
+    for (int i = 0; i < n * n; ++i) if (!isfinite(P[i])) return ORC_NONFINITE;
+    for (int i = 0; i < n; ++i) if (!isfinite(qv[i])) return ORC_NONFINITE;
+    for (int i = 0; i < m * n; ++i) if (!isfinite(A[i])) return ORC_NONFINITE;
+    for (int i = 0; i < m; ++i) if (isnan(l[i]) || isnan(u[i])) return ORC_NONFINITE;
+    memcpy(w.P, P, n * n * sizeof(double));
+    memcpy(w.q, qv, n * sizeof(double));
+    memcpy(w.A, A, m * n * sizeof(double));
+    for (int i = 0; i < m; ++i) { w.l[i] = fmax(l[i], -INFTY); w.u[i] = fmin(u[i], INFTY); }
+    qp_scale(&w, s->scaling);
+    for (int i = 0; i < m; ++i) {
+        if (w.l[i] < -INFTY * MIN_SCALING && w.u[i] > INFTY * MIN_SCALING) w.ctype[i] = -1;
+        else if (w.u[i] - w.l[i] < RHO_TOL) w.ctype[i] = 1;
+        else w.ctype[i] = 0;
+    }
+    w.rho = s->rho;
+    set_rho_vec(&w);
+    qp_factor(&w, s->sigma);
+    memset(w.x, 0, sizeof(w.x));
+    memset(w.z, 0, sizeof(w.z));
+    memset(w.y, 0, sizeof(w.y));
+    int status = ORC_MAX_ITER, it, pol = 0;
+    double alpha = s->alpha;
+    for (it = 1; it <= s->max_iter; ++it) {
+        double xt[ORC_MAXX], zt[ORC_MAXC], rhs[ORC_MAXX];
+        for (int j = 0; j < n; ++j) {
+            double t = s->sigma * w.x[j] - w.q[j];
+            for (int i = 0; i < m; ++i) t += w.A[i * n + j] * (w.rho_vec[i] * w.z[i] - w.y[i]);
+            rhs[j] = t;
+        }
+        memcpy(xt, rhs, n * sizeof(double));
+        chol_solve(w.L, n, xt);
+        for (int i = 0; i < m; ++i) { double t = 0; for (int j = 0; j < n; ++j) t += w.A[i * n + j] * xt[j]; zt[i] = t; }
+        for (int j = 0; j < n; ++j) w.x[j] = alpha * xt[j] + (1 - alpha) * w.x[j];
+        for (int i = 0; i < m; ++i) {
+            double zr = alpha * zt[i] + (1 - alpha) * w.z[i];
+            double zn = zr + w.y[i] / w.rho_vec[i];
+            zn = zn < w.l[i] ? w.l[i] : (zn > w.u[i] ? w.u[i] : zn);
+            w.dy[i] = w.rho_vec[i] * (zr - zn);
+            w.y[i] += w.dy[i];
+            w.z[i] = zn;
+        }
+        int check = s->check_termination > 0 && it % s->check_termination == 0;
+        int adapt = s->adaptive_rho && s->adaptive_rho_interval > 0 && it % s->adaptive_rho_interval == 0;
+        if (check || adapt) qp_residuals(&w, w.x, w.z, w.y, s->eps_abs, s->eps_rel);
+        if (check) {
+            if (w.pri_res < w.eps_pri && w.dua_res < w.eps_dua) {
+                if (!s->exact) { status = ORC_SOLVED; break; }
+                if (qp_polish(&w, s, 1)) { status = ORC_SOLVED; pol = 1; break; }
+                /* tight ADMM-only fallback */
+                static __thread QPW t2;
+                memcpy(&t2, &w, sizeof(QPW));
+                qp_residuals(&t2, w.x, w.z, w.y, s->eps_fallback, s->eps_fallback);
+                if (t2.pri_res < t2.eps_pri && t2.dua_res < t2.eps_dua) { status = ORC_SOLVED; break; }
+            } else if (qp_primal_infeasible(&w, s->eps_prim_inf)) {
+                status = ORC_PRIMAL_INFEASIBLE;
+                break;
+            }
+        }
+        if (adapt) {
+            double pr = w.pri_res_s / (fmax(w.nAx_s, w.nz_s) + DIVISION_TOL);
+            double dr = w.dua_res_s / (fmax(fmax(w.nq_s, w.nAty_s), w.nPx_s) + DIVISION_TOL);
+            double rn = w.rho * sqrt(pr / (dr + DIVISION_TOL));
+            rn = fmin(fmax(rn, RHO_MIN), RHO_MAX);
+            if (rn > w.rho * s->adaptive_rho_tolerance || rn < w.rho / s->adaptive_rho_tolerance) {
+                w.rho = rn;
+                set_rho_vec(&w);
+                qp_factor(&w, s->sigma);
+            }
+        }
+    }
+    if (status == ORC_SOLVED && s->polish && !s->exact && !pol) pol = qp_polish(&w, s, 0);
+    *iters = it > s->max_iter ? s->max_iter : it;
+    *polished = pol;
+    for (int j = 0; j < n; ++j) x[j] = w.D[j] * w.x[j];
+    for (int i = 0; i < m; ++i) y[i] = w.E[i] * w.y[i] / w.c;
+    return status;
+}
+
+/* ------------------------------------------------------------------------ */
+/* controller entry: QPIK / QPIKStep / QPIKCubic                            */
+/* ------------------------------------------------------------------------ */
+void oracle_default_params(int kind, OracleParams* p, int exact) {
+    memset(p, 0, sizeof(*p));
+    for (int i = 0; i < 6; ++i) {
+        p->kp[i] = kind == 0 ? 100 : 400;   /* robot_controller.cpp:12 / MoMa :15 */
+        p->kv[i] = kind == 0 ? 20 : 0;      /* MoMa QPIKStep has no Kv term (:177) */
+    }
+    p->alpha_cbf = 50;
+    p->w_reg = kind == 0 ? 1.0 : 0.01;
+    p->slack_w = 1000;
+    p->man_min = 0.01;
+    p->dist_min = 0.05;
+    p->mode = 1;
+    OracleSettings* s = &p->solver;
+    s->rho = 0.1; s->sigma = 1e-6; s->alpha = 1.6;
+    s->eps_abs = 1e-3; s->eps_rel = 1e-3; s->eps_prim_inf = 1e-4;
+    s->max_iter = 4000; s->check_termination = 25; s->scaling = 10;
+    s->adaptive_rho = 1; s->adaptive_rho_interval = 25; s->adaptive_rho_tolerance = 5;
+    s->polish = exact ? 1 : 0; s->polish_refine_iter = 3; s->delta = 1e-6;
+    s->exact = exact; s->eps_exact = 1e-9; s->eps_fallback = 1e-7;
+}
+
+int oracle_qpik_one(const OracleModel* m, const OracleParams* p, const double* q, const double* qdot,
+                    const double* x_target, const double* xdot_target, const double* x_init,
+                    const double* xdot_init, double* out, OracleDiag* diag) {
+    int nv = m->nv;
+    Kin k;
+    kin_fk(m, q, &k);
+    double J[6 * ORC_MAXJ];
+    point_jacobian(m, &k, m->ee_joint, k.pe, J);
+    int moma = m->kind == 1;
+    int na = moma ? m->n_wheel + m->n_arm : nv;
+    /* selection matrix (MoMa robot_data.cpp:24-25,115-120) */
+    double S[ORC_MAXJ * ORC_MAXJ];
+    if (moma) {
+        memset(S, 0, sizeof(double) * nv * na);
+        for (int i = 0; i < m->n_arm; ++i) S[(m->mani_start + i) * na + m->act_mani_start + i] = 1;
+        for (int i = 0; i < m->n_wheel; ++i) S[(m->mobi_start + i) * na + m->act_mobi_start + i] = 1;
+        double yaw = q[m->virtual_start + 2], cy = cos(yaw), sy = sin(yaw);
+        double Rz[9] = {cy, -sy, 0, sy, cy, 0, 0, 0, 1};
+        for (int r = 0; r < 3; ++r)
+            for (int wcol = 0; wcol < m->n_wheel; ++wcol) {
+                double s = 0;
+                for (int c = 0; c < 3; ++c) s += Rz[3 * r + c] * m->J_mobile[c][wcol];
+                S[(m->virtual_start + r) * na + m->act_mobi_start + wcol] = s;
+            }
+    }
+    /* task error and desired task velocity */
+    double xdot_des[6];
+    if (p->mode == 0) memcpy(xdot_des, xdot_target, sizeof(xdot_des));
+    else {
+        double xt[12], xdt[6];
+        if (p->mode == 2) task_space_cubic(x_target, xdot_target, x_init, xdot_init, p->t, p->t0, p->duration, xt, xdt);
+        else { memcpy(xt, x_target, sizeof(xt)); memcpy(xdt, xdot_target, sizeof(xdt)); }
+        double Rt[9], pt[3];
+        pose_unpack(xt, Rt, pt);
+        double xd[6];  /* getVelocity = J qdot (robot_data.cpp:419-422) */
+        for (int i = 0; i < 6; ++i) { double s = 0; for (int c = 0; c < nv; ++c) s += J[i * nv + c] * qdot[c]; xd[i] = s; }
+        double e[6];
+        for (int i = 0; i < 3; ++i) e[i] = pt[i] - k.pe[i];
+        /* getPhi(R_target, R) = -1/2 sum_i Rt[:,i] x R[:,i] */
+        double phi[3] = {0, 0, 0};
+        for (int i = 0; i < 3; ++i) {
+            double a[3] = {Rt[i], Rt[3 + i], Rt[6 + i]}, b[3] = {k.Te[i], k.Te[3 + i], k.Te[6 + i]}, c[3];
+            cross3(a, b, c);
+            phi[0] += c[0]; phi[1] += c[1]; phi[2] += c[2];
+        }
+        for (int i = 0; i < 3; ++i) e[3 + i] = -0.5 * phi[i];
+        for (int i = 0; i < 6; ++i)
+            xdot_des[i] = moma ? p->kp[i] * e[i] + xdt[i] : p->kp[i] * e[i] + p->kv[i] * (xdt[i] - xd[i]);
+    }
+    /* manipulability + min distance */
+    double man, mgrad[ORC_MAXJ], dist, dgrad[ORC_MAXJ];
+    int pair;
+    int c0 = moma ? m->mani_start : 0, narm = moma ? m->n_arm : nv;
+    manip(m, &k, J, c0, narm, &man, mgrad);
+    min_distance(m, &k, &dist, dgrad, &pair);
+    /* QP assembly */
+    static __thread double P[ORC_MAXX * ORC_MAXX], A[ORC_MAXC * ORC_MAXX];
+    double qv[ORC_MAXX], l[ORC_MAXC], u[ORC_MAXC];
+    int nx, nc;
+    double a = p->alpha_cbf;
+    if (!moma) {
+        int n = nv;
+        nx = 3 * n + 2;
+        int ng = 2 * n + 2;
+        nc = nx + ng;
+        memset(P, 0, sizeof(double) * nx * nx);
+        memset(A, 0, sizeof(double) * nc * nx);
+        for (int i = 0; i < n; ++i)
+            for (int j = 0; j < n; ++j) {
+                double s = 0;
+                for (int r = 0; r < 6; ++r) s += J[r * nv + i] * J[r * nv + j];
+                P[i * nx + j] = 2 * s + (i == j ? p->w_reg : 0);
+            }
+        for (int i = 0; i < n; ++i) { double s = 0; for (int r = 0; r < 6; ++r) s += J[r * nv + i] * xdot_des[r]; qv[i] = -2 * s; }
+        for (int i = n; i < nx; ++i) qv[i] = p->slack_w;
+        for (int i = 0; i < nx; ++i) A[i * nx + i] = 1;
+        for (int i = 0; i < n; ++i) { l[i] = -m->vel[i]; u[i] = m->vel[i]; }
+        for (int i = n; i < nx; ++i) { l[i] = 0; u[i] = INFTY; }
+        double* G = A + nx * nx;
+        double* lg = l + nx;
+        for (int i = 0; i < n; ++i) {
+            G[i * nx + i] = 1; G[i * nx + n + i] = 1; lg[i] = -a * (q[i] - m->lower[i]);
+            G[(n + i) * nx + i] = -1; G[(n + i) * nx + 2 * n + i] = 1; lg[n + i] = -a * (m->upper[i] - q[i]);
+        }
+        for (int c = 0; c < n; ++c) { G[(2 * n) * nx + c] = mgrad[c]; G[(2 * n + 1) * nx + c] = dgrad[c]; }
+        G[(2 * n) * nx + 3 * n] = 1; G[(2 * n + 1) * nx + 3 * n + 1] = 1;
+        lg[2 * n] = -a * (man - p->man_min);
+        lg[2 * n + 1] = -a * (dist - p->dist_min);
+        for (int i = nx; i < nc; ++i) u[i] = INFTY;
+    } else {
+        int n = m->n_arm;
+        nx = na;
+        int ng = 2 * n + 2;
+        nc = nx + ng;
+        double Jt[6 * ORC_MAXJ];
+        for (int r = 0; r < 6; ++r)
+            for (int c = 0; c < na; ++c) { double s = 0; for (int j = 0; j < nv; ++j) s += J[r * nv + j] * S[j * na + c]; Jt[r * na + c] = s; }
+        memset(A, 0, sizeof(double) * nc * nx);
+        for (int i = 0; i < na; ++i)
+            for (int j = 0; j < na; ++j) {
+                double s = 0;
+                for (int r = 0; r < 6; ++r) s += Jt[r * na + i] * Jt[r * na + j];
+                P[i * nx + j] = 2 * s + (i == j ? p->w_reg : 0);
+            }
+        for (int i = 0; i < na; ++i) { double s = 0; for (int r = 0; r < 6; ++r) s += Jt[r * na + i] * xdot_des[r]; qv[i] = -2 * s; }
+        for (int i = 0; i < nx; ++i) { A[i * nx + i] = 1; l[i] = -INFTY; u[i] = INFTY; }
+        double* G = A + nx * nx;
+        double* lg = l + nx;
+        int as = m->act_mani_start, js = m->mani_start;
+        for (int i = 0; i < n; ++i) {
+            G[i * nx + as + i] = 1; lg[i] = -a * (q[js + i] - m->lower[js + i]);
+            G[(n + i) * nx + as + i] = -1; lg[n + i] = -a * (m->upper[js + i] - q[js + i]);
+        }
+        for (int c = 0; c < n; ++c) { G[(2 * n) * nx + as + c] = mgrad[c]; G[(2 * n + 1) * nx + as + c] = dgrad[js + c]; }
+        lg[2 * n] = -a * (man - p->man_min);
+        lg[2 * n + 1] = -a * (dist - p->dist_min);
+        for (int i = nx; i < nc; ++i) u[i] = INFTY;
+    }
+    double x[ORC_MAXX], y[ORC_MAXC];
+    int iters = 0, pol = 0;
+    int st = oracle_solve_qp(nx, nc, P, qv, A, l, u, &p->solver, x, y, &iters, &pol);
+    /* QP_IK.cpp:53-67 / MoMa :43-57: zero on any non-Solved status */
+    for (int i = 0; i < na; ++i) out[i] = st == ORC_SOLVED ? x[i] : 0.0;
+    if (diag) {
+        for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) diag->pose[3 * r + c] = k.Te[3 * r + c];
+        memcpy(diag->pose + 9, k.pe, 3 * sizeof(double));
+        memcpy(diag->J, J, 6 * nv * sizeof(double));
+        memcpy(diag->xdot_des, xdot_des, sizeof(xdot_des));
+        diag->man = man;
+        memcpy(diag->man_grad, mgrad, narm * sizeof(double));
+        diag->dist = dist;
+        memcpy(diag->dist_grad, dgrad, nv * sizeof(double));
+        diag->pair = pair;
+        diag->iters = iters;
+        diag->polished = pol;
+    }
+    return st;
+}
+
+/* ------------------------------------------------------------------------ */
+/* batched SoA driver with a thread pool                                    */
+/* ------------------------------------------------------------------------ */
+typedef struct Job {
+    const OracleModel* m; const OracleParams* p; int64_t B, lo, hi;
+    const double *q, *qdot, *xt, *xdt, *xi, *xdi;
+    double* out; int32_t* status; int32_t* iters; int64_t fails;
+} Job;
+
+static void* worker(void* arg) {
+    Job* j = (Job*)arg;
+    const OracleModel* m = j->m;
+    int nv = m->nv, na = m->kind == 1 ? m->n_wheel + m->n_arm : nv;
+    for (int64_t b = j->lo; b < j->hi; ++b) {
+        double q[ORC_MAXJ], qd[ORC_MAXJ], xt[12], xdt[6], xi[12], xdi[6], out[ORC_MAXJ];
+        for (int i = 0; i < nv; ++i) { q[i] = j->q[i * j->B + b]; qd[i] = j->qdot[i * j->B + b]; }
+        for (int i = 0; i < 12; ++i) xt[i] = j->xt ? j->xt[i * j->B + b] : 0;
+        for (int i = 0; i < 6; ++i) xdt[i] = j->xdt[i * j->B + b];
+        for (int i = 0; i < 12; ++i) xi[i] = j->xi ? j->xi[i * j->B + b] : 0;
+        for (int i = 0; i < 6; ++i) xdi[i] = j->xdi ? j->xdi[i * j->B + b] : 0;
+        OracleDiag dg;
+        int st = oracle_qpik_one(m, j->p, q, qd, xt, xdt, xi, xdi, out, &dg);
+        for (int i = 0; i < na; ++i) j->out[i * j->B + b] = out[i];
+        if (j->status) j->status[b] = st;
+        if (j->iters) j->iters[b] = dg.iters;
+        if (st != ORC_SOLVED) j->fails++;
+    }
+    return NULL;
+}
+
+int64_t oracle_qpik_batch(const OracleModel* m, const OracleParams* p, int64_t B, const double* q,
+                          const double* qdot, const double* x_target, const double* xdot_target,
+                          const double* x_init, const double* xdot_init, double* out, int32_t* status,
+                          int32_t* iters, int nthreads) {
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    Job jobs[256];
+    pthread_t th[256];
+    int64_t per = (B + nthreads - 1) / nthreads;
+    for (int t = 0; t < nthreads; ++t) {
+        Job* j = &jobs[t];
+        j->m = m; j->p = p; j->B = B; j->lo = t * per; j->hi = (t + 1) * per < B ? (t + 1) * per : B;
+        if (j->lo > B) j->lo = B;
+        j->q = q; j->qdot = qdot; j->xt = x_target; j->xdt = xdot_target; j->xi = x_init; j->xdi = xdot_init;
+        j->out = out; j->status = status; j->iters = iters; j->fails = 0;
+        pthread_create(&th[t], NULL, worker, j);
+    }
+    int64_t fails = 0;
+    for (int t = 0; t < nthreads; ++t) { pthread_join(th[t], NULL); fails += jobs[t].fails; }
+    return fails;
+}
+
+/* ------------------------------------------------------------------------ */
+/* stage helpers for tests                                                  */
+/* ------------------------------------------------------------------------ */
+void oracle_fk_pose(const OracleModel* m, const double* q, double* pose12, double* J) {
+    Kin k;
+    kin_fk(m, q, &k);
+    memcpy(pose12, k.Te, 12 * sizeof(double));
+    if (J) point_jacobian(m, &k, m->ee_joint, k.pe, J);
+}
+void oracle_min_distance(const OracleModel* m, const double* q, double* dist, double* grad, int* pair) {
+    Kin k;
+    kin_fk(m, q, &k);
+    min_distance(m, &k, dist, grad, pair);
+}
+void oracle_pair_distance(const OracleModel* m, const double* q, int pair, double* d, double* pA, double* pB) {
+    Kin k;
+    kin_fk(m, q, &k);
+    Shape a, b;
+    make_shape(m, &k, m->pair_a[pair], &a);
+    make_shape(m, &k, m->pair_b[pair], &b);
+    *d = shape_distance(&a, &b, pA, pB);
+}
+void oracle_manipulability(const OracleModel* m, const double* q, double* man, double* grad) {
+    Kin k;
+    kin_fk(m, q, &k);
+    double J[6 * ORC_MAXJ];
+    point_jacobian(m, &k, m->ee_joint, k.pe, J);
+    int c0 = m->kind == 1 ? m->mani_start : 0, nc = m->kind == 1 ? m->n_arm : m->nv;
+    manip(m, &k, J, c0, nc, man, grad);
+}

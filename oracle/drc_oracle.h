@@ -1,0 +1,126 @@
+/*
+ * ORACLE / TEST INFRASTRUCTURE ONLY.
+ *
+ * Plain-C restatement of the reference QP-IK hot path
+ * (YoungWook0533/dyros_robot_controller v0.3.0), used by tests/, by
+ * __graft_entry__.smoke() and by bench.py's cpu_baseline leg as the checker
+ * and the CPU baseline.  It is never linked into, or called by, the product
+ * library (dyros_robot_controller_amd/libdrc_amd.so).
+ *
+ * What it restates (file:line in the reference):
+ *   kinematics       src/manipulator/robot_data.cpp:101-107,378-422
+ *   manipulability   src/manipulator/robot_data.cpp:519-553
+ *   min distance     src/manipulator/robot_data.cpp:424-494 (hpp-fcl GJK/EPA
+ *                    semantics restated: parity unpinned)
+ *   task helpers     include/math_type_define.h:62-298,563-570,633-687
+ *   QP assembly      src/manipulator/QP_IK.cpp:7-131,
+ *                    src/mobile_manipulator/QP_IK.cpp:7-128,
+ *                    include/dyros_robot_controller/QP_base.h:65-227
+ *   QP solve         QP_base.h:100-180 -> OSQP's ADMM (Stellato et al. 2020)
+ *                    restated: Ruiz scaling, rho vector, adaptive rho,
+ *                    termination, primal-infeasibility test and polish
+ *   controllers      src/manipulator/robot_controller.cpp:277-317,
+ *                    src/mobile_manipulator/robot_controller.cpp:147-197
+ *   mobile FK Jac.   src/mobile/robot_data.cpp:138-176,
+ *                    src/mobile_manipulator/robot_data.cpp:107-124
+ */
+#ifndef DRC_ORACLE_H
+#define DRC_ORACLE_H
+#include <stdint.h>
+
+#define ORC_MAXJ 32
+#define ORC_MAXG 96
+#define ORC_MAXP 1024
+#define ORC_MAXX 32
+#define ORC_MAXC 64
+
+typedef struct OracleModel {
+    int nv;                          /* number of 1-DoF joints              */
+    int parent[ORC_MAXJ + 1];        /* joint parent (0 = universe)         */
+    int jtype[ORC_MAXJ + 1];         /* 0 revolute, 1 prismatic             */
+    double jplace[ORC_MAXJ + 1][12]; /* R (row-major 9) + p (3), in parent  */
+    double axis[ORC_MAXJ + 1][3];
+    double lower[ORC_MAXJ], upper[ORC_MAXJ], vel[ORC_MAXJ];
+    int ee_joint;                    /* task frame parent joint             */
+    double ee_place[12];
+    int ngeom;
+    int gparent[ORC_MAXG];
+    int gtype[ORC_MAXG];             /* 0 sphere, 1 cylinder, 2 box         */
+    double gplace[ORC_MAXG][12];
+    double gparam[ORC_MAXG][3];      /* sphere r | cyl r,h/2 | box half ext */
+    int npairs;
+    int pair_a[ORC_MAXP], pair_b[ORC_MAXP];
+    /* whole-body (mobile manipulator) description; kind 0 = manipulator */
+    int kind;                        /* 0 manipulator, 1 mobile manipulator */
+    int n_arm, n_wheel;              /* MoMa: arm dof, wheel count          */
+    int virtual_start, mani_start, mobi_start;   /* JointIndex            */
+    int act_mani_start, act_mobi_start;          /* ActuatorIndex         */
+    double J_mobile[3][8];           /* base twist / wheel velocity (3xW)   */
+} OracleModel;
+
+typedef struct OracleSettings {
+    double rho, sigma, alpha;
+    double eps_abs, eps_rel, eps_prim_inf;
+    int max_iter, check_termination, scaling;
+    int adaptive_rho, adaptive_rho_interval;
+    double adaptive_rho_tolerance;
+    int polish, polish_refine_iter;
+    double delta;
+    int exact;                       /* certified polish + tight fallback   */
+    double eps_exact;                /* strict KKT acceptance               */
+    double eps_fallback;             /* ADMM-only tight termination         */
+} OracleSettings;
+
+typedef struct OracleParams {
+    double kp[6], kv[6];
+    double alpha_cbf, w_reg, slack_w, man_min, dist_min;
+    int mode;                        /* 0 QPIK, 1 QPIKStep, 2 QPIKCubic     */
+    double t, t0, duration;          /* QPIKCubic timing                    */
+    OracleSettings solver;
+} OracleParams;
+
+/* per-instance diagnostics (stage parity) */
+typedef struct OracleDiag {
+    double pose[12];                 /* R row-major + p                    */
+    double J[6 * ORC_MAXJ];          /* 6 x nv row-major                   */
+    double xdot_des[6];
+    double man, man_grad[ORC_MAXJ];
+    double dist, dist_grad[ORC_MAXJ];
+    int pair;
+    int iters;
+    int polished;
+} OracleDiag;
+
+enum { ORC_SOLVED = 1, ORC_MAX_ITER = -2, ORC_PRIMAL_INFEASIBLE = -3, ORC_NONFINITE = -10 };
+
+void oracle_default_params(int kind, OracleParams* p, int exact);
+
+/* One QPIK* solve (reference semantics) for one instance.
+ * Manipulator: q, qdot[nv]; MoMa: q, qdot are the full joint vectors [nv].
+ * x_target: 12 (R col-major 9, p 3); xdot_target: 6; for mode 2 also
+ * x_init/xdot_init.  out: nv (manipulator) or A = n_wheel + n_arm (MoMa,
+ * actuator order).  Returns status. */
+int oracle_qpik_one(const OracleModel* m, const OracleParams* p,
+                    const double* q, const double* qdot,
+                    const double* x_target, const double* xdot_target,
+                    const double* x_init, const double* xdot_init,
+                    double* out, OracleDiag* diag);
+
+/* Batched SoA driver ([field][B] layout, the product's HBM layout) with a
+ * pthread pool of nthreads workers.  Returns number of non-solved. */
+int64_t oracle_qpik_batch(const OracleModel* m, const OracleParams* p, int64_t B,
+                          const double* q, const double* qdot,
+                          const double* x_target, const double* xdot_target,
+                          const double* x_init, const double* xdot_init,
+                          double* out, int32_t* status, int32_t* iters, int nthreads);
+
+/* stage helpers exposed for tests */
+void oracle_fk_pose(const OracleModel* m, const double* q, double* pose12, double* J6xn);
+void oracle_min_distance(const OracleModel* m, const double* q, double* dist, double* grad, int* pair);
+void oracle_pair_distance(const OracleModel* m, const double* q, int pair, double* d, double* pA, double* pB);
+void oracle_manipulability(const OracleModel* m, const double* q, double* man, double* grad);
+int oracle_solve_qp(int nx, int nc, const double* P, const double* qv, const double* A,
+                    const double* l, const double* u, const OracleSettings* s,
+                    double* x, double* y, int* iters, int* polished);
+
+#endif

@@ -1,0 +1,277 @@
+"""ORACLE / TEST INFRASTRUCTURE ONLY — ctypes front-end of the C restatement
+(``oracle/drc_oracle.c``).  Only tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg import this module, as the checker.
+
+The model handed to the C oracle is built by the *oracle's own* numpy URDF
+parser (``pyref_model.py``), independently of the product's C++ parser, so
+a parser mistake in either shows up as a parity failure.
+"""
+import ctypes as C
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+import pyref_model  # noqa: E402
+
+MAXJ, MAXG, MAXP = 32, 96, 1024
+
+SOLVED, MAX_ITER, PRIMAL_INFEASIBLE, NONFINITE = 1, -2, -3, -10
+
+
+class OracleModel(C.Structure):
+    _fields_ = [
+        ("nv", C.c_int),
+        ("parent", C.c_int * (MAXJ + 1)),
+        ("jtype", C.c_int * (MAXJ + 1)),
+        ("jplace", (C.c_double * 12) * (MAXJ + 1)),
+        ("axis", (C.c_double * 3) * (MAXJ + 1)),
+        ("lower", C.c_double * MAXJ),
+        ("upper", C.c_double * MAXJ),
+        ("vel", C.c_double * MAXJ),
+        ("ee_joint", C.c_int),
+        ("ee_place", C.c_double * 12),
+        ("ngeom", C.c_int),
+        ("gparent", C.c_int * MAXG),
+        ("gtype", C.c_int * MAXG),
+        ("gplace", (C.c_double * 12) * MAXG),
+        ("gparam", (C.c_double * 3) * MAXG),
+        ("npairs", C.c_int),
+        ("pair_a", C.c_int * MAXP),
+        ("pair_b", C.c_int * MAXP),
+        ("kind", C.c_int),
+        ("n_arm", C.c_int),
+        ("n_wheel", C.c_int),
+        ("virtual_start", C.c_int),
+        ("mani_start", C.c_int),
+        ("mobi_start", C.c_int),
+        ("act_mani_start", C.c_int),
+        ("act_mobi_start", C.c_int),
+        ("J_mobile", (C.c_double * 8) * 3),
+    ]
+
+
+class OracleSettings(C.Structure):
+    _fields_ = [
+        ("rho", C.c_double), ("sigma", C.c_double), ("alpha", C.c_double),
+        ("eps_abs", C.c_double), ("eps_rel", C.c_double), ("eps_prim_inf", C.c_double),
+        ("max_iter", C.c_int), ("check_termination", C.c_int), ("scaling", C.c_int),
+        ("adaptive_rho", C.c_int), ("adaptive_rho_interval", C.c_int),
+        ("adaptive_rho_tolerance", C.c_double),
+        ("polish", C.c_int), ("polish_refine_iter", C.c_int),
+        ("delta", C.c_double),
+        ("exact", C.c_int),
+        ("eps_exact", C.c_double),
+        ("eps_fallback", C.c_double),
+    ]
+
+
+class OracleParams(C.Structure):
+    _fields_ = [
+        ("kp", C.c_double * 6), ("kv", C.c_double * 6),
+        ("alpha_cbf", C.c_double), ("w_reg", C.c_double), ("slack_w", C.c_double),
+        ("man_min", C.c_double), ("dist_min", C.c_double),
+        ("mode", C.c_int),
+        ("t", C.c_double), ("t0", C.c_double), ("duration", C.c_double),
+        ("solver", OracleSettings),
+    ]
+
+
+class OracleDiag(C.Structure):
+    _fields_ = [
+        ("pose", C.c_double * 12),
+        ("J", C.c_double * (6 * MAXJ)),
+        ("xdot_des", C.c_double * 6),
+        ("man", C.c_double), ("man_grad", C.c_double * MAXJ),
+        ("dist", C.c_double), ("dist_grad", C.c_double * MAXJ),
+        ("pair", C.c_int), ("iters", C.c_int), ("polished", C.c_int),
+    ]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        so = os.path.join(HERE, "libdrc_oracle.so")
+        if not os.path.exists(so):
+            subprocess.check_call(["make", "-s", "-C", HERE])
+        _lib = C.CDLL(so)
+        d = C.POINTER(C.c_double)
+        _lib.oracle_qpik_one.restype = C.c_int
+        _lib.oracle_qpik_batch.restype = C.c_int64
+        _lib.oracle_qpik_batch.argtypes = [C.POINTER(OracleModel), C.POINTER(OracleParams), C.c_int64,
+                                           d, d, d, d, d, d, d, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.c_int]
+        _lib.oracle_solve_qp.restype = C.c_int
+    return _lib
+
+
+def _se3_to12(T):
+    out = np.zeros(12)
+    out[:9] = T[:3, :3].reshape(-1)     # row-major R
+    out[9:] = T[:3, 3]
+    return out
+
+
+def robots_dir():
+    return os.path.join(HERE, "..", "dyros_robot_controller_amd", "robots")
+
+
+def mecanum_fk_jacobian(radius, positions, angles, rollers):
+    """Mobile::RobotData::MecanumFKJacobian (src/mobile/robot_data.cpp:149-176)."""
+    from pyref import pinv_cod
+    Jinv = np.zeros((len(rollers), 3))
+    for i, (pp, pt, g) in enumerate(zip(positions, angles, rollers)):
+        A1 = np.array([[1, 0, -pp[1]], [0, 1, pp[0]]])
+        A2 = np.array([[np.cos(pt), np.sin(pt)], [-np.sin(pt), np.cos(pt)]])
+        A3 = np.array([[1, np.tan(g)]])
+        Jinv[i] = (1.0 / radius) * (A3 @ A2 @ A1)
+    return pinv_cod(Jinv)
+
+
+def differential_fk_jacobian(radius, width):
+    """Mobile::RobotData::DifferentialFKJacobian (src/mobile/robot_data.cpp:138-147)."""
+    return np.array([[radius / 2, radius / 2], [0, 0], [-radius / width, radius / width]])
+
+
+ROBOTS = {
+    "fr3": dict(urdf="fr3/fr3.urdf", srdf="fr3/fr3.srdf", ee="fr3_link8", kind=0),
+    "ur5e": dict(urdf="ur5e/ur5e.urdf", srdf="ur5e/ur5e.srdf", ee="tool0", kind=0),
+    "husky_fr3": dict(urdf="husky_fr3/husky_fr3.urdf", srdf="husky_fr3/husky_fr3.srdf", ee="fr3_link8", kind=1,
+                      n_arm=7, n_wheel=2, joint_index=(0, 3, 10), actuator_index=(0, 7),
+                      J_mobile=lambda: differential_fk_jacobian(0.165, 0.555)),
+    "xls_fr3": dict(urdf="xls_fr3/xls_fr3.urdf", srdf="xls_fr3/xls_fr3.srdf", ee="fr3_link8", kind=1,
+                    n_arm=7, n_wheel=4, joint_index=(0, 3, 10), actuator_index=(0, 7),
+                    J_mobile=lambda: mecanum_fk_jacobian(
+                        0.120, [(0.2225, 0.2045), (0.2225, -0.2045), (-0.2225, 0.2045), (-0.2225, -0.2045)],
+                        [0, 0, 0, 0], [-np.pi / 4, np.pi / 4, np.pi / 4, -np.pi / 4])),
+}
+
+
+def load(robot):
+    """Returns (pyref Model, OracleModel, spec)."""
+    spec = ROBOTS[robot]
+    rd = robots_dir()
+    pm = pyref_model.load_urdf(os.path.join(rd, spec["urdf"]), os.path.join(rd, spec["srdf"]))
+    om = OracleModel()
+    om.nv = pm.nv
+    for j in range(1, pm.nv + 1):
+        om.parent[j] = pm.jparent[j]
+        om.jtype[j] = pm.jtype[j]
+        for i, v in enumerate(_se3_to12(pm.jplacement[j])):
+            om.jplace[j][i] = v
+        for i in range(3):
+            om.axis[j][i] = pm.jaxis[j][i]
+        om.lower[j - 1] = pm.lower[j - 1]
+        om.upper[j - 1] = pm.upper[j - 1]
+        om.vel[j - 1] = pm.vel[j - 1]
+    jid, place = pm.frames[spec["ee"]]
+    om.ee_joint = jid
+    for i, v in enumerate(_se3_to12(place)):
+        om.ee_place[i] = v
+    om.ngeom = len(pm.geoms)
+    for g, geo in enumerate(pm.geoms):
+        om.gparent[g] = geo["parent_joint"]
+        om.gtype[g] = geo["type"]
+        for i, v in enumerate(_se3_to12(geo["placement"])):
+            om.gplace[g][i] = v
+        for i in range(3):
+            om.gparam[g][i] = geo["params"][i]
+    om.npairs = len(pm.pairs)
+    for p, (a, b) in enumerate(pm.pairs):
+        om.pair_a[p] = a
+        om.pair_b[p] = b
+    om.kind = spec["kind"]
+    if spec["kind"] == 1:
+        om.n_arm, om.n_wheel = spec["n_arm"], spec["n_wheel"]
+        om.virtual_start, om.mani_start, om.mobi_start = spec["joint_index"]
+        om.act_mani_start, om.act_mobi_start = spec["actuator_index"]
+        Jm = spec["J_mobile"]()
+        for r in range(3):
+            for c in range(spec["n_wheel"]):
+                om.J_mobile[r][c] = Jm[r, c]
+    return pm, om, spec
+
+
+def default_params(kind, exact=True):
+    p = OracleParams()
+    lib().oracle_default_params(C.c_int(kind), C.byref(p), C.c_int(1 if exact else 0))
+    return p
+
+
+def _ptr(a):
+    return a.ctypes.data_as(C.POINTER(C.c_double)) if a is not None else None
+
+
+def qpik_one(om, params, q, qdot, x_target=None, xdot_target=None, x_init=None, xdot_init=None):
+    nv = om.nv
+    na = om.n_wheel + om.n_arm if om.kind == 1 else nv
+    q = np.ascontiguousarray(q, float)
+    qdot = np.ascontiguousarray(qdot, float)
+    xt = np.ascontiguousarray(x_target if x_target is not None else np.zeros(12), float)
+    xdt = np.ascontiguousarray(xdot_target if xdot_target is not None else np.zeros(6), float)
+    xi = np.ascontiguousarray(x_init if x_init is not None else np.zeros(12), float)
+    xdi = np.ascontiguousarray(xdot_init if xdot_init is not None else np.zeros(6), float)
+    out = np.zeros(na)
+    dg = OracleDiag()
+    st = lib().oracle_qpik_one(C.byref(om), C.byref(params), _ptr(q), _ptr(qdot), _ptr(xt), _ptr(xdt),
+                               _ptr(xi), _ptr(xdi), _ptr(out), C.byref(dg))
+    return st, out, dg
+
+
+def qpik_batch(om, params, q, qdot, x_target, xdot_target, x_init=None, xdot_init=None, nthreads=1):
+    """SoA batch ([field][B]) exactly like the product's HBM layout."""
+    B = q.shape[1]
+    na = om.n_wheel + om.n_arm if om.kind == 1 else om.nv
+    out = np.zeros((na, B))
+    status = np.zeros(B, np.int32)
+    iters = np.zeros(B, np.int32)
+    arrs = [np.ascontiguousarray(a, float) if a is not None else None for a in (q, qdot, x_target, xdot_target, x_init, xdot_init)]
+    lib().oracle_qpik_batch(C.byref(om), C.byref(params), C.c_int64(B), *[_ptr(a) for a in arrs], _ptr(out),
+                            status.ctypes.data_as(C.POINTER(C.c_int32)), iters.ctypes.data_as(C.POINTER(C.c_int32)),
+                            C.c_int(nthreads))
+    return out, status, iters
+
+
+def fk_pose(om, q):
+    pose = np.zeros(12)
+    J = np.zeros(6 * om.nv)
+    lib().oracle_fk_pose(C.byref(om), _ptr(np.ascontiguousarray(q, float)), _ptr(pose), _ptr(J))
+    return pose, J.reshape(6, om.nv)
+
+
+def min_distance(om, q):
+    d = C.c_double()
+    g = np.zeros(om.nv)
+    p = C.c_int()
+    lib().oracle_min_distance(C.byref(om), _ptr(np.ascontiguousarray(q, float)), C.byref(d), _ptr(g), C.byref(p))
+    return d.value, g, p.value
+
+
+def pair_distance(om, q, pair):
+    d = C.c_double()
+    pA, pB = np.zeros(3), np.zeros(3)
+    lib().oracle_pair_distance(C.byref(om), _ptr(np.ascontiguousarray(q, float)), C.c_int(pair), C.byref(d), _ptr(pA), _ptr(pB))
+    return d.value, pA, pB
+
+
+def manipulability(om, q):
+    m = C.c_double()
+    n = om.n_arm if om.kind == 1 else om.nv
+    g = np.zeros(n)
+    lib().oracle_manipulability(C.byref(om), _ptr(np.ascontiguousarray(q, float)), C.byref(m), _ptr(g))
+    return m.value, g
+
+
+def solve_qp(P, qv, A, l, u, settings):
+    n, m = P.shape[0], A.shape[0]
+    x, y = np.zeros(n), np.zeros(m)
+    it, pol = C.c_int(), C.c_int()
+    arrs = [np.ascontiguousarray(a, float) for a in (P, qv, A, l, u)]
+    st = lib().oracle_solve_qp(C.c_int(n), C.c_int(m), *[_ptr(a) for a in arrs], C.byref(settings),
+                               _ptr(x), _ptr(y), C.byref(it), C.byref(pol))
+    return st, x, y, it.value, pol.value
