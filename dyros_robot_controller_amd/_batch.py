@@ -1,0 +1,78 @@
+"""Batched device-side entry: torch tensors in HBM -> C-ABI -> HIP kernel.
+
+torch is used as plumbing only (device allocations and the current HIP
+stream); the arithmetic happens in ``libdrc_amd.so``.
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import _capi
+
+_FIELD_SHAPES = {"q": "dof", "qdot": "dof", "x_target": 12, "xdot_target": 6, "x_init": 12, "xdot_init": 6}
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def as_device(a, device):
+    """float64, contiguous, on ``device`` (a torch.device)."""
+    torch = _torch()
+    if a is None:
+        return None
+    if not isinstance(a, torch.Tensor):
+        a = torch.as_tensor(np.asarray(a, dtype=np.float64))
+    return a.to(device=device, dtype=torch.float64).contiguous()
+
+
+def _ptr(t):
+    return C.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def check_shapes(dof, B, **fields):
+    for k, v in fields.items():
+        if v is None:
+            continue
+        rows = dof if _FIELD_SHAPES[k] == "dof" else _FIELD_SHAPES[k]
+        if tuple(v.shape) != (rows, B):
+            raise ValueError("%s must be [%d][B=%d] (field-major SoA), got %s" % (k, rows, B, tuple(v.shape)))
+
+
+def qpik_batch(model, params, q, qdot, x_target=None, xdot_target=None, x_init=None, xdot_init=None,
+               out=None, status=None, iters=None, stream=None):
+    """Launch ``drc_qpik_batch`` on device tensors laid out [field][B]."""
+    torch = _torch()
+    dev = q.device
+    B = q.shape[1]
+    check_shapes(model.dof, B, q=q, qdot=qdot, x_target=x_target, xdot_target=xdot_target,
+                 x_init=x_init, xdot_init=xdot_init)
+    if out is None:
+        out = torch.empty((model.actuated_dof, B), dtype=torch.float64, device=dev)
+    if status is None:
+        status = torch.empty(B, dtype=torch.int32, device=dev)
+    if stream is None:
+        stream = torch.cuda.current_stream(dev).cuda_stream
+    _capi.check(_capi.lib().drc_qpik_batch(
+        model.handle, C.byref(params), C.c_int64(B), _ptr(q), _ptr(qdot), _ptr(x_target), _ptr(xdot_target),
+        _ptr(x_init), _ptr(xdot_init), _ptr(out), _ptr(status), _ptr(iters), C.c_void_p(stream)))
+    return out, status
+
+
+def stages_batch(model, params, q, qdot, x_target=None, xdot_target=None, x_init=None, xdot_init=None):
+    """Stage outputs (pose, J, manipulability, min distance, task velocity)."""
+    torch = _torch()
+    dev = q.device
+    B = q.shape[1]
+    nv = model.dof
+    mani = model.mani_dof
+    f = lambda r: torch.zeros((r, B), dtype=torch.float64, device=dev)
+    pose, jac, man, dist, xdd = f(12), f(6 * nv), f(1 + mani), f(1 + nv), f(6)
+    pair = torch.zeros(B, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    _capi.check(_capi.lib().drc_qpik_stages_batch(
+        model.handle, C.byref(params), C.c_int64(B), _ptr(q), _ptr(qdot), _ptr(x_target), _ptr(xdot_target),
+        _ptr(x_init), _ptr(xdot_init), _ptr(pose), _ptr(jac), _ptr(man), _ptr(dist), _ptr(pair), _ptr(xdd),
+        C.c_void_p(stream)))
+    return dict(pose=pose, jac=jac, man=man, dist=dist, pair=pair, xdot_des=xdd)

@@ -1,0 +1,57 @@
+// Robot model: host-side URDF/SRDF build and the flat device image the
+// kernels read.  Restates Pinocchio's model/geometry build as the reference
+// uses it in Manipulator::RobotData::RobotData (src/manipulator/robot_data.cpp:7-70).
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace drc_amd {
+
+constexpr int kMaxJoints = 16;    // 1-DoF joints (XLS-FR3 needs 14)
+constexpr int kMaxGeoms = 64;
+constexpr int kMaxPairs = 512;
+constexpr int kMaxFrames = 64;
+constexpr int kMaxWheels = 8;
+
+enum JointType : int { kRevolute = 0, kPrismatic = 1 };
+enum GeomType : int { kSphere = 0, kCylinder = 1, kBox = 2 };
+
+// Flat, POD model image in HBM.  Transforms are 12 doubles: R row-major, p.
+struct DevModel {
+  int nv, ngeom, npairs, nframes;
+  int kind;                        // 0 manipulator, 1 mobile manipulator
+  int n_arm, n_wheel;
+  int virtual_start, mani_start, mobi_start;
+  int act_mani_start, act_mobi_start;
+  int parent[kMaxJoints + 1];
+  int jtype[kMaxJoints + 1];
+  uint32_t anc[kMaxJoints + 1];    // bit (k-1) set iff joint k supports joint j (inclusive)
+  double jplace[kMaxJoints + 1][12];
+  double axis[kMaxJoints + 1][3];
+  double lower[kMaxJoints], upper[kMaxJoints], vel[kMaxJoints];
+  int frame_joint[kMaxFrames];
+  double frame_place[kMaxFrames][12];
+  int gparent[kMaxGeoms];
+  int gtype[kMaxGeoms];
+  double gplace[kMaxGeoms][12];
+  double gparam[kMaxGeoms][3];     // sphere r | cylinder r, h/2 | box half extents
+  double gbound[kMaxGeoms];        // conservative core/bounding radius for the broad phase
+  int16_t pair_a[kMaxPairs], pair_b[kMaxPairs];
+  double J_mobile[3][kMaxWheels];  // base twist = J_mobile * wheel velocity
+};
+
+struct HostModel {
+  DevModel dev{};
+  std::vector<std::string> joint_names;   // index j-1
+  std::vector<std::string> frame_names;   // link (BODY) frames, index = frame id
+  std::vector<std::string> geom_names;
+  std::vector<double> effort;
+};
+
+// Returns 0 on success, DRC_ERR_* otherwise; err gets a readable reason.
+int build_model_from_urdf(const std::string& urdf_path, const std::string& srdf_path,
+                          HostModel* out, std::string* err);
+
+}  // namespace drc_amd

@@ -1,0 +1,1933 @@
+// MI355X-native batched QP-IK: one wavefront per robot instance.
+//
+// Hot path of the reference (SURVEY.md §3 call stacks A and C), fused into a
+// single kernel per control cycle:
+//   FK / LWA frame Jacobian        robot_data.cpp:101-107,392-402
+//   task error (+ cubic profile)   math_type_define.h:633-687, robot_controller.cpp:292-317
+//   manipulability + gradient      robot_data.cpp:519-553 (MoMa :439-475)
+//   min self-distance + gradient   robot_data.cpp:424-494 (hpp-fcl GJK/EPA semantics)
+//   QP assembly                    QP_IK.cpp:69-131 (MoMa QP_IK.cpp:59-128), QP_base.h:202-227
+//   QP solve                       QP_base.h:100-180 -> OSQP ADMM (+ polish) restated
+//   zero-on-failure                QP_IK.cpp:53-67
+//
+// HBM layout: every batched array is field-major [F][B] so each field is a
+// contiguous, coalesced stream over the batch.  Model constants (~12 KB)
+// stay in L2/scalar cache; per-instance working state lives in LDS.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+
+#include "../../include/drc_amd.h"
+#include "model.hpp"
+#include "qpik_device.hpp"
+
+namespace drc_amd {
+
+// Kernel parameters, passed by value.  LDS offsets (in doubles) are laid out
+// by the host from the model dimensions (see plan_layout()).
+struct KParams {
+  double kp[6], kv[6], ff, alpha_cbf, w_reg, slack_w, man_min, dist_min;
+  double t, t0, duration;
+  double frame_place[12];
+  int frame_joint, mode, stages;
+  int nv, nx, ng, np, na, m, narm, c0;
+  drc_solver_settings s;
+  // persistent QP region
+  int oP, oG, oQ, oAB, oL, oU, oD, oE, oRho, oX, oZ, oY, oDY, oXT, oZT, oT1, oT2, oRed, oSc;
+  // union region (kinematics | K^-1 | polish)
+  int oU0;
+  int kT, kZ, kTe, kJ, kTg, kq, kqd, kA6, kAi, kW, kPart, kPd, kPf, kxdd, kmg, kdg, kJt, kSv, kScr;
+  int lds_doubles;
+};
+
+
+// ---- diagnostic phase stamps (built only with -DDRC_PHASE_TIMING) ---------
+#ifdef DRC_PHASE_TIMING
+__device__ unsigned long long g_phase_cycles[32];
+#define PH_DECL unsigned long long ph_prev = __builtin_amdgcn_s_memtime(), ph_acc[16] = {0};
+#define PH(k)                                              \
+  do {                                                     \
+    unsigned long long t_ = __builtin_amdgcn_s_memtime();  \
+    ph_acc[k] += t_ - ph_prev;                             \
+    ph_prev = t_;                                          \
+  } while (0)
+#define PH_FLUSH(base)                                                            \
+  do {                                                                            \
+    if (lane_id() == 0)                                                           \
+      for (int k_ = 0; k_ < 16; ++k_) atomicAdd(&g_phase_cycles[(base) + k_], ph_acc[k_]); \
+  } while (0)
+#else
+#define PH_DECL
+#define PH(k) do {} while (0)
+#define PH_FLUSH(base) do {} while (0)
+#endif
+
+// scalar slots in the oSc region
+enum { SC_C = 0, SC_RHO, SC_MAN, SC_DIST, SC_PAIR, SC_PRI, SC_DUA, SC_EPSP, SC_EPSD, SC_PRIS, SC_DUAS,
+       SC_NAX, SC_NZ, SC_NPX, SC_NATY, SC_NQ, SC_NF, SC_NR, SC_WIN, SC_COUNT };
+
+// ------------------------------------------------------------------------
+// small serial helpers (lane 0)
+// ------------------------------------------------------------------------
+// Serial 6x6 kernels run by one lane; every work array lives in LDS
+// (ws, 160 doubles) so nothing is a dynamically indexed private array.
+__device__ double det_lu6(const double* A, double* M) {
+  for (int i = 0; i < 36; ++i) M[i] = A[i];
+  double det = 1;
+  for (int c = 0; c < 6; ++c) {
+    int p = c;
+    for (int r = c + 1; r < 6; ++r)
+      if (fabs(M[r * 6 + c]) > fabs(M[p * 6 + c])) p = r;
+    if (M[p * 6 + c] == 0) return 0;
+    if (p != c) {
+      for (int j = 0; j < 6; ++j) {
+        double t = M[c * 6 + j];
+        M[c * 6 + j] = M[p * 6 + j];
+        M[p * 6 + j] = t;
+      }
+      det = -det;
+    }
+    det *= M[c * 6 + c];
+    for (int r = c + 1; r < 6; ++r) {
+      double f = M[r * 6 + c] / M[c * 6 + c];
+      for (int j = c; j < 6; ++j) M[r * 6 + j] -= f * M[c * 6 + j];
+    }
+  }
+  return det;
+}
+
+// column-pivoted Householder QR rank with |R_ii| > 1e-6 max|R_ii| (Eigen COD)
+__device__ int rank_cpqr6(const double* A, double* ws) {
+  double *M = ws, *cn = ws + 36, *piv = ws + 42, *v = ws + 48;
+  double maxpiv = 0;
+  for (int i = 0; i < 36; ++i) M[i] = A[i];
+  for (int k = 0; k < 6; ++k) {
+    for (int j = k; j < 6; ++j) {
+      double s = 0;
+      for (int i = k; i < 6; ++i) s += M[i * 6 + j] * M[i * 6 + j];
+      cn[j] = s;
+    }
+    int p = k;
+    for (int j = k + 1; j < 6; ++j)
+      if (cn[j] > cn[p]) p = j;
+    if (p != k)
+      for (int i = 0; i < 6; ++i) {
+        double t = M[i * 6 + k];
+        M[i * 6 + k] = M[i * 6 + p];
+        M[i * 6 + p] = t;
+      }
+    double nrm = sqrt(cn[p]);
+    piv[k] = nrm;
+    maxpiv = fmax(maxpiv, nrm);
+    if (nrm == 0) {
+      for (int r = k + 1; r < 6; ++r) piv[r] = 0;
+      break;
+    }
+    double alpha = M[k * 6 + k] > 0 ? -nrm : nrm, vn = 0;
+    for (int i = k; i < 6; ++i) v[i] = M[i * 6 + k];
+    v[k] -= alpha;
+    for (int i = k; i < 6; ++i) vn += v[i] * v[i];
+    if (vn > 0)
+      for (int j = k; j < 6; ++j) {
+        double s = 0;
+        for (int i = k; i < 6; ++i) s += v[i] * M[i * 6 + j];
+        s = 2 * s / vn;
+        for (int i = k; i < 6; ++i) M[i * 6 + j] -= s * v[i];
+      }
+  }
+  int r = 0;
+  for (int k = 0; k < 6; ++k) r += piv[k] > 1e-6 * maxpiv;
+  return r;
+}
+
+// DyrosMath::PinvCOD of the symmetric PSD 6x6 JJ^T (math_type_define.h:563)
+__device__ void pinv_cod6(const double* A, double* X, double* ws) {
+  int r = rank_cpqr6(A, ws);
+  double* L = ws;  // rank work is dead now
+  double* e = ws + 36;
+  bool ok = r == 6;
+  if (ok) {
+    for (int i = 0; i < 36; ++i) L[i] = A[i];
+    for (int j = 0; j < 6 && ok; ++j) {
+      double s = L[j * 6 + j];
+      for (int k = 0; k < j; ++k) s -= L[j * 6 + k] * L[j * 6 + k];
+      if (!(s > 0)) {
+        ok = false;
+        break;
+      }
+      double d = sqrt(s);
+      L[j * 6 + j] = d;
+      for (int i = j + 1; i < 6; ++i) {
+        double t = L[i * 6 + j];
+        for (int k = 0; k < j; ++k) t -= L[i * 6 + k] * L[j * 6 + k];
+        L[i * 6 + j] = t / d;
+      }
+    }
+  }
+  if (ok) {
+    for (int c = 0; c < 6; ++c) {
+      for (int i = 0; i < 6; ++i) e[i] = i == c ? 1.0 : 0.0;
+      for (int i = 0; i < 6; ++i) {
+        double t = e[i];
+        for (int k = 0; k < i; ++k) t -= L[i * 6 + k] * e[k];
+        e[i] = t / L[i * 6 + i];
+      }
+      for (int i = 5; i >= 0; --i) {
+        double t = e[i];
+        for (int k = i + 1; k < 6; ++k) t -= L[k * 6 + i] * e[k];
+        e[i] = t / L[i * 6 + i];
+      }
+      for (int i = 0; i < 6; ++i) X[i * 6 + c] = e[i];
+    }
+    return;
+  }
+  // rank-deficient: Moore-Penrose via symmetric Jacobi on the top-r modes
+  double *M = ws, *V = ws + 36, *w = ws + 72, *idx = ws + 78;
+  for (int i = 0; i < 36; ++i) {
+    M[i] = A[i];
+    V[i] = (i % 7 == 0) ? 1.0 : 0.0;
+  }
+  for (int sweep = 0; sweep < 60; ++sweep) {
+    double off = 0;
+    for (int i = 0; i < 6; ++i)
+      for (int j = i + 1; j < 6; ++j) off += M[i * 6 + j] * M[i * 6 + j];
+    if (off < 1e-300) break;
+    for (int p = 0; p < 6; ++p)
+      for (int q = p + 1; q < 6; ++q) {
+        if (fabs(M[p * 6 + q]) < 1e-300) continue;
+        double th = (M[q * 6 + q] - M[p * 6 + p]) / (2 * M[p * 6 + q]);
+        double t = (th >= 0 ? 1 : -1) / (fabs(th) + sqrt(th * th + 1));
+        double c = 1 / sqrt(t * t + 1), s = t * c;
+        for (int k = 0; k < 6; ++k) {
+          double a = M[k * 6 + p], b = M[k * 6 + q];
+          M[k * 6 + p] = c * a - s * b;
+          M[k * 6 + q] = s * a + c * b;
+        }
+        for (int k = 0; k < 6; ++k) {
+          double a = M[p * 6 + k], b = M[q * 6 + k];
+          M[p * 6 + k] = c * a - s * b;
+          M[q * 6 + k] = s * a + c * b;
+        }
+        for (int k = 0; k < 6; ++k) {
+          double a = V[k * 6 + p], b = V[k * 6 + q];
+          V[k * 6 + p] = c * a - s * b;
+          V[k * 6 + q] = s * a + c * b;
+        }
+      }
+  }
+  for (int i = 0; i < 6; ++i) {
+    w[i] = M[i * 7];
+    idx[i] = i;
+  }
+  for (int i = 0; i < 6; ++i)
+    for (int j = i + 1; j < 6; ++j)
+      if (fabs(w[(int)idx[j]]) > fabs(w[(int)idx[i]])) {
+        double t = idx[i];
+        idx[i] = idx[j];
+        idx[j] = t;
+      }
+  for (int i = 0; i < 36; ++i) X[i] = 0;
+  for (int kk = 0; kk < r; ++kk) {
+    int e2 = (int)idx[kk];
+    for (int i = 0; i < 6; ++i)
+      for (int j = 0; j < 6; ++j) X[i * 6 + j] += V[i * 6 + e2] * V[j * 6 + e2] / w[e2];
+  }
+}
+
+__device__ double cubic(double t, double t0, double tf, double x0, double xf, double xd0, double xdf) {
+  if (t < t0) return x0;
+  if (t > tf) return xf;
+  double e = t - t0, T = tf - t0, T2 = T * T, T3 = T2 * T, dx = xf - x0;
+  return x0 + xd0 * e + (3 * dx / T2 - 2 * xd0 / T - xdf / T) * e * e + (-2 * dx / T3 + (xd0 + xdf) / T2) * e * e * e;
+}
+__device__ double cubic_dot(double t, double t0, double tf, double x0, double xf, double xd0, double xdf) {
+  if (t < t0) return xd0;
+  if (t > tf) return xdf;
+  double e = t - t0, T = tf - t0, T2 = T * T, T3 = T2 * T, dx = xf - x0;
+  return xd0 + 2 * (3 * dx / T2 - 2 * xd0 / T - xdf / T) * e + 3 * (-2 * dx / T3 + (xd0 + xdf) / T2) * e * e;
+}
+// principal log of a rotation matrix (row-major) as an axis-angle vector
+__device__ V3 so3_log(const double* R) {
+  double c = (R[0] + R[4] + R[8] - 1) / 2;
+  c = c > 1 ? 1 : (c < -1 ? -1 : c);
+  double th = acos(c);
+  V3 v = v3(R[7] - R[5], R[2] - R[6], R[3] - R[1]);
+  if (th < 1e-8) return 0.5 * v;
+  if (M_PI - th < 1e-6) {
+    double B[9];
+    for (int i = 0; i < 9; ++i) B[i] = R[i] / 2;
+    B[0] += 0.5;
+    B[4] += 0.5;
+    B[8] += 0.5;
+    int k = 0;
+    if (B[4] > B[k * 4]) k = 1;
+    if (B[8] > B[k * 4]) k = 2;
+    double s = sqrt(B[k * 4]);
+    V3 a = v3(B[k] / s, B[3 + k] / s, B[6 + k] / s);
+    if (dot(a, v) < 0) a = -1.0 * a;
+    return th * a;
+  }
+  return (th / (2 * sin(th))) * v;
+}
+__device__ void so3_exp(V3 w, double* R) {
+  double th = sqrt(dot(w, w));
+  double K[9] = {0, -w.z, w.y, w.z, 0, -w.x, -w.y, w.x, 0}, K2[9];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) K2[3 * i + j] = K[3 * i] * K[j] + K[3 * i + 1] * K[3 + j] + K[3 * i + 2] * K[6 + j];
+  double a = th < 1e-12 ? 1 : sin(th) / th, b = th < 1e-12 ? 0 : (1 - cos(th)) / (th * th);
+  for (int i = 0; i < 9; ++i) R[i] = (i % 4 == 0 ? 1 : 0) + a * K[i] + b * K2[i];
+}
+
+// ------------------------------------------------------------------------
+// OSQP residuals (lane-parallel): fills SC_* slots.  x, z, y in LDS (scaled)
+// ------------------------------------------------------------------------
+__device__ __forceinline__ void residuals(const KParams& kp, double* S, const double* x, const double* z, const double* y,
+                          double eps_abs, double eps_rel) {
+  const int l = lane_id(), nx = kp.nx, ng = kp.ng, np = kp.np;
+  const double *P = S + kp.oP, *G = S + kp.oG, *q = S + kp.oQ, *ab = S + kp.oAB, *D = S + kp.oD, *E = S + kp.oE;
+  double pr = 0, prs = 0, nAx = 0, nz = 0, nAxs = 0, nzs = 0;
+  double dr = 0, drs = 0, nPx = 0, nAty = 0, nq = 0, nPxs = 0, nAtys = 0, nqs = 0;
+  if (l < nx) {  // bound row l and variable l
+    double ax = ab[l] * x[l], r = ax - z[l];
+    prs = fabs(r);
+    pr = fabs(r / E[l]);
+    nAx = fabs(ax / E[l]);
+    nz = fabs(z[l] / E[l]);
+    nAxs = fabs(ax);
+    nzs = fabs(z[l]);
+    double px = 0;
+    if (l < np)
+      for (int c = 0; c < np; ++c) px += P[l * np + c] * x[c];
+    double aty = ab[l] * y[l];
+    for (int i = 0; i < ng; ++i) aty += G[i * nx + l] * y[nx + i];
+    double rr = px + q[l] + aty;
+    drs = fabs(rr);
+    dr = fabs(rr / D[l]);
+    nPx = fabs(px / D[l]);
+    nAty = fabs(aty / D[l]);
+    nq = fabs(q[l] / D[l]);
+    nPxs = fabs(px);
+    nAtys = fabs(aty);
+    nqs = fabs(q[l]);
+  }
+  if (l < ng) {
+    double ax = 0;
+    for (int j = 0; j < nx; ++j) ax += G[l * nx + j] * x[j];
+    int row = nx + l;
+    double r = ax - z[row];
+    prs = fmax(prs, fabs(r));
+    pr = fmax(pr, fabs(r / E[row]));
+    nAx = fmax(nAx, fabs(ax / E[row]));
+    nz = fmax(nz, fabs(z[row] / E[row]));
+    nAxs = fmax(nAxs, fabs(ax));
+    nzs = fmax(nzs, fabs(z[row]));
+  }
+  pr = wave_max(pr);
+  prs = wave_max(prs);
+  nAx = wave_max(nAx);
+  nz = wave_max(nz);
+  nAxs = wave_max(nAxs);
+  nzs = wave_max(nzs);
+  dr = wave_max(dr);
+  drs = wave_max(drs);
+  nPx = wave_max(nPx);
+  nAty = wave_max(nAty);
+  nq = wave_max(nq);
+  nPxs = wave_max(nPxs);
+  nAtys = wave_max(nAtys);
+  nqs = wave_max(nqs);
+  double c = S[kp.oSc + SC_C];
+  if (l == 0) {
+    double* sc = S + kp.oSc;
+    sc[SC_PRI] = pr;
+    sc[SC_DUA] = dr / c;
+    sc[SC_PRIS] = prs;
+    sc[SC_DUAS] = drs;
+    sc[SC_NAX] = nAxs;
+    sc[SC_NZ] = nzs;
+    sc[SC_NPX] = nPxs;
+    sc[SC_NATY] = nAtys;
+    sc[SC_NQ] = nqs;
+    sc[SC_EPSP] = eps_abs + eps_rel * fmax(nAx, nz);
+    sc[SC_EPSD] = eps_abs + eps_rel * fmax(fmax(nPx, nAty), nq) / c;
+  }
+  wsync();
+}
+
+// K = P + sigma I + A^T diag(rho) A, inverted in place (Gauss-Jordan, SPD)
+__device__ __forceinline__ void factor_kinv(const KParams& kp, double* S) {
+  const int l = lane_id(), nx = kp.nx, ng = kp.ng, np = kp.np;
+  const double *P = S + kp.oP, *G = S + kp.oG, *ab = S + kp.oAB, *rho = S + kp.oRho;
+  double* K = S + kp.oU0;
+  if (l < nx) {
+    for (int c = 0; c < nx; ++c) {
+      double s = (l < np && c < np) ? P[l * np + c] : 0.0;
+      if (c == l) s += kp.s.sigma + ab[l] * ab[l] * rho[l];
+      for (int i = 0; i < ng; ++i) s += G[i * nx + l] * rho[nx + i] * G[i * nx + c];
+      K[l * nx + c] = s;
+    }
+  }
+  wsync();
+  for (int k = 0; k < nx; ++k) {
+    if (l == k) {
+      double p = 1.0 / K[k * nx + k];
+      K[k * nx + k] = 1.0;
+      for (int j = 0; j < nx; ++j) K[k * nx + j] *= p;
+    }
+    wsync();
+    if (l < nx && l != k) {
+      double f = K[l * nx + k];
+      K[l * nx + k] = 0.0;
+      for (int j = 0; j < nx; ++j) K[l * nx + j] -= f * K[k * nx + j];
+    }
+    wsync();
+  }
+}
+
+__device__ __forceinline__ void set_rho(const KParams& kp, double* S, double rho) {
+  const int l = lane_id(), nx = kp.nx, ng = kp.ng;
+  const double *lo = S + kp.oL, *up = S + kp.oU;
+  double* rv = S + kp.oRho;
+  for (int row = l; row < nx + ng; row += 64) {
+    double a = lo[row], b = up[row];
+    bool loose = a < -kInf * kMinScaling && b > kInf * kMinScaling;
+    bool eq = !loose && b - a < kRhoTol;
+    rv[row] = loose ? kRhoMin : (eq ? kRhoEqRatio * rho : rho);
+  }
+  if (l == 0) S[kp.oSc + SC_RHO] = rho;
+  wsync();
+}
+
+// Primal infeasibility certificate (OSQP / Banjac et al.) on the last dy
+__device__ __forceinline__ bool primal_infeasible(const KParams& kp, double* S, double eps) {
+  const int l = lane_id(), nx = kp.nx, ng = kp.ng;
+  const double *lo = S + kp.oL, *up = S + kp.oU, *E = S + kp.oE, *dyv = S + kp.oDY, *G = S + kp.oG,
+               *ab = S + kp.oAB, *D = S + kp.oD;
+  double* dy = S + kp.oT1;
+  double nrm = 0, lhs = 0;
+  for (int row = l; row < nx + ng; row += 64) {
+    double d = dyv[row], a = lo[row], b = up[row];
+    bool lb_inf = a < -kInf * kMinScaling, ub_inf = b > kInf * kMinScaling;
+    if (lb_inf && ub_inf) d = 0;
+    else if (ub_inf) d = fmin(d, 0.0);
+    else if (lb_inf) d = fmax(d, 0.0);
+    dy[row] = d;
+    nrm = fmax(nrm, fabs(E[row] * d));
+    lhs += d > 0 ? b * d : (d < 0 ? a * d : 0.0);
+  }
+  nrm = wave_max(nrm);
+  lhs = wave_sum(lhs);
+  wsync();
+  if (nrm <= kDivTol || !(lhs < -eps * nrm)) return false;
+  double viol = 0;
+  if (l < nx) {
+    double s = ab[l] * dy[l];
+    for (int i = 0; i < ng; ++i) s += G[i * nx + l] * dy[nx + i];
+    viol = fabs(s / D[l]);
+  }
+  viol = wave_max(viol);
+  return viol < eps * nrm;
+}
+
+// argmax with ties toward the smaller index (row order of the oracle scans)
+__device__ __forceinline__ void wave_argmax(double& v, int& idx) {
+  double nv = -v;
+  wave_argmin(nv, idx);
+  v = -nv;
+}
+
+__device__ __forceinline__ int pk(int i, int j) { return i * (i + 1) / 2 + j; }
+// solve (L D L^T) b = b in place: L packed unit-lower, D in dg
+__device__ __forceinline__ void ldl_solve(const double* L, const double* dg, int N, double* b) {
+  const int l = lane_id();
+  for (int j = 0; j < N; ++j) {  // L y = b (column oriented)
+    const double bj = b[j];
+    for (int i = l; i < N; i += 64)
+      if (i > j) b[i] -= L[pk(i, j)] * bj;
+    wsync();
+  }
+  for (int i = l; i < N; i += 64) b[i] /= dg[i];
+  wsync();
+  for (int j = N - 1; j >= 0; --j) {  // L^T x = y
+    const double bj = b[j];
+    for (int i = l; i < N; i += 64)
+      if (i < j) b[i] -= L[pk(j, i)] * bj;
+    wsync();
+  }
+}
+
+// Equality-constrained QP on the flagged rows (OSQP polish's reduced KKT):
+// bound-active variables are fixed at their bound (eliminated exactly), the
+// active G rows enter [P_FF + dI, G_RF^T; G_RF, -dI] solved by a packed
+// left-looking LDL^T with iterative refinement against the unregularised
+// system.  Writes the full primal xx[nx] and dual yy[m] (scaled space).
+// Flags: actb (bound row l) / actg (G row l) held by lane l.
+__device__ __forceinline__ bool eqp(const KParams& kp, double* S, int actb, int actg, double* xx, double* yy) {
+  const int l = lane_id(), nx = kp.nx, ng = kp.ng, np = kp.np, m = kp.m;
+  const double *P = S + kp.oP, *G = S + kp.oG, *q = S + kp.oQ, *ab = S + kp.oAB, *lo = S + kp.oL,
+               *up = S + kp.oU;
+  unsigned long long freeMask = __ballot(l < nx && actb == 0);
+  unsigned long long rowMask = __ballot(l < ng && actg != 0);
+  const int nF = __popcll(freeMask), nR = __popcll(rowMask), N = nF + nR;
+  double* U = S + kp.oU0;
+  int* Fidx = reinterpret_cast<int*>(U);  // 64 ints
+  int* Ridx = Fidx + 64;                   // 64 ints
+  double* rhs = U + 64 + 64 + 128;         // [N]  (xx, yy live at U+64 / U+128)
+  double* sol = rhs + 64;
+  double* res = sol + 64;
+  double* vv = res + 64;
+  double* dg = vv + 64;
+  double* L = dg + 64;  // packed lower triangle N(N+1)/2
+  if (l < nx && actb == 0) Fidx[__popcll(freeMask & ((1ull << l) - 1))] = l;
+  if (l < ng && actg != 0) Ridx[__popcll(rowMask & ((1ull << l) - 1))] = l;
+  if (l < nx) xx[l] = actb == 0 ? 0.0 : (actb < 0 ? lo[l] : up[l]) / ab[l];
+  wsync();
+  const double dl = kp.s.delta;
+  for (int i = l; i < N; i += 64) {  // K (packed rows i >= j) and rhs; lane i owns row i
+    if (i < nF) {
+      int fi = Fidx[i];
+      for (int j = 0; j <= i; ++j) {
+        int fj = Fidx[j];
+        double v = (fi < np && fj < np) ? P[fi * np + fj] : 0.0;
+        L[pk(i, j)] = v + (i == j ? dl : 0.0);
+      }
+      double r = -q[fi];
+      if (fi < np)
+        for (int c = 0; c < np; ++c)
+          if (xx[c] != 0.0) r -= P[fi * np + c] * xx[c];
+      rhs[i] = r;
+    } else {
+      int gi = Ridx[i - nF], row = nx + gi;
+      for (int j = 0; j < nF; ++j) L[pk(i, j)] = G[gi * nx + Fidx[j]];
+      for (int j = nF; j <= i; ++j) L[pk(i, j)] = (i == j) ? -dl : 0.0;
+      // the lane owning G row gi knows its side; read it back through the flags
+      double r = 0;
+      (void)row;
+      rhs[i] = r;
+    }
+  }
+  // rhs of the active G rows: b = l or u of that row, minus the fixed part
+  if (l < ng && actg != 0) {
+    const int i = nF + __popcll(rowMask & ((1ull << l) - 1)), row = nx + l;
+    double r = actg < 0 ? lo[row] : up[row];
+    for (int c = 0; c < nx; ++c)
+      if (xx[c] != 0.0) r -= G[l * nx + c] * xx[c];
+    rhs[i] = r;
+  }
+  wsync();
+  for (int j = 0; j < N; ++j) {  // left-looking LDL^T, in place
+    for (int k = l; k < j; k += 64) vv[k] = L[pk(j, k)] * dg[k];
+    wsync();
+    double part = 0;
+    for (int k = l; k < j; k += 64) part += L[pk(j, k)] * vv[k];
+    double dj = L[pk(j, j)] - wave_sum(part);
+    if (dj == 0.0) return false;  // uniform
+    for (int i = l; i < N; i += 64)
+      if (i > j) {
+        double t = L[pk(i, j)];
+        for (int k = 0; k < j; ++k) t -= L[pk(i, k)] * vv[k];
+        L[pk(i, j)] = t / dj;
+      }
+    if (l == 0) dg[j] = dj;
+    wsync();
+  }
+  for (int i = l; i < N; i += 64) sol[i] = rhs[i];
+  wsync();
+  ldl_solve(L, dg, N, sol);
+  for (int it = 0; it < kp.s.polish_refine_iter; ++it) {
+    for (int i = l; i < N; i += 64) {
+      double r = rhs[i];
+      if (i < nF) {
+        int fi = Fidx[i];
+        if (fi < np)
+          for (int j = 0; j < nF; ++j) {
+            int fj = Fidx[j];
+            if (fj < np) r -= P[fi * np + fj] * sol[j];
+          }
+        for (int k = 0; k < nR; ++k) r -= G[Ridx[k] * nx + fi] * sol[nF + k];
+      } else {
+        int gi = Ridx[i - nF];
+        for (int j = 0; j < nF; ++j) r -= G[gi * nx + Fidx[j]] * sol[j];
+      }
+      res[i] = r;
+    }
+    wsync();
+    ldl_solve(L, dg, N, res);
+    for (int i = l; i < N; i += 64) sol[i] += res[i];
+    wsync();
+  }
+  for (int i = l; i < nF; i += 64) xx[Fidx[i]] = sol[i];
+  for (int row = l; row < m; row += 64) yy[row] = 0.0;
+  wsync();
+  for (int k = l; k < nR; k += 64) yy[nx + Ridx[k]] = sol[nF + k];
+  wsync();
+  if (l < nx && actb != 0) {  // bound multipliers from stationarity
+    double g = q[l];
+    if (l < np)
+      for (int c = 0; c < np; ++c) g += P[l * np + c] * xx[c];
+    for (int i = 0; i < ng; ++i) g += G[i * nx + l] * yy[nx + i];
+    yy[l] = -g / ab[l];
+  }
+  wsync();
+  return true;
+}
+
+// OSQP polish (polish.c) restated.  strict == 0: OSQP's single attempt and
+// acceptance rule.  strict != 0 (parity mode): accept only a KKT-certified
+// point (residuals at eps_exact, dual signs matching the active bounds); on a
+// wrong ADMM active-set guess continue with a primal active-set method
+// (Nocedal & Wright Alg. 16.3) from the first feasible polished point.  Same
+// decisions, in the same row order, as oracle/drc_oracle.c:qp_polish.
+constexpr int kPolishFeasAttempts = 4, kPolishAsIters = 24;
+__device__ __forceinline__ bool polish(const KParams& kp, double* S, bool strict) {
+  const int l = lane_id(), nx = kp.nx, ng = kp.ng, np = kp.np, m = kp.m;
+  const double *G = S + kp.oG, *ab = S + kp.oAB, *lo = S + kp.oL, *up = S + kp.oU, *E = S + kp.oE;
+  double *x = S + kp.oX, *z = S + kp.oZ, *y = S + kp.oY;
+  (void)np;
+  int actb = 0, actg = 0;
+  if (l < nx) actb = (z[l] - lo[l] < -y[l]) ? -1 : ((up[l] - z[l] < y[l]) ? 1 : 0);
+  if (l < ng) {
+    int r = nx + l;
+    actg = (z[r] - lo[r] < -y[r]) ? -1 : ((up[r] - z[r] < y[r]) ? 1 : 0);
+  }
+  double* U = S + kp.oU0;
+  double* xx = U + 64;       // [nx]
+  double* yy = U + 128;      // [m] (<= 128)
+  double* zz = S + kp.oT2;   // z candidate
+  double* xc = S + kp.oXT;   // feasible iterate of the active-set phase
+  double* sc = S + kp.oSc;
+  const double pr0 = sc[SC_PRI], dr0 = sc[SC_DUA];
+  bool have_feas = false;
+  const int iters = strict ? kPolishFeasAttempts + kPolishAsIters : 1;
+  for (int it = 0; it < iters; ++it) {
+    if (!eqp(kp, S, actb, actg, xx, yy)) break;
+    if (have_feas) {
+      double stepmax = 0, xnorm = 0;
+      if (l < nx) {
+        stepmax = fabs(xx[l] - xc[l]);
+        xnorm = fabs(xc[l]);
+      }
+      stepmax = wave_max(stepmax);
+      xnorm = wave_max(xnorm);
+      if (stepmax > 1e-12 * (1 + xnorm)) {
+        // ratio test along p = xx - xc over the inactive rows
+        double amin = 1.0;
+        int blk = 0x7fffffff, side = 0;
+        if (l < nx && actb == 0) {
+          double axc = ab[l] * xc[l], ap = ab[l] * (xx[l] - xc[l]), a = 2.0;
+          int sd = 0;
+          if (ap < 0 && lo[l] > -kInf * kMinScaling) { a = (lo[l] - axc) / ap; sd = -1; }
+          else if (ap > 0 && up[l] < kInf * kMinScaling) { a = (up[l] - axc) / ap; sd = 1; }
+          if (a < amin) { amin = a; blk = l; side = sd; }
+        }
+        if (l < ng && actg == 0) {
+          const int row = nx + l;
+          double axc = 0, ap = 0, a = 2.0;
+          for (int j = 0; j < nx; ++j) {
+            axc += G[l * nx + j] * xc[j];
+            ap += G[l * nx + j] * (xx[j] - xc[j]);
+          }
+          int sd = 0;
+          if (ap < 0 && lo[row] > -kInf * kMinScaling) { a = (lo[row] - axc) / ap; sd = -1; }
+          else if (ap > 0 && up[row] < kInf * kMinScaling) { a = (up[row] - axc) / ap; sd = 1; }
+          if (a < amin) { amin = a; blk = row; side = sd; }
+        }
+        int enc = blk == 0x7fffffff ? blk : blk * 4 + (side + 1);
+        wave_argmin(amin, enc);
+        const double alpha = amin < 0 ? 0.0 : amin;
+        wsync();
+        if (l < nx) xc[l] += alpha * (xx[l] - xc[l]);
+        wsync();
+        if (enc != 0x7fffffff && amin < 1.0) {
+          const int row = enc >> 2, sd = (enc & 3) - 1;
+          if (row < nx) { if (l == row) actb = sd; }
+          else if (l == row - nx) actg = sd;
+          continue;
+        }
+      }
+    }
+    // candidate point: z = clamp(A x), residuals, certification
+    double axb = 0, axg = 0;
+    if (l < nx) {
+      axb = ab[l] * xx[l];
+      zz[l] = fmin(fmax(axb, lo[l]), up[l]);
+    }
+    if (l < ng) {
+      for (int j = 0; j < nx; ++j) axg += G[l * nx + j] * xx[j];
+      zz[nx + l] = fmin(fmax(axg, lo[nx + l]), up[nx + l]);
+    }
+    wsync();
+    residuals(kp, S, xx, zz, yy, kp.s.eps_exact, kp.s.eps_exact);
+    const double pr1 = sc[SC_PRI], dr1 = sc[SC_DUA], epsp = sc[SC_EPSP], epsd = sc[SC_EPSD], c = sc[SC_C];
+    bool ok = (pr1 < pr0 && dr1 < dr0) || (pr1 < pr0 && dr0 < 1e-10) || (dr1 < dr0 && pr0 < 1e-10);
+    double wv = 0;
+    int worst = 0x7fffffff;
+    bool feasible = pr1 <= epsp;
+    if (strict) {
+      ok = feasible && dr1 <= epsd;
+      if (l < nx && actb != 0 && lo[l] != up[l]) {
+        double yi = E[l] * yy[l] / c, viol = actb < 0 ? yi - epsd : -yi - epsd;
+        if (viol > wv) { wv = viol; worst = l; }
+      }
+      if (l < ng && actg != 0 && lo[nx + l] != up[nx + l]) {
+        double yi = E[nx + l] * yy[nx + l] / c, viol = actg < 0 ? yi - epsd : -yi - epsd;
+        if (viol > wv) { wv = viol; worst = nx + l; }
+      }
+      wave_argmax(wv, worst);
+      if (worst != 0x7fffffff) ok = false;
+      if (!ok && feasible && !have_feas) {
+        if (l < nx) xc[l] = xx[l];
+        have_feas = true;
+      }
+    }
+    if (ok) {
+      if (l < nx) x[l] = xx[l];
+      for (int row = l; row < m; row += 64) {
+        y[row] = yy[row];
+        z[row] = zz[row];
+      }
+      wsync();
+      return true;
+    }
+    if (!strict) break;
+    if (have_feas) {
+      if (worst == 0x7fffffff) break;  // KKT residual failure, not an active-set issue
+      if (worst < nx) { if (l == worst) actb = 0; }
+      else if (l == worst - nx) actg = 0;
+      if (l < nx) xc[l] = xx[l];
+      wsync();
+    } else {
+      if (it >= kPolishFeasAttempts - 1) break;
+      double av = 0;
+      int add = 0x7fffffff;
+      if (l < nx && actb == 0) {
+        double vlo = (lo[l] - axb) / E[l] - epsp, vhi = (axb - up[l]) / E[l] - epsp;
+        if (vlo > av) { av = vlo; add = l * 4 + 0; }
+        if (vhi > av) { av = vhi; add = l * 4 + 2; }
+      }
+      if (l < ng && actg == 0) {
+        const int row = nx + l;
+        double vlo = (lo[row] - axg) / E[row] - epsp, vhi = (axg - up[row]) / E[row] - epsp;
+        if (vlo > av) { av = vlo; add = row * 4 + 0; }
+        if (vhi > av) { av = vhi; add = row * 4 + 2; }
+      }
+      wave_argmax(av, add);
+      if (add == 0x7fffffff) {
+        if (worst == 0x7fffffff) break;
+        if (worst < nx) { if (l == worst) actb = 0; }
+        else if (l == worst - nx) actg = 0;
+      } else {
+        const int row = add >> 2, sd = (add & 3) - 1;
+        if (row < nx) { if (l == row) actb = sd; }
+        else if (l == row - nx) actg = sd;
+      }
+    }
+  }
+  if (l == 0) {  // restore the ADMM residuals for the caller
+    sc[SC_PRI] = pr0;
+    sc[SC_DUA] = dr0;
+  }
+  wsync();
+  return false;
+}
+
+// ------------------------------------------------------------------------
+// the fused per-instance solve
+// ------------------------------------------------------------------------
+struct IO {
+  int64_t B;
+  const double *q, *qdot, *xt, *xdt, *xi, *xdi;
+  double* out;
+  int32_t *status, *iters;
+  double *st_pose, *st_jac, *st_man, *st_dist, *st_xdd;
+  int32_t* st_pair;
+  EpaWs* epa_ws;
+};
+
+__global__ void __launch_bounds__(64) task_kernel(const DevModel* __restrict__ M, const KParams kp, const IO io) {
+  extern __shared__ __attribute__((aligned(16))) double S[];
+  const int l = lane_id();
+  const int nv = kp.nv;
+  const int64_t B = io.B;
+  EpaWs* ews = io.epa_ws + blockIdx.x;
+  PH_DECL
+  for (int64_t b = blockIdx.x; b < B; b += gridDim.x) {
+    // ---------------- state in ----------------
+    double* qv = S + kp.kq;
+    double* qd = S + kp.kqd;
+    if (l < nv) {
+      qv[l] = io.q[l * B + b];
+      qd[l] = io.qdot[l * B + b];
+    }
+    wsync();
+    // ---------------- FK: local joint transforms, then the chain ------------
+    double* T = S + kp.kT;  // (nv+1) x 12
+    double* Zw = S + kp.kZ;  // (nv+1) x 3
+    if (l < 12) T[l] = (l == 0 || l == 4 || l == 8) ? 1.0 : 0.0;
+    double* loc = S + kp.kTg;  // scratch: local transforms nv x 12 (before geometry poses)
+    if (l >= 1 && l <= nv) {
+      const int j = l;
+      double Mj[12];
+      const double* ax = M->axis[j];
+      const double qq = qv[j - 1];
+      if (M->jtype[j] == kRevolute) {
+        double c = cos(qq), s = sin(qq), C = 1 - c, x = ax[0], y = ax[1], z = ax[2];
+        Mj[0] = c + x * x * C; Mj[1] = x * y * C - z * s; Mj[2] = x * z * C + y * s;
+        Mj[3] = y * x * C + z * s; Mj[4] = c + y * y * C; Mj[5] = y * z * C - x * s;
+        Mj[6] = z * x * C - y * s; Mj[7] = z * y * C + x * s; Mj[8] = c + z * z * C;
+        Mj[9] = Mj[10] = Mj[11] = 0;
+      } else {
+        Mj[0] = Mj[4] = Mj[8] = 1;
+        Mj[1] = Mj[2] = Mj[3] = Mj[5] = Mj[6] = Mj[7] = 0;
+        Mj[9] = ax[0] * qq; Mj[10] = ax[1] * qq; Mj[11] = ax[2] * qq;
+      }
+      double Lj[12];
+      tmul(M->jplace[j], Mj, Lj);
+      for (int i = 0; i < 12; ++i) loc[(j - 1) * 12 + i] = Lj[i];
+    }
+    wsync();
+    for (int j = 1; j <= nv; ++j) {  // oMi[j] = oMi[parent] * local[j]; 12 lanes
+      const double* a = T + M->parent[j] * 12;
+      const double* bb = loc + (j - 1) * 12;
+      double v = 0;
+      if (l < 9) {
+        int r = l / 3, c = l % 3;
+        v = a[3 * r] * bb[c] + a[3 * r + 1] * bb[3 + c] + a[3 * r + 2] * bb[6 + c];
+      } else if (l < 12) {
+        int r = l - 9;
+        v = a[3 * r] * bb[9] + a[3 * r + 1] * bb[10] + a[3 * r + 2] * bb[11] + a[9 + r];
+      }
+      wsync();
+      if (l < 12) T[j * 12 + l] = v;
+      wsync();
+    }
+    double* Te = S + kp.kTe;
+    if (l >= 1 && l <= nv) st3(Zw + 3 * l, rot(T + 12 * l, ld3(M->axis[l])));
+    if (l == 0) tmul(T + 12 * kp.frame_joint, kp.frame_place, Te);
+    wsync();
+    // geometry poses
+    double* Tg = S + kp.kTg;
+    for (int g = l; g < M->ngeom; g += 64) {
+      double out[12];
+      tmul(T + 12 * M->gparent[g], M->gplace[g], out);
+      for (int i = 0; i < 12; ++i) Tg[g * 12 + i] = out[i];
+    }
+    PH(0);
+    // ---------------- frame Jacobian (LWA), 6 x nv row-major -------------
+    double* J = S + kp.kJ;
+    const V3 pe = v3(Te[9], Te[10], Te[11]);
+    const uint32_t anc_e = M->anc[kp.frame_joint];
+    if (l < nv) {
+      const int j = l + 1;
+      V3 lin = v3(0, 0, 0), ang = v3(0, 0, 0);
+      if (anc_e & (1u << l)) {
+        V3 z = ld3(Zw + 3 * j);
+        if (M->jtype[j] == kRevolute) {
+          lin = cross(z, pe - v3(T[12 * j + 9], T[12 * j + 10], T[12 * j + 11]));
+          ang = z;
+        } else {
+          lin = z;
+        }
+      }
+      J[0 * nv + l] = lin.x; J[1 * nv + l] = lin.y; J[2 * nv + l] = lin.z;
+      J[3 * nv + l] = ang.x; J[4 * nv + l] = ang.y; J[5 * nv + l] = ang.z;
+    }
+    wsync();
+    // ---------------- task velocity ---------------------------------------
+    double* xdd = S + kp.kxdd;
+    if (l == 0) {
+      if (kp.mode == DRC_MODE_QPIK) {
+        for (int i = 0; i < 6; ++i) xdd[i] = io.xdt[i * B + b];
+      } else {
+        double xt[12], xdt[6];
+        for (int i = 0; i < 12; ++i) xt[i] = io.xt[i * B + b];
+        for (int i = 0; i < 6; ++i) xdt[i] = io.xdt[i * B + b];
+        if (kp.mode == DRC_MODE_QPIK_CUBIC) {  // getTaskSpaceCubic (math_type_define.h:647)
+          double xi[12], xdi[6], Rt[9], Ri[9];
+          for (int i = 0; i < 12; ++i) xi[i] = io.xi[i * B + b];
+          for (int i = 0; i < 6; ++i) xdi[i] = io.xdi[i * B + b];
+          for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c) {
+              Rt[3 * r + c] = xt[3 * c + r];
+              Ri[3 * r + c] = xi[3 * c + r];
+            }
+          const double t = kp.t, t0 = kp.t0, tf = kp.t0 + kp.duration;
+          double pd[3], vd[3];
+          for (int i = 0; i < 3; ++i) {
+            pd[i] = cubic(t, t0, tf, xi[9 + i], xt[9 + i], xdi[i], xdt[i]);
+            vd[i] = cubic_dot(t, t0, tf, xi[9 + i], xt[9 + i], xdi[i], xdt[i]);
+          }
+          double RiT_Rt[9], Rd[9];
+          for (int a = 0; a < 3; ++a)
+            for (int c = 0; c < 3; ++c)
+              RiT_Rt[3 * a + c] = Ri[a] * Rt[c] + Ri[3 + a] * Rt[3 + c] + Ri[6 + a] * Rt[6 + c];
+          V3 r = so3_log(RiT_Rt);
+          if (t >= tf) {
+            for (int i = 0; i < 9; ++i) Rd[i] = Rt[i];
+          } else if (t < t0) {
+            for (int i = 0; i < 9; ++i) Rd[i] = Ri[i];
+          } else {
+            double E3[9];
+            so3_exp(cubic(t, t0, tf, 0, 1, 0, 0) * r, E3);
+            for (int a = 0; a < 3; ++a)
+              for (int c = 0; c < 3; ++c)
+                Rd[3 * a + c] = Ri[3 * a] * E3[c] + Ri[3 * a + 1] * E3[3 + c] + Ri[3 * a + 2] * E3[6 + c];
+          }
+          V3 rd = v3(cubic_dot(t, t0, tf, 0, r.x, 0, 0), cubic_dot(t, t0, tf, 0, r.y, 0, 0),
+                     cubic_dot(t, t0, tf, 0, r.z, 0, 0));
+          rd = v3(Ri[0] * rd.x + Ri[1] * rd.y + Ri[2] * rd.z, Ri[3] * rd.x + Ri[4] * rd.y + Ri[5] * rd.z,
+                  Ri[6] * rd.x + Ri[7] * rd.y + Ri[8] * rd.z);
+          double tau = (t - t0) / (tf - t0);
+          if (tau < 0 || tau > 1) rd = v3(0, 0, 0);
+          for (int r0 = 0; r0 < 3; ++r0)
+            for (int c = 0; c < 3; ++c) xt[3 * c + r0] = Rd[3 * r0 + c];
+          for (int i = 0; i < 3; ++i) {
+            xt[9 + i] = pd[i];
+            xdt[i] = vd[i];
+          }
+          xdt[3] = rd.x; xdt[4] = rd.y; xdt[5] = rd.z;
+        }
+        // getTaskSpaceError (math_type_define.h:633) with getPhi (:283)
+        double e[6], xdot[6];
+        for (int i = 0; i < 3; ++i) e[i] = xt[9 + i] - Te[9 + i];
+        V3 phi = v3(0, 0, 0);
+        for (int i = 0; i < 3; ++i)
+          phi = phi + cross(v3(xt[3 * i], xt[3 * i + 1], xt[3 * i + 2]), v3(Te[i], Te[3 + i], Te[6 + i]));
+        e[3] = -0.5 * phi.x; e[4] = -0.5 * phi.y; e[5] = -0.5 * phi.z;
+        for (int r = 0; r < 6; ++r) {  // getVelocity = J qdot (robot_data.cpp:419-422)
+          double s = 0;
+          for (int c = 0; c < nv; ++c) s += J[r * nv + c] * qd[c];
+          xdot[r] = s;
+        }
+        for (int i = 0; i < 6; ++i)
+          xdd[i] = kp.kp[i] * e[i] + kp.kv[i] * (xdt[i] - xdot[i]) + kp.ff * xdt[i];
+      }
+    }
+    PH(1);
+    // ---------------- manipulability (arm columns c0..c0+narm) -------------
+    const int narm = kp.narm, c0 = kp.c0;
+    double* A6 = S + kp.kA6;
+    double* Ai = S + kp.kAi;
+    if (l < 36) {
+      int a = l / 6, bb = l % 6;
+      double s = 0;
+      for (int c = 0; c < narm; ++c) s += J[a * nv + c0 + c] * J[bb * nv + c0 + c];
+      A6[l] = s;
+    }
+    wsync();
+    if (l == 0) {
+      double* ws = S + kp.kScr;
+      S[kp.oSc + SC_MAN] = sqrt(det_lu6(A6, ws));
+      pinv_cod6(A6, Ai, ws);
+    }
+    wsync();
+    double* W = S + kp.kW;  // narm x 6 = Jr^T Ai
+    for (int e = l; e < narm * 6; e += 64) {
+      int c = e / 6, a = e % 6;
+      double s = 0;
+      for (int i = 0; i < 6; ++i) s += J[i * nv + c0 + c] * Ai[i * 6 + a];
+      W[e] = s;
+    }
+    wsync();
+    double* part = S + kp.kPart;
+    for (int e = l; e < narm * narm; e += 64) {
+      const int kk = e / narm, c = e % narm;
+      const int jk = c0 + kk + 1, ji = c0 + c + 1;  // joint ids of q_k and column i
+      double acc = 0;
+      if ((anc_e & (1u << (jk - 1))) && (anc_e & (1u << (ji - 1)))) {
+        V3 zk = ld3(Zw + 3 * jk), zi = ld3(Zw + 3 * ji);
+        V3 pk_ = v3(T[12 * jk + 9], T[12 * jk + 10], T[12 * jk + 11]);
+        V3 pi_ = v3(T[12 * ji + 9], T[12 * ji + 10], T[12 * ji + 11]);
+        const bool krev = M->jtype[jk] == kRevolute;
+        V3 dpe = krev ? cross(zk, pe - pk_) : zk;
+        const bool moves_i = jk != ji && (M->anc[ji] & (1u << (jk - 1)));
+        V3 dzi = (moves_i && krev) ? cross(zk, zi) : v3(0, 0, 0);
+        V3 dpi = moves_i ? (krev ? cross(zk, pi_ - pk_) : zk) : v3(0, 0, 0);
+        V3 lin, ang;
+        if (M->jtype[ji] == kRevolute) {
+          lin = cross(dzi, pe - pi_) + cross(zi, dpe - dpi);
+          ang = dzi;
+        } else {
+          lin = dzi;
+          ang = v3(0, 0, 0);
+        }
+        const double* w = W + c * 6;
+        acc = lin.x * w[0] + lin.y * w[1] + lin.z * w[2] + ang.x * w[3] + ang.y * w[4] + ang.z * w[5];
+      }
+      part[e] = acc;
+    }
+    wsync();
+    double* mg = S + kp.kmg;
+    if (l < narm) {
+      double s = 0;
+      for (int c = 0; c < narm; ++c) s += part[l * narm + c];
+      mg[l] = S[kp.oSc + SC_MAN] * s;
+    }
+    PH(2);
+    // ---------------- self-collision distance (broad + narrow phase) -------
+    double* pd = S + kp.kPd;
+    double* pf = S + kp.kPf;
+    double ub = 1e300;
+    for (int p = l; p < M->npairs; p += 64) {
+      const int ga = M->pair_a[p], gb = M->pair_b[p];
+      Shape A{M->gtype[ga], Tg + 12 * ga, M->gparam[ga][0], M->gparam[ga][1], M->gparam[ga][2]};
+      Shape Bs{M->gtype[gb], Tg + 12 * gb, M->gparam[gb][0], M->gparam[gb][1], M->gparam[gb][2]};
+      if (A.type == kSphere || Bs.type == kSphere) {
+        V3 pA, pB;
+        double d = sphere_pair(A, Bs, &pA, &pB);
+        pd[p] = d;
+        pf[p] = 1.0;
+        ub = fmin(ub, d);
+      } else {
+        V3 a0, a1, b0, b1;
+        double ra, rb;
+        core_segment(A, M->gbound[ga], &a0, &a1, &ra);
+        core_segment(Bs, M->gbound[gb], &b0, &b1, &rb);
+        pd[p] = seg_seg_dist(a0, a1, b0, b1) - ra - rb;
+        pf[p] = 0.0;
+      }
+    }
+    ub = -wave_max(-ub);
+    wsync();
+    PH(3);
+    // exact GJK/EPA only where the swept-core bound can still win
+    for (int p = l; p < M->npairs; p += 64) {
+      if (pf[p] == 0.0 && pd[p] - 1e-9 <= ub) {
+        const int ga = M->pair_a[p], gb = M->pair_b[p];
+        Shape A{M->gtype[ga], Tg + 12 * ga, M->gparam[ga][0], M->gparam[ga][1], M->gparam[ga][2]};
+        Shape Bs{M->gtype[gb], Tg + 12 * gb, M->gparam[gb][0], M->gparam[gb][1], M->gparam[gb][2]};
+        GjkOut g = gjk(A, Bs, nullptr);
+        if (g.intersect) {
+          pf[p] = 2.0;  // penetrating: EPA below, one pair at a time
+        } else {
+          pd[p] = g.dist;
+          pf[p] = 1.0;
+        }
+      }
+    }
+    wsync();
+    PH(4);
+    // EPA shares one per-wave workspace: serialise the (rare) penetrating pairs
+    for (int p0 = 0; p0 < M->npairs; p0 += 64) {
+      unsigned long long need = __ballot(p0 + l < M->npairs && pf[p0 + l] == 2.0);
+      while (need) {
+        const int ln = __ffsll(static_cast<long long>(need)) - 1;
+        need &= need - 1;
+        if (l == ln) {
+          const int p = p0 + l, ga = M->pair_a[p], gb = M->pair_b[p];
+          Shape A{M->gtype[ga], Tg + 12 * ga, M->gparam[ga][0], M->gparam[ga][1], M->gparam[ga][2]};
+          Shape Bs{M->gtype[gb], Tg + 12 * gb, M->gparam[gb][0], M->gparam[gb][1], M->gparam[gb][2]};
+          GjkOut g = gjk(A, Bs, ews);
+          pd[p] = epa(A, Bs, g.ns, ews);
+          pf[p] = 1.0;
+        }
+      }
+    }
+    wsync();
+    PH(5);
+    double bestd = 1.7976931348623157e308;
+    int besti = 0x7fffffff;
+    for (int p = l; p < M->npairs; p += 64)
+      if (pf[p] != 0.0 && pd[p] < bestd) {
+        bestd = pd[p];
+        besti = p;
+      }
+    wave_argmin(bestd, besti);
+    // witness points of the winner (recomputed by one lane: same arithmetic)
+    double* dgv = S + kp.kdg;
+    double* red = S + kp.oRed;
+    if (l == 0) {
+      S[kp.oSc + SC_DIST] = bestd;
+      S[kp.oSc + SC_PAIR] = besti;
+      V3 pA = v3(0, 0, 0), pB = v3(0, 0, 0);
+      if (besti < M->npairs) {
+        const int ga = M->pair_a[besti], gb = M->pair_b[besti];
+        Shape A{M->gtype[ga], Tg + 12 * ga, M->gparam[ga][0], M->gparam[ga][1], M->gparam[ga][2]};
+        Shape Bs{M->gtype[gb], Tg + 12 * gb, M->gparam[gb][0], M->gparam[gb][1], M->gparam[gb][2]};
+        if (A.type == kSphere || Bs.type == kSphere) {
+          sphere_pair(A, Bs, &pA, &pB);
+        } else {
+          GjkOut g = gjk(A, Bs, ews);
+          if (g.intersect) {
+            epa(A, Bs, g.ns, ews);
+            pA = ld3(ews->out);
+            pB = ld3(ews->out + 3);
+          } else {
+            pA = g.pA;
+            pB = g.pB;
+          }
+        }
+      }
+      st3(red, pA);
+      st3(red + 3, pB);
+    }
+    wsync();
+    PH(6);
+    if (l < nv) {  // grad d = n^T (J_B(pB) - J_A(pA)), sign flipped when penetrating
+      double g = 0;
+      if (besti < M->npairs) {
+        const int jA = M->gparent[M->pair_a[besti]], jB = M->gparent[M->pair_b[besti]];
+        V3 pA = ld3(red), pB = ld3(red + 3), n = pB - pA;
+        n = (1.0 / sqrt(dot(n, n))) * n;
+        const int j = l + 1;
+        V3 z = ld3(Zw + 3 * j), pj = v3(T[12 * j + 9], T[12 * j + 10], T[12 * j + 11]);
+        const bool rev = M->jtype[j] == kRevolute;
+        V3 cA = v3(0, 0, 0), cB = v3(0, 0, 0);
+        if (jA > 0 && (M->anc[jA] & (1u << l))) cA = rev ? cross(z, pA - pj) : z;
+        if (jB > 0 && (M->anc[jB] & (1u << l))) cB = rev ? cross(z, pB - pj) : z;
+        g = dot(n, cB - cA);
+        if (bestd < 0) g = -g;
+      }
+      dgv[l] = g;
+    }
+    wsync();
+    PH(7);
+    // ---------------- task data out (HBM, [field][B]) -----------------------
+    if (io.st_pose && l < 12) {
+      // R row-major -> column-major storage, then p
+      double v = l < 9 ? Te[(l % 3) * 3 + l / 3] : Te[l];
+      io.st_pose[l * B + b] = v;
+    }
+    for (int e = l; e < 6 * nv; e += 64) io.st_jac[(int64_t)e * B + b] = J[e];
+    if (l == 0) io.st_man[b] = S[kp.oSc + SC_MAN];
+    if (l < narm) io.st_man[(int64_t)(1 + l) * B + b] = mg[l];
+    if (l == 0) io.st_dist[b] = bestd;
+    if (l < nv) io.st_dist[(int64_t)(1 + l) * B + b] = dgv[l];
+    if (l == 0) io.st_pair[b] = besti < M->npairs ? besti : -1;
+    if (l < 6) io.st_xdd[l * B + b] = xdd[l];
+    wsync();
+  }
+  PH_FLUSH(0);
+}
+
+// QP kernel: assembles and solves the QP of each instance from the task data
+// written by task_kernel (same [field][B] buffers).
+__global__ void __launch_bounds__(64) qp_kernel(const DevModel* __restrict__ M, const KParams kp, const IO io) {
+  extern __shared__ __attribute__((aligned(16))) double S[];
+  const int l = lane_id();
+  const int nv = kp.nv, narm = kp.narm;
+  const int64_t B = io.B;
+  PH_DECL
+  for (int64_t b = blockIdx.x; b < B; b += gridDim.x) {
+    double* qv = S + kp.kq;
+    double* J = S + kp.kJ;
+    double* xdd = S + kp.kxdd;
+    double* mg = S + kp.kmg;
+    double* dgv = S + kp.kdg;
+    if (l < nv) {
+      qv[l] = io.q[l * B + b];
+      dgv[l] = io.st_dist[(int64_t)(1 + l) * B + b];
+    }
+    for (int e = l; e < 6 * nv; e += 64) J[e] = io.st_jac[(int64_t)e * B + b];
+    if (l < narm) mg[l] = io.st_man[(int64_t)(1 + l) * B + b];
+    if (l < 6) xdd[l] = io.st_xdd[l * B + b];
+    if (l == 0) {
+      S[kp.oSc + SC_MAN] = io.st_man[b];
+      S[kp.oSc + SC_DIST] = io.st_dist[b];
+    }
+    wsync();
+    const double bestd = S[kp.oSc + SC_DIST];
+    // ---------------- QP assembly (QP_IK.cpp:69-131 / MoMa :59-128) --------
+    const int nx = kp.nx, ng = kp.ng, np = kp.np, m = kp.m;
+    double *P = S + kp.oP, *G = S + kp.oG, *qq = S + kp.oQ, *ab = S + kp.oAB, *lo = S + kp.oL, *up = S + kp.oU;
+    const double alpha = kp.alpha_cbf, man = S[kp.oSc + SC_MAN];
+    double* Jt = S + kp.kJt;  // task Jacobian over the QP's task variables: 6 x np
+    if (M->kind == 0) {
+      for (int e = l; e < 6 * np; e += 64) Jt[e] = J[(e / np) * nv + e % np];
+    } else {
+      // J~ = J S  (mobile_manipulator/robot_data.cpp:407-410); S virtual block = Rz(yaw) J_mobile
+      const double yaw = qv[M->virtual_start + 2], cy = cos(yaw), sy = sin(yaw);
+      for (int e = l; e < 6 * np; e += 64) {
+        const int r = e / np, a = e % np;
+        double v = 0;
+        const int am = a - M->act_mani_start, aw = a - M->act_mobi_start;
+        if (am >= 0 && am < M->n_arm) {
+          v = J[r * nv + M->mani_start + am];
+        } else if (aw >= 0 && aw < M->n_wheel) {
+          const double s0 = cy * M->J_mobile[0][aw] - sy * M->J_mobile[1][aw];
+          const double s1 = sy * M->J_mobile[0][aw] + cy * M->J_mobile[1][aw];
+          const double s2 = M->J_mobile[2][aw];
+          const int vs = M->virtual_start;
+          v = J[r * nv + M->mobi_start + aw] + J[r * nv + vs] * s0 + J[r * nv + vs + 1] * s1 + J[r * nv + vs + 2] * s2;
+        }
+        Jt[e] = v;
+      }
+    }
+    wsync();
+    for (int e = l; e < np * np; e += 64) {
+      const int i = e / np, j = e % np;
+      double s = 0;
+      for (int r = 0; r < 6; ++r) s += Jt[r * np + i] * Jt[r * np + j];
+      P[e] = 2.0 * s + (i == j ? kp.w_reg : 0.0);
+    }
+    for (int e = l; e < ng * nx; e += 64) G[e] = 0.0;
+    if (l < nx) {
+      double qi;
+      if (l < np) {
+        double s = 0;
+        for (int r = 0; r < 6; ++r) s += Jt[r * np + l] * xdd[r];
+        qi = -2.0 * s;
+      } else {
+        qi = kp.slack_w;
+      }
+      qq[l] = qi;
+      ab[l] = 1.0;
+      if (M->kind == 0) {
+        lo[l] = l < nv ? -M->vel[l] : 0.0;
+        up[l] = l < nv ? M->vel[l] : kInf;
+      } else {  // setBoundConstraint is a no-op for MoMa (QP_IK.cpp:75-83)
+        lo[l] = -kInf;
+        up[l] = kInf;
+      }
+    }
+    wsync();
+    if (l < ng) {
+      const int n = narm, row = nx + l;
+      double lval = 0;
+      const int vo = M->kind == 0 ? 0 : M->act_mani_start;  // task-variable offset of the arm
+      const int qo = M->kind == 0 ? 0 : M->mani_start;      // joint offset of the arm
+      if (l < n) {
+        G[l * nx + vo + l] = 1.0;
+        if (M->kind == 0) G[l * nx + n + l] = 1.0;
+        lval = -alpha * (qv[qo + l] - M->lower[qo + l]);
+      } else if (l < 2 * n) {
+        const int i = l - n;
+        G[l * nx + vo + i] = -1.0;
+        if (M->kind == 0) G[l * nx + 2 * n + i] = 1.0;
+        lval = -alpha * (M->upper[qo + i] - qv[qo + i]);
+      } else if (l == 2 * n) {
+        for (int c = 0; c < n; ++c) G[l * nx + vo + c] = mg[c];
+        if (M->kind == 0) G[l * nx + 3 * n] = 1.0;
+        lval = -alpha * (man - kp.man_min);
+      } else {
+        for (int c = 0; c < n; ++c) G[l * nx + vo + c] = dgv[qo + c];
+        if (M->kind == 0) G[l * nx + 3 * n + 1] = 1.0;
+        lval = -alpha * (bestd - kp.dist_min);
+      }
+      lo[row] = lval;
+      up[row] = kInf;
+    }
+    wsync();
+    PH(0);
+    // ---------------- OSQP: scaling ----------------------------------------
+    int status = DRC_STATUS_MAX_ITER, iters = 0;
+    {
+      bool finite = true;
+      for (int e = l; e < np * np; e += 64) finite &= isfinite(P[e]);
+      for (int e = l; e < ng * nx; e += 64) finite &= isfinite(G[e]);
+      if (l < nx) finite &= isfinite(qq[l]);
+      for (int row = l; row < m; row += 64) finite &= !isnan(lo[row]) && !isnan(up[row]);
+      if (!__all(finite)) status = DRC_STATUS_NONFINITE;
+    }
+    double *D = S + kp.oD, *E = S + kp.oE, *x = S + kp.oX, *z = S + kp.oZ, *y = S + kp.oY, *dy = S + kp.oDY;
+    double* sc = S + kp.oSc;
+    if (status != DRC_STATUS_NONFINITE) {
+      if (l < nx) D[l] = 1.0;
+      for (int row = l; row < m; row += 64) E[row] = 1.0;
+      if (l == 0) sc[SC_C] = 1.0;
+      double* Dt = S + kp.oT1;
+      double* Et = S + kp.oT2;
+      wsync();
+      for (int it = 0; it < kp.s.scaling; ++it) {
+        if (l < nx) {
+          double s = fabs(ab[l]);
+          if (l < np)
+            for (int i = 0; i < np; ++i) s = fmax(s, fabs(P[i * np + l]));
+          for (int i = 0; i < ng; ++i) s = fmax(s, fabs(G[i * nx + l]));
+          s = s < kMinScaling ? 1.0 : (s > kMaxScaling ? kMaxScaling : s);
+          Dt[l] = 1.0 / sqrt(s);
+          double eb = fabs(ab[l]);
+          eb = eb < kMinScaling ? 1.0 : (eb > kMaxScaling ? kMaxScaling : eb);
+          Et[l] = 1.0 / sqrt(eb);
+        }
+        if (l < ng) {
+          double s = 0;
+          for (int j = 0; j < nx; ++j) s = fmax(s, fabs(G[l * nx + j]));
+          s = s < kMinScaling ? 1.0 : (s > kMaxScaling ? kMaxScaling : s);
+          Et[nx + l] = 1.0 / sqrt(s);
+        }
+        wsync();
+        if (l < np)
+          for (int c = 0; c < np; ++c) P[l * np + c] *= Dt[l] * Dt[c];
+        if (l < ng)
+          for (int j = 0; j < nx; ++j) G[l * nx + j] *= Et[nx + l] * Dt[j];
+        if (l < nx) {
+          ab[l] *= Et[l] * Dt[l];
+          qq[l] *= Dt[l];
+          D[l] *= Dt[l];
+          E[l] *= Et[l];
+        }
+        if (l < ng) E[nx + l] *= Et[nx + l];
+        wsync();
+        // cost scaling: mean column norm of P vs |q|_inf
+        double cn = 0, qn = 0;
+        if (l < nx) {
+          if (l < np)
+            for (int i = 0; i < np; ++i) cn = fmax(cn, fabs(P[i * np + l]));
+          qn = fabs(qq[l]);
+        }
+        cn = wave_sum(cn) / nx;
+        qn = wave_max(qn);
+        qn = qn < kMinScaling ? 1.0 : (qn > kMaxScaling ? kMaxScaling : qn);
+        double ct = fmax(cn, qn);
+        ct = ct < kMinScaling ? 1.0 : (ct > kMaxScaling ? kMaxScaling : ct);
+        ct = 1.0 / ct;
+        if (l < np)
+          for (int c = 0; c < np; ++c) P[l * np + c] *= ct;
+        if (l < nx) qq[l] *= ct;
+        if (l == 0) sc[SC_C] *= ct;
+        wsync();
+      }
+      for (int row = l; row < m; row += 64) {
+        lo[row] = fmax(lo[row], -kInf) * E[row];
+        up[row] = fmin(up[row], kInf) * E[row];
+      }
+      wsync();
+      PH(1);
+      set_rho(kp, S, kp.s.rho);
+      factor_kinv(kp, S);
+      if (l < nx) x[l] = 0.0;
+      for (int row = l; row < m; row += 64) z[row] = y[row] = 0.0;
+      wsync();
+      PH(2);
+      // ---------------- OSQP: ADMM ----------------------------------------
+      const double* K = S + kp.oU0;
+      const double* rv = S + kp.oRho;
+      double* w = S + kp.oT1;
+      double* xt = S + kp.oXT;
+      const double sig = kp.s.sigma, al = kp.s.alpha;
+      int it;
+      for (it = 1; it <= kp.s.max_iter; ++it) {
+        for (int row = l; row < m; row += 64) w[row] = rv[row] * z[row] - y[row];
+        wsync();
+        if (l < nx) {
+          double r = sig * x[l] - qq[l] + ab[l] * w[l];
+          for (int i = 0; i < ng; ++i) r += G[i * nx + l] * w[nx + i];
+          xt[l] = r;
+        }
+        wsync();
+        double xtil = 0;
+        if (l < nx) {
+          for (int c = 0; c < nx; ++c) xtil += K[l * nx + c] * xt[c];
+        }
+        wsync();
+        if (l < nx) xt[l] = xtil;
+        wsync();
+        // z~ = A x~ ; relaxation ; projection ; dual update
+        if (l < nx) {
+          const double zr = al * ab[l] * xtil + (1 - al) * z[l];
+          double zn = zr + y[l] / rv[l];
+          zn = fmin(fmax(zn, lo[l]), up[l]);
+          const double d = rv[l] * (zr - zn);
+          dy[l] = d;
+          y[l] += d;
+          z[l] = zn;
+          x[l] = al * xtil + (1 - al) * x[l];
+        }
+        if (l < ng) {
+          const int row = nx + l;
+          double a = 0;
+          for (int j = 0; j < nx; ++j) a += G[l * nx + j] * xt[j];
+          const double zr = al * a + (1 - al) * z[row];
+          double zn = zr + y[row] / rv[row];
+          zn = fmin(fmax(zn, lo[row]), up[row]);
+          const double d = rv[row] * (zr - zn);
+          dy[row] = d;
+          y[row] += d;
+          z[row] = zn;
+        }
+        wsync();
+        PH(3);
+        const bool check = kp.s.check_termination > 0 && it % kp.s.check_termination == 0;
+        const bool adapt = kp.s.adaptive_rho && kp.s.adaptive_rho_interval > 0 && it % kp.s.adaptive_rho_interval == 0;
+        if (check || adapt) residuals(kp, S, x, z, y, kp.s.eps_abs, kp.s.eps_rel);
+        if (check) {
+          const bool conv = sc[SC_PRI] < sc[SC_EPSP] && sc[SC_DUA] < sc[SC_EPSD];
+          // parity mode: a certified polish is exact whatever the ADMM
+          // residual, so also try it every 4th check (slow-ADMM vertices)
+          if (kp.s.exact && !conv && it % (4 * kp.s.check_termination) == 0) {
+            if (polish(kp, S, true)) {
+              status = DRC_STATUS_SOLVED;
+              break;
+            }
+            factor_kinv(kp, S);  // polish used the union region
+            residuals(kp, S, x, z, y, kp.s.eps_abs, kp.s.eps_rel);
+          }
+          if (conv) {
+            if (!kp.s.exact) {
+              status = DRC_STATUS_SOLVED;
+              break;
+            }
+            if (polish(kp, S, true)) {
+              status = DRC_STATUS_SOLVED;
+              break;
+            }
+            factor_kinv(kp, S);  // polish used the union region
+            residuals(kp, S, x, z, y, kp.s.eps_fallback, kp.s.eps_fallback);
+            if (sc[SC_PRI] < sc[SC_EPSP] && sc[SC_DUA] < sc[SC_EPSD]) {
+              status = DRC_STATUS_SOLVED;
+              break;
+            }
+          } else if (primal_infeasible(kp, S, kp.s.eps_prim_inf)) {
+            status = DRC_STATUS_PRIMAL_INFEASIBLE;
+            break;
+          }
+        }
+        if (adapt) {
+          const double pr = sc[SC_PRIS] / (fmax(sc[SC_NAX], sc[SC_NZ]) + kDivTol);
+          const double dr = sc[SC_DUAS] / (fmax(fmax(sc[SC_NQ], sc[SC_NATY]), sc[SC_NPX]) + kDivTol);
+          const double rho = sc[SC_RHO];
+          double rn = rho * sqrt(pr / (dr + kDivTol));
+          rn = fmin(fmax(rn, kRhoMin), kRhoMax);
+          if (rn > rho * kp.s.adaptive_rho_tolerance || rn < rho / kp.s.adaptive_rho_tolerance) {
+            set_rho(kp, S, rn);
+            factor_kinv(kp, S);
+          }
+        }
+      }
+      PH(4);
+      iters = it > kp.s.max_iter ? kp.s.max_iter : it;
+      if (status == DRC_STATUS_SOLVED && kp.s.polish && !kp.s.exact) polish(kp, S, false);
+    }
+    PH(5);
+    // ---------------- outputs (zero on failure, QP_IK.cpp:56-61) ------------
+    if (l < kp.na) io.out[(int64_t)l * B + b] = status == DRC_STATUS_SOLVED ? D[l] * x[l] : 0.0;
+    if (l == 0) {
+      io.status[b] = status;
+      if (io.iters) io.iters[b] = iters;
+    }
+    wsync();
+  }
+  PH_FLUSH(16);
+}
+
+}  // namespace drc_amd
+
+// ==========================================================================
+// host side: the C-ABI (include/drc_amd.h)
+// ==========================================================================
+namespace drc_amd {
+
+struct drc_model_impl {
+  HostModel hm;
+  DevModel* d_model = nullptr;
+  int device = 0;
+  drc_kinematic_param kparam{};
+  drc_joint_index jidx{};
+  drc_actuator_index aidx{};
+  EpaWs* epa_ws = nullptr;
+  int64_t epa_count = 0;
+  void* pool = nullptr;  // task data when the caller does not keep it
+  int64_t pool_bytes = 0;
+  std::mutex mu;
+};
+
+static thread_local std::string g_last_error;
+static int set_err(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+#define HIP_TRY(expr)                                                                   \
+  do {                                                                                  \
+    hipError_t e_ = (expr);                                                             \
+    if (e_ != hipSuccess) return set_err(DRC_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+// DyrosMath::PinvCOD on a small dense matrix (host, model build only):
+// Moore-Penrose inverse via the normal equations' symmetric eigen-system,
+// rank cut at 1e-6 relative (math_type_define.h:7,563-570).
+static void pinv_small(const double* A, int r, int c, double* X /* c x r */) {
+  // X = (A^T A)^+ A^T with (A^T A) symmetric c x c (c <= 3 here)
+  double N[9] = {0}, V[9], w[3];
+  for (int i = 0; i < c; ++i)
+    for (int j = 0; j < c; ++j)
+      for (int k = 0; k < r; ++k) N[i * c + j] += A[k * c + i] * A[k * c + j];
+  for (int i = 0; i < c * c; ++i) V[i] = (i % (c + 1) == 0) ? 1.0 : 0.0;
+  for (int sweep = 0; sweep < 60; ++sweep) {
+    double off = 0;
+    for (int i = 0; i < c; ++i)
+      for (int j = i + 1; j < c; ++j) off += N[i * c + j] * N[i * c + j];
+    if (off < 1e-300) break;
+    for (int p = 0; p < c; ++p)
+      for (int q = p + 1; q < c; ++q) {
+        if (std::fabs(N[p * c + q]) < 1e-300) continue;
+        double th = (N[q * c + q] - N[p * c + p]) / (2 * N[p * c + q]);
+        double t = (th >= 0 ? 1 : -1) / (std::fabs(th) + std::sqrt(th * th + 1));
+        double cs = 1 / std::sqrt(t * t + 1), sn = t * cs;
+        for (int k = 0; k < c; ++k) {
+          double a = N[k * c + p], b = N[k * c + q];
+          N[k * c + p] = cs * a - sn * b;
+          N[k * c + q] = sn * a + cs * b;
+        }
+        for (int k = 0; k < c; ++k) {
+          double a = N[p * c + k], b = N[q * c + k];
+          N[p * c + k] = cs * a - sn * b;
+          N[q * c + k] = sn * a + cs * b;
+        }
+        for (int k = 0; k < c; ++k) {
+          double a = V[k * c + p], b = V[k * c + q];
+          V[k * c + p] = cs * a - sn * b;
+          V[k * c + q] = sn * a + cs * b;
+        }
+      }
+  }
+  double wmax = 0;
+  for (int i = 0; i < c; ++i) {
+    w[i] = N[i * c + i];
+    wmax = std::fmax(wmax, std::fabs(w[i]));
+  }
+  double Ni[9] = {0};
+  for (int e = 0; e < c; ++e) {
+    if (std::sqrt(std::fabs(w[e])) <= 1e-6 * std::sqrt(wmax)) continue;
+    for (int i = 0; i < c; ++i)
+      for (int j = 0; j < c; ++j) Ni[i * c + j] += V[i * c + e] * V[j * c + e] / w[e];
+  }
+  for (int i = 0; i < c; ++i)
+    for (int k = 0; k < r; ++k) {
+      double s = 0;
+      for (int j = 0; j < c; ++j) s += Ni[i * c + j] * A[k * c + j];
+      X[i * r + k] = s;
+    }
+}
+
+// Mobile::RobotData::computeFKJacobian for the config-independent drives
+// (src/mobile/robot_data.cpp:138-176).
+static int mobile_fk_jacobian(const drc_kinematic_param& p, int* W, double out[3][kMaxWheels]) {
+  for (int r = 0; r < 3; ++r)
+    for (int c = 0; c < kMaxWheels; ++c) out[r][c] = 0;
+  if (p.type == DRC_DRIVE_DIFFERENTIAL) {
+    *W = 2;
+    out[0][0] = p.wheel_radius / 2.;
+    out[0][1] = p.wheel_radius / 2.;
+    out[2][0] = -p.wheel_radius / p.base_width;
+    out[2][1] = p.wheel_radius / p.base_width;
+    return DRC_OK;
+  }
+  if (p.type == DRC_DRIVE_MECANUM) {
+    const int n = p.n_wheels;
+    if (n < 1 || n > kMaxWheels) return set_err(DRC_ERR_INVALID_ARGUMENT, "mecanum wheel count out of range");
+    double Jinv[kMaxWheels * 3], X[3 * kMaxWheels];
+    for (int i = 0; i < n; ++i) {
+      const double r = p.wheel_radius, g = p.roller_angles[i], px = p.base2wheel_positions[i][0],
+                   py = p.base2wheel_positions[i][1], pt = p.base2wheel_angles[i];
+      // (1/r) [1 tan g] [[cos pt, sin pt], [-sin pt, cos pt]] [[1 0 -py], [0 1 px]]
+      const double a0 = std::cos(pt) - std::tan(g) * std::sin(pt), a1 = std::sin(pt) + std::tan(g) * std::cos(pt);
+      Jinv[i * 3 + 0] = a0 / r;
+      Jinv[i * 3 + 1] = a1 / r;
+      Jinv[i * 3 + 2] = (-a0 * py + a1 * px) / r;
+    }
+    pinv_small(Jinv, n, 3, X);
+    for (int r = 0; r < 3; ++r)
+      for (int c = 0; c < n; ++c) out[r][c] = X[r * n + c];
+    *W = n;
+    return DRC_OK;
+  }
+  return set_err(DRC_ERR_UNSUPPORTED, "caster drive: the FK Jacobian depends on steer angles (not supported by the batched whole-body kernel)");
+}
+
+static int upload(drc_model_impl* m) {
+  HIP_TRY(hipSetDevice(m->device));
+  HIP_TRY(hipMalloc(&m->d_model, sizeof(DevModel)));
+  HIP_TRY(hipMemcpy(m->d_model, &m->hm.dev, sizeof(DevModel), hipMemcpyHostToDevice));
+  return DRC_OK;
+}
+
+// LDS plan: persistent QP region + a union of (kinematics | K^-1 | polish)
+static int plan_layout(const DevModel& M, KParams* k, bool task_only) {
+  int off = 0;
+  auto take = [&](int n) {
+    int o = off;
+    off += (n + 1) & ~1;  // keep 16-byte alignment
+    return o;
+  };
+  const int nx = k->nx, ng = k->ng, np = k->np, m = k->m, nv = M.nv;
+  if (task_only) {  // task_kernel: scalars + kinematics only
+    k->oRed = take(64);
+    k->oSc = take(32);
+  } else {
+  k->oP = take(np * np);
+  k->oG = take(ng * nx);
+  k->oQ = take(nx);
+  k->oAB = take(nx);
+  k->oL = take(m);
+  k->oU = take(m);
+  k->oD = take(nx);
+  k->oE = take(m);
+  k->oRho = take(m);
+  k->oX = take(nx);
+  k->oZ = take(m);
+  k->oY = take(m);
+  k->oDY = take(m);
+  k->oXT = take(nx);
+  k->oZT = take(m);
+  k->oT1 = take(m > nx ? m : nx);
+  k->oT2 = take(m > nx ? m : nx);
+  k->oRed = take(64);
+  k->oSc = take(32);
+  }
+  k->oU0 = off;
+  // kinematics view of the union
+  int u = k->oU0;
+  auto takeu = [&](int n) {
+    int o = u;
+    u += (n + 1) & ~1;
+    return o;
+  };
+  k->kT = takeu((nv + 1) * 12);
+  k->kZ = takeu((nv + 1) * 3);
+  k->kTe = takeu(12);
+  k->kJ = takeu(6 * nv);
+  const int ng_ = M.ngeom > nv ? M.ngeom : nv;
+  k->kTg = takeu(ng_ * 12);
+  k->kq = takeu(nv);
+  k->kqd = takeu(nv);
+  k->kA6 = takeu(36);
+  k->kAi = takeu(36);
+  k->kW = takeu(k->narm * 6);
+  k->kPart = takeu(k->narm * k->narm);
+  k->kPd = takeu(M.npairs);
+  k->kPf = takeu(M.npairs);
+  k->kxdd = takeu(6);
+  k->kmg = takeu(k->narm);
+  k->kdg = takeu(nv);
+  k->kJt = takeu(6 * np);
+  k->kSv = takeu(3 * kMaxWheels);
+  k->kScr = takeu(96);
+  int kin_end = u;
+  int kinv_end = k->oU0 + nx * nx;
+  const int N = nx + ng;
+  int pol_end = k->oU0 + 64 + 64 + 128 + 64 * 5 + N * (N + 1) / 2;
+  int end = kin_end;
+  if (!task_only) {
+    end = end > kinv_end ? end : kinv_end;
+    end = end > pol_end ? end : pol_end;
+  }
+  k->lds_doubles = end;
+  if (end * 8 > 160 * 1024) return set_err(DRC_ERR_UNSUPPORTED, "model too large for the per-wave LDS plan");
+  return DRC_OK;
+}
+
+static int make_kparams(const drc_model_impl* mm, const drc_qpik_params* p, int stages, KParams* k) {
+  const DevModel& M = mm->hm.dev;
+  std::memset(k, 0, sizeof(*k));
+  for (int i = 0; i < 6; ++i) {
+    k->kp[i] = p->kp[i];
+    k->kv[i] = p->kv[i];
+  }
+  k->ff = p->feedforward;
+  k->alpha_cbf = p->alpha_cbf;
+  k->w_reg = p->w_reg;
+  k->slack_w = p->slack_w;
+  k->man_min = p->man_min;
+  k->dist_min = p->dist_min;
+  k->t = p->t;
+  k->t0 = p->t0;
+  k->duration = p->duration;
+  if (p->frame_id < 0 || p->frame_id >= M.nframes)
+    return set_err(DRC_ERR_UNKNOWN_LINK, "params.frame_id does not name a link of the model");
+  if (M.frame_joint[p->frame_id] == 0)
+    return set_err(DRC_ERR_UNKNOWN_LINK, "task frame is attached to the universe (no joint moves it)");
+  k->frame_joint = M.frame_joint[p->frame_id];
+  std::memcpy(k->frame_place, M.frame_place[p->frame_id], sizeof(k->frame_place));
+  if (p->mode < DRC_MODE_QPIK || p->mode > DRC_MODE_QPIK_CUBIC) return set_err(DRC_ERR_INVALID_ARGUMENT, "bad mode");
+  k->mode = p->mode;
+  k->stages = stages;
+  k->s = p->solver;
+  k->nv = M.nv;
+  if (M.kind == 0) {
+    k->narm = M.nv;
+    k->c0 = 0;
+    k->np = M.nv;
+    k->nx = 3 * M.nv + 2;  // QP_IK.cpp:24-28
+    k->na = M.nv;
+  } else {
+    k->narm = M.n_arm;
+    k->c0 = M.mani_start;
+    k->np = M.n_arm + M.n_wheel;
+    k->nx = k->np;  // MoMa QP_IK.cpp:20
+    k->na = k->np;
+  }
+  k->ng = 2 * k->narm + 2;
+  k->m = k->nx + k->ng;
+  if (k->nx > 64 || k->ng > 64 || k->narm > 8)
+    return set_err(DRC_ERR_UNSUPPORTED, "QP larger than one wavefront's row mapping");
+  if (k->s.max_iter < 1 || k->s.check_termination < 0) return set_err(DRC_ERR_INVALID_ARGUMENT, "bad solver settings");
+  return plan_layout(M, k, stages != 0);
+}
+
+static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int stages, int64_t B, const double* q,
+                  const double* qdot, const double* xt, const double* xdt, const double* xi, const double* xdi,
+                  double* out, int32_t* status, int32_t* iters, double* pose, double* jac, double* man,
+                  double* dist, int32_t* pair, double* xdd, void* stream) {
+  drc_model_impl* m = const_cast<drc_model_impl*>(cm);
+  if (!m || !params) return set_err(DRC_ERR_INVALID_ARGUMENT, "null model/params");
+  if (B < 0) return set_err(DRC_ERR_INVALID_ARGUMENT, "negative batch");
+  if (B == 0) return DRC_OK;
+  if (!q || !qdot || !xdt) return set_err(DRC_ERR_INVALID_ARGUMENT, "q, qdot and xdot_target are required");
+  if (params->mode != DRC_MODE_QPIK && !xt) return set_err(DRC_ERR_INVALID_ARGUMENT, "x_target required for QPIKStep/QPIKCubic");
+  if (params->mode == DRC_MODE_QPIK_CUBIC && (!xi || !xdi))
+    return set_err(DRC_ERR_INVALID_ARGUMENT, "x_init/xdot_init required for QPIKCubic");
+  if (!stages && (!out || !status)) return set_err(DRC_ERR_INVALID_ARGUMENT, "qdot_out and status are required");
+  KParams kt, kq;
+  int rc = make_kparams(m, params, 1, &kt);
+  if (rc) return rc;
+  if (!stages) {
+    rc = make_kparams(m, params, 0, &kq);
+    if (rc) return rc;
+  }
+  HIP_TRY(hipSetDevice(m->device));
+  const int64_t grid = B < 8192 ? B : 8192;
+  const int nv = m->hm.dev.nv, narm = kt.narm;
+  // task data: ~ (6 nv + narm + nv + 9) doubles per instance, model-owned pool
+  const int64_t per = 6 * nv + (1 + narm) + (1 + nv) + 6 + 1;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  {
+    std::lock_guard<std::mutex> g(m->mu);
+    if (m->epa_count < grid) {
+      if (m->epa_ws) HIP_TRY(hipFree(m->epa_ws));
+      m->epa_ws = nullptr;
+      HIP_TRY(hipMalloc(&m->epa_ws, sizeof(EpaWs) * grid));
+      m->epa_count = grid;
+    }
+    const bool need_pool = !jac || !man || !dist || !xdd || !pair;
+    if (need_pool && m->pool_bytes < per * B * 8) {
+      if (m->pool) HIP_TRY(hipFree(m->pool));
+      m->pool = nullptr;
+      HIP_TRY(hipMalloc(&m->pool, per * B * 8));
+      m->pool_bytes = per * B * 8;
+    }
+    double* pool = reinterpret_cast<double*>(m->pool);
+    if (!jac) jac = pool;
+    if (!man) man = pool + 6 * nv * B;
+    if (!dist) dist = pool + (6 * nv + 1 + narm) * B;
+    if (!xdd) xdd = pool + (6 * nv + 2 + narm + nv) * B;
+    if (!pair) pair = reinterpret_cast<int32_t*>(pool + (6 * nv + 8 + narm + nv) * B);
+  }
+  IO io{B, q, qdot, xt, xdt, xi, xdi, out, status, iters, pose, jac, man, dist, xdd, pair, m->epa_ws};
+  hipLaunchKernelGGL(task_kernel, dim3(static_cast<unsigned>(grid)), dim3(64),
+                     static_cast<size_t>(kt.lds_doubles) * sizeof(double), st, m->d_model, kt, io);
+  HIP_TRY(hipGetLastError());
+  if (!stages) {
+    hipLaunchKernelGGL(qp_kernel, dim3(static_cast<unsigned>(grid)), dim3(64),
+                       static_cast<size_t>(kq.lds_doubles) * sizeof(double), st, m->d_model, kq, io);
+    HIP_TRY(hipGetLastError());
+  }
+  return DRC_OK;
+}
+
+}  // namespace drc_amd
+
+using drc_amd::drc_model_impl;
+struct drc_model : drc_model_impl {};
+
+extern "C" {
+
+const char* drc_error_string(int code) {
+  switch (code) {
+    case DRC_OK: return "ok";
+    case DRC_ERR_INVALID_ARGUMENT: return "invalid argument";
+    case DRC_ERR_FILE: return "file does not exist";
+    case DRC_ERR_PARSE: return "parse error";
+    case DRC_ERR_UNSUPPORTED: return "unsupported model";
+    case DRC_ERR_UNKNOWN_LINK: return "link name not found in URDF";
+    case DRC_ERR_HIP: return "HIP runtime error";
+    case DRC_ERR_SIZE_MISMATCH: return "size mismatch";
+    default: return "unknown error";
+  }
+}
+const char* drc_last_error(void) { return drc_amd::g_last_error.c_str(); }
+
+#ifdef DRC_PHASE_TIMING
+// diagnostic build only: accumulated per-phase s_memtime cycles (32 slots)
+int drc_debug_phase_cycles(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(drc_amd::g_phase_cycles), sizeof(unsigned long long) * 32) != hipSuccess)
+    return DRC_ERR_HIP;
+  if (reset) {
+    unsigned long long z[32] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(drc_amd::g_phase_cycles), z, sizeof(z)) != hipSuccess) return DRC_ERR_HIP;
+  }
+  return DRC_OK;
+}
+#endif
+
+int drc_model_create_manipulator(const char* urdf, const char* srdf, const char* packages, int device,
+                                 drc_model** out) {
+  (void)packages;  // collision meshes are not supported: primitives only
+  if (!urdf || !out) return drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "null argument");
+  auto* m = new drc_model();
+  std::string err;
+  int rc = drc_amd::build_model_from_urdf(urdf, srdf ? srdf : "", &m->hm, &err);
+  if (rc) {
+    delete m;
+    return drc_amd::set_err(rc, err);
+  }
+  m->hm.dev.kind = 0;
+  m->device = device;
+  rc = drc_amd::upload(m);
+  if (rc) {
+    delete m;
+    return rc;
+  }
+  *out = m;
+  return DRC_OK;
+}
+
+int drc_model_create_mobile_manipulator(const drc_kinematic_param* param, const drc_joint_index* ji,
+                                        const drc_actuator_index* ai, const char* urdf, const char* srdf,
+                                        const char* packages, int device, drc_model** out) {
+  (void)packages;
+  if (!param || !ji || !ai || !urdf || !out) return drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "null argument");
+  auto* m = new drc_model();
+  std::string err;
+  int rc = drc_amd::build_model_from_urdf(urdf, srdf ? srdf : "", &m->hm, &err);
+  if (rc) {
+    delete m;
+    return drc_amd::set_err(rc, err);
+  }
+  drc_amd::DevModel& d = m->hm.dev;
+  int W = 0;
+  rc = drc_amd::mobile_fk_jacobian(*param, &W, d.J_mobile);
+  if (rc) {
+    delete m;
+    return rc;
+  }
+  // MobileManipulator::RobotData ctor (mobile_manipulator/robot_data.cpp:18-25)
+  const int virtual_dof = 3;
+  d.kind = 1;
+  d.n_wheel = W;
+  d.n_arm = d.nv - (virtual_dof + W);  // every joint 1-DoF, no extra joints
+  d.virtual_start = ji->virtual_start;
+  d.mani_start = ji->mani_start;
+  d.mobi_start = ji->mobi_start;
+  d.act_mani_start = ai->mani_start;
+  d.act_mobi_start = ai->mobi_start;
+  if (d.n_arm < 1 || d.n_arm > 8 || ji->virtual_start + 3 > d.nv || ji->mani_start + d.n_arm > d.nv ||
+      ji->mobi_start + W > d.nv || ai->mani_start + d.n_arm > d.n_arm + W || ai->mobi_start + W > d.n_arm + W) {
+    delete m;
+    return drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "JointIndex/ActuatorIndex inconsistent with the URDF dof");
+  }
+  m->kparam = *param;
+  m->jidx = *ji;
+  m->aidx = *ai;
+  m->device = device;
+  rc = drc_amd::upload(m);
+  if (rc) {
+    delete m;
+    return rc;
+  }
+  *out = m;
+  return DRC_OK;
+}
+
+void drc_model_destroy(drc_model* m) {
+  if (!m) return;
+  (void)hipSetDevice(m->device);
+  if (m->d_model) (void)hipFree(m->d_model);
+  if (m->epa_ws) (void)hipFree(m->epa_ws);
+  if (m->pool) (void)hipFree(m->pool);
+  delete m;
+}
+
+int drc_model_info(const drc_model* m, int* dof, int* act, int* mani, int* mobi, int* ngeom, int* npairs) {
+  if (!m) return drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "null model");
+  const drc_amd::DevModel& d = m->hm.dev;
+  if (dof) *dof = d.nv;
+  if (act) *act = d.kind == 1 ? d.n_arm + d.n_wheel : d.nv;
+  if (mani) *mani = d.kind == 1 ? d.n_arm : d.nv;
+  if (mobi) *mobi = d.kind == 1 ? d.n_wheel : 0;
+  if (ngeom) *ngeom = d.ngeom;
+  if (npairs) *npairs = d.npairs;
+  return DRC_OK;
+}
+
+int drc_model_limits(const drc_model* m, double* q_lb, double* q_ub, double* qd_lb, double* qd_ub) {
+  if (!m) return drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "null model");
+  const drc_amd::DevModel& d = m->hm.dev;
+  for (int i = 0; i < d.nv; ++i) {
+    if (q_lb) q_lb[i] = d.lower[i];
+    if (q_ub) q_ub[i] = d.upper[i];
+    if (qd_lb) qd_lb[i] = -d.vel[i];
+    if (qd_ub) qd_ub[i] = d.vel[i];
+  }
+  return DRC_OK;
+}
+
+int drc_model_find_frame(const drc_model* m, const char* name, int* id) {
+  if (!m || !name || !id) return drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "null argument");
+  const auto& names = m->hm.frame_names;
+  for (size_t i = 0; i < names.size(); ++i)
+    if (names[i] == name) {
+      *id = static_cast<int>(i);
+      return DRC_OK;
+    }
+  *id = -1;
+  return drc_amd::set_err(DRC_ERR_UNKNOWN_LINK, std::string("Link name ") + name + " not found in URDF.");
+}
+
+int drc_model_mobile_fk_jacobian(const drc_model* m, double* J) {
+  if (!m || !J) return drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "null argument");
+  const drc_amd::DevModel& d = m->hm.dev;
+  if (d.kind != 1) return drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "not a mobile manipulator");
+  for (int r = 0; r < 3; ++r)
+    for (int c = 0; c < d.n_wheel; ++c) J[r * d.n_wheel + c] = d.J_mobile[r][c];
+  return DRC_OK;
+}
+
+int drc_default_qpik_params(const drc_model* m, int exact, drc_qpik_params* p) {
+  if (!m || !p) return drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "null argument");
+  std::memset(p, 0, sizeof(*p));
+  const bool moma = m->hm.dev.kind == 1;
+  for (int i = 0; i < 6; ++i) {
+    p->kp[i] = moma ? 400 : 100;  // robot_controller.cpp:12 ; MoMa :15
+    p->kv[i] = moma ? 0 : 20;     // MoMa QPIKStep: Kp*e + xdot_target (:177)
+  }
+  p->feedforward = moma ? 1.0 : 0.0;
+  p->alpha_cbf = 50;
+  p->w_reg = moma ? 0.01 : 1.0;
+  p->slack_w = 1000;
+  p->man_min = 0.01;
+  p->dist_min = 0.05;
+  p->mode = DRC_MODE_QPIK_STEP;
+  p->frame_id = -1;
+  drc_solver_settings& s = p->solver;
+  s.rho = 0.1;
+  s.sigma = 1e-6;
+  s.alpha = 1.6;
+  s.eps_abs = 1e-3;
+  s.eps_rel = 1e-3;
+  s.eps_prim_inf = 1e-4;
+  s.max_iter = 4000;
+  s.check_termination = 25;
+  s.scaling = 10;
+  s.adaptive_rho = 1;
+  s.adaptive_rho_interval = 25;
+  s.adaptive_rho_tolerance = 5;
+  s.polish = exact ? 1 : 0;
+  s.polish_refine_iter = 3;
+  s.delta = 1e-6;
+  s.exact = exact ? 1 : 0;
+  s.eps_exact = 1e-9;
+  s.eps_fallback = 1e-7;
+  return DRC_OK;
+}
+
+int drc_qpik_batch(const drc_model* m, const drc_qpik_params* p, int64_t B, const double* q, const double* qdot,
+                   const double* xt, const double* xdt, const double* xi, const double* xdi, double* out,
+                   int32_t* status, int32_t* iters, void* stream) {
+  return drc_amd::launch(m, p, 0, B, q, qdot, xt, xdt, xi, xdi, out, status, iters, nullptr, nullptr, nullptr,
+                         nullptr, nullptr, nullptr, stream);
+}
+
+int drc_qpik_stages_batch(const drc_model* m, const drc_qpik_params* p, int64_t B, const double* q,
+                          const double* qdot, const double* xt, const double* xdt, const double* xi,
+                          const double* xdi, double* pose, double* jac, double* man, double* dist, int32_t* pair,
+                          double* xdd, void* stream) {
+  return drc_amd::launch(m, p, 1, B, q, qdot, xt, xdt, xi, xdi, nullptr, nullptr, nullptr, pose, jac, man, dist,
+                         pair, xdd, stream);
+}
+
+}  // extern "C"

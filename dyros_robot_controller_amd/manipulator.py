@@ -1,0 +1,310 @@
+"""``drc.manipulator`` mirror: RobotData + RobotController (QPIK entries).
+
+Mirrors the reference's Python/C++ interface for the hot path
+(src/bindings.cpp:293-321,398-426; drc/manipulator/*.py):
+
+=====================================  =========================================
+reference                              here
+=====================================  =========================================
+``RobotData(urdf, srdf, packages)``    ``RobotData(urdf, srdf, packages, device)``
+``updateState(q, qdot)``               ``updateState`` / ``update_state``
+``getPose/getJacobian/getVelocity``    same names (computed by the HIP kernel)
+``getManipulability(true,false,l)``    ``getManipulability``
+``getMinDistance(true,false,false)``   ``getMinDistance``
+``RobotController(dt, robot_data)``    same
+``QPIK/QPIKStep/QPIKCubic``            same names + snake_case aliases
+(none: one robot per call)             ``QPIK_batch`` / ``QPIK_step_batch`` /
+                                       ``QPIK_cubic_batch`` over [field][B]
+                                       device tensors
+=====================================  =========================================
+
+Every result comes from ``libdrc_amd.so``; single-instance calls are B=1
+launches of the same kernel (there is no CPU path).
+"""
+import sys
+
+import numpy as np
+
+from . import _batch, _capi
+from ._capi import C
+
+
+def pose_to12(T):
+    """4x4 homogeneous (Eigen::Affine3d::matrix()) -> [R col-major(9), p(3)]."""
+    T = np.asarray(T, dtype=np.float64)
+    return np.concatenate([T[:3, :3].T.reshape(-1), T[:3, 3]])
+
+
+def pose_from12(v):
+    v = np.asarray(v, dtype=np.float64)
+    T = np.eye(4)
+    T[:3, :3] = v[:9].reshape(3, 3).T
+    T[:3, 3] = v[9:12]
+    return T
+
+
+def _default_device():
+    import torch
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+class _ModelHandle:
+    """Owns a ``drc_model*`` (device copy of the robot model)."""
+
+    def __init__(self, handle, device):
+        self.handle = handle
+        self.device = device
+        dof, act, mani, mobi, ng, npair = (C.c_int() for _ in range(6))
+        _capi.check(_capi.lib().drc_model_info(handle, *(C.byref(v) for v in (dof, act, mani, mobi, ng, npair))))
+        self.dof, self.actuated_dof, self.mani_dof, self.mobi_dof = dof.value, act.value, mani.value, mobi.value
+        self.n_geoms, self.n_pairs = ng.value, npair.value
+
+    def frame_id(self, link_name):
+        fid = C.c_int()
+        _capi.check(_capi.lib().drc_model_find_frame(self.handle, link_name.encode(), C.byref(fid)))
+        return fid.value
+
+    def close(self):
+        if self.handle:
+            _capi.lib().drc_model_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class RobotData:
+    """Manipulator::RobotData (include/dyros_robot_controller/manipulator/robot_data.h:49)."""
+
+    def __init__(self, urdf_path, srdf_path="", packages_path="", device=None):
+        import torch
+        self.device = torch.device(device) if device is not None else _default_device()
+        h = C.c_void_p()
+        _capi.check(_capi.lib().drc_model_create_manipulator(
+            urdf_path.encode(), (srdf_path or "").encode(), (packages_path or "").encode(),
+            C.c_int(self.device.index or 0), C.byref(h)))
+        self.model = _ModelHandle(h, self.device)
+        n = self.model.dof
+        self._lims = [np.zeros(n) for _ in range(4)]
+        _capi.check(_capi.lib().drc_model_limits(h, *(a.ctypes.data_as(C.POINTER(C.c_double)) for a in self._lims)))
+        self.q_ = np.zeros(n)
+        self.qdot_ = np.zeros(n)
+
+    # -- state ---------------------------------------------------------------
+    def updateState(self, q, qdot):
+        q, qdot = np.asarray(q, float).reshape(-1), np.asarray(qdot, float).reshape(-1)
+        if q.size != self.getDof() or qdot.size != self.getDof():
+            raise ValueError("q and qdot must have size dof")
+        self.q_, self.qdot_ = q.copy(), qdot.copy()
+        return True
+
+    update_state = updateState
+
+    def getDof(self):
+        return self.model.dof
+
+    get_dof = getDof
+
+    def getJointPosition(self):
+        return self.q_.copy()
+
+    def getJointVelocity(self):
+        return self.qdot_.copy()
+
+    def getJointPositionLimit(self):
+        return self._lims[0].copy(), self._lims[1].copy()
+
+    def getJointVelocityLimit(self):
+        return self._lims[2].copy(), self._lims[3].copy()
+
+    # -- task-space getters through the kernel's stage outputs ---------------
+    def _stages(self, q, qdot, link_name):
+        p = QPIKParamsBuilder(self.model, exact=True).params(link_name, mode=_capi.MODE_QPIK)
+        dq = _batch.as_device(np.asarray(q, float).reshape(-1, 1), self.device)
+        dqd = _batch.as_device(np.asarray(qdot, float).reshape(-1, 1), self.device)
+        z6 = _batch.as_device(np.zeros((6, 1)), self.device)
+        st = _batch.stages_batch(self.model, p, dq, dqd, None, z6)
+        return {k: v.cpu().numpy()[..., 0] for k, v in st.items()}
+
+    def computePose(self, q, link_name):
+        return pose_from12(self._stages(q, np.zeros_like(q), link_name)["pose"])
+
+    def computeJacobian(self, q, link_name):
+        return self._stages(q, np.zeros_like(q), link_name)["jac"].reshape(6, self.getDof())
+
+    def computeVelocity(self, q, qdot, link_name):
+        return self.computeJacobian(q, link_name) @ np.asarray(qdot, float)
+
+    def getPose(self, link_name):
+        """Pose at the current q (the reference returns the frame
+        cached by the last getFrameJacobian; we return FK(q))."""
+        return self.computePose(self.q_, link_name)
+
+    def getJacobian(self, link_name):
+        return self.computeJacobian(self.q_, link_name)
+
+    def getVelocity(self, link_name):
+        return self.getJacobian(link_name) @ self.qdot_
+
+    def getManipulability(self, with_grad=True, with_graddot=False, link_name=None):
+        if with_graddot:
+            raise NotImplementedError("grad_dot is outside the QPIK hot path (SURVEY §8f)")
+        st = self._stages(self.q_, self.qdot_, link_name)
+        return ManipulabilityResult(st["man"][0], st["man"][1:] if with_grad else np.zeros(self.getDof()))
+
+    def getMinDistance(self, with_grad=True, with_graddot=False, verbose=False):
+        if with_graddot:
+            raise NotImplementedError("grad_dot is outside the QPIK hot path (SURVEY §8f)")
+        link = None
+        for cand in ("fr3_link8", "tool0"):
+            try:
+                self.model.frame_id(cand)
+                link = cand
+                break
+            except _capi.DrcError:
+                pass
+        st = self._stages(self.q_, self.qdot_, link)
+        return MinDistResult(st["dist"][0], st["dist"][1:] if with_grad else np.zeros(self.getDof()))
+
+    get_pose, get_jacobian, get_velocity = getPose, getJacobian, getVelocity
+    get_manipulability, get_min_distance = getManipulability, getMinDistance
+    compute_pose, compute_jacobian, compute_velocity = computePose, computeJacobian, computeVelocity
+
+
+class ManipulabilityResult:
+    """type_define.h:116-132"""
+
+    def __init__(self, manipulability, grad):
+        self.manipulability = float(manipulability)
+        self.grad = np.asarray(grad, float)
+        self.grad_dot = np.zeros_like(self.grad)
+
+
+class MinDistResult:
+    """type_define.h:88-104"""
+
+    def __init__(self, distance, grad):
+        self.distance = float(distance)
+        self.grad = np.asarray(grad, float)
+        self.grad_dot = np.zeros_like(self.grad)
+
+
+class QPIKParamsBuilder:
+    """Fills ``drc_qpik_params`` from the reference defaults of the model kind."""
+
+    def __init__(self, model, exact=True):
+        self.model = model
+        self.base = _capi.QPIKParams()
+        _capi.check(_capi.lib().drc_default_qpik_params(model.handle, C.c_int(1 if exact else 0), C.byref(self.base)))
+
+    def params(self, link_name, mode, kp=None, kv=None, t=0.0, t0=0.0, duration=1.0):
+        p = _capi.QPIKParams()
+        C.pointer(p)[0] = self.base
+        p.frame_id = self.model.frame_id(link_name)
+        p.mode = mode
+        if kp is not None:
+            for i in range(6):
+                p.kp[i] = float(kp[i])
+        if kv is not None:
+            for i in range(6):
+                p.kv[i] = float(kv[i])
+        p.t, p.t0, p.duration = float(t), float(t0), float(duration)
+        return p
+
+
+class RobotController:
+    """Manipulator::RobotController QPIK entries
+    (src/manipulator/robot_controller.cpp:7-19,277-317).
+
+    ``solver_mode``: "exact" (default) returns the certified QP optimum
+    (parity contract); "osqp_default" runs the reference's OSQP
+    settings (eps 1e-3, no polish) — the same algorithm, reference accuracy.
+    """
+
+    def __init__(self, dt, robot_data, solver_mode="exact"):
+        self.dt_ = dt
+        self.robot_data_ = robot_data
+        self.dof_ = robot_data.getDof()
+        self.Kp_task_ = np.full(6, 100.0)
+        self.Kv_task_ = np.full(6, 20.0)
+        self.set_solver_mode(solver_mode)
+
+    def set_solver_mode(self, mode):
+        if mode not in ("exact", "osqp_default"):
+            raise ValueError("solver_mode must be 'exact' or 'osqp_default'")
+        self.solver_mode = mode
+        self._pb = QPIKParamsBuilder(self.robot_data_.model, exact=(mode == "exact"))
+
+    def setTaskGain(self, Kp, Kv):
+        Kp, Kv = np.asarray(Kp, float).reshape(-1), np.asarray(Kv, float).reshape(-1)
+        if Kp.size != 6 or Kv.size != 6:
+            raise RuntimeError("Kp and Kv must be of size 6.")
+        self.Kp_task_, self.Kv_task_ = Kp, Kv
+
+    def setTaskKpGain(self, Kp):
+        Kp = np.asarray(Kp, float).reshape(-1)
+        if Kp.size != 6:
+            raise RuntimeError("Kp must be of size 6.")
+        self.Kp_task_ = Kp
+
+    def setTaskKvGain(self, Kv):
+        Kv = np.asarray(Kv, float).reshape(-1)
+        if Kv.size != 6:
+            raise RuntimeError("Kv must be of size 6.")
+        self.Kv_task_ = Kv
+
+    set_task_gain, set_task_kp_gain, set_task_kv_gain = setTaskGain, setTaskKpGain, setTaskKvGain
+
+    # -- batched entries (device tensors, [field][B]) --------------------------
+    def _run(self, mode, link_name, q, qdot, x_target, xdot_target, x_init=None, xdot_init=None,
+             t=0.0, t0=0.0, duration=1.0, iters=None):
+        p = self._pb.params(link_name, mode, self.Kp_task_, self.Kv_task_, t, t0, duration)
+        dev = self.robot_data_.device
+        return _batch.qpik_batch(self.robot_data_.model, p, _batch.as_device(q, dev), _batch.as_device(qdot, dev),
+                                 _batch.as_device(x_target, dev), _batch.as_device(xdot_target, dev),
+                                 _batch.as_device(x_init, dev), _batch.as_device(xdot_init, dev), iters=iters)
+
+    def QPIK_batch(self, q, qdot, xdot_target, link_name):
+        return self._run(_capi.MODE_QPIK, link_name, q, qdot, None, xdot_target)
+
+    def QPIK_step_batch(self, q, qdot, x_target, xdot_target, link_name, iters=None):
+        return self._run(_capi.MODE_QPIK_STEP, link_name, q, qdot, x_target, xdot_target, iters=iters)
+
+    def QPIK_cubic_batch(self, q, qdot, x_target, xdot_target, x_init, xdot_init, current_time, init_time,
+                         duration, link_name):
+        return self._run(_capi.MODE_QPIK_CUBIC, link_name, q, qdot, x_target, xdot_target, x_init, xdot_init,
+                         current_time, init_time, duration)
+
+    # -- single-instance entries (reference signatures; B = 1 launches) -------
+    def _one(self, out_status):
+        out, status = out_status
+        out, st = out.cpu().numpy()[:, 0], int(status.cpu().numpy()[0])
+        if st != _capi.STATUS_SOLVED:
+            print("QP IK failed to compute optimal joint velocity.", file=sys.stderr)
+            out = np.zeros(self.dof_)
+        return out
+
+    def _state(self):
+        rd = self.robot_data_
+        return rd.q_.reshape(-1, 1), rd.qdot_.reshape(-1, 1)
+
+    def QPIK(self, xdot_target, link_name):
+        q, qd = self._state()
+        return self._one(self.QPIK_batch(q, qd, np.asarray(xdot_target, float).reshape(6, 1), link_name))
+
+    def QPIKStep(self, x_target, xdot_target, link_name):
+        q, qd = self._state()
+        return self._one(self.QPIK_step_batch(q, qd, pose_to12(x_target).reshape(12, 1),
+                                              np.asarray(xdot_target, float).reshape(6, 1), link_name))
+
+    def QPIKCubic(self, x_target, xdot_target, x_init, xdot_init, current_time, init_time, duration, link_name):
+        q, qd = self._state()
+        return self._one(self.QPIK_cubic_batch(
+            q, qd, pose_to12(x_target).reshape(12, 1), np.asarray(xdot_target, float).reshape(6, 1),
+            pose_to12(x_init).reshape(12, 1), np.asarray(xdot_init, float).reshape(6, 1),
+            current_time, init_time, duration, link_name))
+
+    QPIK_step, QPIK_cubic = QPIKStep, QPIKCubic

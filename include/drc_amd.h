@@ -1,0 +1,190 @@
+/*
+ * drc_amd.h — C-ABI of the MI355X-native batched QP-IK solver.
+ *
+ * This is the drop-in boundary for the per-control-cycle hot path of
+ * YoungWook0533/dyros_robot_controller.  Plain C: opaque
+ * handles, plain pointers and sizes, integer return codes, no C++ types and
+ * no exceptions cross it.  Every entry point names the reference interface
+ * it replaces (file:line in the reference tree).
+ *
+ * Conventions
+ *  - Batched arrays are structure-of-arrays, field-major: element (f, b) of
+ *    a [F][B] array is at ptr[f * B + b].  All batched pointers are DEVICE
+ *    pointers owned by the caller (HBM resident); `stream` is a hipStream_t
+ *    (NULL = default stream).  Calls are asynchronous on that stream and
+ *    reentrant per stream.
+ *  - Poses are 12 doubles: R column-major (9) then p (3) — Eigen::Affine3d
+ *    `linear()` memory order followed by `translation()`.
+ *  - Velocities / twists are [v(3); w(3)] in the world frame
+ *    (Pinocchio LOCAL_WORLD_ALIGNED, robot_data.cpp:401).
+ */
+#ifndef DRC_AMD_H
+#define DRC_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- return codes ------------------------------------------------------ */
+enum {
+    DRC_OK = 0,
+    DRC_ERR_INVALID_ARGUMENT = 1,
+    DRC_ERR_FILE = 2,            /* URDF missing: reference std::exit()s (robot_data.cpp:17-18) */
+    DRC_ERR_PARSE = 3,
+    DRC_ERR_UNSUPPORTED = 4,     /* model outside the kernel's limits          */
+    DRC_ERR_UNKNOWN_LINK = 5,    /* reference: stderr + zero result (:395-399) */
+    DRC_ERR_HIP = 6,
+    DRC_ERR_SIZE_MISMATCH = 7    /* reference: std::runtime_error (robot_controller.cpp:23-26) */
+};
+
+/* ---- per-instance solve status (mirrors OSQP status values) ------------ */
+enum {
+    DRC_STATUS_SOLVED = 1,
+    DRC_STATUS_MAX_ITER = -2,
+    DRC_STATUS_PRIMAL_INFEASIBLE = -3,
+    DRC_STATUS_NONFINITE = -10
+};
+
+/* ---- controller entry points (robot_controller.h) ---------------------- */
+enum {
+    DRC_MODE_QPIK = 0,           /* QPIK(xdot_target)              manipulator/robot_controller.cpp:277 */
+    DRC_MODE_QPIK_STEP = 1,      /* QPIKStep(x_target, xdot_target)                                :292 */
+    DRC_MODE_QPIK_CUBIC = 2      /* QPIKCubic(x_t, xd_t, x_i, xd_i, t, t0, T)                     :303 */
+};
+
+/* ---- mobile base description (type_define.h:58-72 KinematicParam) ------ */
+enum { DRC_DRIVE_DIFFERENTIAL = 0, DRC_DRIVE_MECANUM = 1, DRC_DRIVE_CASTER = 2 };
+#define DRC_MAX_WHEELS 8
+typedef struct drc_kinematic_param {
+    int type;
+    double wheel_radius;
+    double max_lin_speed, max_ang_speed, max_lin_acc, max_ang_acc;
+    double base_width;                              /* differential */
+    int n_wheels;                                   /* mecanum / caster entries used */
+    double roller_angles[DRC_MAX_WHEELS];
+    double base2wheel_positions[DRC_MAX_WHEELS][2];
+    double base2wheel_angles[DRC_MAX_WHEELS];
+    double wheel_offset;                            /* caster */
+} drc_kinematic_param;
+
+/* type_define.h:151-156 / :167-171 */
+typedef struct drc_joint_index { int virtual_start, mani_start, mobi_start; } drc_joint_index;
+typedef struct drc_actuator_index { int mani_start, mobi_start; } drc_actuator_index;
+
+/* ---- QP solver settings: OSQP's ADMM (QP_base.h:143-165) --------------- */
+typedef struct drc_solver_settings {
+    double rho, sigma, alpha;          /* 0.1, 1e-6, 1.6                    */
+    double eps_abs, eps_rel;           /* 1e-3, 1e-3 (reference: defaults)  */
+    double eps_prim_inf;               /* 1e-4                              */
+    int max_iter;                      /* 4000                              */
+    int check_termination;             /* 25                                */
+    int scaling;                       /* 10 Ruiz iterations                */
+    int adaptive_rho;                  /* 1                                 */
+    int adaptive_rho_interval;         /* 25                                */
+    double adaptive_rho_tolerance;     /* 5                                 */
+    int polish;                        /* reference: 0                      */
+    int polish_refine_iter;            /* 3                                 */
+    double delta;                      /* 1e-6                              */
+    int exact;                         /* 1: certified polish + tight fallback (parity mode) */
+    double eps_exact;                  /* 1e-9 KKT acceptance of a polished point */
+    double eps_fallback;               /* 1e-7 ADMM-only termination when polish keeps failing */
+} drc_solver_settings;
+
+/* ---- QPIK parameters (controller gains + QP constants) ----------------- */
+typedef struct drc_qpik_params {
+    double kp[6], kv[6];               /* manipulator: 100 / 20 (robot_controller.cpp:12-13)
+                                          MoMa: 400 / 0 (mobile_manipulator/robot_controller.cpp:15) */
+    double feedforward;                /* MoMa QPIKStep adds xdot_target (:177): 1; manipulator 0 */
+    double alpha_cbf;                  /* 50      (QP_IK.cpp:101)           */
+    double w_reg;                      /* 1.0 / 0.01 (QP_IK.cpp:81, MoMa :71) */
+    double slack_w;                    /* 1000    (QP_IK.cpp:83-86)         */
+    double man_min;                    /* 0.01    (QP_IK.cpp:122)           */
+    double dist_min;                   /* 0.05    (QP_IK.cpp:130)           */
+    int mode;                          /* DRC_MODE_*                        */
+    int frame_id;                      /* from drc_model_find_frame         */
+    double t, t0, duration;            /* QPIKCubic timing                  */
+    drc_solver_settings solver;
+} drc_qpik_params;
+
+typedef struct drc_model drc_model;     /* opaque; owns its device copy */
+
+/* Manipulator::RobotData(urdf, srdf, packages)  manipulator/robot_data.h:49,
+ * robot_data.cpp:7-70 (model, collision pairs, limits).  `device` = HIP
+ * device ordinal that receives the model constants. */
+int drc_model_create_manipulator(const char* urdf_path, const char* srdf_path,
+                                 const char* packages_path, int device, drc_model** out);
+
+/* MobileManipulator::RobotData(param, joint_idx, actuator_idx, urdf, srdf, packages)
+ * mobile_manipulator/robot_data.h:55, robot_data.cpp:7-44. */
+int drc_model_create_mobile_manipulator(const drc_kinematic_param* param,
+                                        const drc_joint_index* joint_idx,
+                                        const drc_actuator_index* actuator_idx,
+                                        const char* urdf_path, const char* srdf_path,
+                                        const char* packages_path, int device, drc_model** out);
+
+void drc_model_destroy(drc_model* model);
+
+/* getDof / getActuatordDof / getManipulatorDof / getMobileDof
+ * (manipulator/robot_data.h, mobile_manipulator/robot_data.h) and the
+ * collision model size (geometries, active pairs). */
+int drc_model_info(const drc_model* model, int* dof, int* actuated_dof, int* mani_dof,
+                   int* mobi_dof, int* n_geoms, int* n_pairs);
+
+/* getJointPositionLimit / getJointVelocityLimit (robot_data.h) — host arrays [dof] */
+int drc_model_limits(const drc_model* model, double* q_lb, double* q_ub, double* qdot_lb,
+                     double* qdot_ub);
+
+/* pinocchio Model::getFrameId(link_name) as used by every getter
+ * (robot_data.cpp:380,394): DRC_ERR_UNKNOWN_LINK when absent. */
+int drc_model_find_frame(const drc_model* model, const char* link_name, int* frame_id);
+
+/* Mobile FK Jacobian J_mobile (3 x W, row-major) of the base
+ * (mobile/robot_data.cpp:123-176); host array. */
+int drc_model_mobile_fk_jacobian(const drc_model* model, double* J3xW);
+
+/* Reference defaults for the model kind (robot_controller ctor gains, QP
+ * constants, OSQP defaults).  exact=0: the reference's OSQP settings
+ * (eps 1e-3, no polish); exact=1: certified-optimal settings used for
+ * parity. */
+int drc_default_qpik_params(const drc_model* model, int exact, drc_qpik_params* params);
+
+/* Batched QPIK / QPIKStep / QPIKCubic.
+ *   Manipulator  (robot_controller.cpp:277-317): q, qdot [dof][B].
+ *   Mobile manip (mobile_manipulator/robot_controller.cpp:147-197): q, qdot
+ *       are the full joint vectors [dof][B] in JointIndex order
+ *       (getJointVector, mobile_manipulator/robot_data.cpp:418-427).
+ *   x_target [12][B] (modes STEP/CUBIC), xdot_target [6][B],
+ *   x_init [12][B] / xdot_init [6][B] (mode CUBIC only, else NULL).
+ *   qdot_out [na][B]: manipulator na = dof (QPIK returns qdot);
+ *       MoMa na = actuated dof in ActuatorIndex order (eta, split into
+ *       (qdot_mobile, qdot_arm) by ActuatorIndex, :161-164).
+ *   status [B] (DRC_STATUS_*), iters [B] (may be NULL).
+ * Non-solved instances get a zero output (QP_IK.cpp:56-61). */
+int drc_qpik_batch(const drc_model* model, const drc_qpik_params* params, int64_t B,
+                   const double* q, const double* qdot, const double* x_target,
+                   const double* xdot_target, const double* x_init, const double* xdot_init,
+                   double* qdot_out, int32_t* status, int32_t* iters, void* stream);
+
+/* Stage outputs of the same kernel for parity checks: per instance
+ *   pose [12][B]  (getPose with the pose at the current q — SURVEY Q1),
+ *   jac  [6*dof][B] row-major (getJacobian, LWA),
+ *   man  [1+mani][B] (manipulability, grad)  (getManipulability(true,false)),
+ *   dist [1+dof][B]  (distance, grad)        (getMinDistance(true,false,false)),
+ *   pair [B] (argmin collision pair), xdot_des [6][B] (the QP's task velocity).
+ * Any output pointer may be NULL. */
+int drc_qpik_stages_batch(const drc_model* model, const drc_qpik_params* params, int64_t B,
+                          const double* q, const double* qdot, const double* x_target,
+                          const double* xdot_target, const double* x_init,
+                          const double* xdot_init, double* pose, double* jac, double* man,
+                          double* dist, int32_t* pair, double* xdot_des, void* stream);
+
+const char* drc_error_string(int code);
+/* Thread-local detail of the last failing call (parse position, HIP error). */
+const char* drc_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DRC_AMD_H */

@@ -9,6 +9,7 @@
 #include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
+#include <stdio.h>
 
 #define INFTY 1e30               /* OSQP_INFTY                               */
 #define MIN_SCALING 1e-4
@@ -409,8 +410,8 @@ static int gjk(const Shape* A, const Shape* B, SV* S, int* ns, double* lam, doub
     return 0;
 }
 
-#define EPA_MAXV 160
-#define EPA_MAXF 320
+#define EPA_MAXV 320
+#define EPA_MAXF 640
 static double epa(const Shape* A, const Shape* B, SV* S, int ns, double* pA, double* pB) {
     static const double dirs[6][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}, {-1, 0, 0}, {0, -1, 0}, {0, 0, -1}};
     SV V[EPA_MAXV];
@@ -445,18 +446,27 @@ static double epa(const Shape* A, const Shape* B, SV* S, int ns, double* pA, dou
             sub3(V[F[f][2]].w, V[F[f][0]].w, e2);
             cross3(e1, e2, nn);
             double L = norm3(nn);
-            for (int c = 0; c < 3; ++c) fn[f][c] = nn[c] / L;
-            fdist[f] = dot3(fn[f], V[F[f][0]].w);
+            for (int c = 0; c < 3; ++c) fn[f][c] = L > 1e-300 ? nn[c] / L : 0.0;
+            fdist[f] = L > 1e-300 ? dot3(fn[f], V[F[f][0]].w) : INFINITY;
             if (fdist[f] < bd) { bd = fdist[f]; best = f; }
         }
         SV w;
         sup_md(A, B, fn[best], &w);
         if (dot3(fn[best], w.w) - fdist[best] <= 1e-12 || nvx >= EPA_MAXV) break;
+        /* a support point that is already a vertex cannot expand the polytope
+         * (flat caps / box faces): stop instead of adding degenerate faces */
+        int dupv = 0;
+        for (int i = 0; i < nvx; ++i) {
+            double d[3];
+            sub3(w.w, V[i].w, d);
+            if (fabs(d[0]) <= 1e-14 && fabs(d[1]) <= 1e-14 && fabs(d[2]) <= 1e-14) dupv = 1;
+        }
+        if (dupv) break;
         V[nvx] = w;
         int vi = nvx++;
         int E[EPA_MAXF][2], ne = 0, keep[EPA_MAXF][3], nk = 0;
         for (int f = 0; f < nf; ++f) {
-            if (dot3(fn[f], w.w) - fdist[f] > 0) {
+            if (dot3(fn[f], w.w) - fdist[f] > 1e-12) {
                 for (int e = 0; e < 3; ++e) {
                     int a = F[f][e], b = F[f][(e + 1) % 3], found = -1;
                     for (int x = 0; x < ne; ++x) if (E[x][0] == b && E[x][1] == a) { found = x; break; }
@@ -470,6 +480,7 @@ static double epa(const Shape* A, const Shape* B, SV* S, int ns, double* pA, dou
         for (int f = 0; f < nk; ++f) { F[nf][0] = keep[f][0]; F[nf][1] = keep[f][1]; F[nf][2] = keep[f][2]; ++nf; }
         for (int e = 0; e < ne; ++e) { F[nf][0] = E[e][0]; F[nf][1] = E[e][1]; F[nf][2] = vi; ++nf; }
     }
+    if (getenv("ORC_DEBUG")) fprintf(stderr, "epa exit nvx %d nf %d\n", nvx, nf);
     /* recompute the closest face of the final polytope */
     double bd = INFINITY;
     for (int f = 0; f < nf; ++f) {
@@ -478,8 +489,8 @@ static double epa(const Shape* A, const Shape* B, SV* S, int ns, double* pA, dou
         sub3(V[F[f][2]].w, V[F[f][0]].w, e2);
         cross3(e1, e2, nn);
         double L = norm3(nn);
-        for (int c = 0; c < 3; ++c) fn[f][c] = nn[c] / L;
-        fdist[f] = dot3(fn[f], V[F[f][0]].w);
+        for (int c = 0; c < 3; ++c) fn[f][c] = L > 1e-300 ? nn[c] / L : 0.0;
+        fdist[f] = L > 1e-300 ? dot3(fn[f], V[F[f][0]].w) : INFINITY;
         if (fdist[f] < bd) { bd = fdist[f]; best = f; }
     }
     const double *a = V[F[best][0]].w, *b = V[F[best][1]].w, *c = V[F[best][2]].w;
@@ -861,18 +872,17 @@ static void ldlt_solve(const double* L, const double* Dg, int N, double* b) {
     for (int i = N - 1; i >= 0; --i) { double t = b[i]; for (int k = i + 1; k < N; ++k) t -= L[k * N + i] * b[k]; b[i] = t; }
 }
 
-/* OSQP polish (polish.c) restated; on success writes x, z, y (scaled).
- * strict != 0 additionally certifies KKT and dual signs. */
-static int qp_polish(QPW* w, const OracleSettings* s, int strict) {
+/* Equality-constrained QP on the rows flagged active (flag -1: A_i x = l_i,
+ * +1: A_i x = u_i): OSQP polish's reduced KKT [P+dI, A_r^T; A_r, -dI] with
+ * iterative refinement against the unregularised system (polish.c). */
+static int qp_eqp(const QPW* w, const OracleSettings* s, const int* flag, double* xp, double* yp) {
     int n = w->n, m = w->m;
+    static __thread double K[(ORC_MAXX + ORC_MAXC) * (ORC_MAXX + ORC_MAXC)], K0[(ORC_MAXX + ORC_MAXC) * (ORC_MAXX + ORC_MAXC)];
     int act[ORC_MAXC], nact = 0;
     double b[ORC_MAXC];
-    for (int i = 0; i < m; ++i) {
-        if (w->z[i] - w->l[i] < -w->y[i]) { act[nact] = i; b[nact++] = w->l[i]; }
-        else if (w->u[i] - w->z[i] < w->y[i]) { act[nact] = i; b[nact++] = w->u[i]; }
-    }
+    for (int i = 0; i < m; ++i)
+        if (flag[i]) { act[nact] = i; b[nact++] = flag[i] < 0 ? w->l[i] : w->u[i]; }
     int N = n + nact;
-    static __thread double K[(ORC_MAXX + ORC_MAXC) * (ORC_MAXX + ORC_MAXC)], K0[(ORC_MAXX + ORC_MAXC) * (ORC_MAXX + ORC_MAXC)];
     double Dg[ORC_MAXX + ORC_MAXC], rhs[ORC_MAXX + ORC_MAXC], sol[ORC_MAXX + ORC_MAXC], r[ORC_MAXX + ORC_MAXC];
     for (int i = 0; i < N * N; ++i) K0[i] = 0;
     for (int i = 0; i < n; ++i) for (int j = 0; j < n; ++j) K0[i * N + j] = w->P[i * n + j];
@@ -891,40 +901,115 @@ static int qp_polish(QPW* w, const OracleSettings* s, int strict) {
         ldlt_solve(K, Dg, N, r);
         for (int i = 0; i < N; ++i) sol[i] += r[i];
     }
-    double xp[ORC_MAXX], yp[ORC_MAXC], zp[ORC_MAXC];
     for (int i = 0; i < n; ++i) xp[i] = sol[i];
     for (int i = 0; i < m; ++i) yp[i] = 0;
     for (int a = 0; a < nact; ++a) yp[act[a]] = sol[n + a];
-    for (int i = 0; i < m; ++i) {
-        double t = 0;
-        for (int j = 0; j < n; ++j) t += w->A[i * n + j] * xp[j];
-        zp[i] = t < w->l[i] ? w->l[i] : (t > w->u[i] ? w->u[i] : t);
-    }
-    double pr0 = w->pri_res, dr0 = w->dua_res;
-    static __thread QPW tmp;  /* residuals of the polished point */
-    memcpy(&tmp, w, sizeof(QPW));
-    qp_residuals(&tmp, xp, zp, yp, s->eps_exact, s->eps_exact);
-    int ok = (tmp.pri_res < pr0 && tmp.dua_res < dr0) || (tmp.pri_res < pr0 && dr0 < 1e-10) || (tmp.dua_res < dr0 && pr0 < 1e-10);
-    if (strict) {
-        /* certified optimum: KKT residuals at eps_exact and dual signs that
-         * match the guessed active bounds (y<=0 at l, y>=0 at u) */
-        ok = tmp.pri_res <= tmp.eps_pri && tmp.dua_res <= tmp.eps_dua;
-        for (int a = 0; a < nact && ok; ++a) {
-            int i = act[a];
-            if (w->l[i] == w->u[i]) continue;
-            double yi = w->E[i] * yp[i] / w->c;
-            int lower = b[a] == w->l[i];
-            if (lower && yi > tmp.eps_dua) ok = 0;
-            if (!lower && yi < -tmp.eps_dua) ok = 0;
+    return 1;
+}
+
+/* OSQP polish (polish.c) restated; on success writes x, z, y (scaled).
+ * strict == 0: OSQP's single attempt with its acceptance rule.
+ * strict != 0 (parity mode): the polished point must be KKT-certified
+ * (residuals at eps_exact, dual signs matching the active bounds).  When the
+ * ADMM active-set guess is wrong, continue with a primal active-set method
+ * (Nocedal & Wright Alg. 16.3) from the first feasible polished point:
+ * drop the worst wrong-sign multiplier, step to the equality-QP minimiser
+ * with a ratio test, add the blocking row.  Exact on termination. */
+#define POLISH_FEAS_ATTEMPTS 4
+#define POLISH_AS_ITERS 24
+static int qp_polish(QPW* w, const OracleSettings* s, int strict) {
+    int n = w->n, m = w->m;
+    int flag[ORC_MAXC];  /* -1 lower-active, +1 upper-active, 0 inactive */
+    for (int i = 0; i < m; ++i)
+        flag[i] = (w->z[i] - w->l[i] < -w->y[i]) ? -1 : ((w->u[i] - w->z[i] < w->y[i]) ? 1 : 0);
+    const double pr0 = w->pri_res, dr0 = w->dua_res;
+    static __thread QPW tmp;
+    double xp[ORC_MAXX], yp[ORC_MAXC], zp[ORC_MAXC], ax[ORC_MAXC], xc[ORC_MAXX];
+    int have_feasible = 0;
+    for (int it = 0; it < (strict ? POLISH_FEAS_ATTEMPTS + POLISH_AS_ITERS : 1); ++it) {
+        if (!qp_eqp(w, s, flag, xp, yp)) return 0;
+        double stepmax = 0, xnorm = 0;
+        if (have_feasible) {
+            for (int j = 0; j < n; ++j) { stepmax = fmax(stepmax, fabs(xp[j] - xc[j])); xnorm = fmax(xnorm, fabs(xc[j])); }
+        }
+        if (have_feasible && stepmax > 1e-12 * (1 + xnorm)) {
+            /* ratio test along p = xp - xc over the inactive rows */
+            double amin = 1.0;
+            int blk = -1, side = 0;
+            for (int i = 0; i < m; ++i) {
+                if (flag[i]) continue;
+                double axc = 0, ap = 0;
+                for (int j = 0; j < n; ++j) { axc += w->A[i * n + j] * xc[j]; ap += w->A[i * n + j] * (xp[j] - xc[j]); }
+                double a = 2.0;
+                int sd = 0;
+                if (ap < 0 && w->l[i] > -INFTY * MIN_SCALING) { a = (w->l[i] - axc) / ap; sd = -1; }
+                else if (ap > 0 && w->u[i] < INFTY * MIN_SCALING) { a = (w->u[i] - axc) / ap; sd = 1; }
+                if (a < amin) { amin = a; blk = i; side = sd; }
+            }
+            double alpha = amin < 0 ? 0 : amin;
+            for (int j = 0; j < n; ++j) xc[j] += alpha * (xp[j] - xc[j]);
+            if (blk >= 0) { flag[blk] = side; continue; }
+            /* full step: xc is the EQP minimiser, fall through to the checks */
+        }
+        for (int i = 0; i < m; ++i) {
+            double t = 0;
+            for (int j = 0; j < n; ++j) t += w->A[i * n + j] * xp[j];
+            ax[i] = t;
+            zp[i] = t < w->l[i] ? w->l[i] : (t > w->u[i] ? w->u[i] : t);
+        }
+        memcpy(&tmp, w, sizeof(QPW));
+        qp_residuals(&tmp, xp, zp, yp, s->eps_exact, s->eps_exact);
+        int ok = (tmp.pri_res < pr0 && tmp.dua_res < dr0) || (tmp.pri_res < pr0 && dr0 < 1e-10) || (tmp.dua_res < dr0 && pr0 < 1e-10);
+        int worst = -1;
+        double wv = 0;
+        if (strict) {
+            int feasible = tmp.pri_res <= tmp.eps_pri;
+            ok = feasible && tmp.dua_res <= tmp.eps_dua;
+            for (int i = 0; i < m; ++i) {
+                if (!flag[i] || w->l[i] == w->u[i]) continue;
+                double yi = w->E[i] * yp[i] / w->c;
+                double viol = flag[i] < 0 ? yi - tmp.eps_dua : -yi - tmp.eps_dua;
+                if (viol > wv) { wv = viol; worst = i; }
+            }
+            if (worst >= 0) ok = 0;
+            if (getenv("ORC_DEBUG"))
+                fprintf(stderr, "polish it %d feas %d pri %.2e dua %.2e worst %d (%.2e) havefeas %d\n", it, feasible,
+                        tmp.pri_res, tmp.dua_res, worst, wv, have_feasible);
+            if (!ok && feasible && !have_feasible) { memcpy(xc, xp, n * sizeof(double)); have_feasible = 1; }
+        }
+        if (ok) {
+            memcpy(w->x, xp, n * sizeof(double));
+            memcpy(w->y, yp, m * sizeof(double));
+            memcpy(w->z, zp, m * sizeof(double));
+            w->pri_res = tmp.pri_res;
+            w->dua_res = tmp.dua_res;
+            return 1;
+        }
+        if (!strict) return 0;
+        if (have_feasible) {
+            if (worst < 0) return 0;   /* KKT residual failure, not an active-set issue */
+            flag[worst] = 0;
+            memcpy(xc, xp, n * sizeof(double));
+        } else {
+            if (it >= POLISH_FEAS_ATTEMPTS - 1) return 0;
+            /* not yet feasible: add the most violated inactive row */
+            int add = -1, af = 0;
+            double av = 0;
+            for (int i = 0; i < m; ++i) {
+                if (flag[i]) continue;
+                double lo = (w->l[i] - ax[i]) / w->E[i] - tmp.eps_pri, hi = (ax[i] - w->u[i]) / w->E[i] - tmp.eps_pri;
+                if (lo > av) { av = lo; add = i; af = -1; }
+                if (hi > av) { av = hi; add = i; af = 1; }
+            }
+            if (add < 0) {
+                if (worst < 0) return 0;
+                flag[worst] = 0;
+            } else {
+                flag[add] = af;
+            }
         }
     }
-    if (!ok) return 0;
-    memcpy(w->x, xp, n * sizeof(double));
-    memcpy(w->y, yp, m * sizeof(double));
-    memcpy(w->z, zp, m * sizeof(double));
-    w->pri_res = tmp.pri_res;
-    w->dua_res = tmp.dua_res;
-    return 1;
+    return 0;
 }
 
 int oracle_solve_qp(int n, int m, const double* P, const double* qv, const double* A,
@@ -977,7 +1062,13 @@ int oracle_solve_qp(int n, int m, const double* P, const double* qv, const doubl
         int adapt = s->adaptive_rho && s->adaptive_rho_interval > 0 && it % s->adaptive_rho_interval == 0;
         if (check || adapt) qp_residuals(&w, w.x, w.z, w.y, s->eps_abs, s->eps_rel);
         if (check) {
-            if (w.pri_res < w.eps_pri && w.dua_res < w.eps_dua) {
+            int conv = w.pri_res < w.eps_pri && w.dua_res < w.eps_dua;
+            /* parity mode: a certified polish is exact whatever the ADMM
+             * residual, so also try it every 4th check (slow-ADMM vertices) */
+            if (s->exact && !conv && it % (4 * s->check_termination) == 0 && qp_polish(&w, s, 1)) {
+                status = ORC_SOLVED; pol = 1; break;
+            }
+            if (conv) {
                 if (!s->exact) { status = ORC_SOLVED; break; }
                 if (qp_polish(&w, s, 1)) { status = ORC_SOLVED; pol = 1; break; }
                 /* tight ADMM-only fallback */

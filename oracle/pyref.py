@@ -664,6 +664,8 @@ def epa_penetration(gA, TA, gB, TB, tol=1e-12, max_iter=256):
         a, b, c = P[f[0]], P[f[1]], P[f[2]]
         nrm = np.cross(b - a, c - a)
         L = np.linalg.norm(nrm)
+        if L <= 1e-300:
+            return np.zeros(3), np.inf
         nrm = nrm / L
         return nrm, nrm @ a
 
@@ -674,12 +676,14 @@ def epa_penetration(gA, TA, gB, TB, tol=1e-12, max_iter=256):
         w = _support_md(gA, TA, gB, TB, nrm)
         if nrm @ w[0] - dist <= tol:
             break
+        if any(np.max(np.abs(w[0] - x)) <= 1e-14 for x in P):
+            break   # support point already a vertex: cannot expand (flat features)
         V.append(w); P.append(w[0])
         vi = len(P) - 1
         edges = []
         keep = []
         for f, (fn, fdist) in zip(faces, fd):
-            if fn @ w[0] - fdist > 0:
+            if fn @ w[0] - fdist > 1e-12:
                 for e in ((f[0], f[1]), (f[1], f[2]), (f[2], f[0])):
                     r = (e[1], e[0])
                     if r in edges:

@@ -1,0 +1,43 @@
+"""Shared helpers for the parity tests (test infrastructure)."""
+import numpy as np
+
+import oracle as O
+from dyros_robot_controller_amd import manipulator, robot_path, workload, _batch, _capi
+
+LINK = {"fr3": "fr3_link8", "ur5e": "tool0", "husky_fr3": "fr3_link8", "xls_fr3": "fr3_link8"}
+
+
+def make_manipulator(robot, device):
+    rd = manipulator.RobotData(robot_path(robot), robot_path(robot, "srdf"), device=device)
+    return rd
+
+
+def stage_pose(model, device, q, qd, link):
+    pb = manipulator.QPIKParamsBuilder(model, exact=True)
+    p = pb.params(link, _capi.MODE_QPIK)
+    B = q.shape[1]
+    st = _batch.stages_batch(model, p, _batch.as_device(q, device), _batch.as_device(qd, device), None,
+                             _batch.as_device(np.zeros((6, B)), device))
+    return {k: v.cpu().numpy() for k, v in st.items()}
+
+
+def step_inputs(rd, robot, seed, B, device, offset=0):
+    lo, hi = rd.getJointPositionLimit()
+    _, vmax = rd.getJointVelocityLimit()
+    q, qd = workload.joint_states(lo, hi, vmax, seed, B, offset)
+    st = stage_pose(rd.model, device, q, qd, LINK[robot])
+    xt, xdt = workload.perturb_targets(st["pose"], seed, B, offset)
+    return q, qd, xt, xdt
+
+
+def oracle_batch(robot, q, qd, xt, xdt, exact=True, xi=None, xdi=None, mode=1, t=0.0, t0=0.0, T=1.0, nthreads=8):
+    pm, om, spec = O.load(robot)
+    par = O.default_params(spec["kind"], exact=exact)
+    par.mode = mode
+    par.t, par.t0, par.duration = t, t0, T
+    out, status, iters = O.qpik_batch(om, par, q, qd, xt, xdt, xi, xdi, nthreads=nthreads)
+    return out, status, iters, om
+
+
+def task_residual(J, dq):
+    return np.max(np.abs(J @ dq))
