@@ -276,150 +276,195 @@ DRC_HD __noinline__ GjkOut gjk(const Shape A, const Shape B, EpaWs* ws) {
   return o;
 }
 
-// Expanding polytope (EPA) for penetrating cores, lane-serial, polytope in
-// a per-wave global workspace (rare path: ~1-3% of random FR3 postures).
-constexpr int kEpaMaxV = 320, kEpaMaxF = 640;
+// Expanding polytope (EPA) with face adjacency (Bullet/libccd style): the
+// visible region is flood-filled from the closest face across shared edges
+// (explicit DFS stack, same visiting order as the recursive oracle), so the
+// horizon is a single loop and the polytope stays a closed 2-manifold even
+// when flat features (cylinder caps, box faces) make the support mapping
+// degenerate.  Lane-serial, polytope in a per-wave global workspace (rare
+// path: penetrating candidate pairs only).
+constexpr int kEpaMaxV = 256, kEpaMaxF = 512;
 struct EpaWs {
   SV V[kEpaMaxV];
-  int F[kEpaMaxF][3];
-  int K[kEpaMaxF][3];
-  int E[kEpaMaxF][2];
-  double fn[kEpaMaxF][4];
+  int fv[kEpaMaxF][3], ff[kEpaMaxF][3], fe[kEpaMaxF][3];
+  int fpass[kEpaMaxF], alive[kEpaMaxF];
+  int stk_f[kEpaMaxF], stk_e[kEpaMaxF], stk_s[kEpaMaxF];
+  double fn[kEpaMaxF][3], fd[kEpaMaxF];
   double out[6];
+  int nv, nf, pass, hcf, hff, hnf, fail;
 };
 DRC_HD __forceinline__ void epa_seed(EpaWs* ws, int i, V3 w, V3 a) {
   ws->V[i].w = w;
   ws->V[i].a = a;
   ws->V[i].b = a - w;
 }
-// The GJK simplex arrives in ws->V[0..ns) (copied by the caller) so no
-// private array crosses the call; witness points come back in ws->out.
-DRC_HD __noinline__ double epa(const Shape A, const Shape B, int ns, EpaWs* ws) {
-  SV* V = ws->V;
-  int nvx = ns, nf = 0;
-  for (int di = 0; di < 6 && nvx < 4; ++di) {
+DRC_HD __forceinline__ int epa_newface(EpaWs* E, int a, int b, int c) {
+  if (E->nf >= kEpaMaxF) {
+    E->fail = 1;
+    return -1;
+  }
+  const int f = E->nf++;
+  E->fv[f][0] = a;
+  E->fv[f][1] = b;
+  E->fv[f][2] = c;
+  E->alive[f] = 1;
+  E->fpass[f] = 0;
+  V3 nn = cross(E->V[b].w - E->V[a].w, E->V[c].w - E->V[a].w);
+  const double L = sqrt(dot(nn, nn));
+  if (!(L > 1e-300)) {
+    E->fail = 1;
+    E->alive[f] = 0;
+    return -1;
+  }
+  nn = (1.0 / L) * nn;
+  E->fn[f][0] = nn.x;
+  E->fn[f][1] = nn.y;
+  E->fn[f][2] = nn.z;
+  E->fd[f] = dot(nn, E->V[a].w);
+  return f;
+}
+DRC_HD __forceinline__ void epa_bind(EpaWs* E, int f0, int e0, int f1, int e1) {
+  E->ff[f0][e0] = f1;
+  E->fe[f0][e0] = e1;
+  E->ff[f1][e1] = f0;
+  E->fe[f1][e1] = e0;
+}
+// iterative form of btGjkEpa2::expand over the three edges of `best`
+DRC_HD __forceinline__ bool epa_expand_all(EpaWs* E, int w, int best) {
+  const V3 ww = E->V[w].w;
+  for (int j = 0; j < 3; ++j) {
+    int sp = 0;
+    E->stk_f[0] = E->ff[best][j];
+    E->stk_e[0] = E->fe[best][j];
+    E->stk_s[0] = 0;
+    sp = 1;
+    while (sp > 0) {
+      const int f = E->stk_f[sp - 1], e = E->stk_e[sp - 1], st = E->stk_s[sp - 1];
+      if (st == 0) {
+        if (E->fpass[f] == E->pass) {
+          --sp;
+          continue;
+        }
+        const int e1 = e == 2 ? 0 : e + 1;
+        const V3 n = v3(E->fn[f][0], E->fn[f][1], E->fn[f][2]);
+        if (dot(n, ww) - E->fd[f] < -1e-12) {
+          const int nf = epa_newface(E, E->fv[f][e1], E->fv[f][e], w);
+          if (nf < 0) return false;
+          epa_bind(E, nf, 0, f, e);
+          if (E->hcf >= 0) epa_bind(E, E->hcf, 1, nf, 2);
+          else E->hff = nf;
+          E->hcf = nf;
+          ++E->hnf;
+          --sp;
+          continue;
+        }
+        E->fpass[f] = E->pass;
+        E->stk_s[sp - 1] = 1;
+        if (sp >= kEpaMaxF) return false;
+        E->stk_f[sp] = E->ff[f][e1];
+        E->stk_e[sp] = E->fe[f][e1];
+        E->stk_s[sp] = 0;
+        ++sp;
+      } else if (st == 1) {
+        const int e2 = e == 0 ? 2 : e - 1;
+        E->stk_s[sp - 1] = 2;
+        if (sp >= kEpaMaxF) return false;
+        E->stk_f[sp] = E->ff[f][e2];
+        E->stk_e[sp] = E->fe[f][e2];
+        E->stk_s[sp] = 0;
+        ++sp;
+      } else {
+        E->alive[f] = 0;
+        --sp;
+      }
+    }
+  }
+  return true;
+}
+
+// The GJK simplex arrives in ws->V[0..ns) (epa_seed) so no private array
+// crosses the call; witness points come back in ws->out.
+DRC_HD __noinline__ double epa(const Shape A, const Shape B, int ns, EpaWs* E) {
+  E->nv = ns;
+  E->nf = 0;
+  E->pass = 0;
+  E->fail = 0;
+  for (int di = 0; di < 6 && E->nv < 4; ++di) {
     const double sgn = di < 3 ? 1.0 : -1.0;
     const int ax = di % 3;
     SV w = sup_md(A, B, v3(ax == 0 ? sgn : 0.0, ax == 1 ? sgn : 0.0, ax == 2 ? sgn : 0.0));
     bool ok = true;
-    for (int i = 0; i < nvx; ++i) {
-      V3 d = w.w - V[i].w;
+    for (int i = 0; i < E->nv; ++i) {
+      V3 d = w.w - E->V[i].w;
       ok &= sqrt(dot(d, d)) > 1e-12;
     }
-    if (ok) V[nvx++] = w;
+    if (ok) E->V[E->nv++] = w;
   }
-  for (int t = 0; t < 4; ++t) {
-    // faces (0,1,2|3) (0,3,1|2) (0,2,3|1) (1,3,2|0), oriented away from the opposite vertex
-    const int f0 = t == 3 ? 1 : 0, f1 = t == 0 ? 1 : (t == 1 ? 3 : (t == 2 ? 2 : 3)),
-              f2 = t == 0 ? 2 : (t == 1 ? 1 : (t == 2 ? 3 : 2)), fo = 3 - t;
-    V3 nn = cross(V[f1].w - V[f0].w, V[f2].w - V[f0].w);
-    V3 o = V[fo].w - V[f0].w;
-    ws->F[nf][0] = f0;
-    if (dot(nn, o) <= 0) {
-      ws->F[nf][1] = f1;
-      ws->F[nf][2] = f2;
-    } else {
-      ws->F[nf][1] = f2;
-      ws->F[nf][2] = f1;
+  {  // orient the tetrahedron so that face (0,1,2) looks away from vertex 3
+    V3 nn = cross(E->V[1].w - E->V[0].w, E->V[2].w - E->V[0].w);
+    if (dot(nn, E->V[3].w - E->V[0].w) > 0) {
+      SV t = E->V[0];
+      E->V[0] = E->V[1];
+      E->V[1] = t;
     }
-    ++nf;
   }
-  int best = 0;
-  for (int it = 0; it < 256; ++it) {
-    best = -1;
-    double bd = 1e300;
-    for (int f = 0; f < nf; ++f) {
-      V3 nn = cross(V[ws->F[f][1]].w - V[ws->F[f][0]].w, V[ws->F[f][2]].w - V[ws->F[f][0]].w);
-      double L = sqrt(dot(nn, nn));
-      nn = L > 1e-300 ? (1.0 / L) * nn : v3(0, 0, 0);
-      double dd = L > 1e-300 ? dot(nn, V[ws->F[f][0]].w) : 1e300;
-      ws->fn[f][0] = nn.x;
-      ws->fn[f][1] = nn.y;
-      ws->fn[f][2] = nn.z;
-      ws->fn[f][3] = dd;
-      if (dd < bd) {
-        bd = dd;
-        best = f;
-      }
-    }
-    V3 bn = v3(ws->fn[best][0], ws->fn[best][1], ws->fn[best][2]);
-    SV w = sup_md(A, B, bn);
-    if (dot(bn, w.w) - ws->fn[best][3] <= 1e-12 || nvx >= kEpaMaxV) break;
-    // a support point that is already a vertex cannot expand the polytope
-    // (flat caps / box faces): stop instead of adding degenerate faces
-    bool dupv = false;
-    for (int i = 0; i < nvx; ++i) {
-      V3 d = w.w - V[i].w;
-      dupv |= fabs(d.x) <= 1e-14 && fabs(d.y) <= 1e-14 && fabs(d.z) <= 1e-14;
-    }
-    if (dupv) break;
-    V[nvx] = w;
-    int vi = nvx++;
-    int ne = 0, nk = 0;
-    for (int f = 0; f < nf; ++f) {
-      V3 fnn = v3(ws->fn[f][0], ws->fn[f][1], ws->fn[f][2]);
-      if (dot(fnn, w.w) - ws->fn[f][3] > 1e-12) {
-        for (int e = 0; e < 3; ++e) {
-          int a = ws->F[f][e], b = ws->F[f][(e + 1) % 3], found = -1;
-          for (int x = 0; x < ne; ++x)
-            if (ws->E[x][0] == b && ws->E[x][1] == a) {
-              found = x;
-              break;
-            }
-          if (found >= 0) {
-            for (int x = found; x < ne - 1; ++x) {
-              ws->E[x][0] = ws->E[x + 1][0];
-              ws->E[x][1] = ws->E[x + 1][1];
-            }
-            --ne;
-          } else {
-            ws->E[ne][0] = a;
-            ws->E[ne][1] = b;
-            ++ne;
-          }
+  const int t0 = epa_newface(E, 0, 1, 2), t1 = epa_newface(E, 1, 0, 3), t2 = epa_newface(E, 2, 1, 3),
+            t3 = epa_newface(E, 0, 2, 3);
+  if (!E->fail) {
+    epa_bind(E, t0, 0, t1, 0);
+    epa_bind(E, t0, 1, t2, 0);
+    epa_bind(E, t0, 2, t3, 0);
+    epa_bind(E, t1, 1, t3, 2);
+    epa_bind(E, t1, 2, t2, 1);
+    epa_bind(E, t2, 2, t3, 1);
+    for (int it = 0; it < 255; ++it) {
+      int best = -1;
+      double bd = 1e300;
+      for (int f = 0; f < E->nf; ++f)
+        if (E->alive[f] && E->fd[f] < bd) {
+          bd = E->fd[f];
+          best = f;
         }
-      } else {
-        ws->K[nk][0] = ws->F[f][0];
-        ws->K[nk][1] = ws->F[f][1];
-        ws->K[nk][2] = ws->F[f][2];
-        ++nk;
+      const V3 bn = v3(E->fn[best][0], E->fn[best][1], E->fn[best][2]);
+      SV w = sup_md(A, B, bn);
+      if (dot(bn, w.w) - E->fd[best] <= 1e-12 || E->nv >= kEpaMaxV) break;
+      bool dupv = false;
+      for (int i = 0; i < E->nv; ++i) {
+        V3 d = w.w - E->V[i].w;
+        dupv |= fabs(d.x) <= 1e-14 && fabs(d.y) <= 1e-14 && fabs(d.z) <= 1e-14;
       }
-    }
-    if (nk + ne > kEpaMaxF) break;
-    nf = 0;
-    for (int f = 0; f < nk; ++f) {
-      ws->F[nf][0] = ws->K[f][0];
-      ws->F[nf][1] = ws->K[f][1];
-      ws->F[nf][2] = ws->K[f][2];
-      ++nf;
-    }
-    for (int e = 0; e < ne; ++e) {
-      ws->F[nf][0] = ws->E[e][0];
-      ws->F[nf][1] = ws->E[e][1];
-      ws->F[nf][2] = vi;
-      ++nf;
+      if (dupv) break;
+      const int wi = E->nv;
+      E->V[E->nv++] = w;
+      E->pass++;
+      E->hcf = -1;
+      E->hff = -1;
+      E->hnf = 0;
+      E->fpass[best] = E->pass;
+      const bool valid = epa_expand_all(E, wi, best);
+      if (!valid || E->hnf < 3 || E->fail) {
+        E->nv--;
+        break;
+      }
+      epa_bind(E, E->hcf, 1, E->hff, 2);
+      E->alive[best] = 0;
     }
   }
   double bd = 1e300;
-  V3 bn = v3(0, 0, 1);
-  for (int f = 0; f < nf; ++f) {
-    V3 nn = cross(V[ws->F[f][1]].w - V[ws->F[f][0]].w, V[ws->F[f][2]].w - V[ws->F[f][0]].w);
-    double L = sqrt(dot(nn, nn));
-    nn = L > 1e-300 ? (1.0 / L) * nn : v3(0, 0, 0);
-    double dd = L > 1e-300 ? dot(nn, V[ws->F[f][0]].w) : 1e300;
-    if (dd < bd) {
-      bd = dd;
+  int best = 0;
+  for (int f = 0; f < E->nf; ++f)
+    if (E->alive[f] && E->fd[f] < bd) {
+      bd = E->fd[f];
       best = f;
-      bn = nn;
     }
-  }
-  const SV &a = V[ws->F[best][0]], &b = V[ws->F[best][1]], &c = V[ws->F[best][2]];
+  const V3 bn = v3(E->fn[best][0], E->fn[best][1], E->fn[best][2]);
+  const SV &a = E->V[E->fv[best][0]], &b = E->V[E->fv[best][1]], &c = E->V[E->fv[best][2]];
   V3 p = bd * bn, v0 = b.w - a.w, v1 = c.w - a.w, v2 = p - a.w;
   double d00 = dot(v0, v0), d01 = dot(v0, v1), d11 = dot(v1, v1), d20 = dot(v2, v0), d21 = dot(v2, v1);
   double den = d00 * d11 - d01 * d01;
   double l1 = (d11 * d20 - d01 * d21) / den, l2 = (d00 * d21 - d01 * d20) / den, l0 = 1 - l1 - l2;
-  st3(ws->out, l0 * a.a + l1 * b.a + l2 * c.a);
-  st3(ws->out + 3, l0 * a.b + l1 * b.b + l2 * c.b);
+  st3(E->out, l0 * a.a + l1 * b.a + l2 * c.a);
+  st3(E->out + 3, l0 * a.b + l1 * b.b + l2 * c.b);
   return -bd;
 }
 

@@ -1680,18 +1680,21 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
     if (rc) return rc;
   }
   HIP_TRY(hipSetDevice(m->device));
+  // grid-stride launches; the task kernel's grid is capped so its per-wave
+  // EPA workspaces (~60 KB each) stay modest
   const int64_t grid = B < 8192 ? B : 8192;
+  const int64_t grid_task = B < 4096 ? B : 4096;
   const int nv = m->hm.dev.nv, narm = kt.narm;
   // task data: ~ (6 nv + narm + nv + 9) doubles per instance, model-owned pool
   const int64_t per = 6 * nv + (1 + narm) + (1 + nv) + 6 + 1;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   {
     std::lock_guard<std::mutex> g(m->mu);
-    if (m->epa_count < grid) {
+    if (m->epa_count < grid_task) {
       if (m->epa_ws) HIP_TRY(hipFree(m->epa_ws));
       m->epa_ws = nullptr;
-      HIP_TRY(hipMalloc(&m->epa_ws, sizeof(EpaWs) * grid));
-      m->epa_count = grid;
+      HIP_TRY(hipMalloc(&m->epa_ws, sizeof(EpaWs) * grid_task));
+      m->epa_count = grid_task;
     }
     const bool need_pool = !jac || !man || !dist || !xdd || !pair;
     if (need_pool && m->pool_bytes < per * B * 8) {
@@ -1708,7 +1711,7 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
     if (!pair) pair = reinterpret_cast<int32_t*>(pool + (6 * nv + 8 + narm + nv) * B);
   }
   IO io{B, q, qdot, xt, xdt, xi, xdi, out, status, iters, pose, jac, man, dist, xdd, pair, m->epa_ws};
-  hipLaunchKernelGGL(task_kernel, dim3(static_cast<unsigned>(grid)), dim3(64),
+  hipLaunchKernelGGL(task_kernel, dim3(static_cast<unsigned>(grid_task)), dim3(64),
                      static_cast<size_t>(kt.lds_doubles) * sizeof(double), st, m->d_model, kt, io);
   HIP_TRY(hipGetLastError());
   if (!stages) {

@@ -410,99 +410,132 @@ static int gjk(const Shape* A, const Shape* B, SV* S, int* ns, double* lam, doub
     return 0;
 }
 
-#define EPA_MAXV 320
-#define EPA_MAXF 640
+#define EPA_MAXV 256
+#define EPA_MAXF 512
+/* Expanding polytope with face adjacency (Bullet/libccd style): the visible
+ * region is flood-filled from the closest face across shared edges, so the
+ * horizon is always a single loop and the polytope stays a valid closed
+ * 2-manifold even when flat features (cylinder caps, box faces) make the
+ * support mapping degenerate.  Same decisions as the device version. */
+typedef struct Epa {
+    SV V[EPA_MAXV];
+    int nv, nf, pass;
+    int fv[EPA_MAXF][3], ff[EPA_MAXF][3], fe[EPA_MAXF][3], fpass[EPA_MAXF], alive[EPA_MAXF];
+    double fn[EPA_MAXF][3], fd[EPA_MAXF];
+    int hcf, hff, hnf, fail;
+} Epa;
+
+static int epa_newface(Epa* E, int a, int b, int c) {
+    if (E->nf >= EPA_MAXF) { E->fail = 1; return -1; }
+    int f = E->nf++;
+    E->fv[f][0] = a; E->fv[f][1] = b; E->fv[f][2] = c;
+    E->alive[f] = 1; E->fpass[f] = 0;
+    double e1[3], e2[3], nn[3];
+    sub3(E->V[b].w, E->V[a].w, e1);
+    sub3(E->V[c].w, E->V[a].w, e2);
+    cross3(e1, e2, nn);
+    double L = norm3(nn);
+    if (!(L > 1e-300)) { E->fail = 1; E->alive[f] = 0; return -1; }
+    for (int k = 0; k < 3; ++k) E->fn[f][k] = nn[k] / L;
+    E->fd[f] = dot3(E->fn[f], E->V[a].w);
+    return f;
+}
+static void epa_bind(Epa* E, int f0, int e0, int f1, int e1) {
+    E->ff[f0][e0] = f1; E->fe[f0][e0] = e1;
+    E->ff[f1][e1] = f0; E->fe[f1][e1] = e0;
+}
+/* recursive horizon walk (btGjkEpa2::expand) */
+static int epa_expand(Epa* E, int w, int f, int e) {
+    static const int i1m3[3] = {1, 2, 0}, i2m3[3] = {2, 0, 1};
+    if (E->fpass[f] == E->pass) return 1;
+    const int e1 = i1m3[e];
+    if (dot3(E->fn[f], E->V[w].w) - E->fd[f] < -1e-12) {
+        int nf = epa_newface(E, E->fv[f][e1], E->fv[f][e], w);
+        if (nf < 0) return 0;
+        epa_bind(E, nf, 0, f, e);
+        if (E->hcf >= 0) epa_bind(E, E->hcf, 1, nf, 2); else E->hff = nf;
+        E->hcf = nf;
+        ++E->hnf;
+        return 1;
+    }
+    const int e2 = i2m3[e];
+    E->fpass[f] = E->pass;
+    if (epa_expand(E, w, E->ff[f][e1], E->fe[f][e1]) && epa_expand(E, w, E->ff[f][e2], E->fe[f][e2])) {
+        E->alive[f] = 0;
+        return 1;
+    }
+    return 0;
+}
+
 static double epa(const Shape* A, const Shape* B, SV* S, int ns, double* pA, double* pB) {
     static const double dirs[6][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}, {-1, 0, 0}, {0, -1, 0}, {0, 0, -1}};
-    SV V[EPA_MAXV];
-    int F[EPA_MAXF][3], nf = 0, nvx = ns;
-    for (int i = 0; i < ns; ++i) V[i] = S[i];
-    for (int di = 0; di < 6 && nvx < 4; ++di) {
+    static __thread Epa E;
+    E.nv = ns; E.nf = 0; E.pass = 0; E.fail = 0;
+    for (int i = 0; i < ns; ++i) E.V[i] = S[i];
+    for (int di = 0; di < 6 && E.nv < 4; ++di) {
         SV w;
         sup_md(A, B, dirs[di], &w);
         int ok = 1;
-        for (int i = 0; i < nvx; ++i) { double d[3]; sub3(w.w, V[i].w, d); if (norm3(d) <= 1e-12) ok = 0; }
-        if (ok) V[nvx++] = w;
+        for (int i = 0; i < E.nv; ++i) { double d[3]; sub3(w.w, E.V[i].w, d); if (norm3(d) <= 1e-12) ok = 0; }
+        if (ok) E.V[E.nv++] = w;
     }
-    static const int tf[4][4] = {{0, 1, 2, 3}, {0, 3, 1, 2}, {0, 2, 3, 1}, {1, 3, 2, 0}};
-    for (int t = 0; t < 4; ++t) {
+    /* orient the tetrahedron so that face (0,1,2) looks away from vertex 3 */
+    {
         double e1[3], e2[3], nn[3], o[3];
-        sub3(V[tf[t][1]].w, V[tf[t][0]].w, e1);
-        sub3(V[tf[t][2]].w, V[tf[t][0]].w, e2);
+        sub3(E.V[1].w, E.V[0].w, e1);
+        sub3(E.V[2].w, E.V[0].w, e2);
         cross3(e1, e2, nn);
-        sub3(V[tf[t][3]].w, V[tf[t][0]].w, o);
-        if (dot3(nn, o) <= 0) { F[nf][0] = tf[t][0]; F[nf][1] = tf[t][1]; F[nf][2] = tf[t][2]; }
-        else { F[nf][0] = tf[t][0]; F[nf][1] = tf[t][2]; F[nf][2] = tf[t][1]; }
-        ++nf;
+        sub3(E.V[3].w, E.V[0].w, o);
+        if (dot3(nn, o) > 0) { SV t = E.V[0]; E.V[0] = E.V[1]; E.V[1] = t; }
     }
-    double fn[EPA_MAXF][3], fdist[EPA_MAXF];
+    int t0 = epa_newface(&E, 0, 1, 2), t1 = epa_newface(&E, 1, 0, 3), t2 = epa_newface(&E, 2, 1, 3),
+        t3 = epa_newface(&E, 0, 2, 3);
     int best = 0;
-    for (int it = 0; it < 256; ++it) {
-        best = -1;
-        double bd = INFINITY;
-        for (int f = 0; f < nf; ++f) {
-            double e1[3], e2[3], nn[3];
-            sub3(V[F[f][1]].w, V[F[f][0]].w, e1);
-            sub3(V[F[f][2]].w, V[F[f][0]].w, e2);
-            cross3(e1, e2, nn);
-            double L = norm3(nn);
-            for (int c = 0; c < 3; ++c) fn[f][c] = L > 1e-300 ? nn[c] / L : 0.0;
-            fdist[f] = L > 1e-300 ? dot3(fn[f], V[F[f][0]].w) : INFINITY;
-            if (fdist[f] < bd) { bd = fdist[f]; best = f; }
+    if (!E.fail) {
+        epa_bind(&E, t0, 0, t1, 0); epa_bind(&E, t0, 1, t2, 0); epa_bind(&E, t0, 2, t3, 0);
+        epa_bind(&E, t1, 1, t3, 2); epa_bind(&E, t1, 2, t2, 1); epa_bind(&E, t2, 2, t3, 1);
+        for (int it = 0; it < 255; ++it) {
+            best = -1;
+            double bd = INFINITY;
+            for (int f = 0; f < E.nf; ++f)
+                if (E.alive[f] && E.fd[f] < bd) { bd = E.fd[f]; best = f; }
+            SV w;
+            sup_md(A, B, E.fn[best], &w);
+            if (dot3(E.fn[best], w.w) - E.fd[best] <= 1e-12 || E.nv >= EPA_MAXV) break;
+            int dupv = 0;
+            for (int i = 0; i < E.nv; ++i) {
+                double d[3];
+                sub3(w.w, E.V[i].w, d);
+                if (fabs(d[0]) <= 1e-14 && fabs(d[1]) <= 1e-14 && fabs(d[2]) <= 1e-14) dupv = 1;
+            }
+            if (dupv) break;
+            int wi = E.nv;
+            E.V[E.nv++] = w;
+            E.pass++;
+            E.hcf = -1; E.hff = -1; E.hnf = 0;
+            E.fpass[best] = E.pass;
+            int valid = 1;
+            for (int j = 0; j < 3 && valid; ++j) valid = epa_expand(&E, wi, E.ff[best][j], E.fe[best][j]);
+            if (!valid || E.hnf < 3 || E.fail) { E.nv--; break; }  /* keep the last consistent polytope */
+            epa_bind(&E, E.hcf, 1, E.hff, 2);
+            E.alive[best] = 0;
         }
-        SV w;
-        sup_md(A, B, fn[best], &w);
-        if (dot3(fn[best], w.w) - fdist[best] <= 1e-12 || nvx >= EPA_MAXV) break;
-        /* a support point that is already a vertex cannot expand the polytope
-         * (flat caps / box faces): stop instead of adding degenerate faces */
-        int dupv = 0;
-        for (int i = 0; i < nvx; ++i) {
-            double d[3];
-            sub3(w.w, V[i].w, d);
-            if (fabs(d[0]) <= 1e-14 && fabs(d[1]) <= 1e-14 && fabs(d[2]) <= 1e-14) dupv = 1;
-        }
-        if (dupv) break;
-        V[nvx] = w;
-        int vi = nvx++;
-        int E[EPA_MAXF][2], ne = 0, keep[EPA_MAXF][3], nk = 0;
-        for (int f = 0; f < nf; ++f) {
-            if (dot3(fn[f], w.w) - fdist[f] > 1e-12) {
-                for (int e = 0; e < 3; ++e) {
-                    int a = F[f][e], b = F[f][(e + 1) % 3], found = -1;
-                    for (int x = 0; x < ne; ++x) if (E[x][0] == b && E[x][1] == a) { found = x; break; }
-                    if (found >= 0) { for (int x = found; x < ne - 1; ++x) { E[x][0] = E[x + 1][0]; E[x][1] = E[x + 1][1]; } --ne; }
-                    else { E[ne][0] = a; E[ne][1] = b; ++ne; }
-                }
-            } else { keep[nk][0] = F[f][0]; keep[nk][1] = F[f][1]; keep[nk][2] = F[f][2]; ++nk; }
-        }
-        if (nk + ne > EPA_MAXF) break;
-        nf = 0;
-        for (int f = 0; f < nk; ++f) { F[nf][0] = keep[f][0]; F[nf][1] = keep[f][1]; F[nf][2] = keep[f][2]; ++nf; }
-        for (int e = 0; e < ne; ++e) { F[nf][0] = E[e][0]; F[nf][1] = E[e][1]; F[nf][2] = vi; ++nf; }
     }
-    if (getenv("ORC_DEBUG")) fprintf(stderr, "epa exit nvx %d nf %d\n", nvx, nf);
-    /* recompute the closest face of the final polytope */
+    if (getenv("ORC_DEBUG")) fprintf(stderr, "epa exit nvx %d nf %d fail %d\n", E.nv, E.nf, E.fail);
     double bd = INFINITY;
-    for (int f = 0; f < nf; ++f) {
-        double e1[3], e2[3], nn[3];
-        sub3(V[F[f][1]].w, V[F[f][0]].w, e1);
-        sub3(V[F[f][2]].w, V[F[f][0]].w, e2);
-        cross3(e1, e2, nn);
-        double L = norm3(nn);
-        for (int c = 0; c < 3; ++c) fn[f][c] = L > 1e-300 ? nn[c] / L : 0.0;
-        fdist[f] = L > 1e-300 ? dot3(fn[f], V[F[f][0]].w) : INFINITY;
-        if (fdist[f] < bd) { bd = fdist[f]; best = f; }
-    }
-    const double *a = V[F[best][0]].w, *b = V[F[best][1]].w, *c = V[F[best][2]].w;
-    double p[3] = {fn[best][0] * bd, fn[best][1] * bd, fn[best][2] * bd};
+    best = 0;
+    for (int f = 0; f < E.nf; ++f)
+        if (E.alive[f] && E.fd[f] < bd) { bd = E.fd[f]; best = f; }
+    const double *a = E.V[E.fv[best][0]].w, *b = E.V[E.fv[best][1]].w, *c = E.V[E.fv[best][2]].w;
+    double p[3] = {E.fn[best][0] * bd, E.fn[best][1] * bd, E.fn[best][2] * bd};
     double v0[3], v1[3], v2[3];
     sub3(b, a, v0); sub3(c, a, v1); sub3(p, a, v2);
     double d00 = dot3(v0, v0), d01 = dot3(v0, v1), d11 = dot3(v1, v1), d20 = dot3(v2, v0), d21 = dot3(v2, v1);
     double den = d00 * d11 - d01 * d01;
     double l1 = (d11 * d20 - d01 * d21) / den, l2 = (d00 * d21 - d01 * d20) / den, l0 = 1 - l1 - l2;
     for (int k = 0; k < 3; ++k) {
-        pA[k] = l0 * V[F[best][0]].a[k] + l1 * V[F[best][1]].a[k] + l2 * V[F[best][2]].a[k];
-        pB[k] = l0 * V[F[best][0]].b[k] + l1 * V[F[best][1]].b[k] + l2 * V[F[best][2]].b[k];
+        pA[k] = l0 * E.V[E.fv[best][0]].a[k] + l1 * E.V[E.fv[best][1]].a[k] + l2 * E.V[E.fv[best][2]].a[k];
+        pB[k] = l0 * E.V[E.fv[best][0]].b[k] + l1 * E.V[E.fv[best][1]].b[k] + l2 * E.V[E.fv[best][2]].b[k];
     }
     return -bd;
 }

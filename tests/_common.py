@@ -41,3 +41,20 @@ def oracle_batch(robot, q, qd, xt, xdt, exact=True, xi=None, xdi=None, mode=1, t
 
 def task_residual(J, dq):
     return np.max(np.abs(J @ dq))
+
+
+def nonsmooth_min_distance(om, q, h=1e-7, tol=1e-3):
+    """True where the oracle's min self-distance is not differentiable at q
+    (one-sided derivatives differ): argmin switches between pairs, or the
+    witness points are not unique (parallel flat/cylindrical features, e.g.
+    UR5e's three parallel joint axes).  The reference's gradient
+    (robot_data.cpp:476-494) is ill-defined there — SURVEY H2."""
+    d0 = O.min_distance(om, q)[0]
+    for k in range(len(q)):
+        e = np.zeros(len(q))
+        e[k] = h
+        fwd = (O.min_distance(om, q + e)[0] - d0) / h
+        bwd = (d0 - O.min_distance(om, q - e)[0]) / h
+        if abs(fwd - bwd) > tol:
+            return True
+    return False
