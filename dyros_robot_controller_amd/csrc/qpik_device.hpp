@@ -125,154 +125,194 @@ DRC_HD __forceinline__ SV sup_md(const Shape& A, const Shape& B, V3 d) {
   return o;
 }
 
-// Simplex storage in registers; pick() selects by runtime index with
-// conditional moves so no private array is ever dynamically indexed.
-struct Simplex {
-  V3 w0, w1, w2, w3;   // support points of the Minkowski difference A - B
-  V3 a0, a1, a2, a3;   // matching support points on A (B = a - w)
+// GJK simplex vertex: support point w = a - b of the Minkowski difference and
+// the matching support point a on A (b = a - w).
+struct SV2 {
+  V3 w, a;
 };
-DRC_HD __forceinline__ V3 pick(V3 s0, V3 s1, V3 s2, V3 s3, int i) {
-  return i == 0 ? s0 : (i == 1 ? s1 : (i == 2 ? s2 : s3));
-}
-DRC_HD __forceinline__ V3 simplex_w(const Simplex& S, int i) { return pick(S.w0, S.w1, S.w2, S.w3, i); }
-DRC_HD __forceinline__ V3 simplex_a(const Simplex& S, int i) { return pick(S.a0, S.a1, S.a2, S.a3, i); }
-DRC_HD __forceinline__ void simplex_set(Simplex& S, int i, V3 w, V3 a) {
-  if (i == 0) { S.w0 = w; S.a0 = a; }
-  else if (i == 1) { S.w1 = w; S.a1 = a; }
-  else if (i == 2) { S.w2 = w; S.a2 = a; }
-  else { S.w3 = w; S.a3 = a; }
-}
 
-// Closest point of conv(S[0..n)) to the origin: exhaustive sub-simplex
-// search, same visiting order (masks from 2^n-1 down to 1) and tolerances as
-// oracle/drc_oracle.c.  Compacts the kept vertices to the front.
-DRC_HD __forceinline__ int closest_simplex(Simplex& S, int n, V3* v, double* l0o, double* l1o, double* l2o,
-                                               double* l3o) {
-  double best = 0.0, b0 = 0, b1 = 0, b2 = 0, b3 = 0;
-  int bmask = 0;
-  for (int mask = (1 << n) - 1; mask > 0; --mask) {
-    int k = __builtin_popcount(mask);
-    int i0 = __builtin_ffs(mask) - 1;
-    int r1 = mask & (mask - 1), i1 = __builtin_ffs(r1) - 1;
-    int r2 = r1 & (r1 - 1), i2 = __builtin_ffs(r2) - 1;
-    int r3 = r2 & (r2 - 1), i3 = __builtin_ffs(r3) - 1;
-    const V3 w0 = simplex_w(S, i0);
-    double l0 = 1, l1 = 0, l2 = 0, l3 = 0;
-    bool valid = true;
-    if (k > 1) {
-      V3 D0 = simplex_w(S, i1) - w0;
-      V3 D1 = k > 2 ? simplex_w(S, i2) - w0 : v3(0, 0, 0);
-      V3 D2 = k > 3 ? simplex_w(S, i3) - w0 : v3(0, 0, 0);
-      double mu0 = 0, mu1 = 0, mu2 = 0;
-      if (k == 2) {
-        double G0 = dot(D0, D0), r0 = -dot(D0, w0);
-        valid = G0 > 0;
-        mu0 = valid ? r0 / G0 : 0;
-      } else if (k == 3) {
-        double G0 = dot(D0, D0), G1 = dot(D0, D1), G3 = dot(D1, D0), G4 = dot(D1, D1);
-        double r0 = -dot(D0, w0), r1 = -dot(D1, w0);
-        double det = G0 * G4 - G1 * G3;
-        valid = fabs(det) >= 1e-300;
-        mu0 = valid ? (r0 * G4 - G1 * r1) / det : 0;
-        mu1 = valid ? (G0 * r1 - r0 * G3) / det : 0;
-      } else {
-        double a = dot(D0, D0), b = dot(D0, D1), c = dot(D0, D2), dd = dot(D1, D0), e = dot(D1, D1),
-               f = dot(D1, D2), g = dot(D2, D0), h = dot(D2, D1), ii = dot(D2, D2);
-        double r0 = -dot(D0, w0), r1 = -dot(D1, w0), r2 = -dot(D2, w0);
-        double det = a * (e * ii - f * h) - b * (dd * ii - f * g) + c * (dd * h - e * g);
-        valid = fabs(det) >= 1e-300;
-        if (valid) {
-          mu0 = (r0 * (e * ii - f * h) - b * (r1 * ii - f * r2) + c * (r1 * h - e * r2)) / det;
-          mu1 = (a * (r1 * ii - f * r2) - r0 * (dd * ii - f * g) + c * (dd * r2 - r1 * g)) / det;
-          mu2 = (a * (e * r2 - r1 * h) - b * (dd * r2 - r1 * g) + r0 * (dd * h - e * g)) / det;
-        }
-      }
-      l0 = 1 - (mu0 + mu1 + mu2);
-      l1 = mu0;
-      l2 = mu1;
-      l3 = mu2;
-      valid = valid && !(l0 < -1e-14) && !(l1 < -1e-14) && !(k > 2 && l2 < -1e-14) && !(k > 3 && l3 < -1e-14);
-    }
-    if (valid) {
-      V3 p = l0 * w0;
-      if (k > 1) p = p + l1 * simplex_w(S, i1);
-      if (k > 2) p = p + l2 * simplex_w(S, i2);
-      if (k > 3) p = p + l3 * simplex_w(S, i3);
-      double dv = dot(p, p);
-      if (bmask == 0 || dv < best - 1e-18) {
-        best = dv;
-        bmask = mask;
-        *v = p;
-        b0 = l0; b1 = l1; b2 = l2; b3 = l3;
-      }
-    }
+// Closest point of conv(S[0..N)) to the origin: exhaustive sub-simplex
+// search, same visiting order (masks from 2^N-1 down to 1) and tolerances as
+// oracle/drc_oracle.c:closest_simplex.  The mask loop is expanded at compile
+// time (template recursion), so the simplex is only ever indexed with
+// constants and stays in registers.
+constexpr int cs_popc(int m) { return m == 0 ? 0 : (m & 1) + cs_popc(m >> 1); }
+constexpr int cs_bit(int m, int k) {  // index of the k-th set bit of m
+  return (m & 1) ? (k == 0 ? 0 : 1 + cs_bit(m >> 1, k - 1)) : 1 + cs_bit(m >> 1, k);
+}
+struct CsBest {
+  double best, l[4];
+  int mask;
+  V3 v;
+};
+template <int MASK>
+DRC_HD __forceinline__ void cs_try(const SV2 (&S)[4], CsBest& B) {
+  constexpr int k = cs_popc(MASK);
+  constexpr int i0 = cs_bit(MASK, 0), i1 = k > 1 ? cs_bit(MASK, 1) : 0, i2 = k > 2 ? cs_bit(MASK, 2) : 0,
+                i3 = k > 3 ? cs_bit(MASK, 3) : 0;
+  double l0 = 1, l1 = 0, l2 = 0, l3 = 0;
+  const V3 w0 = S[i0].w;
+  if (k == 2) {
+    const V3 D0 = S[i1].w - w0;
+    const double G0 = dot(D0, D0), r0 = -dot(D0, w0);
+    if (!(G0 > 0)) return;
+    l1 = r0 / G0;
+    l0 = 1 - l1;
+    if (l0 < -1e-14 || l1 < -1e-14) return;
+  } else if (k == 3) {
+    const V3 D0 = S[i1].w - w0, D1 = S[i2].w - w0;
+    const double G0 = dot(D0, D0), G1 = dot(D0, D1), G3 = dot(D1, D0), G4 = dot(D1, D1);
+    const double r0 = -dot(D0, w0), r1 = -dot(D1, w0);
+    const double det = G0 * G4 - G1 * G3;
+    if (fabs(det) < 1e-300) return;
+    l1 = (r0 * G4 - G1 * r1) / det;
+    l2 = (G0 * r1 - r0 * G3) / det;
+    l0 = 1 - (l1 + l2);
+    if (l0 < -1e-14 || l1 < -1e-14 || l2 < -1e-14) return;
+  } else if (k == 4) {
+    const V3 D0 = S[i1].w - w0, D1 = S[i2].w - w0, D2 = S[i3].w - w0;
+    const double a = dot(D0, D0), b = dot(D0, D1), c = dot(D0, D2), dd = dot(D1, D0), e = dot(D1, D1),
+                 f = dot(D1, D2), g = dot(D2, D0), h = dot(D2, D1), ii = dot(D2, D2);
+    const double r0 = -dot(D0, w0), r1 = -dot(D1, w0), r2 = -dot(D2, w0);
+    const double det = a * (e * ii - f * h) - b * (dd * ii - f * g) + c * (dd * h - e * g);
+    if (fabs(det) < 1e-300) return;
+    l1 = (r0 * (e * ii - f * h) - b * (r1 * ii - f * r2) + c * (r1 * h - e * r2)) / det;
+    l2 = (a * (r1 * ii - f * r2) - r0 * (dd * ii - f * g) + c * (dd * r2 - r1 * g)) / det;
+    l3 = (a * (e * r2 - r1 * h) - b * (dd * r2 - r1 * g) + r0 * (dd * h - e * g)) / det;
+    l0 = 1 - ((l1 + l2) + l3);
+    if (l0 < -1e-14 || l1 < -1e-14 || l2 < -1e-14 || l3 < -1e-14) return;
   }
-  Simplex T = S;
+  V3 p = l0 * w0;
+  if (k > 1) p = p + l1 * S[i1].w;
+  if (k > 2) p = p + l2 * S[i2].w;
+  if (k > 3) p = p + l3 * S[i3].w;
+  const double dv = dot(p, p);
+  if (B.mask == 0 || dv < B.best - 1e-18) {
+    B.best = dv;
+    B.mask = MASK;
+    B.v = p;
+    B.l[0] = l0;
+    B.l[1] = l1;
+    B.l[2] = l2;
+    B.l[3] = l3;
+  }
+}
+template <int MASK>
+struct CsLoop {
+  DRC_HD static __forceinline__ void run(const SV2 (&S)[4], CsBest& B) {
+    cs_try<MASK>(S, B);
+    CsLoop<MASK - 1>::run(S, B);
+  }
+};
+template <>
+struct CsLoop<0> {
+  DRC_HD static __forceinline__ void run(const SV2 (&)[4], CsBest&) {}
+};
+template <int N>
+DRC_HD __forceinline__ int closest_n(SV2 (&S)[4], V3* v, double (&lam)[4]) {
+  CsBest B;
+  B.best = 0;
+  B.mask = 0;
+  B.v = v3(0, 0, 0);
+  B.l[0] = B.l[1] = B.l[2] = B.l[3] = 0;
+  CsLoop<(1 << N) - 1>::run(S, B);
+  const int bmask = B.mask;
+  *v = B.v;
+  const double b0 = B.l[0], b1 = B.l[1], b2 = B.l[2], b3 = B.l[3];
+  // compact kept vertices to the front with selects only
+  SV2 T[4] = {S[0], S[0], S[0], S[0]};
   int k = 0;
-  for (int i = 0; i < n; ++i)
-    if (bmask & (1 << i)) simplex_set(T, k++, simplex_w(S, i), simplex_a(S, i));
-  S = T;
-  *l0o = b0; *l1o = b1; *l2o = b2; *l3o = b3;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const bool keep = (bmask >> i) & 1;
+#pragma unroll
+    for (int t = 0; t <= i; ++t) {
+      const bool here = keep && k == t;
+      T[t].w = v3(here ? S[i].w.x : T[t].w.x, here ? S[i].w.y : T[t].w.y, here ? S[i].w.z : T[t].w.z);
+      T[t].a = v3(here ? S[i].a.x : T[t].a.x, here ? S[i].a.y : T[t].a.y, here ? S[i].a.z : T[t].a.z);
+    }
+    k += keep;
+  }
+#pragma unroll
+  for (int t = 0; t < 4; ++t) S[t] = T[t];
+  lam[0] = b0;
+  lam[1] = b1;
+  lam[2] = b2;
+  lam[3] = b3;
   return k;
 }
 
-// GJK on the cores (all state register-resident inside this function).
-// Returns {intersect, dist, pA, pB}; on intersection the final simplex is
-// written to ws->V[0..ns) for EPA and ns is returned.
-struct GjkOut {
-  int intersect, ns;
-  double dist;
-  V3 pA, pB;
+// GJK on the cores (same iteration, tolerances and duplicate test as
+// oracle/drc_oracle.c:gjk).  The simplex stays in registers.
+struct GjkState {
+  SV2 S[4];
+  double lam[4];
+  V3 v;
+  int n, intersect;
 };
-struct EpaWs;
-DRC_HD __forceinline__ void epa_seed(EpaWs* ws, int i, V3 w, V3 a);
-DRC_HD __noinline__ GjkOut gjk(const Shape A, const Shape B, EpaWs* ws) {
-  Simplex S;
-  S.w0 = S.w1 = S.w2 = S.w3 = v3(0, 0, 0);
-  S.a0 = S.a1 = S.a2 = S.a3 = v3(0, 0, 0);
+DRC_HD __forceinline__ void gjk_run(const Shape& A, const Shape& B, GjkState& g) {
+  SV2(&S)[4] = g.S;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) S[i].w = S[i].a = v3(0, 0, 0);
+  g.lam[0] = 1;
+  g.lam[1] = g.lam[2] = g.lam[3] = 0;
   V3 v = v3(A.T[9] - B.T[9], A.T[10] - B.T[10], A.T[11] - B.T[11]);
   if (dot(v, v) < 1e-24) v = v3(1, 0, 0);
   int n = 0;
-  double l0 = 1, l1 = 0, l2 = 0, l3 = 0;
-  GjkOut o;
-  o.intersect = 0;
+  g.intersect = 0;
   for (int it = 0; it < 128; ++it) {
-    SV w = sup_md(A, B, -1.0 * v);
-    double vv = dot(v, v);
+    const SV w = sup_md(A, B, -1.0 * v);
+    const double vv = dot(v, v);
     if (n > 0 && vv - dot(v, w.w) <= 1e-12 * sqrt(vv)) break;
     bool dup = false;
-    for (int i = 0; i < n; ++i) {
-      V3 si = simplex_w(S, i);
-      dup |= (si.x == w.w.x && si.y == w.w.y && si.z == w.w.z);
-    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dup |= i < n && S[i].w.x == w.w.x && S[i].w.y == w.w.y && S[i].w.z == w.w.z;
     if (dup) break;
-    simplex_set(S, n, w.w, w.a);
+    SV2 nw;
+    nw.w = w.w;
+    nw.a = w.a;
+    // append with selects (a dynamic S[n] store would force S into scratch)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const bool here = i == n;
+      S[i].w = v3(here ? nw.w.x : S[i].w.x, here ? nw.w.y : S[i].w.y, here ? nw.w.z : S[i].w.z);
+      S[i].a = v3(here ? nw.a.x : S[i].a.x, here ? nw.a.y : S[i].a.y, here ? nw.a.z : S[i].a.z);
+    }
     ++n;
-    n = closest_simplex(S, n, &v, &l0, &l1, &l2, &l3);
+    if (n == 1) n = closest_n<1>(S, &v, g.lam);
+    else if (n == 2) n = closest_n<2>(S, &v, g.lam);
+    else if (n == 3) n = closest_n<3>(S, &v, g.lam);
+    else n = closest_n<4>(S, &v, g.lam);
     if (n == 4 || dot(v, v) < 1e-24) {
-      o.intersect = 1;
+      g.intersect = 1;
       break;
     }
   }
-  o.ns = n;
-  if (o.intersect) {
-    if (ws)
-      for (int i = 0; i < n; ++i) epa_seed(ws, i, simplex_w(S, i), simplex_a(S, i));
-    o.dist = 0;
-    o.pA = o.pB = v3(0, 0, 0);
-    return o;
-  }
+  g.n = n;
+  g.v = v;
+}
+// separation distance and witnesses (valid when !intersect)
+struct GjkDist {
+  int intersect;
+  double dist;
+  V3 pA, pB;
+};
+DRC_HD __noinline__ GjkDist gjk(const Shape A, const Shape B) {
+  GjkState g;
+  gjk_run(A, B, g);
+  GjkDist o;
+  o.intersect = g.intersect;
   // witnesses: sum_i lam_i a_i and sum_i lam_i b_i (oracle accumulation order)
   V3 pA = v3(0, 0, 0), pB = v3(0, 0, 0);
-  for (int i = 0; i < n; ++i) {
-    const double li = i == 0 ? l0 : (i == 1 ? l1 : (i == 2 ? l2 : l3));
-    const V3 ai = simplex_a(S, i), bi = ai - simplex_w(S, i);
-    pA = pA + li * ai;
-    pB = pB + li * bi;
-  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    if (i < g.n) {
+      pA = pA + g.lam[i] * g.S[i].a;
+      pB = pB + g.lam[i] * (g.S[i].a - g.S[i].w);
+    }
   o.pA = pA;
   o.pB = pB;
-  o.dist = sqrt(dot(v, v));
+  o.dist = sqrt(dot(g.v, g.v));
   return o;
 }
 
@@ -281,35 +321,43 @@ DRC_HD __noinline__ GjkOut gjk(const Shape A, const Shape B, EpaWs* ws) {
 // (explicit DFS stack, same visiting order as the recursive oracle), so the
 // horizon is a single loop and the polytope stays a closed 2-manifold even
 // when flat features (cylinder caps, box faces) make the support mapping
-// degenerate.  Lane-serial, polytope in a per-wave global workspace (rare
-// path: penetrating candidate pairs only).
-constexpr int kEpaMaxV = 256, kEpaMaxF = 512;
-struct EpaWs {
-  SV V[kEpaMaxV];
-  int fv[kEpaMaxF][3], ff[kEpaMaxF][3], fe[kEpaMaxF][3];
-  int fpass[kEpaMaxF], alive[kEpaMaxF];
-  int stk_f[kEpaMaxF], stk_e[kEpaMaxF], stk_s[kEpaMaxF];
+// degenerate.  The polytope lives in a per-workgroup L2-resident buffer; the closest-face scan is spread
+// over the wave, the expansion is lane-0 serial.  Same caps and decisions as
+// oracle/drc_oracle.c:epa.
+constexpr int kEpaMaxV = 128, kEpaMaxF = 256;
+struct EpaPoly {
+  double vw[kEpaMaxV][3], va[kEpaMaxV][3];
   double fn[kEpaMaxF][3], fd[kEpaMaxF];
   double out[6];
-  int nv, nf, pass, hcf, hff, hnf, fail;
+  int16_t fv[kEpaMaxF][3], ff[kEpaMaxF][3], fpass[kEpaMaxF], stk_f[kEpaMaxF];
+  int16_t freel[kEpaMaxF], deadl[kEpaMaxF], newl[kEpaMaxF];  // recycled slots; this pass's kills / births
+  int8_t fe[kEpaMaxF][3], alive[kEpaMaxF], stk_e[kEpaMaxF], stk_s[kEpaMaxF];
+  int nv, nf, pass, hcf, hff, hnf, fail, stop, nfree, ndead, nnew;
 };
-DRC_HD __forceinline__ void epa_seed(EpaWs* ws, int i, V3 w, V3 a) {
-  ws->V[i].w = w;
-  ws->V[i].a = a;
-  ws->V[i].b = a - w;
+DRC_HD __forceinline__ V3 epa_vw(const EpaPoly* E, int i) { return v3(E->vw[i][0], E->vw[i][1], E->vw[i][2]); }
+DRC_HD __forceinline__ V3 epa_va(const EpaPoly* E, int i) { return v3(E->va[i][0], E->va[i][1], E->va[i][2]); }
+DRC_HD __forceinline__ void epa_addv(EpaPoly* E, V3 w, V3 a) {
+  st3(E->vw[E->nv], w);
+  st3(E->va[E->nv], a);
+  E->nv++;
 }
-DRC_HD __forceinline__ int epa_newface(EpaWs* E, int a, int b, int c) {
-  if (E->nf >= kEpaMaxF) {
+DRC_HD __forceinline__ int epa_newface(EpaPoly* E, int a, int b, int c) {
+  int f;
+  if (E->nfree > 0) {
+    f = E->freel[--E->nfree];
+  } else if (E->nf < kEpaMaxF) {
+    f = E->nf++;
+  } else {
     E->fail = 1;
     return -1;
   }
-  const int f = E->nf++;
+  E->newl[E->nnew++] = f;
   E->fv[f][0] = a;
   E->fv[f][1] = b;
   E->fv[f][2] = c;
   E->alive[f] = 1;
   E->fpass[f] = 0;
-  V3 nn = cross(E->V[b].w - E->V[a].w, E->V[c].w - E->V[a].w);
+  V3 nn = cross(epa_vw(E, b) - epa_vw(E, a), epa_vw(E, c) - epa_vw(E, a));
   const double L = sqrt(dot(nn, nn));
   if (!(L > 1e-300)) {
     E->fail = 1;
@@ -317,27 +365,24 @@ DRC_HD __forceinline__ int epa_newface(EpaWs* E, int a, int b, int c) {
     return -1;
   }
   nn = (1.0 / L) * nn;
-  E->fn[f][0] = nn.x;
-  E->fn[f][1] = nn.y;
-  E->fn[f][2] = nn.z;
-  E->fd[f] = dot(nn, E->V[a].w);
+  st3(E->fn[f], nn);
+  E->fd[f] = dot(nn, epa_vw(E, a));
   return f;
 }
-DRC_HD __forceinline__ void epa_bind(EpaWs* E, int f0, int e0, int f1, int e1) {
+DRC_HD __forceinline__ void epa_bind(EpaPoly* E, int f0, int e0, int f1, int e1) {
   E->ff[f0][e0] = f1;
   E->fe[f0][e0] = e1;
   E->ff[f1][e1] = f0;
   E->fe[f1][e1] = e0;
 }
 // iterative form of btGjkEpa2::expand over the three edges of `best`
-DRC_HD __forceinline__ bool epa_expand_all(EpaWs* E, int w, int best) {
-  const V3 ww = E->V[w].w;
+DRC_HD inline bool epa_expand_all(EpaPoly* E, int w, int best) {
+  const V3 ww = epa_vw(E, w);
   for (int j = 0; j < 3; ++j) {
-    int sp = 0;
     E->stk_f[0] = E->ff[best][j];
     E->stk_e[0] = E->fe[best][j];
     E->stk_s[0] = 0;
-    sp = 1;
+    int sp = 1;
     while (sp > 0) {
       const int f = E->stk_f[sp - 1], e = E->stk_e[sp - 1], st = E->stk_s[sp - 1];
       if (st == 0) {
@@ -346,8 +391,7 @@ DRC_HD __forceinline__ bool epa_expand_all(EpaWs* E, int w, int best) {
           continue;
         }
         const int e1 = e == 2 ? 0 : e + 1;
-        const V3 n = v3(E->fn[f][0], E->fn[f][1], E->fn[f][2]);
-        if (dot(n, ww) - E->fd[f] < -1e-12) {
+        if (dot(ld3(E->fn[f]), ww) - E->fd[f] < -1e-12) {
           const int nf = epa_newface(E, E->fv[f][e1], E->fv[f][e], w);
           if (nf < 0) return false;
           epa_bind(E, nf, 0, f, e);
@@ -375,37 +419,48 @@ DRC_HD __forceinline__ bool epa_expand_all(EpaWs* E, int w, int best) {
         ++sp;
       } else {
         E->alive[f] = 0;
+        E->deadl[E->ndead++] = f;
         --sp;
       }
     }
   }
   return true;
 }
-
-// The GJK simplex arrives in ws->V[0..ns) (epa_seed) so no private array
-// crosses the call; witness points come back in ws->out.
-DRC_HD __noinline__ double epa(const Shape A, const Shape B, int ns, EpaWs* E) {
-  E->nv = ns;
+// rerun GJK and build the initial tetrahedron from its final simplex
+// (lane-serial)
+DRC_HD __noinline__ void epa_init(const Shape A, const Shape B, EpaPoly* E) {
+  GjkState g;
+  gjk_run(A, B, g);
+  E->nv = 0;
   E->nf = 0;
   E->pass = 0;
   E->fail = 0;
+  E->nfree = 0;
+  E->nnew = 0;
+  for (int i = 0; i < 4; ++i)
+    if (i < g.n) epa_addv(E, g.S[i].w, g.S[i].a);
   for (int di = 0; di < 6 && E->nv < 4; ++di) {
     const double sgn = di < 3 ? 1.0 : -1.0;
     const int ax = di % 3;
-    SV w = sup_md(A, B, v3(ax == 0 ? sgn : 0.0, ax == 1 ? sgn : 0.0, ax == 2 ? sgn : 0.0));
+    const SV w = sup_md(A, B, v3(ax == 0 ? sgn : 0.0, ax == 1 ? sgn : 0.0, ax == 2 ? sgn : 0.0));
     bool ok = true;
     for (int i = 0; i < E->nv; ++i) {
-      V3 d = w.w - E->V[i].w;
+      const V3 d = w.w - epa_vw(E, i);
       ok &= sqrt(dot(d, d)) > 1e-12;
     }
-    if (ok) E->V[E->nv++] = w;
+    if (ok) epa_addv(E, w.w, w.a);
   }
   {  // orient the tetrahedron so that face (0,1,2) looks away from vertex 3
-    V3 nn = cross(E->V[1].w - E->V[0].w, E->V[2].w - E->V[0].w);
-    if (dot(nn, E->V[3].w - E->V[0].w) > 0) {
-      SV t = E->V[0];
-      E->V[0] = E->V[1];
-      E->V[1] = t;
+    const V3 nn = cross(epa_vw(E, 1) - epa_vw(E, 0), epa_vw(E, 2) - epa_vw(E, 0));
+    if (dot(nn, epa_vw(E, 3) - epa_vw(E, 0)) > 0) {
+      for (int c = 0; c < 3; ++c) {
+        double t = E->vw[0][c];
+        E->vw[0][c] = E->vw[1][c];
+        E->vw[1][c] = t;
+        t = E->va[0][c];
+        E->va[0][c] = E->va[1][c];
+        E->va[1][c] = t;
+      }
     }
   }
   const int t0 = epa_newface(E, 0, 1, 2), t1 = epa_newface(E, 1, 0, 3), t2 = epa_newface(E, 2, 1, 3),
@@ -417,55 +472,77 @@ DRC_HD __noinline__ double epa(const Shape A, const Shape B, int ns, EpaWs* E) {
     epa_bind(E, t1, 1, t3, 2);
     epa_bind(E, t1, 2, t2, 1);
     epa_bind(E, t2, 2, t3, 1);
-    for (int it = 0; it < 255; ++it) {
-      int best = -1;
-      double bd = 1e300;
-      for (int f = 0; f < E->nf; ++f)
-        if (E->alive[f] && E->fd[f] < bd) {
-          bd = E->fd[f];
-          best = f;
-        }
-      const V3 bn = v3(E->fn[best][0], E->fn[best][1], E->fn[best][2]);
-      SV w = sup_md(A, B, bn);
-      if (dot(bn, w.w) - E->fd[best] <= 1e-12 || E->nv >= kEpaMaxV) break;
-      bool dupv = false;
-      for (int i = 0; i < E->nv; ++i) {
-        V3 d = w.w - E->V[i].w;
-        dupv |= fabs(d.x) <= 1e-14 && fabs(d.y) <= 1e-14 && fabs(d.z) <= 1e-14;
-      }
-      if (dupv) break;
-      const int wi = E->nv;
-      E->V[E->nv++] = w;
-      E->pass++;
-      E->hcf = -1;
-      E->hff = -1;
-      E->hnf = 0;
-      E->fpass[best] = E->pass;
-      const bool valid = epa_expand_all(E, wi, best);
-      if (!valid || E->hnf < 3 || E->fail) {
-        E->nv--;
-        break;
-      }
-      epa_bind(E, E->hcf, 1, E->hff, 2);
-      E->alive[best] = 0;
+  }
+  E->stop = E->fail;
+}
+// one expansion step from face `best` (lane-serial); sets E->stop when done
+DRC_HD __noinline__ void epa_step(const Shape A, const Shape B, EpaPoly* E, int best) {
+  const V3 bn = ld3(E->fn[best]);
+  const SV w = sup_md(A, B, bn);
+  if (dot(bn, w.w) - E->fd[best] <= 1e-12 || E->nv >= kEpaMaxV) {
+    E->stop = 1;
+    return;
+  }
+  for (int i = 0; i < E->nv; ++i) {  // support point already a vertex: cannot expand
+    const V3 d = w.w - epa_vw(E, i);
+    if (fabs(d.x) <= 1e-14 && fabs(d.y) <= 1e-14 && fabs(d.z) <= 1e-14) {
+      E->stop = 1;
+      return;
     }
   }
+  const int wi = E->nv;
+  epa_addv(E, w.w, w.a);
+  E->pass++;
+  E->hcf = -1;
+  E->hff = -1;
+  E->hnf = 0;
+  E->ndead = 0;
+  E->nnew = 0;
+  E->fpass[best] = E->pass;
+  const bool valid = epa_expand_all(E, wi, best);
+  if (!valid || E->hnf < 3 || E->fail) {  // roll back to the last closed polytope
+    for (int i = 0; i < E->nnew; ++i) E->alive[E->newl[i]] = 0;
+    for (int i = 0; i < E->ndead; ++i) E->alive[E->deadl[i]] = 1;
+    E->nv--;
+    E->stop = 1;
+    return;
+  }
+  epa_bind(E, E->hcf, 1, E->hff, 2);
+  E->alive[best] = 0;
+  for (int i = 0; i < E->ndead; ++i) E->freel[E->nfree++] = E->deadl[i];
+  E->freel[E->nfree++] = best;
+}
+// witness points on the closest face (lane-serial); returns -depth
+DRC_HD __noinline__ double epa_finish(EpaPoly* E, int best) {
+  const double bd = E->fd[best];
+  const V3 bn = ld3(E->fn[best]);
+  const int i0 = E->fv[best][0], i1 = E->fv[best][1], i2 = E->fv[best][2];
+  const V3 aw = epa_vw(E, i0), bw = epa_vw(E, i1), cw = epa_vw(E, i2);
+  const V3 p = bd * bn, v0 = bw - aw, v1 = cw - aw, v2 = p - aw;
+  const double d00 = dot(v0, v0), d01 = dot(v0, v1), d11 = dot(v1, v1), d20 = dot(v2, v0), d21 = dot(v2, v1);
+  const double den = d00 * d11 - d01 * d01;
+  const double l1 = (d11 * d20 - d01 * d21) / den, l2 = (d00 * d21 - d01 * d20) / den, l0 = 1 - l1 - l2;
+  const V3 aa = epa_va(E, i0), ba = epa_va(E, i1), ca = epa_va(E, i2);
+  st3(E->out, l0 * aa + l1 * ba + l2 * ca);
+  st3(E->out + 3, l0 * (aa - aw) + l1 * (ba - bw) + l2 * (ca - cw));
+  return -bd;
+}
+// closest alive face by a serial scan (host / oracle-style reference)
+DRC_HD inline int epa_best_serial(const EpaPoly* E) {
+  int best = -1;
   double bd = 1e300;
-  int best = 0;
   for (int f = 0; f < E->nf; ++f)
     if (E->alive[f] && E->fd[f] < bd) {
       bd = E->fd[f];
       best = f;
     }
-  const V3 bn = v3(E->fn[best][0], E->fn[best][1], E->fn[best][2]);
-  const SV &a = E->V[E->fv[best][0]], &b = E->V[E->fv[best][1]], &c = E->V[E->fv[best][2]];
-  V3 p = bd * bn, v0 = b.w - a.w, v1 = c.w - a.w, v2 = p - a.w;
-  double d00 = dot(v0, v0), d01 = dot(v0, v1), d11 = dot(v1, v1), d20 = dot(v2, v0), d21 = dot(v2, v1);
-  double den = d00 * d11 - d01 * d01;
-  double l1 = (d11 * d20 - d01 * d21) / den, l2 = (d00 * d21 - d01 * d20) / den, l0 = 1 - l1 - l2;
-  st3(E->out, l0 * a.a + l1 * b.a + l2 * c.a);
-  st3(E->out + 3, l0 * a.b + l1 * b.b + l2 * c.b);
-  return -bd;
+  return best;
+}
+// lane-serial driver (host harness and single-lane use)
+DRC_HD inline double epa_serial(const Shape& A, const Shape& B, EpaPoly* E) {
+  epa_init(A, B, E);
+  for (int it = 0; it < 255 && !E->stop; ++it) epa_step(A, B, E, epa_best_serial(E));
+  return epa_finish(E, epa_best_serial(E));
 }
 
 // signed distance + closest surface point of a solid cylinder / box

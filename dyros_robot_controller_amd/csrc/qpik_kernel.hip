@@ -282,12 +282,25 @@ __device__ void so3_exp(V3 w, double* R) {
   for (int i = 0; i < 9; ++i) R[i] = (i % 4 == 0 ? 1 : 0) + a * K[i] + b * K2[i];
 }
 
+// Compile-time QP dimensions (nx variables, ng general rows, np = leading
+// block of P).  Dims<0,0,0> is the runtime-sized fallback; the named robots
+// get fully unrolled inner products (LDS loads issued ahead of the FMAs).
+template <int NX, int NG, int NP>
+struct Dims {
+  static constexpr int nx = NX, ng = NG, np = NP;
+};
+#define DNX (QD::nx ? QD::nx : kp.nx)
+#define DNG (QD::ng ? QD::ng : kp.ng)
+#define DNP (QD::np ? QD::np : kp.np)
+#define DM (DNX + DNG)
+
 // ------------------------------------------------------------------------
 // OSQP residuals (lane-parallel): fills SC_* slots.  x, z, y in LDS (scaled)
 // ------------------------------------------------------------------------
+template <class QD>
 __device__ __forceinline__ void residuals(const KParams& kp, double* S, const double* x, const double* z, const double* y,
                           double eps_abs, double eps_rel) {
-  const int l = lane_id(), nx = kp.nx, ng = kp.ng, np = kp.np;
+  const int l = lane_id(), nx = DNX, ng = DNG, np = DNP;
   const double *P = S + kp.oP, *G = S + kp.oG, *q = S + kp.oQ, *ab = S + kp.oAB, *D = S + kp.oD, *E = S + kp.oE;
   double pr = 0, prs = 0, nAx = 0, nz = 0, nAxs = 0, nzs = 0;
   double dr = 0, drs = 0, nPx = 0, nAty = 0, nq = 0, nPxs = 0, nAtys = 0, nqs = 0;
@@ -359,8 +372,9 @@ __device__ __forceinline__ void residuals(const KParams& kp, double* S, const do
 }
 
 // K = P + sigma I + A^T diag(rho) A, inverted in place (Gauss-Jordan, SPD)
+template <class QD>
 __device__ __forceinline__ void factor_kinv(const KParams& kp, double* S) {
-  const int l = lane_id(), nx = kp.nx, ng = kp.ng, np = kp.np;
+  const int l = lane_id(), nx = DNX, ng = DNG, np = DNP;
   const double *P = S + kp.oP, *G = S + kp.oG, *ab = S + kp.oAB, *rho = S + kp.oRho;
   double* K = S + kp.oU0;
   if (l < nx) {
@@ -388,8 +402,9 @@ __device__ __forceinline__ void factor_kinv(const KParams& kp, double* S) {
   }
 }
 
+template <class QD>
 __device__ __forceinline__ void set_rho(const KParams& kp, double* S, double rho) {
-  const int l = lane_id(), nx = kp.nx, ng = kp.ng;
+  const int l = lane_id(), nx = DNX, ng = DNG;
   const double *lo = S + kp.oL, *up = S + kp.oU;
   double* rv = S + kp.oRho;
   for (int row = l; row < nx + ng; row += 64) {
@@ -403,8 +418,9 @@ __device__ __forceinline__ void set_rho(const KParams& kp, double* S, double rho
 }
 
 // Primal infeasibility certificate (OSQP / Banjac et al.) on the last dy
+template <class QD>
 __device__ __forceinline__ bool primal_infeasible(const KParams& kp, double* S, double eps) {
-  const int l = lane_id(), nx = kp.nx, ng = kp.ng;
+  const int l = lane_id(), nx = DNX, ng = DNG;
   const double *lo = S + kp.oL, *up = S + kp.oU, *E = S + kp.oE, *dyv = S + kp.oDY, *G = S + kp.oG,
                *ab = S + kp.oAB, *D = S + kp.oD;
   double* dy = S + kp.oT1;
@@ -466,8 +482,9 @@ __device__ __forceinline__ void ldl_solve(const double* L, const double* dg, int
 // left-looking LDL^T with iterative refinement against the unregularised
 // system.  Writes the full primal xx[nx] and dual yy[m] (scaled space).
 // Flags: actb (bound row l) / actg (G row l) held by lane l.
+template <class QD>
 __device__ __forceinline__ bool eqp(const KParams& kp, double* S, int actb, int actg, double* xx, double* yy) {
-  const int l = lane_id(), nx = kp.nx, ng = kp.ng, np = kp.np, m = kp.m;
+  const int l = lane_id(), nx = DNX, ng = DNG, np = DNP, m = DM;
   const double *P = S + kp.oP, *G = S + kp.oG, *q = S + kp.oQ, *ab = S + kp.oAB, *lo = S + kp.oL,
                *up = S + kp.oU;
   unsigned long long freeMask = __ballot(l < nx && actb == 0);
@@ -583,8 +600,9 @@ __device__ __forceinline__ bool eqp(const KParams& kp, double* S, int actb, int 
 // (Nocedal & Wright Alg. 16.3) from the first feasible polished point.  Same
 // decisions, in the same row order, as oracle/drc_oracle.c:qp_polish.
 constexpr int kPolishFeasAttempts = 4, kPolishAsIters = 24;
+template <class QD>
 __device__ __forceinline__ bool polish(const KParams& kp, double* S, bool strict) {
-  const int l = lane_id(), nx = kp.nx, ng = kp.ng, np = kp.np, m = kp.m;
+  const int l = lane_id(), nx = DNX, ng = DNG, np = DNP, m = DM;
   const double *G = S + kp.oG, *ab = S + kp.oAB, *lo = S + kp.oL, *up = S + kp.oU, *E = S + kp.oE;
   double *x = S + kp.oX, *z = S + kp.oZ, *y = S + kp.oY;
   (void)np;
@@ -604,7 +622,7 @@ __device__ __forceinline__ bool polish(const KParams& kp, double* S, bool strict
   bool have_feas = false;
   const int iters = strict ? kPolishFeasAttempts + kPolishAsIters : 1;
   for (int it = 0; it < iters; ++it) {
-    if (!eqp(kp, S, actb, actg, xx, yy)) break;
+    if (!eqp<QD>(kp, S, actb, actg, xx, yy)) break;
     if (have_feas) {
       double stepmax = 0, xnorm = 0;
       if (l < nx) {
@@ -661,7 +679,7 @@ __device__ __forceinline__ bool polish(const KParams& kp, double* S, bool strict
       zz[nx + l] = fmin(fmax(axg, lo[nx + l]), up[nx + l]);
     }
     wsync();
-    residuals(kp, S, xx, zz, yy, kp.s.eps_exact, kp.s.eps_exact);
+    residuals<QD>(kp, S, xx, zz, yy, kp.s.eps_exact, kp.s.eps_exact);
     const double pr1 = sc[SC_PRI], dr1 = sc[SC_DUA], epsp = sc[SC_EPSP], epsd = sc[SC_EPSD], c = sc[SC_C];
     bool ok = (pr1 < pr0 && dr1 < dr0) || (pr1 < pr0 && dr0 < 1e-10) || (dr1 < dr0 && pr0 < 1e-10);
     double wv = 0;
@@ -745,15 +763,20 @@ struct IO {
   int32_t *status, *iters;
   double *st_pose, *st_jac, *st_man, *st_dist, *st_xdd;
   int32_t* st_pair;
-  EpaWs* epa_ws;
+  EpaPoly* epa_ws;
 };
 
-__global__ void __launch_bounds__(64) task_kernel(const DevModel* __restrict__ M, const KParams kp, const IO io) {
+// Occupancy target of the task kernel (waves per SIMD): the lane-serial
+// narrow phase and task-velocity code would otherwise take all 512 registers.
+#ifndef DRC_TASK_WAVES
+#define DRC_TASK_WAVES 2
+#endif
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRC_TASK_WAVES, 8))) task_kernel(const DevModel* __restrict__ M, const KParams kp, const IO io) {
   extern __shared__ __attribute__((aligned(16))) double S[];
   const int l = lane_id();
   const int nv = kp.nv;
   const int64_t B = io.B;
-  EpaWs* ews = io.epa_ws + blockIdx.x;
+  EpaPoly* ews = io.epa_ws + blockIdx.x;
   PH_DECL
   for (int64_t b = blockIdx.x; b < B; b += gridDim.x) {
     // ---------------- state in ----------------
@@ -919,12 +942,46 @@ __global__ void __launch_bounds__(64) task_kernel(const DevModel* __restrict__ M
       A6[l] = s;
     }
     wsync();
-    if (l == 0) {
-      double* ws = S + kp.kScr;
-      S[kp.oSc + SC_MAN] = sqrt(det_lu6(A6, ws));
-      pinv_cod6(A6, Ai, ws);
+    {
+      // JJ^T (SPD) inverted by six lane-parallel Jordan exchanges (36 lanes),
+      // det = product of the pivots.  Ill-conditioned JJ^T (Frobenius
+      // condition estimate >= 1e5) takes the serial COD path (rank by pivoted
+      // QR, Moore-Penrose on the kept modes), matching DyrosMath::PinvCOD's
+      // threshold semantics (math_type_define.h:563).
+      double piv_min = 1e300, det = 1;
+      if (l < 36) Ai[l] = A6[l];
+      wsync();
+      const int ii = l / 6, jj = l % 6;
+      for (int k = 0; k < 6; ++k) {
+        const double akk = Ai[k * 6 + k];
+        double nv_ = 0;
+        if (l < 36) {
+          const double aij = Ai[l], aik = Ai[ii * 6 + k], akj = Ai[k * 6 + jj];
+          if (ii == k && jj == k) nv_ = 1.0 / akk;
+          else if (ii == k) nv_ = akj / akk;
+          else if (jj == k) nv_ = -aik / akk;
+          else nv_ = aij - aik * akj / akk;
+        }
+        piv_min = fmin(piv_min, akk);
+        det *= akk;
+        wsync();
+        if (l < 36) Ai[l] = nv_;
+        wsync();
+      }
+      // kappa_2 <= |A|_F |A^-1|_F; below 1e5 the pivoted QR of PinvCOD keeps
+      // every mode (|R_55|/|R_00| >= 1/kappa_2 > COD_THRESHOLD 1e-6)
+      const double fa = wave_sum(l < 36 ? A6[l] * A6[l] : 0.0), fi = wave_sum(l < 36 ? Ai[l] * Ai[l] : 0.0);
+      if (!(piv_min > 0) || !(fa * fi < 1e10)) {  // uniform
+        if (l == 0) {
+          double* ws = S + kp.kScr;
+          S[kp.oSc + SC_MAN] = sqrt(det_lu6(A6, ws));
+          pinv_cod6(A6, Ai, ws);
+        }
+      } else if (l == 0) {
+        S[kp.oSc + SC_MAN] = sqrt(det);
+      }
+      wsync();
     }
-    wsync();
     double* W = S + kp.kW;  // narm x 6 = Jr^T Ai
     for (int e = l; e < narm * 6; e += 64) {
       int c = e / 6, a = e % 6;
@@ -969,8 +1026,14 @@ __global__ void __launch_bounds__(64) task_kernel(const DevModel* __restrict__ M
     }
     PH(2);
     // ---------------- self-collision distance (broad + narrow phase) -------
+    // Each lane owns pairs p = l, l+64, ... and keeps its running minimum with
+    // witness points in registers (ties -> lowest pair index, the oracle's
+    // first-strict-min rule), so the winner's witnesses never get recomputed.
     double* pd = S + kp.kPd;
     double* pf = S + kp.kPf;
+    double bestd = 1.7976931348623157e308;
+    int besti = 0x7fffffff;
+    V3 bpA = v3(0, 0, 0), bpB = v3(0, 0, 0);
     double ub = 1e300;
     for (int p = l; p < M->npairs; p += 64) {
       const int ga = M->pair_a[p], gb = M->pair_b[p];
@@ -978,11 +1041,16 @@ __global__ void __launch_bounds__(64) task_kernel(const DevModel* __restrict__ M
       Shape Bs{M->gtype[gb], Tg + 12 * gb, M->gparam[gb][0], M->gparam[gb][1], M->gparam[gb][2]};
       if (A.type == kSphere || Bs.type == kSphere) {
         V3 pA, pB;
-        double d = sphere_pair(A, Bs, &pA, &pB);
-        pd[p] = d;
+        const double d = sphere_pair(A, Bs, &pA, &pB);
         pf[p] = 1.0;
         ub = fmin(ub, d);
-      } else {
+        if (d < bestd) {  // p increases within this pass
+          bestd = d;
+          besti = p;
+          bpA = pA;
+          bpB = pB;
+        }
+      } else {  // swept-core lower bound
         V3 a0, a1, b0, b1;
         double ra, rb;
         core_segment(A, M->gbound[ga], &a0, &a1, &ra);
@@ -992,79 +1060,84 @@ __global__ void __launch_bounds__(64) task_kernel(const DevModel* __restrict__ M
       }
     }
     ub = -wave_max(-ub);
-    wsync();
     PH(3);
-    // exact GJK/EPA only where the swept-core bound can still win
+    // exact GJK only where the swept-core bound can still win
     for (int p = l; p < M->npairs; p += 64) {
       if (pf[p] == 0.0 && pd[p] - 1e-9 <= ub) {
         const int ga = M->pair_a[p], gb = M->pair_b[p];
         Shape A{M->gtype[ga], Tg + 12 * ga, M->gparam[ga][0], M->gparam[ga][1], M->gparam[ga][2]};
         Shape Bs{M->gtype[gb], Tg + 12 * gb, M->gparam[gb][0], M->gparam[gb][1], M->gparam[gb][2]};
-        GjkOut g = gjk(A, Bs, nullptr);
+        const GjkDist g = gjk(A, Bs);
         if (g.intersect) {
-          pf[p] = 2.0;  // penetrating: EPA below, one pair at a time
+          pf[p] = 2.0;  // penetrating: EPA below
         } else {
-          pd[p] = g.dist;
           pf[p] = 1.0;
+          if (g.dist < bestd || (g.dist == bestd && p < besti)) {
+            bestd = g.dist;
+            besti = p;
+            bpA = g.pA;
+            bpB = g.pB;
+          }
         }
       }
     }
     wsync();
     PH(4);
-    // EPA shares one per-wave workspace: serialise the (rare) penetrating pairs
+    // EPA: one penetrating pair at a time; the owning lane expands the
+    // polytope, the whole wave scans for the closest face
     for (int p0 = 0; p0 < M->npairs; p0 += 64) {
       unsigned long long need = __ballot(p0 + l < M->npairs && pf[p0 + l] == 2.0);
       while (need) {
         const int ln = __ffsll(static_cast<long long>(need)) - 1;
         need &= need - 1;
-        if (l == ln) {
-          const int p = p0 + l, ga = M->pair_a[p], gb = M->pair_b[p];
-          Shape A{M->gtype[ga], Tg + 12 * ga, M->gparam[ga][0], M->gparam[ga][1], M->gparam[ga][2]};
-          Shape Bs{M->gtype[gb], Tg + 12 * gb, M->gparam[gb][0], M->gparam[gb][1], M->gparam[gb][2]};
-          GjkOut g = gjk(A, Bs, ews);
-          pd[p] = epa(A, Bs, g.ns, ews);
-          pf[p] = 1.0;
+        const int p = p0 + ln, ga = M->pair_a[p], gb = M->pair_b[p];
+        const Shape A{M->gtype[ga], Tg + 12 * ga, M->gparam[ga][0], M->gparam[ga][1], M->gparam[ga][2]};
+        const Shape Bs{M->gtype[gb], Tg + 12 * gb, M->gparam[gb][0], M->gparam[gb][1], M->gparam[gb][2]};
+        if (l == ln) epa_init(A, Bs, ews);
+        wsync();
+        for (int it = 0; it <= 255; ++it) {
+          const int stop = ews->stop;
+          double fdm = 1e300;
+          int fb = 0x7fffffff;
+          for (int f = l; f < ews->nf; f += 64)
+            if (ews->alive[f] && ews->fd[f] < fdm) {
+              fdm = ews->fd[f];
+              fb = f;
+            }
+          wave_argmin(fdm, fb);
+          if (stop || it == 255) {
+            if (l == ln) {
+              const double d = epa_finish(ews, fb == 0x7fffffff ? 0 : fb);
+              if (d < bestd || (d == bestd && p < besti)) {
+                bestd = d;
+                besti = p;
+                bpA = ld3(ews->out);
+                bpB = ld3(ews->out + 3);
+              }
+            }
+            break;
+          }
+          if (l == ln) epa_step(A, Bs, ews, fb);
+          wsync();
         }
+        wsync();
       }
     }
-    wsync();
     PH(5);
-    double bestd = 1.7976931348623157e308;
-    int besti = 0x7fffffff;
-    for (int p = l; p < M->npairs; p += 64)
-      if (pf[p] != 0.0 && pd[p] < bestd) {
-        bestd = pd[p];
-        besti = p;
-      }
+    const double myd = bestd;
+    const int myi = besti;
     wave_argmin(bestd, besti);
-    // witness points of the winner (recomputed by one lane: same arithmetic)
     double* dgv = S + kp.kdg;
     double* red = S + kp.oRed;
+    if (myi == besti && myi < M->npairs) {  // the winning lane publishes its witnesses
+      st3(red, bpA);
+      st3(red + 3, bpB);
+    }
     if (l == 0) {
       S[kp.oSc + SC_DIST] = bestd;
       S[kp.oSc + SC_PAIR] = besti;
-      V3 pA = v3(0, 0, 0), pB = v3(0, 0, 0);
-      if (besti < M->npairs) {
-        const int ga = M->pair_a[besti], gb = M->pair_b[besti];
-        Shape A{M->gtype[ga], Tg + 12 * ga, M->gparam[ga][0], M->gparam[ga][1], M->gparam[ga][2]};
-        Shape Bs{M->gtype[gb], Tg + 12 * gb, M->gparam[gb][0], M->gparam[gb][1], M->gparam[gb][2]};
-        if (A.type == kSphere || Bs.type == kSphere) {
-          sphere_pair(A, Bs, &pA, &pB);
-        } else {
-          GjkOut g = gjk(A, Bs, ews);
-          if (g.intersect) {
-            epa(A, Bs, g.ns, ews);
-            pA = ld3(ews->out);
-            pB = ld3(ews->out + 3);
-          } else {
-            pA = g.pA;
-            pB = g.pB;
-          }
-        }
-      }
-      st3(red, pA);
-      st3(red + 3, pB);
     }
+    (void)myd;
     wsync();
     PH(6);
     if (l < nv) {  // grad d = n^T (J_B(pB) - J_A(pA)), sign flipped when penetrating
@@ -1106,6 +1179,7 @@ __global__ void __launch_bounds__(64) task_kernel(const DevModel* __restrict__ M
 
 // QP kernel: assembles and solves the QP of each instance from the task data
 // written by task_kernel (same [field][B] buffers).
+template <class QD>
 __global__ void __launch_bounds__(64) qp_kernel(const DevModel* __restrict__ M, const KParams kp, const IO io) {
   extern __shared__ __attribute__((aligned(16))) double S[];
   const int l = lane_id();
@@ -1132,7 +1206,7 @@ __global__ void __launch_bounds__(64) qp_kernel(const DevModel* __restrict__ M, 
     wsync();
     const double bestd = S[kp.oSc + SC_DIST];
     // ---------------- QP assembly (QP_IK.cpp:69-131 / MoMa :59-128) --------
-    const int nx = kp.nx, ng = kp.ng, np = kp.np, m = kp.m;
+    const int nx = DNX, ng = DNG, np = DNP, m = DM;
     double *P = S + kp.oP, *G = S + kp.oG, *qq = S + kp.oQ, *ab = S + kp.oAB, *lo = S + kp.oL, *up = S + kp.oU;
     const double alpha = kp.alpha_cbf, man = S[kp.oSc + SC_MAN];
     double* Jt = S + kp.kJt;  // task Jacobian over the QP's task variables: 6 x np
@@ -1288,8 +1362,8 @@ __global__ void __launch_bounds__(64) qp_kernel(const DevModel* __restrict__ M, 
       }
       wsync();
       PH(1);
-      set_rho(kp, S, kp.s.rho);
-      factor_kinv(kp, S);
+      set_rho<QD>(kp, S, kp.s.rho);
+      factor_kinv<QD>(kp, S);
       if (l < nx) x[l] = 0.0;
       for (int row = l; row < m; row += 64) z[row] = y[row] = 0.0;
       wsync();
@@ -1305,14 +1379,24 @@ __global__ void __launch_bounds__(64) qp_kernel(const DevModel* __restrict__ M, 
         for (int row = l; row < m; row += 64) w[row] = rv[row] * z[row] - y[row];
         wsync();
         if (l < nx) {
-          double r = sig * x[l] - qq[l] + ab[l] * w[l];
-          for (int i = 0; i < ng; ++i) r += G[i * nx + l] * w[nx + i];
-          xt[l] = r;
+          double r0 = sig * x[l] - qq[l] + ab[l] * w[l], r1 = 0.0;
+#pragma unroll
+          for (int i = 0; i < ng; i += 2) {
+            r0 += G[i * nx + l] * w[nx + i];
+            if (i + 1 < ng) r1 += G[(i + 1) * nx + l] * w[nx + i + 1];
+          }
+          xt[l] = r0 + r1;
         }
         wsync();
         double xtil = 0;
         if (l < nx) {
-          for (int c = 0; c < nx; ++c) xtil += K[l * nx + c] * xt[c];
+          double a0 = 0, a1 = 0;
+#pragma unroll
+          for (int c = 0; c < nx; c += 2) {
+            a0 += K[l * nx + c] * xt[c];
+            if (c + 1 < nx) a1 += K[l * nx + c + 1] * xt[c + 1];
+          }
+          xtil = a0 + a1;
         }
         wsync();
         if (l < nx) xt[l] = xtil;
@@ -1330,8 +1414,13 @@ __global__ void __launch_bounds__(64) qp_kernel(const DevModel* __restrict__ M, 
         }
         if (l < ng) {
           const int row = nx + l;
-          double a = 0;
-          for (int j = 0; j < nx; ++j) a += G[l * nx + j] * xt[j];
+          double a0 = 0, a1 = 0;
+#pragma unroll
+          for (int j = 0; j < nx; j += 2) {
+            a0 += G[l * nx + j] * xt[j];
+            if (j + 1 < nx) a1 += G[l * nx + j + 1] * xt[j + 1];
+          }
+          const double a = a0 + a1;
           const double zr = al * a + (1 - al) * z[row];
           double zn = zr + y[row] / rv[row];
           zn = fmin(fmax(zn, lo[row]), up[row]);
@@ -1344,35 +1433,35 @@ __global__ void __launch_bounds__(64) qp_kernel(const DevModel* __restrict__ M, 
         PH(3);
         const bool check = kp.s.check_termination > 0 && it % kp.s.check_termination == 0;
         const bool adapt = kp.s.adaptive_rho && kp.s.adaptive_rho_interval > 0 && it % kp.s.adaptive_rho_interval == 0;
-        if (check || adapt) residuals(kp, S, x, z, y, kp.s.eps_abs, kp.s.eps_rel);
+        if (check || adapt) residuals<QD>(kp, S, x, z, y, kp.s.eps_abs, kp.s.eps_rel);
         if (check) {
           const bool conv = sc[SC_PRI] < sc[SC_EPSP] && sc[SC_DUA] < sc[SC_EPSD];
           // parity mode: a certified polish is exact whatever the ADMM
           // residual, so also try it every 4th check (slow-ADMM vertices)
           if (kp.s.exact && !conv && it % (4 * kp.s.check_termination) == 0) {
-            if (polish(kp, S, true)) {
+            if (polish<QD>(kp, S, true)) {
               status = DRC_STATUS_SOLVED;
               break;
             }
-            factor_kinv(kp, S);  // polish used the union region
-            residuals(kp, S, x, z, y, kp.s.eps_abs, kp.s.eps_rel);
+            factor_kinv<QD>(kp, S);  // polish used the union region
+            residuals<QD>(kp, S, x, z, y, kp.s.eps_abs, kp.s.eps_rel);
           }
           if (conv) {
             if (!kp.s.exact) {
               status = DRC_STATUS_SOLVED;
               break;
             }
-            if (polish(kp, S, true)) {
+            if (polish<QD>(kp, S, true)) {
               status = DRC_STATUS_SOLVED;
               break;
             }
-            factor_kinv(kp, S);  // polish used the union region
-            residuals(kp, S, x, z, y, kp.s.eps_fallback, kp.s.eps_fallback);
+            factor_kinv<QD>(kp, S);  // polish used the union region
+            residuals<QD>(kp, S, x, z, y, kp.s.eps_fallback, kp.s.eps_fallback);
             if (sc[SC_PRI] < sc[SC_EPSP] && sc[SC_DUA] < sc[SC_EPSD]) {
               status = DRC_STATUS_SOLVED;
               break;
             }
-          } else if (primal_infeasible(kp, S, kp.s.eps_prim_inf)) {
+          } else if (primal_infeasible<QD>(kp, S, kp.s.eps_prim_inf)) {
             status = DRC_STATUS_PRIMAL_INFEASIBLE;
             break;
           }
@@ -1384,14 +1473,14 @@ __global__ void __launch_bounds__(64) qp_kernel(const DevModel* __restrict__ M, 
           double rn = rho * sqrt(pr / (dr + kDivTol));
           rn = fmin(fmax(rn, kRhoMin), kRhoMax);
           if (rn > rho * kp.s.adaptive_rho_tolerance || rn < rho / kp.s.adaptive_rho_tolerance) {
-            set_rho(kp, S, rn);
-            factor_kinv(kp, S);
+            set_rho<QD>(kp, S, rn);
+            factor_kinv<QD>(kp, S);
           }
         }
       }
       PH(4);
       iters = it > kp.s.max_iter ? kp.s.max_iter : it;
-      if (status == DRC_STATUS_SOLVED && kp.s.polish && !kp.s.exact) polish(kp, S, false);
+      if (status == DRC_STATUS_SOLVED && kp.s.polish && !kp.s.exact) polish<QD>(kp, S, false);
     }
     PH(5);
     // ---------------- outputs (zero on failure, QP_IK.cpp:56-61) ------------
@@ -1419,7 +1508,7 @@ struct drc_model_impl {
   drc_kinematic_param kparam{};
   drc_joint_index jidx{};
   drc_actuator_index aidx{};
-  EpaWs* epa_ws = nullptr;
+  EpaPoly* epa_ws = nullptr;
   int64_t epa_count = 0;
   void* pool = nullptr;  // task data when the caller does not keep it
   int64_t pool_bytes = 0;
@@ -1693,7 +1782,7 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
     if (m->epa_count < grid_task) {
       if (m->epa_ws) HIP_TRY(hipFree(m->epa_ws));
       m->epa_ws = nullptr;
-      HIP_TRY(hipMalloc(&m->epa_ws, sizeof(EpaWs) * grid_task));
+      HIP_TRY(hipMalloc(&m->epa_ws, sizeof(EpaPoly) * grid_task));
       m->epa_count = grid_task;
     }
     const bool need_pool = !jac || !man || !dist || !xdd || !pair;
@@ -1715,8 +1804,20 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
                      static_cast<size_t>(kt.lds_doubles) * sizeof(double), st, m->d_model, kt, io);
   HIP_TRY(hipGetLastError());
   if (!stages) {
-    hipLaunchKernelGGL(qp_kernel, dim3(static_cast<unsigned>(grid)), dim3(64),
-                       static_cast<size_t>(kq.lds_doubles) * sizeof(double), st, m->d_model, kq, io);
+    const size_t lds = static_cast<size_t>(kq.lds_doubles) * sizeof(double);
+    const dim3 g(static_cast<unsigned>(grid)), blk(64);
+    // compile-time QP shapes of the bundled robots; anything else runs the
+    // runtime-sized instantiation
+    if (kq.nx == 23 && kq.ng == 16 && kq.np == 7)
+      hipLaunchKernelGGL((qp_kernel<Dims<23, 16, 7>>), g, blk, lds, st, m->d_model, kq, io);  // FR3
+    else if (kq.nx == 20 && kq.ng == 14 && kq.np == 6)
+      hipLaunchKernelGGL((qp_kernel<Dims<20, 14, 6>>), g, blk, lds, st, m->d_model, kq, io);  // UR5e
+    else if (kq.nx == 9 && kq.ng == 16 && kq.np == 9)
+      hipLaunchKernelGGL((qp_kernel<Dims<9, 16, 9>>), g, blk, lds, st, m->d_model, kq, io);  // Husky-FR3
+    else if (kq.nx == 11 && kq.ng == 16 && kq.np == 11)
+      hipLaunchKernelGGL((qp_kernel<Dims<11, 16, 11>>), g, blk, lds, st, m->d_model, kq, io);  // XLS-FR3
+    else
+      hipLaunchKernelGGL((qp_kernel<Dims<0, 0, 0>>), g, blk, lds, st, m->d_model, kq, io);
     HIP_TRY(hipGetLastError());
   }
   return DRC_OK;

@@ -410,8 +410,8 @@ static int gjk(const Shape* A, const Shape* B, SV* S, int* ns, double* lam, doub
     return 0;
 }
 
-#define EPA_MAXV 256
-#define EPA_MAXF 512
+#define EPA_MAXV 128
+#define EPA_MAXF 256
 /* Expanding polytope with face adjacency (Bullet/libccd style): the visible
  * region is flood-filled from the closest face across shared edges, so the
  * horizon is always a single loop and the polytope stays a valid closed
@@ -422,12 +422,16 @@ typedef struct Epa {
     int nv, nf, pass;
     int fv[EPA_MAXF][3], ff[EPA_MAXF][3], fe[EPA_MAXF][3], fpass[EPA_MAXF], alive[EPA_MAXF];
     double fn[EPA_MAXF][3], fd[EPA_MAXF];
-    int hcf, hff, hnf, fail;
+    int freel[EPA_MAXF], deadl[EPA_MAXF], newl[EPA_MAXF];  /* recycled slots; this pass's kills / births */
+    int hcf, hff, hnf, fail, nfree, ndead, nnew;
 } Epa;
 
 static int epa_newface(Epa* E, int a, int b, int c) {
-    if (E->nf >= EPA_MAXF) { E->fail = 1; return -1; }
-    int f = E->nf++;
+    int f;
+    if (E->nfree > 0) f = E->freel[--E->nfree];
+    else if (E->nf < EPA_MAXF) f = E->nf++;
+    else { E->fail = 1; return -1; }
+    E->newl[E->nnew++] = f;
     E->fv[f][0] = a; E->fv[f][1] = b; E->fv[f][2] = c;
     E->alive[f] = 1; E->fpass[f] = 0;
     double e1[3], e2[3], nn[3];
@@ -462,6 +466,7 @@ static int epa_expand(Epa* E, int w, int f, int e) {
     E->fpass[f] = E->pass;
     if (epa_expand(E, w, E->ff[f][e1], E->fe[f][e1]) && epa_expand(E, w, E->ff[f][e2], E->fe[f][e2])) {
         E->alive[f] = 0;
+        E->deadl[E->ndead++] = f;
         return 1;
     }
     return 0;
@@ -470,7 +475,7 @@ static int epa_expand(Epa* E, int w, int f, int e) {
 static double epa(const Shape* A, const Shape* B, SV* S, int ns, double* pA, double* pB) {
     static const double dirs[6][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}, {-1, 0, 0}, {0, -1, 0}, {0, 0, -1}};
     static __thread Epa E;
-    E.nv = ns; E.nf = 0; E.pass = 0; E.fail = 0;
+    E.nv = ns; E.nf = 0; E.pass = 0; E.fail = 0; E.nfree = 0; E.nnew = 0;
     for (int i = 0; i < ns; ++i) E.V[i] = S[i];
     for (int di = 0; di < 6 && E.nv < 4; ++di) {
         SV w;
@@ -512,16 +517,22 @@ static double epa(const Shape* A, const Shape* B, SV* S, int ns, double* pA, dou
             int wi = E.nv;
             E.V[E.nv++] = w;
             E.pass++;
-            E.hcf = -1; E.hff = -1; E.hnf = 0;
+            E.hcf = -1; E.hff = -1; E.hnf = 0; E.ndead = 0; E.nnew = 0;
             E.fpass[best] = E.pass;
             int valid = 1;
             for (int j = 0; j < 3 && valid; ++j) valid = epa_expand(&E, wi, E.ff[best][j], E.fe[best][j]);
-            if (!valid || E.hnf < 3 || E.fail) { E.nv--; break; }  /* keep the last consistent polytope */
+            if (!valid || E.hnf < 3 || E.fail) {  /* roll back to the last closed polytope */
+                for (int i = 0; i < E.nnew; ++i) E.alive[E.newl[i]] = 0;
+                for (int i = 0; i < E.ndead; ++i) E.alive[E.deadl[i]] = 1;
+                E.nv--;
+                break;
+            }
             epa_bind(&E, E.hcf, 1, E.hff, 2);
             E.alive[best] = 0;
+            for (int i = 0; i < E.ndead; ++i) E.freel[E.nfree++] = E.deadl[i];
+            E.freel[E.nfree++] = best;
         }
     }
-    if (getenv("ORC_DEBUG")) fprintf(stderr, "epa exit nvx %d nf %d fail %d\n", E.nv, E.nf, E.fail);
     double bd = INFINITY;
     best = 0;
     for (int f = 0; f < E.nf; ++f)
@@ -1369,6 +1380,16 @@ void oracle_pair_distance(const OracleModel* m, const double* q, int pair, doubl
     Shape a, b;
     make_shape(m, &k, m->pair_a[pair], &a);
     make_shape(m, &k, m->pair_b[pair], &b);
+    *d = shape_distance(&a, &b, pA, pB);
+}
+/* narrow phase on two free shapes (T: R row-major then p), for checking the
+ * device narrow-phase code in isolation */
+void oracle_shape_distance(int ta, const double* TA, const double* prmA, int tb, const double* TB,
+                           const double* prmB, double* d, double* pA, double* pB) {
+    Shape a, b;
+    a.type = ta; b.type = tb;
+    memcpy(a.T, TA, sizeof(a.T)); memcpy(b.T, TB, sizeof(b.T));
+    memcpy(a.prm, prmA, sizeof(a.prm)); memcpy(b.prm, prmB, sizeof(b.prm));
     *d = shape_distance(&a, &b, pA, pB);
 }
 void oracle_manipulability(const OracleModel* m, const double* q, double* man, double* grad) {

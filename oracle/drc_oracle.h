@@ -118,6 +118,8 @@ int64_t oracle_qpik_batch(const OracleModel* m, const OracleParams* p, int64_t B
 void oracle_fk_pose(const OracleModel* m, const double* q, double* pose12, double* J6xn);
 void oracle_min_distance(const OracleModel* m, const double* q, double* dist, double* grad, int* pair);
 void oracle_pair_distance(const OracleModel* m, const double* q, int pair, double* d, double* pA, double* pB);
+void oracle_shape_distance(int ta, const double* TA, const double* prmA, int tb, const double* TB,
+                           const double* prmB, double* d, double* pA, double* pB);
 void oracle_manipulability(const OracleModel* m, const double* q, double* man, double* grad);
 int oracle_solve_qp(int nx, int nc, const double* P, const double* qv, const double* A,
                     const double* l, const double* u, const OracleSettings* s,

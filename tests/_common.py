@@ -2,6 +2,7 @@
 import numpy as np
 
 import oracle as O
+import pyref as R
 from dyros_robot_controller_amd import manipulator, robot_path, workload, _batch, _capi
 
 LINK = {"fr3": "fr3_link8", "ur5e": "tool0", "husky_fr3": "fr3_link8", "xls_fr3": "fr3_link8"}
@@ -19,6 +20,25 @@ def stage_pose(model, device, q, qd, link):
     st = _batch.stages_batch(model, p, _batch.as_device(q, device), _batch.as_device(qd, device), None,
                              _batch.as_device(np.zeros((6, B)), device))
     return {k: v.cpu().numpy() for k, v in st.items()}
+
+
+def stage_step(model, device, q, qd, xt, xdt, link):
+    """Stage outputs of the QPIKStep pipeline (same params as the solve)."""
+    pb = manipulator.QPIKParamsBuilder(model, exact=True)
+    p = pb.params(link, _capi.MODE_QPIK_STEP)
+    st = _batch.stages_batch(model, p, _batch.as_device(q, device), _batch.as_device(qd, device),
+                             _batch.as_device(xt, device), _batch.as_device(xdt, device))
+    return {k: v.cpu().numpy() for k, v in st.items()}
+
+
+def qp_from_stages(pm, q, st, b, link):
+    """Exact optimum (numpy IPM, oracle/pyref.py) of the manipulator QP built
+    from one instance's device stage data (QP_IK.cpp:59-128)."""
+    man = (st["man"][0, b], st["man"][1:, b])
+    dist = (st["dist"][0, b], st["dist"][1:, b])
+    P, qv, A, l, u = R.build_qp_manipulator(pm, q[:, b], st["xdot_des"][:, b], link, man=man, dist=dist)
+    x, _, status = R.solve_qp_exact(P, qv, A, l, u)
+    return x[:pm.nv] if x is not None else None
 
 
 def step_inputs(rd, robot, seed, B, device, offset=0):

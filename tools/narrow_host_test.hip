@@ -1,11 +1,12 @@
-// Host-side harness for the device narrow-phase code (runs on CPU, no GPU):
-// reads "type T(12) prm(3)" pairs on stdin, prints d pA pB.
+// Host-side harness for the device narrow-phase code (compiled for the CPU,
+// no GPU needed): reads "type T(12) prm(3)" pairs on stdin, prints d pA pB.
+// Used by tests/test_narrow_host.py to check qpik_device.hpp against the
+// oracle's shape_distance.
 #include <cstdio>
-#include <vector>
 #include "../dyros_robot_controller_amd/csrc/qpik_device.hpp"
 using namespace drc_amd;
 int main() {
-  static EpaWs ws;
+  static EpaPoly ws;
   int ta, tb;
   double TA[12], TB[12], pa[3], pb[3];
   while (scanf("%d", &ta) == 1) {
@@ -20,9 +21,9 @@ int main() {
     if (ta == kSphere || tb == kSphere) {
       d = sphere_pair(A, B, &pA, &pB);
     } else {
-      GjkOut g = gjk(A, B, &ws);
+      const GjkDist g = gjk(A, B);
       if (g.intersect) {
-        d = epa(A, B, g.ns, &ws);
+        d = epa_serial(A, B, &ws);
         pA = ld3(ws.out);
         pB = ld3(ws.out + 3);
       } else {
