@@ -76,8 +76,9 @@ def cpu_baseline(robot, q, qd, xt, xdt, budget_s=1.5):
 
 
 def load_traffic(robot, B):
-    """Per-launch HBM bytes from the committed rocprofv3 PMC summary
-    (tools/collect_pmc.sh), if it matches this workload; else None."""
+    """HBM bytes per drc_qpik_batch call (both kernels) from the committed
+    rocprofv3 PMC summary (tools/pmc_summary.py), if it matches this workload
+    and this build; else None."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as fh:
@@ -123,9 +124,15 @@ def main():
     def step():
         return ctrl.QPIK_step_batch(dq, dqd, dxt, dxdt, link, iters=iters)
 
+    from dyros_robot_controller_amd import _capi
+    import ctypes as C
+    handle = rd.model.handle
     for _ in range(args.warmup):
         out, status = step()
     torch.cuda.synchronize()
+    # per-kernel durations: HIP events recorded by the library on the launch
+    # stream around task_kernel and qp_kernel of every timed step
+    _capi.check(_capi.lib().drc_debug_kernel_timing(handle, 1))
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -140,7 +147,12 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
-    kernel_ms = ev0.elapsed_time(ev1) / args.steps   # HIP events on the launch stream
+    step_event_ms = ev0.elapsed_time(ev1) / args.steps   # HIP events on the launch stream
+    tk, tq, nc = C.c_double(), C.c_double(), C.c_int()
+    _capi.check(_capi.lib().drc_debug_kernel_times(handle, C.byref(tk), C.byref(tq), C.byref(nc)))
+    _capi.check(_capi.lib().drc_debug_kernel_timing(handle, 0))
+    task_ms, qp_ms = tk.value / max(nc.value, 1), tq.value / max(nc.value, 1)
+    kernel_ms = task_ms + qp_ms
     t = torch.tensor([wall], dtype=torch.float64, device=dev)
     n_bad = torch.tensor([float((status != 1).sum().item())], dtype=torch.float64, device=dev)
     it_mean = torch.tensor([float(iters.double().mean().item())], dtype=torch.float64, device=dev)
@@ -171,8 +183,10 @@ def main():
                        "parallelism": "dp%d (instances sharded, no data-path collective)" % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "drc_qpik_batch step = task_kernel + qp_kernel (one stream)",
-                         "bytes_per_solve": algorithmic_bytes(nv), "kernel_ms": kernel_ms,
+                         "kernel": "drc_qpik_batch = task_kernel + qp_kernel (one stream, one launch each)",
+                         "bytes_per_solve": algorithmic_bytes(nv), "bytes_per_launch": per_launch_bytes,
+                         "kernel_ms": kernel_ms, "task_kernel_ms": task_ms, "qp_kernel_ms": qp_ms,
+                         "step_event_ms": step_event_ms,
                          "fp64_valu_estimate": {"achieved_tflops": fl, "peak_tflops": FP64_VECTOR_PEAK_TFS,
                                                 "frac": fl / FP64_VECTOR_PEAK_TFS,
                                                 "flops_per_solve": flops_per_solve(nv, it_mean.item())}},

@@ -35,8 +35,8 @@ MAX_WHEELS = 8
 EXPORTED_SYMBOLS = (
     "drc_model_create_manipulator", "drc_model_create_mobile_manipulator", "drc_model_destroy",
     "drc_model_info", "drc_model_limits", "drc_model_find_frame", "drc_model_mobile_fk_jacobian",
-    "drc_default_qpik_params", "drc_qpik_batch", "drc_qpik_stages_batch", "drc_error_string",
-    "drc_last_error",
+    "drc_default_qpik_params", "drc_qpik_batch", "drc_qpik_stages_batch", "drc_debug_kernel_timing",
+    "drc_debug_kernel_times", "drc_error_string", "drc_last_error",
 )
 
 
@@ -120,6 +120,8 @@ def _load():
     lib.drc_qpik_batch.argtypes = [vp, C.POINTER(QPIKParams), C.c_int64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     lib.drc_qpik_stages_batch.argtypes = [vp, C.POINTER(QPIKParams), C.c_int64, vp, vp, vp, vp, vp, vp,
                                           vp, vp, vp, vp, vp, vp, vp]
+    lib.drc_debug_kernel_timing.argtypes = [vp, C.c_int]
+    lib.drc_debug_kernel_times.argtypes = [vp, dp, dp, ip]
     for name in EXPORTED_SYMBOLS:
         if name not in ("drc_model_destroy", "drc_error_string", "drc_last_error"):
             getattr(lib, name).restype = C.c_int

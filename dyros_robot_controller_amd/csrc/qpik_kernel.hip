@@ -20,6 +20,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <vector>
 
 #include "../../include/drc_amd.h"
 #include "model.hpp"
@@ -35,6 +36,8 @@ struct KParams {
   double frame_place[12];
   int frame_joint, mode, stages;
   int nv, nx, ng, np, na, m, narm, c0;
+  int xcd_map;                         // XCD-aware instance order (grid % 8 == 0)
+  int rJac, rMan, rDist, rXdd, rQ, rLen;  // per-instance task record (doubles)
   drc_solver_settings s;
   // persistent QP region
   int oP, oG, oQ, oAB, oL, oU, oD, oE, oRho, oX, oZ, oY, oDY, oXT, oZT, oT1, oT2, oRed, oSc;
@@ -449,6 +452,116 @@ __device__ __forceinline__ bool primal_infeasible(const KParams& kp, double* S, 
   return viol < eps * nrm;
 }
 
+// ------------------------------------------------------------------------
+// Register-resident ADMM (compile-time QP shapes).  Per iteration
+//   rhs = sigma x - q + A^T (rho z - y),  x~ = K^-1 rhs,  G x~ = (G K^-1) rhs,
+// so two broadcast passes (the G-row duals, then rhs) give x~ and the G-row
+// values together.  Lane l keeps column l of G and rows l of K^-1 and
+// G K^-1 in VGPRs; the vectors move by v_readlane (no LDS traffic inside
+// the iteration).  Same algebra as the LDS path, different summation order.
+// ------------------------------------------------------------------------
+__device__ __forceinline__ double bcast(double v, int lane) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane(static_cast<int>(b), lane);
+  const int hi = __builtin_amdgcn_readlane(static_cast<int>(b >> 32), lane);
+  return __hiloint2double(hi, lo);
+}
+
+// G K^-1 (NG x NX) into LDS after K^-1 (once per factorisation; out of line
+// so the ADMM loop's register file stays free)
+template <class QD>
+__device__ __noinline__ void prep_admm_mats(const KParams& kp, double* S) {
+  constexpr int NX = QD::nx, NG = QD::ng;
+  const int l = lane_id();
+  const double* K = S + kp.oU0;
+  double* GK = S + kp.oU0 + NX * NX;
+  const double* G = S + kp.oG;
+  for (int e = l; e < NG * NX; e += 64) {
+    const int i = e / NX, c = e % NX;
+    double s = 0;
+    for (int k = 0; k < NX; ++k) s += G[i * NX + k] * K[k * NX + c];
+    GK[e] = s;
+  }
+  wsync();
+}
+
+// lane l: column l of G (rhs), row l of K^-1 (x~), row l of G K^-1 (G x~)
+template <class QD>
+__device__ __forceinline__ void load_admm_regs(const KParams& kp, const double* S, double (&Gc)[QD::ng],
+                                               double (&Kr)[QD::nx], double (&GKr)[QD::nx]) {
+  constexpr int NX = QD::nx, NG = QD::ng;
+  const int l = lane_id();
+  const double* K = S + kp.oU0;
+  const double* GK = S + kp.oU0 + NX * NX;
+  const double* G = S + kp.oG;
+  const int lb = l < NX ? l : 0, lg = l < NG ? l : 0;
+#pragma unroll
+  for (int i = 0; i < NG; ++i) Gc[i] = G[i * NX + lb];
+#pragma unroll
+  for (int c = 0; c < NX; ++c) Kr[c] = K[lb * NX + c];
+#pragma unroll
+  for (int c = 0; c < NX; ++c) GKr[c] = GK[lg * NX + c];
+}
+
+// Termination / polish / adaptive-rho block of the register ADMM, out of
+// line (runs every check_termination iterations).  Works on the published
+// LDS iterate.  Returns 0 = continue, 1 = continue after reloading the
+// registers (K^-1 or rho changed, or the iterate was touched), 2 = stop.
+template <class QD>
+__device__ __noinline__ int admm_check(const KParams& kp, double* S, int it, int check, int adapt, int* status) {
+  double *x = S + kp.oX, *z = S + kp.oZ, *y = S + kp.oY, *sc = S + kp.oSc;
+  int reload = 0;
+  residuals<QD>(kp, S, x, z, y, kp.s.eps_abs, kp.s.eps_rel);
+  if (check) {
+    const bool conv = sc[SC_PRI] < sc[SC_EPSP] && sc[SC_DUA] < sc[SC_EPSD];
+    // parity mode: a certified polish is exact whatever the ADMM residual,
+    // so also try it every 4th check (slow-ADMM vertices)
+    if (kp.s.exact && !conv && it % (4 * kp.s.check_termination) == 0) {
+      if (polish<QD>(kp, S, true)) {
+        *status = DRC_STATUS_SOLVED;
+        return 2;
+      }
+      factor_kinv<QD>(kp, S);  // polish used the union region
+      residuals<QD>(kp, S, x, z, y, kp.s.eps_abs, kp.s.eps_rel);
+      reload = 1;
+    }
+    if (conv) {
+      if (!kp.s.exact) {
+        *status = DRC_STATUS_SOLVED;
+        return 2;
+      }
+      if (polish<QD>(kp, S, true)) {
+        *status = DRC_STATUS_SOLVED;
+        return 2;
+      }
+      factor_kinv<QD>(kp, S);
+      residuals<QD>(kp, S, x, z, y, kp.s.eps_fallback, kp.s.eps_fallback);
+      if (sc[SC_PRI] < sc[SC_EPSP] && sc[SC_DUA] < sc[SC_EPSD]) {
+        *status = DRC_STATUS_SOLVED;
+        return 2;
+      }
+      reload = 1;
+    } else if (primal_infeasible<QD>(kp, S, kp.s.eps_prim_inf)) {
+      *status = DRC_STATUS_PRIMAL_INFEASIBLE;
+      return 2;
+    }
+  }
+  if (adapt) {
+    const double pr = sc[SC_PRIS] / (fmax(sc[SC_NAX], sc[SC_NZ]) + kDivTol);
+    const double dr = sc[SC_DUAS] / (fmax(fmax(sc[SC_NQ], sc[SC_NATY]), sc[SC_NPX]) + kDivTol);
+    const double rho = sc[SC_RHO];
+    double rn = rho * sqrt(pr / (dr + kDivTol));
+    rn = fmin(fmax(rn, kRhoMin), kRhoMax);
+    if (rn > rho * kp.s.adaptive_rho_tolerance || rn < rho / kp.s.adaptive_rho_tolerance) {
+      set_rho<QD>(kp, S, rn);
+      factor_kinv<QD>(kp, S);
+      reload = 1;
+    }
+  }
+  if (reload) prep_admm_mats<QD>(kp, S);
+  return reload;
+}
+
 // argmax with ties toward the smaller index (row order of the oracle scans)
 __device__ __forceinline__ void wave_argmax(double& v, int& idx) {
   double nv = -v;
@@ -756,6 +869,26 @@ __device__ __forceinline__ bool polish(const KParams& kp, double* S, bool strict
 // ------------------------------------------------------------------------
 // the fused per-instance solve
 // ------------------------------------------------------------------------
+// Instance order.  With xcd_map, the instances of each 128-B line of a
+// [field][B] row (16 doubles) are handled by workgroups of one XCD (blocks
+// are dealt to the 8 XCDs round-robin), so a line is fetched once per L2 and
+// stores to it merge there before write-back; otherwise plain grid-stride.
+// Placement only affects speed, never which instances run.
+struct InstSeq {
+  int64_t j0, step, n;
+  int xcd, map;
+  __device__ __forceinline__ InstSeq(int64_t B, int map_) {
+    map = map_;
+    xcd = blockIdx.x & 7;
+    j0 = map ? (blockIdx.x >> 3) : blockIdx.x;
+    step = map ? (gridDim.x >> 3) : gridDim.x;
+    n = map ? ((B + 127) >> 7) << 4 : B;
+  }
+  __device__ __forceinline__ int64_t at(int64_t j) const {
+    return map ? ((((j >> 4) << 3) + xcd) << 4) + (j & 15) : j;
+  }
+};
+
 struct IO {
   int64_t B;
   const double *q, *qdot, *xt, *xdt, *xi, *xdi;
@@ -763,6 +896,8 @@ struct IO {
   int32_t *status, *iters;
   double *st_pose, *st_jac, *st_man, *st_dist, *st_xdd;
   int32_t* st_pair;
+  double* rec;  // product path: per-instance task record [B][rec_stride] (coalesced)
+  int64_t rec_stride;
   EpaPoly* epa_ws;
 };
 
@@ -771,14 +906,21 @@ struct IO {
 #ifndef DRC_TASK_WAVES
 #define DRC_TASK_WAVES 2
 #endif
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRC_TASK_WAVES, 8))) task_kernel(const DevModel* __restrict__ M, const KParams kp, const IO io) {
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRC_TASK_WAVES, 8))) task_kernel(const DevModel* __restrict__ M0, const KParams kp, const IO io) {
   extern __shared__ __attribute__((aligned(16))) double S[];
   const int l = lane_id();
   const int nv = kp.nv;
   const int64_t B = io.B;
   EpaPoly* ews = io.epa_ws + blockIdx.x;
   PH_DECL
-  for (int64_t b = blockIdx.x; b < B; b += gridDim.x) {
+  const InstSeq seq(B, kp.xcd_map);
+  for (int64_t j = seq.j0; j < seq.n; j += seq.step) {
+    const int64_t b = seq.at(j);
+    if (b >= B) continue;
+    // re-derive the model pointer each instance: keeps LICM from hoisting
+    // model-constant loads out of the instance loop into spilled registers
+    const DevModel* M = M0;
+    asm volatile("" : "+s"(M));
     // ---------------- state in ----------------
     double* qv = S + kp.kq;
     double* qd = S + kp.kqd;
@@ -1159,337 +1301,492 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRC_TAS
     }
     wsync();
     PH(7);
-    // ---------------- task data out (HBM, [field][B]) -----------------------
-    if (io.st_pose && l < 12) {
-      // R row-major -> column-major storage, then p
-      double v = l < 9 ? Te[(l % 3) * 3 + l / 3] : Te[l];
-      io.st_pose[l * B + b] = v;
+    // ---------------- task data out -----------------------------------------
+    if (io.rec) {  // product path: one coalesced record per instance
+      double* rec = io.rec + b * io.rec_stride;
+      for (int e = l; e < kp.rLen; e += 64) {
+        double v;
+        if (e < kp.rMan) v = J[e];
+        else if (e == kp.rMan) v = S[kp.oSc + SC_MAN];
+        else if (e < kp.rDist) v = mg[e - kp.rMan - 1];
+        else if (e == kp.rDist) v = bestd;
+        else if (e < kp.rXdd) v = dgv[e - kp.rDist - 1];
+        else if (e < kp.rQ) v = xdd[e - kp.rXdd];
+        else v = qv[e - kp.rQ];
+        rec[e] = v;
+      }
+    } else {  // stage outputs, [field][B]
+      if (io.st_pose && l < 12) {
+        // R row-major -> column-major storage, then p
+        double v = l < 9 ? Te[(l % 3) * 3 + l / 3] : Te[l];
+        io.st_pose[l * B + b] = v;
+      }
+      if (io.st_jac)
+        for (int e = l; e < 6 * nv; e += 64) io.st_jac[(int64_t)e * B + b] = J[e];
+      if (io.st_man) {
+        if (l == 0) io.st_man[b] = S[kp.oSc + SC_MAN];
+        if (l < narm) io.st_man[(int64_t)(1 + l) * B + b] = mg[l];
+      }
+      if (io.st_dist) {
+        if (l == 0) io.st_dist[b] = bestd;
+        if (l < nv) io.st_dist[(int64_t)(1 + l) * B + b] = dgv[l];
+      }
+      if (io.st_pair && l == 0) io.st_pair[b] = besti < M->npairs ? besti : -1;
+      if (io.st_xdd && l < 6) io.st_xdd[l * B + b] = xdd[l];
     }
-    for (int e = l; e < 6 * nv; e += 64) io.st_jac[(int64_t)e * B + b] = J[e];
-    if (l == 0) io.st_man[b] = S[kp.oSc + SC_MAN];
-    if (l < narm) io.st_man[(int64_t)(1 + l) * B + b] = mg[l];
-    if (l == 0) io.st_dist[b] = bestd;
-    if (l < nv) io.st_dist[(int64_t)(1 + l) * B + b] = dgv[l];
-    if (l == 0) io.st_pair[b] = besti < M->npairs ? besti : -1;
-    if (l < 6) io.st_xdd[l * B + b] = xdd[l];
     wsync();
   }
   PH_FLUSH(0);
 }
 
-// QP kernel: assembles and solves the QP of each instance from the task data
-// written by task_kernel (same [field][B] buffers).
+// ---- QP kernel phases ------------------------------------------------------
 template <class QD>
-__global__ void __launch_bounds__(64) qp_kernel(const DevModel* __restrict__ M, const KParams kp, const IO io) {
-  extern __shared__ __attribute__((aligned(16))) double S[];
+__device__ __forceinline__ void qp_assemble(const DevModel* M, const KParams& kp, double* S, const IO& io, int64_t b) {
   const int l = lane_id();
   const int nv = kp.nv, narm = kp.narm;
-  const int64_t B = io.B;
-  PH_DECL
-  for (int64_t b = blockIdx.x; b < B; b += gridDim.x) {
-    double* qv = S + kp.kq;
-    double* J = S + kp.kJ;
-    double* xdd = S + kp.kxdd;
-    double* mg = S + kp.kmg;
-    double* dgv = S + kp.kdg;
-    if (l < nv) {
-      qv[l] = io.q[l * B + b];
-      dgv[l] = io.st_dist[(int64_t)(1 + l) * B + b];
+  double* qv = S + kp.kq;
+  double* J = S + kp.kJ;
+  double* xdd = S + kp.kxdd;
+  double* mg = S + kp.kmg;
+  double* dgv = S + kp.kdg;
+  {  // task record written by task_kernel (one coalesced read)
+    const double* rec = io.rec + b * io.rec_stride;
+    for (int e = l; e < kp.rLen; e += 64) {
+      const double v = rec[e];
+      if (e < kp.rMan) J[e] = v;
+      else if (e == kp.rMan) S[kp.oSc + SC_MAN] = v;
+      else if (e < kp.rDist) mg[e - kp.rMan - 1] = v;
+      else if (e == kp.rDist) S[kp.oSc + SC_DIST] = v;
+      else if (e < kp.rXdd) dgv[e - kp.rDist - 1] = v;
+      else if (e < kp.rQ) xdd[e - kp.rXdd] = v;
+      else qv[e - kp.rQ] = v;
     }
-    for (int e = l; e < 6 * nv; e += 64) J[e] = io.st_jac[(int64_t)e * B + b];
-    if (l < narm) mg[l] = io.st_man[(int64_t)(1 + l) * B + b];
-    if (l < 6) xdd[l] = io.st_xdd[l * B + b];
-    if (l == 0) {
-      S[kp.oSc + SC_MAN] = io.st_man[b];
-      S[kp.oSc + SC_DIST] = io.st_dist[b];
-    }
-    wsync();
-    const double bestd = S[kp.oSc + SC_DIST];
-    // ---------------- QP assembly (QP_IK.cpp:69-131 / MoMa :59-128) --------
-    const int nx = DNX, ng = DNG, np = DNP, m = DM;
-    double *P = S + kp.oP, *G = S + kp.oG, *qq = S + kp.oQ, *ab = S + kp.oAB, *lo = S + kp.oL, *up = S + kp.oU;
-    const double alpha = kp.alpha_cbf, man = S[kp.oSc + SC_MAN];
-    double* Jt = S + kp.kJt;  // task Jacobian over the QP's task variables: 6 x np
-    if (M->kind == 0) {
-      for (int e = l; e < 6 * np; e += 64) Jt[e] = J[(e / np) * nv + e % np];
-    } else {
-      // J~ = J S  (mobile_manipulator/robot_data.cpp:407-410); S virtual block = Rz(yaw) J_mobile
-      const double yaw = qv[M->virtual_start + 2], cy = cos(yaw), sy = sin(yaw);
-      for (int e = l; e < 6 * np; e += 64) {
-        const int r = e / np, a = e % np;
-        double v = 0;
-        const int am = a - M->act_mani_start, aw = a - M->act_mobi_start;
-        if (am >= 0 && am < M->n_arm) {
-          v = J[r * nv + M->mani_start + am];
-        } else if (aw >= 0 && aw < M->n_wheel) {
-          const double s0 = cy * M->J_mobile[0][aw] - sy * M->J_mobile[1][aw];
-          const double s1 = sy * M->J_mobile[0][aw] + cy * M->J_mobile[1][aw];
-          const double s2 = M->J_mobile[2][aw];
-          const int vs = M->virtual_start;
-          v = J[r * nv + M->mobi_start + aw] + J[r * nv + vs] * s0 + J[r * nv + vs + 1] * s1 + J[r * nv + vs + 2] * s2;
-        }
-        Jt[e] = v;
+  }
+  wsync();
+  const double bestd = S[kp.oSc + SC_DIST];
+  // ---------------- QP assembly (QP_IK.cpp:69-131 / MoMa :59-128) --------
+  const int nx = DNX, ng = DNG, np = DNP, m = DM;
+  double *P = S + kp.oP, *G = S + kp.oG, *qq = S + kp.oQ, *ab = S + kp.oAB, *lo = S + kp.oL, *up = S + kp.oU;
+  const double alpha = kp.alpha_cbf, man = S[kp.oSc + SC_MAN];
+  double* Jt = S + kp.kJt;  // task Jacobian over the QP's task variables: 6 x np
+  if (M->kind == 0) {
+    for (int e = l; e < 6 * np; e += 64) Jt[e] = J[(e / np) * nv + e % np];
+  } else {
+    // J~ = J S  (mobile_manipulator/robot_data.cpp:407-410); S virtual block = Rz(yaw) J_mobile
+    const double yaw = qv[M->virtual_start + 2], cy = cos(yaw), sy = sin(yaw);
+    for (int e = l; e < 6 * np; e += 64) {
+      const int r = e / np, a = e % np;
+      double v = 0;
+      const int am = a - M->act_mani_start, aw = a - M->act_mobi_start;
+      if (am >= 0 && am < M->n_arm) {
+        v = J[r * nv + M->mani_start + am];
+      } else if (aw >= 0 && aw < M->n_wheel) {
+        const double s0 = cy * M->J_mobile[0][aw] - sy * M->J_mobile[1][aw];
+        const double s1 = sy * M->J_mobile[0][aw] + cy * M->J_mobile[1][aw];
+        const double s2 = M->J_mobile[2][aw];
+        const int vs = M->virtual_start;
+        v = J[r * nv + M->mobi_start + aw] + J[r * nv + vs] * s0 + J[r * nv + vs + 1] * s1 + J[r * nv + vs + 2] * s2;
       }
+      Jt[e] = v;
     }
-    wsync();
-    for (int e = l; e < np * np; e += 64) {
-      const int i = e / np, j = e % np;
+  }
+  wsync();
+  for (int e = l; e < np * np; e += 64) {
+    const int i = e / np, j = e % np;
+    double s = 0;
+    for (int r = 0; r < 6; ++r) s += Jt[r * np + i] * Jt[r * np + j];
+    P[e] = 2.0 * s + (i == j ? kp.w_reg : 0.0);
+  }
+  for (int e = l; e < ng * nx; e += 64) G[e] = 0.0;
+  if (l < nx) {
+    double qi;
+    if (l < np) {
       double s = 0;
-      for (int r = 0; r < 6; ++r) s += Jt[r * np + i] * Jt[r * np + j];
-      P[e] = 2.0 * s + (i == j ? kp.w_reg : 0.0);
+      for (int r = 0; r < 6; ++r) s += Jt[r * np + l] * xdd[r];
+      qi = -2.0 * s;
+    } else {
+      qi = kp.slack_w;
     }
-    for (int e = l; e < ng * nx; e += 64) G[e] = 0.0;
-    if (l < nx) {
-      double qi;
-      if (l < np) {
+    qq[l] = qi;
+    ab[l] = 1.0;
+    if (M->kind == 0) {
+      lo[l] = l < nv ? -M->vel[l] : 0.0;
+      up[l] = l < nv ? M->vel[l] : kInf;
+    } else {  // setBoundConstraint is a no-op for MoMa (QP_IK.cpp:75-83)
+      lo[l] = -kInf;
+      up[l] = kInf;
+    }
+  }
+  wsync();
+  if (l < ng) {
+    const int n = narm, row = nx + l;
+    double lval = 0;
+    const int vo = M->kind == 0 ? 0 : M->act_mani_start;  // task-variable offset of the arm
+    const int qo = M->kind == 0 ? 0 : M->mani_start;      // joint offset of the arm
+    if (l < n) {
+      G[l * nx + vo + l] = 1.0;
+      if (M->kind == 0) G[l * nx + n + l] = 1.0;
+      lval = -alpha * (qv[qo + l] - M->lower[qo + l]);
+    } else if (l < 2 * n) {
+      const int i = l - n;
+      G[l * nx + vo + i] = -1.0;
+      if (M->kind == 0) G[l * nx + 2 * n + i] = 1.0;
+      lval = -alpha * (M->upper[qo + i] - qv[qo + i]);
+    } else if (l == 2 * n) {
+      for (int c = 0; c < n; ++c) G[l * nx + vo + c] = mg[c];
+      if (M->kind == 0) G[l * nx + 3 * n] = 1.0;
+      lval = -alpha * (man - kp.man_min);
+    } else {
+      for (int c = 0; c < n; ++c) G[l * nx + vo + c] = dgv[qo + c];
+      if (M->kind == 0) G[l * nx + 3 * n + 1] = 1.0;
+      lval = -alpha * (bestd - kp.dist_min);
+    }
+    lo[row] = lval;
+    up[row] = kInf;
+  }
+  wsync();
+}
+
+// finiteness check + Ruiz equilibration (OSQP scaling.c); returns
+// DRC_STATUS_NONFINITE or DRC_STATUS_MAX_ITER (= not yet solved)
+template <class QD>
+__device__ __forceinline__ int qp_scale(const KParams& kp, double* S) {
+  const int l = lane_id();
+  const int nx = DNX, ng = DNG, np = DNP, m = DM;
+  double *P = S + kp.oP, *G = S + kp.oG, *qq = S + kp.oQ, *ab = S + kp.oAB, *lo = S + kp.oL, *up = S + kp.oU;
+  int status = DRC_STATUS_MAX_ITER;
+  {
+    bool finite = true;
+    for (int e = l; e < np * np; e += 64) finite &= isfinite(P[e]);
+    for (int e = l; e < ng * nx; e += 64) finite &= isfinite(G[e]);
+    if (l < nx) finite &= isfinite(qq[l]);
+    for (int row = l; row < m; row += 64) finite &= !isnan(lo[row]) && !isnan(up[row]);
+    if (!__all(finite)) status = DRC_STATUS_NONFINITE;
+  }
+  double *D = S + kp.oD, *E = S + kp.oE, *x = S + kp.oX, *z = S + kp.oZ, *y = S + kp.oY, *dy = S + kp.oDY;
+  double* sc = S + kp.oSc;
+  if (status != DRC_STATUS_NONFINITE) {
+    if (l < nx) D[l] = 1.0;
+    for (int row = l; row < m; row += 64) E[row] = 1.0;
+    if (l == 0) sc[SC_C] = 1.0;
+    double* Dt = S + kp.oT1;
+    double* Et = S + kp.oT2;
+    wsync();
+    for (int it = 0; it < kp.s.scaling; ++it) {
+      if (l < nx) {
+        double s = fabs(ab[l]);
+        if (l < np)
+          for (int i = 0; i < np; ++i) s = fmax(s, fabs(P[i * np + l]));
+        for (int i = 0; i < ng; ++i) s = fmax(s, fabs(G[i * nx + l]));
+        s = s < kMinScaling ? 1.0 : (s > kMaxScaling ? kMaxScaling : s);
+        Dt[l] = 1.0 / sqrt(s);
+        double eb = fabs(ab[l]);
+        eb = eb < kMinScaling ? 1.0 : (eb > kMaxScaling ? kMaxScaling : eb);
+        Et[l] = 1.0 / sqrt(eb);
+      }
+      if (l < ng) {
         double s = 0;
-        for (int r = 0; r < 6; ++r) s += Jt[r * np + l] * xdd[r];
-        qi = -2.0 * s;
-      } else {
-        qi = kp.slack_w;
+        for (int j = 0; j < nx; ++j) s = fmax(s, fabs(G[l * nx + j]));
+        s = s < kMinScaling ? 1.0 : (s > kMaxScaling ? kMaxScaling : s);
+        Et[nx + l] = 1.0 / sqrt(s);
       }
-      qq[l] = qi;
-      ab[l] = 1.0;
-      if (M->kind == 0) {
-        lo[l] = l < nv ? -M->vel[l] : 0.0;
-        up[l] = l < nv ? M->vel[l] : kInf;
-      } else {  // setBoundConstraint is a no-op for MoMa (QP_IK.cpp:75-83)
-        lo[l] = -kInf;
-        up[l] = kInf;
+      wsync();
+      if (l < np)
+        for (int c = 0; c < np; ++c) P[l * np + c] *= Dt[l] * Dt[c];
+      if (l < ng)
+        for (int j = 0; j < nx; ++j) G[l * nx + j] *= Et[nx + l] * Dt[j];
+      if (l < nx) {
+        ab[l] *= Et[l] * Dt[l];
+        qq[l] *= Dt[l];
+        D[l] *= Dt[l];
+        E[l] *= Et[l];
       }
+      if (l < ng) E[nx + l] *= Et[nx + l];
+      wsync();
+      // cost scaling: mean column norm of P vs |q|_inf
+      double cn = 0, qn = 0;
+      if (l < nx) {
+        if (l < np)
+          for (int i = 0; i < np; ++i) cn = fmax(cn, fabs(P[i * np + l]));
+        qn = fabs(qq[l]);
+      }
+      cn = wave_sum(cn) / nx;
+      qn = wave_max(qn);
+      qn = qn < kMinScaling ? 1.0 : (qn > kMaxScaling ? kMaxScaling : qn);
+      double ct = fmax(cn, qn);
+      ct = ct < kMinScaling ? 1.0 : (ct > kMaxScaling ? kMaxScaling : ct);
+      ct = 1.0 / ct;
+      if (l < np)
+        for (int c = 0; c < np; ++c) P[l * np + c] *= ct;
+      if (l < nx) qq[l] *= ct;
+      if (l == 0) sc[SC_C] *= ct;
+      wsync();
+    }
+    for (int row = l; row < m; row += 64) {
+      lo[row] = fmax(lo[row], -kInf) * E[row];
+      up[row] = fmin(up[row], kInf) * E[row];
     }
     wsync();
-    if (l < ng) {
-      const int n = narm, row = nx + l;
-      double lval = 0;
-      const int vo = M->kind == 0 ? 0 : M->act_mani_start;  // task-variable offset of the arm
-      const int qo = M->kind == 0 ? 0 : M->mani_start;      // joint offset of the arm
-      if (l < n) {
-        G[l * nx + vo + l] = 1.0;
-        if (M->kind == 0) G[l * nx + n + l] = 1.0;
-        lval = -alpha * (qv[qo + l] - M->lower[qo + l]);
-      } else if (l < 2 * n) {
-        const int i = l - n;
-        G[l * nx + vo + i] = -1.0;
-        if (M->kind == 0) G[l * nx + 2 * n + i] = 1.0;
-        lval = -alpha * (M->upper[qo + i] - qv[qo + i]);
-      } else if (l == 2 * n) {
-        for (int c = 0; c < n; ++c) G[l * nx + vo + c] = mg[c];
-        if (M->kind == 0) G[l * nx + 3 * n] = 1.0;
-        lval = -alpha * (man - kp.man_min);
-      } else {
-        for (int c = 0; c < n; ++c) G[l * nx + vo + c] = dgv[qo + c];
-        if (M->kind == 0) G[l * nx + 3 * n + 1] = 1.0;
-        lval = -alpha * (bestd - kp.dist_min);
-      }
-      lo[row] = lval;
-      up[row] = kInf;
     }
-    wsync();
-    PH(0);
-    // ---------------- OSQP: scaling ----------------------------------------
-    int status = DRC_STATUS_MAX_ITER, iters = 0;
-    {
-      bool finite = true;
-      for (int e = l; e < np * np; e += 64) finite &= isfinite(P[e]);
-      for (int e = l; e < ng * nx; e += 64) finite &= isfinite(G[e]);
-      if (l < nx) finite &= isfinite(qq[l]);
-      for (int row = l; row < m; row += 64) finite &= !isnan(lo[row]) && !isnan(up[row]);
-      if (!__all(finite)) status = DRC_STATUS_NONFINITE;
+  return status;
+}
+
+// rho, K^-1 and the ADMM iterations (+ polish); returns the status
+template <class QD>
+__device__ __forceinline__ int qp_admm(const KParams& kp, const KParams& kpl, double* S, int* iters_out) {
+  const int l = lane_id();
+  const int nx = DNX, ng = DNG, m = DM;
+  double *G = S + kp.oG, *qq = S + kp.oQ, *ab = S + kp.oAB, *lo = S + kp.oL, *up = S + kp.oU;
+  double *x = S + kp.oX, *z = S + kp.oZ, *y = S + kp.oY, *dy = S + kp.oDY;
+  double* sc = S + kp.oSc;
+  int status = DRC_STATUS_MAX_ITER;
+  (void)G;
+  set_rho<QD>(kp, S, kp.s.rho);
+  factor_kinv<QD>(kp, S);
+  if (l < nx) x[l] = 0.0;
+  for (int row = l; row < m; row += 64) z[row] = y[row] = 0.0;
+  wsync();
+  // ---------------- OSQP: ADMM ----------------------------------------
+  const double* K = S + kp.oU0;
+  const double* rv = S + kp.oRho;
+  double* w = S + kp.oT1;
+  double* xt = S + kp.oXT;
+  const double sig = kp.s.sigma, al = kp.s.alpha;
+  int it;
+  if constexpr (QD::nx > 0) {
+    constexpr int NX = QD::nx, NG = QD::ng;
+    double Gc[NG], Kr[NX], GKr[NX];
+    prep_admm_mats<QD>(kpl, S);
+    load_admm_regs<QD>(kp, S, Gc, Kr, GKr);
+    const bool hb = l < NX, hg = l < NG;
+    const int lb_ = hb ? l : 0, lg_ = hg ? NX + l : 0;
+    const double ab_l = ab[lb_], q_l = qq[lb_], lo_b = lo[lb_], up_b = up[lb_], lo_g = lo[lg_], up_g = up[lg_];
+    double rb = rv[lb_], rg = rv[lg_];
+    double xl = 0, zb = 0, yb = 0, zg = 0, yg = 0, dyb = 0, dyg = 0;
+    for (it = 1; it <= kp.s.max_iter; ++it) {
+      const double wg = hg ? rg * zg - yg : 0.0;
+      double r0 = hb ? sig * xl - q_l + ab_l * (rb * zb - yb) : 0.0, r1 = 0;
+#pragma unroll
+      for (int i = 0; i < NG; ++i) {
+        const double wi = bcast(wg, i);
+        if (i & 1) r1 += Gc[i] * wi;
+        else r0 += Gc[i] * wi;
+      }
+      const double rhs = hb ? r0 + r1 : 0.0;
+      double x0 = 0, x1 = 0, a0 = 0, a1 = 0;
+#pragma unroll
+      for (int c = 0; c < NX; ++c) {
+        const double rc = bcast(rhs, c);
+        if (c & 1) {
+          x1 += Kr[c] * rc;
+          a1 += GKr[c] * rc;
+        } else {
+          x0 += Kr[c] * rc;
+          a0 += GKr[c] * rc;
+        }
+      }
+      const double xtil = x0 + x1, ag = a0 + a1;
+      if (hb) {  // z~ = A x~ ; relaxation ; projection ; dual update
+        const double zr = al * ab_l * xtil + (1 - al) * zb;
+        double zn = zr + yb / rb;
+        zn = fmin(fmax(zn, lo_b), up_b);
+        dyb = rb * (zr - zn);
+        yb += dyb;
+        zb = zn;
+        xl = al * xtil + (1 - al) * xl;
+      }
+      if (hg) {
+        const double zr = al * ag + (1 - al) * zg;
+        double zn = zr + yg / rg;
+        zn = fmin(fmax(zn, lo_g), up_g);
+        dyg = rg * (zr - zn);
+        yg += dyg;
+        zg = zn;
+      }
+      const bool check = kp.s.check_termination > 0 && it % kp.s.check_termination == 0;
+      const bool adapt = kp.s.adaptive_rho && kp.s.adaptive_rho_interval > 0 && it % kp.s.adaptive_rho_interval == 0;
+      if (!(check || adapt) && it < kp.s.max_iter) continue;
+      // publish the iterate for the (LDS) residual / polish / rho code
+      if (hb) {
+        x[l] = xl;
+        z[l] = zb;
+        y[l] = yb;
+        dy[l] = dyb;
+      }
+      if (hg) {
+        z[NX + l] = zg;
+        y[NX + l] = yg;
+        dy[NX + l] = dyg;
+      }
+      wsync();
+      if (!(check || adapt)) continue;  // last iteration: published for the output
+      const int act = admm_check<QD>(kpl, S, it, check, adapt, &status);
+      if (act == 2) break;
+      const bool reload = act == 1;
+      if (reload) {
+        load_admm_regs<QD>(kp, S, Gc, Kr, GKr);
+        rb = rv[lb_];
+        rg = rv[lg_];
+        if (hb) {
+          xl = x[l];
+          zb = z[l];
+          yb = y[l];
+        }
+        if (hg) {
+          zg = z[NX + l];
+          yg = y[NX + l];
+        }
+      }
     }
-    double *D = S + kp.oD, *E = S + kp.oE, *x = S + kp.oX, *z = S + kp.oZ, *y = S + kp.oY, *dy = S + kp.oDY;
-    double* sc = S + kp.oSc;
-    if (status != DRC_STATUS_NONFINITE) {
-      if (l < nx) D[l] = 1.0;
-      for (int row = l; row < m; row += 64) E[row] = 1.0;
-      if (l == 0) sc[SC_C] = 1.0;
-      double* Dt = S + kp.oT1;
-      double* Et = S + kp.oT2;
+  } else {
+    for (it = 1; it <= kp.s.max_iter; ++it) {
+      for (int row = l; row < m; row += 64) w[row] = rv[row] * z[row] - y[row];
       wsync();
-      for (int it = 0; it < kp.s.scaling; ++it) {
-        if (l < nx) {
-          double s = fabs(ab[l]);
-          if (l < np)
-            for (int i = 0; i < np; ++i) s = fmax(s, fabs(P[i * np + l]));
-          for (int i = 0; i < ng; ++i) s = fmax(s, fabs(G[i * nx + l]));
-          s = s < kMinScaling ? 1.0 : (s > kMaxScaling ? kMaxScaling : s);
-          Dt[l] = 1.0 / sqrt(s);
-          double eb = fabs(ab[l]);
-          eb = eb < kMinScaling ? 1.0 : (eb > kMaxScaling ? kMaxScaling : eb);
-          Et[l] = 1.0 / sqrt(eb);
+      if (l < nx) {
+        double r0 = sig * x[l] - qq[l] + ab[l] * w[l], r1 = 0.0;
+  #pragma unroll
+        for (int i = 0; i < ng; i += 2) {
+          r0 += G[i * nx + l] * w[nx + i];
+          if (i + 1 < ng) r1 += G[(i + 1) * nx + l] * w[nx + i + 1];
         }
-        if (l < ng) {
-          double s = 0;
-          for (int j = 0; j < nx; ++j) s = fmax(s, fabs(G[l * nx + j]));
-          s = s < kMinScaling ? 1.0 : (s > kMaxScaling ? kMaxScaling : s);
-          Et[nx + l] = 1.0 / sqrt(s);
-        }
-        wsync();
-        if (l < np)
-          for (int c = 0; c < np; ++c) P[l * np + c] *= Dt[l] * Dt[c];
-        if (l < ng)
-          for (int j = 0; j < nx; ++j) G[l * nx + j] *= Et[nx + l] * Dt[j];
-        if (l < nx) {
-          ab[l] *= Et[l] * Dt[l];
-          qq[l] *= Dt[l];
-          D[l] *= Dt[l];
-          E[l] *= Et[l];
-        }
-        if (l < ng) E[nx + l] *= Et[nx + l];
-        wsync();
-        // cost scaling: mean column norm of P vs |q|_inf
-        double cn = 0, qn = 0;
-        if (l < nx) {
-          if (l < np)
-            for (int i = 0; i < np; ++i) cn = fmax(cn, fabs(P[i * np + l]));
-          qn = fabs(qq[l]);
-        }
-        cn = wave_sum(cn) / nx;
-        qn = wave_max(qn);
-        qn = qn < kMinScaling ? 1.0 : (qn > kMaxScaling ? kMaxScaling : qn);
-        double ct = fmax(cn, qn);
-        ct = ct < kMinScaling ? 1.0 : (ct > kMaxScaling ? kMaxScaling : ct);
-        ct = 1.0 / ct;
-        if (l < np)
-          for (int c = 0; c < np; ++c) P[l * np + c] *= ct;
-        if (l < nx) qq[l] *= ct;
-        if (l == 0) sc[SC_C] *= ct;
-        wsync();
-      }
-      for (int row = l; row < m; row += 64) {
-        lo[row] = fmax(lo[row], -kInf) * E[row];
-        up[row] = fmin(up[row], kInf) * E[row];
+        xt[l] = r0 + r1;
       }
       wsync();
-      PH(1);
-      set_rho<QD>(kp, S, kp.s.rho);
-      factor_kinv<QD>(kp, S);
-      if (l < nx) x[l] = 0.0;
-      for (int row = l; row < m; row += 64) z[row] = y[row] = 0.0;
+      double xtil = 0;
+      if (l < nx) {
+        double a0 = 0, a1 = 0;
+  #pragma unroll
+        for (int c = 0; c < nx; c += 2) {
+          a0 += K[l * nx + c] * xt[c];
+          if (c + 1 < nx) a1 += K[l * nx + c + 1] * xt[c + 1];
+        }
+        xtil = a0 + a1;
+      }
       wsync();
-      PH(2);
-      // ---------------- OSQP: ADMM ----------------------------------------
-      const double* K = S + kp.oU0;
-      const double* rv = S + kp.oRho;
-      double* w = S + kp.oT1;
-      double* xt = S + kp.oXT;
-      const double sig = kp.s.sigma, al = kp.s.alpha;
-      int it;
-      for (it = 1; it <= kp.s.max_iter; ++it) {
-        for (int row = l; row < m; row += 64) w[row] = rv[row] * z[row] - y[row];
-        wsync();
-        if (l < nx) {
-          double r0 = sig * x[l] - qq[l] + ab[l] * w[l], r1 = 0.0;
-#pragma unroll
-          for (int i = 0; i < ng; i += 2) {
-            r0 += G[i * nx + l] * w[nx + i];
-            if (i + 1 < ng) r1 += G[(i + 1) * nx + l] * w[nx + i + 1];
-          }
-          xt[l] = r0 + r1;
+      if (l < nx) xt[l] = xtil;
+      wsync();
+      // z~ = A x~ ; relaxation ; projection ; dual update
+      if (l < nx) {
+        const double zr = al * ab[l] * xtil + (1 - al) * z[l];
+        double zn = zr + y[l] / rv[l];
+        zn = fmin(fmax(zn, lo[l]), up[l]);
+        const double d = rv[l] * (zr - zn);
+        dy[l] = d;
+        y[l] += d;
+        z[l] = zn;
+        x[l] = al * xtil + (1 - al) * x[l];
+      }
+      if (l < ng) {
+        const int row = nx + l;
+        double a0 = 0, a1 = 0;
+  #pragma unroll
+        for (int j = 0; j < nx; j += 2) {
+          a0 += G[l * nx + j] * xt[j];
+          if (j + 1 < nx) a1 += G[l * nx + j + 1] * xt[j + 1];
         }
-        wsync();
-        double xtil = 0;
-        if (l < nx) {
-          double a0 = 0, a1 = 0;
-#pragma unroll
-          for (int c = 0; c < nx; c += 2) {
-            a0 += K[l * nx + c] * xt[c];
-            if (c + 1 < nx) a1 += K[l * nx + c + 1] * xt[c + 1];
-          }
-          xtil = a0 + a1;
-        }
-        wsync();
-        if (l < nx) xt[l] = xtil;
-        wsync();
-        // z~ = A x~ ; relaxation ; projection ; dual update
-        if (l < nx) {
-          const double zr = al * ab[l] * xtil + (1 - al) * z[l];
-          double zn = zr + y[l] / rv[l];
-          zn = fmin(fmax(zn, lo[l]), up[l]);
-          const double d = rv[l] * (zr - zn);
-          dy[l] = d;
-          y[l] += d;
-          z[l] = zn;
-          x[l] = al * xtil + (1 - al) * x[l];
-        }
-        if (l < ng) {
-          const int row = nx + l;
-          double a0 = 0, a1 = 0;
-#pragma unroll
-          for (int j = 0; j < nx; j += 2) {
-            a0 += G[l * nx + j] * xt[j];
-            if (j + 1 < nx) a1 += G[l * nx + j + 1] * xt[j + 1];
-          }
-          const double a = a0 + a1;
-          const double zr = al * a + (1 - al) * z[row];
-          double zn = zr + y[row] / rv[row];
-          zn = fmin(fmax(zn, lo[row]), up[row]);
-          const double d = rv[row] * (zr - zn);
-          dy[row] = d;
-          y[row] += d;
-          z[row] = zn;
-        }
-        wsync();
-        PH(3);
-        const bool check = kp.s.check_termination > 0 && it % kp.s.check_termination == 0;
-        const bool adapt = kp.s.adaptive_rho && kp.s.adaptive_rho_interval > 0 && it % kp.s.adaptive_rho_interval == 0;
-        if (check || adapt) residuals<QD>(kp, S, x, z, y, kp.s.eps_abs, kp.s.eps_rel);
-        if (check) {
-          const bool conv = sc[SC_PRI] < sc[SC_EPSP] && sc[SC_DUA] < sc[SC_EPSD];
-          // parity mode: a certified polish is exact whatever the ADMM
-          // residual, so also try it every 4th check (slow-ADMM vertices)
-          if (kp.s.exact && !conv && it % (4 * kp.s.check_termination) == 0) {
-            if (polish<QD>(kp, S, true)) {
-              status = DRC_STATUS_SOLVED;
-              break;
-            }
-            factor_kinv<QD>(kp, S);  // polish used the union region
-            residuals<QD>(kp, S, x, z, y, kp.s.eps_abs, kp.s.eps_rel);
-          }
-          if (conv) {
-            if (!kp.s.exact) {
-              status = DRC_STATUS_SOLVED;
-              break;
-            }
-            if (polish<QD>(kp, S, true)) {
-              status = DRC_STATUS_SOLVED;
-              break;
-            }
-            factor_kinv<QD>(kp, S);  // polish used the union region
-            residuals<QD>(kp, S, x, z, y, kp.s.eps_fallback, kp.s.eps_fallback);
-            if (sc[SC_PRI] < sc[SC_EPSP] && sc[SC_DUA] < sc[SC_EPSD]) {
-              status = DRC_STATUS_SOLVED;
-              break;
-            }
-          } else if (primal_infeasible<QD>(kp, S, kp.s.eps_prim_inf)) {
-            status = DRC_STATUS_PRIMAL_INFEASIBLE;
+        const double a = a0 + a1;
+        const double zr = al * a + (1 - al) * z[row];
+        double zn = zr + y[row] / rv[row];
+        zn = fmin(fmax(zn, lo[row]), up[row]);
+        const double d = rv[row] * (zr - zn);
+        dy[row] = d;
+        y[row] += d;
+        z[row] = zn;
+      }
+      wsync();
+      const bool check = kp.s.check_termination > 0 && it % kp.s.check_termination == 0;
+      const bool adapt = kp.s.adaptive_rho && kp.s.adaptive_rho_interval > 0 && it % kp.s.adaptive_rho_interval == 0;
+      if (check || adapt) residuals<QD>(kp, S, x, z, y, kp.s.eps_abs, kp.s.eps_rel);
+      if (check) {
+        const bool conv = sc[SC_PRI] < sc[SC_EPSP] && sc[SC_DUA] < sc[SC_EPSD];
+        // parity mode: a certified polish is exact whatever the ADMM
+        // residual, so also try it every 4th check (slow-ADMM vertices)
+        if (kp.s.exact && !conv && it % (4 * kp.s.check_termination) == 0) {
+          if (polish<QD>(kp, S, true)) {
+            status = DRC_STATUS_SOLVED;
             break;
           }
+          factor_kinv<QD>(kp, S);  // polish used the union region
+          residuals<QD>(kp, S, x, z, y, kp.s.eps_abs, kp.s.eps_rel);
         }
-        if (adapt) {
-          const double pr = sc[SC_PRIS] / (fmax(sc[SC_NAX], sc[SC_NZ]) + kDivTol);
-          const double dr = sc[SC_DUAS] / (fmax(fmax(sc[SC_NQ], sc[SC_NATY]), sc[SC_NPX]) + kDivTol);
-          const double rho = sc[SC_RHO];
-          double rn = rho * sqrt(pr / (dr + kDivTol));
-          rn = fmin(fmax(rn, kRhoMin), kRhoMax);
-          if (rn > rho * kp.s.adaptive_rho_tolerance || rn < rho / kp.s.adaptive_rho_tolerance) {
-            set_rho<QD>(kp, S, rn);
-            factor_kinv<QD>(kp, S);
+        if (conv) {
+          if (!kp.s.exact) {
+            status = DRC_STATUS_SOLVED;
+            break;
           }
+          if (polish<QD>(kp, S, true)) {
+            status = DRC_STATUS_SOLVED;
+            break;
+          }
+          factor_kinv<QD>(kp, S);  // polish used the union region
+          residuals<QD>(kp, S, x, z, y, kp.s.eps_fallback, kp.s.eps_fallback);
+          if (sc[SC_PRI] < sc[SC_EPSP] && sc[SC_DUA] < sc[SC_EPSD]) {
+            status = DRC_STATUS_SOLVED;
+            break;
+          }
+        } else if (primal_infeasible<QD>(kp, S, kp.s.eps_prim_inf)) {
+          status = DRC_STATUS_PRIMAL_INFEASIBLE;
+          break;
         }
       }
-      PH(4);
-      iters = it > kp.s.max_iter ? kp.s.max_iter : it;
-      if (status == DRC_STATUS_SOLVED && kp.s.polish && !kp.s.exact) polish<QD>(kp, S, false);
+      if (adapt) {
+        const double pr = sc[SC_PRIS] / (fmax(sc[SC_NAX], sc[SC_NZ]) + kDivTol);
+        const double dr = sc[SC_DUAS] / (fmax(fmax(sc[SC_NQ], sc[SC_NATY]), sc[SC_NPX]) + kDivTol);
+        const double rho = sc[SC_RHO];
+        double rn = rho * sqrt(pr / (dr + kDivTol));
+        rn = fmin(fmax(rn, kRhoMin), kRhoMax);
+        if (rn > rho * kp.s.adaptive_rho_tolerance || rn < rho / kp.s.adaptive_rho_tolerance) {
+          set_rho<QD>(kp, S, rn);
+          factor_kinv<QD>(kp, S);
+        }
+      }
     }
-    PH(5);
+  }
+  *iters_out = it > kp.s.max_iter ? kp.s.max_iter : it;
+  if (status == DRC_STATUS_SOLVED && kp.s.polish && !kp.s.exact) polish<QD>(kp, S, false);
+  return status;
+}
+
+// QP kernel: assembles and solves the QP of each instance from the task
+// record written by task_kernel.
+template <class QD>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 8)))
+qp_kernel(const DevModel* __restrict__ M0, const KParams kp, const IO io) {
+  extern __shared__ __attribute__((aligned(16))) double S[];
+  // LDS copy of the parameters for the out-of-line (rare) ADMM blocks: a
+  // reference to the kernel argument itself would be copied to scratch
+  __shared__ KParams kpl;
+  const int l = lane_id();
+  {
+    static_assert(sizeof(KParams) % 8 == 0, "KParams copied as 8-byte words");
+    const uint64_t* src = reinterpret_cast<const uint64_t*>(&kp);
+    uint64_t* dst = reinterpret_cast<uint64_t*>(&kpl);
+    for (int e = l; e < static_cast<int>(sizeof(KParams) / 8); e += 64) dst[e] = src[e];
+    wsync();
+  }
+  const int64_t B = io.B;
+  PH_DECL
+  const InstSeq seq(B, kp.xcd_map);
+  for (int64_t j = seq.j0; j < seq.n; j += seq.step) {
+    const int64_t b = seq.at(j);
+    if (b >= B) continue;
+    const DevModel* M = M0;
+    asm volatile("" : "+s"(M));
+    qp_assemble<QD>(M, kp, S, io, b);
+    PH(0);
+    int status = qp_scale<QD>(kp, S), iters = 0;
+    PH(1);
+    if (status != DRC_STATUS_NONFINITE) status = qp_admm<QD>(kp, kpl, S, &iters);
+    PH(3);
     // ---------------- outputs (zero on failure, QP_IK.cpp:56-61) ------------
+    const double *D = S + kp.oD, *x = S + kp.oX;
     if (l < kp.na) io.out[(int64_t)l * B + b] = status == DRC_STATUS_SOLVED ? D[l] * x[l] : 0.0;
     if (l == 0) {
       io.status[b] = status;
       if (io.iters) io.iters[b] = iters;
     }
     wsync();
+    PH(5);
   }
   PH_FLUSH(16);
 }
@@ -1512,6 +1809,8 @@ struct drc_model_impl {
   int64_t epa_count = 0;
   void* pool = nullptr;  // task data when the caller does not keep it
   int64_t pool_bytes = 0;
+  int timing = 0;                 // drc_debug_kernel_timing: HIP events around each launch
+  std::vector<hipEvent_t> events;  // 3 per timed call: before task, between, after qp
   std::mutex mu;
 };
 
@@ -1687,7 +1986,7 @@ static int plan_layout(const DevModel& M, KParams* k, bool task_only) {
   k->kSv = takeu(3 * kMaxWheels);
   k->kScr = takeu(96);
   int kin_end = u;
-  int kinv_end = k->oU0 + nx * nx;
+  int kinv_end = k->oU0 + nx * nx + nx * ng;  // K^-1 and G K^-1
   const int N = nx + ng;
   int pol_end = k->oU0 + 64 + 64 + 128 + 64 * 5 + N * (N + 1) / 2;
   int end = kin_end;
@@ -1742,6 +2041,13 @@ static int make_kparams(const drc_model_impl* mm, const drc_qpik_params* p, int 
   }
   k->ng = 2 * k->narm + 2;
   k->m = k->nx + k->ng;
+  k->rJac = 0;
+  k->rMan = 6 * M.nv;
+  k->rDist = k->rMan + 1 + k->narm;
+  k->rXdd = k->rDist + 1 + M.nv;
+  k->rQ = k->rXdd + 6;
+  k->rLen = k->rQ + M.nv;
+  k->xcd_map = 0;
   if (k->nx > 64 || k->ng > 64 || k->narm > 8)
     return set_err(DRC_ERR_UNSUPPORTED, "QP larger than one wavefront's row mapping");
   if (k->s.max_iter < 1 || k->s.check_termination < 0) return set_err(DRC_ERR_INVALID_ARGUMENT, "bad solver settings");
@@ -1773,10 +2079,11 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
   // EPA workspaces (~60 KB each) stay modest
   const int64_t grid = B < 8192 ? B : 8192;
   const int64_t grid_task = B < 4096 ? B : 4096;
-  const int nv = m->hm.dev.nv, narm = kt.narm;
-  // task data: ~ (6 nv + narm + nv + 9) doubles per instance, model-owned pool
-  const int64_t per = 6 * nv + (1 + narm) + (1 + nv) + 6 + 1;
+  // product path: per-instance task records (rLen doubles padded to whole
+  // 128-B lines) in a model-owned pool; the stage API writes [field][B]
+  const int64_t stride = (kt.rLen + 15) & ~int64_t(15);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  double* rec = nullptr;
   {
     std::lock_guard<std::mutex> g(m->mu);
     if (m->epa_count < grid_task) {
@@ -1785,24 +2092,30 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
       HIP_TRY(hipMalloc(&m->epa_ws, sizeof(EpaPoly) * grid_task));
       m->epa_count = grid_task;
     }
-    const bool need_pool = !jac || !man || !dist || !xdd || !pair;
-    if (need_pool && m->pool_bytes < per * B * 8) {
-      if (m->pool) HIP_TRY(hipFree(m->pool));
-      m->pool = nullptr;
-      HIP_TRY(hipMalloc(&m->pool, per * B * 8));
-      m->pool_bytes = per * B * 8;
+    if (!stages) {
+      if (m->pool_bytes < stride * B * 8) {
+        if (m->pool) HIP_TRY(hipFree(m->pool));
+        m->pool = nullptr;
+        HIP_TRY(hipMalloc(&m->pool, stride * B * 8));
+        m->pool_bytes = stride * B * 8;
+      }
+      rec = reinterpret_cast<double*>(m->pool);
     }
-    double* pool = reinterpret_cast<double*>(m->pool);
-    if (!jac) jac = pool;
-    if (!man) man = pool + 6 * nv * B;
-    if (!dist) dist = pool + (6 * nv + 1 + narm) * B;
-    if (!xdd) xdd = pool + (6 * nv + 2 + narm + nv) * B;
-    if (!pair) pair = reinterpret_cast<int32_t*>(pool + (6 * nv + 8 + narm + nv) * B);
   }
-  IO io{B, q, qdot, xt, xdt, xi, xdi, out, status, iters, pose, jac, man, dist, xdd, pair, m->epa_ws};
+  // XCD-aware order needs grids that are multiples of 8 (both are, from 16 Ki up)
+  kt.xcd_map = kq.xcd_map = B >= 16384 ? 1 : 0;
+  IO io{B, q, qdot, xt, xdt, xi, xdi, out, status, iters, pose, jac, man, dist, xdd, pair, rec, stride, m->epa_ws};
+  hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+  if (m->timing && !stages) {
+    for (auto& e : ev) HIP_TRY(hipEventCreate(&e));
+    std::lock_guard<std::mutex> g(m->mu);
+    for (auto& e : ev) m->events.push_back(e);
+  }
+  if (ev[0]) HIP_TRY(hipEventRecord(ev[0], st));
   hipLaunchKernelGGL(task_kernel, dim3(static_cast<unsigned>(grid_task)), dim3(64),
                      static_cast<size_t>(kt.lds_doubles) * sizeof(double), st, m->d_model, kt, io);
   HIP_TRY(hipGetLastError());
+  if (ev[1]) HIP_TRY(hipEventRecord(ev[1], st));
   if (!stages) {
     const size_t lds = static_cast<size_t>(kq.lds_doubles) * sizeof(double);
     const dim3 g(static_cast<unsigned>(grid)), blk(64);
@@ -1820,6 +2133,7 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
       hipLaunchKernelGGL((qp_kernel<Dims<0, 0, 0>>), g, blk, lds, st, m->d_model, kq, io);
     HIP_TRY(hipGetLastError());
   }
+  if (ev[2]) HIP_TRY(hipEventRecord(ev[2], st));
   return DRC_OK;
 }
 
@@ -1844,6 +2158,34 @@ const char* drc_error_string(int code) {
   }
 }
 const char* drc_last_error(void) { return drc_amd::g_last_error.c_str(); }
+
+int drc_debug_kernel_timing(drc_model* m, int enable) {
+  if (!m) return drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "null model");
+  m->timing = enable != 0;
+  return DRC_OK;
+}
+
+int drc_debug_kernel_times(drc_model* m, double* task_ms, double* qp_ms, int* calls) {
+  if (!m || !task_ms || !qp_ms || !calls) return drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "null argument");
+  std::lock_guard<std::mutex> g(m->mu);
+  double t0 = 0, t1 = 0;
+  const int n = static_cast<int>(m->events.size() / 3);
+  for (int i = 0; i < n; ++i) {
+    hipEvent_t* e = &m->events[3 * i];
+    if (hipEventSynchronize(e[2]) != hipSuccess) return drc_amd::set_err(DRC_ERR_HIP, "hipEventSynchronize");
+    float a = 0, b = 0;
+    if (hipEventElapsedTime(&a, e[0], e[1]) != hipSuccess || hipEventElapsedTime(&b, e[1], e[2]) != hipSuccess)
+      return drc_amd::set_err(DRC_ERR_HIP, "hipEventElapsedTime");
+    t0 += a;
+    t1 += b;
+  }
+  for (hipEvent_t e : m->events) (void)hipEventDestroy(e);
+  m->events.clear();
+  *task_ms = t0;
+  *qp_ms = t1;
+  *calls = n;
+  return DRC_OK;
+}
 
 #ifdef DRC_PHASE_TIMING
 // diagnostic build only: accumulated per-phase s_memtime cycles (32 slots)

@@ -180,6 +180,13 @@ int drc_qpik_stages_batch(const drc_model* model, const drc_qpik_params* params,
                           const double* xdot_init, double* pose, double* jac, double* man,
                           double* dist, int32_t* pair, double* xdot_des, void* stream);
 
+/* Diagnostics (no reference counterpart): when enabled, drc_qpik_batch
+ * records HIP events on its stream around the task and QP kernels;
+ * drc_debug_kernel_times waits for them and returns the summed durations
+ * (ms) and the number of timed calls since the last query. */
+int drc_debug_kernel_timing(drc_model* model, int enable);
+int drc_debug_kernel_times(drc_model* model, double* task_ms, double* qp_ms, int* calls);
+
 const char* drc_error_string(int code);
 /* Thread-local detail of the last failing call (parse position, HIP error). */
 const char* drc_last_error(void);

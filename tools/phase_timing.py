@@ -20,7 +20,7 @@ ctrl.QPIK_step_batch(*args, link); torch.cuda.synchronize()
 _capi.lib().drc_debug_phase_cycles(buf, 0)
 v = np.array(buf[:], dtype=np.float64)
 names_t = ["fk+geoms", "J+taskvel", "manip", "broad+sphere", "gjk cand", "epa", "argmin+witness", "grad"]
-names_q = ["load+assemble", "scaling", "rho+factor", "admm iters", "checks/polish/rho", "tail"]
+names_q = ["load+assemble", "scaling", "-", "rho+factor+admm+checks", "-", "output"]
 tt, tq = v[:8], v[16:22]
 print("task kernel cycles/instance: %.0f" % (tt.sum() / B))
 for n, x in zip(names_t, tt): print("  %-16s %6.1f%%  %8.0f cyc/inst" % (n, 100 * x / tt.sum(), x / B))

@@ -1,0 +1,81 @@
+"""Summarise a tools/profile_round.sh run into committed profiles.
+
+    python tools/pmc_summary.py <tag> [robot batch]
+
+Reads gpurun_out/prof_<tag>/ and writes
+  profiles/<tag>_bench.json          the bench line of that run
+  profiles/<tag>_kernel_stats.csv    rocprofv3 --kernel-trace --stats summary
+  profiles/<tag>_pmc.json            per-kernel FETCH_SIZE / WRITE_SIZE per launch
+  profiles/pmc_traffic.json          the same, as read by bench.py (latest run)
+
+Corrections (MI355X_MICROARCH.md, HBM section): FETCH_SIZE and WRITE_SIZE
+are in KiB; on gfx950 FETCH_SIZE counts half the bytes of a streaming read,
+so it is doubled.  Our loads are 8 B/lane gathers, an access width the guide
+leaves uncalibrated, so the raw values are kept next to the corrected ones.
+"""
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def short(name):
+    for k in ("task_kernel", "qp_kernel"):
+        if k in name:
+            return k
+    return None
+
+
+def counters(d, cname):
+    per = defaultdict(list)
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if row.get("Counter_Name") != cname:
+                    continue
+                k = short(row.get("Kernel_Name", ""))
+                if k:
+                    per[k].append(float(row["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in per.items()}, {k: len(v) for k, v in per.items()}
+
+
+def main():
+    tag = sys.argv[1]
+    robot = sys.argv[2] if len(sys.argv) > 2 else "fr3"
+    batch = int(sys.argv[3]) if len(sys.argv) > 3 else 65536
+    src = os.path.join(ROOT, "gpurun_out", "prof_" + tag)
+    dst = os.path.join(ROOT, "profiles")
+    os.makedirs(dst, exist_ok=True)
+    shutil.copy(os.path.join(src, "bench.json"), os.path.join(dst, tag + "_bench.json"))
+    stats = glob.glob(os.path.join(src, "kt", "**", "*kernel_stats.csv"), recursive=True)
+    shutil.copy(stats[0], os.path.join(dst, tag + "_kernel_stats.csv"))
+    avg = {}
+    with open(stats[0]) as fh:
+        for row in csv.DictReader(fh):
+            k = short(row["Name"])
+            if k:
+                avg[k] = float(row["AverageNs"])
+    fetch, nf = counters(os.path.join(src, "fetch"), "FETCH_SIZE")
+    write, nw = counters(os.path.join(src, "write"), "WRITE_SIZE")
+    kern = {}
+    for k in sorted(set(fetch) | set(write)):
+        kern[k] = {"FETCH_SIZE_KiB_raw": fetch.get(k), "WRITE_SIZE_KiB_raw": write.get(k),
+                   "fetch_bytes": 2 * 1024 * fetch.get(k, 0.0), "write_bytes": 1024 * write.get(k, 0.0),
+                   "dispatches": [nf.get(k, 0), nw.get(k, 0)], "avg_duration_ns": avg.get(k)}
+    out = {"robot": robot, "batch": batch, "tag": tag, "kernels": kern,
+           "hbm_bytes_per_step": sum(v["fetch_bytes"] + v["write_bytes"] for v in kern.values()),
+           "corrections": "FETCH_SIZE KiB x1024 x2 (gfx950 half-count), WRITE_SIZE KiB x1024",
+           "kernel_stats_avg_ns": avg}
+    for name in (tag + "_pmc.json", "pmc_traffic.json"):
+        with open(os.path.join(dst, name), "w") as fh:
+            json.dump(out, fh, indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
