@@ -187,6 +187,9 @@ DRC_HD __forceinline__ void cs_try(const SV2 (&S)[4], CsBest& B) {
   if (k > 2) p = p + l2 * S[i2].w;
   if (k > 3) p = p + l3 * S[i3].w;
   const double dv = dot(p, p);
+  // a tetrahedron spans R^3, so its candidate must be the origin itself; a
+  // nonzero p means a flat, ill-conditioned tetrahedron (oracle: same test)
+  if (k == 4 && dv > 1e-20) return;
   if (B.mask == 0 || dv < B.best - 1e-18) {
     B.best = dv;
     B.mask = MASK;
@@ -267,7 +270,13 @@ DRC_HD __forceinline__ void gjk_run(const Shape& A, const Shape& B, GjkState& g)
     bool dup = false;
 #pragma unroll
     for (int i = 0; i < 4; ++i) dup |= i < n && S[i].w.x == w.w.x && S[i].w.y == w.w.y && S[i].w.z == w.w.z;
-    if (dup) break;
+    // a repeated support point before the gap test passed: the simplex
+    // stalled numerically; v.w <= 0 means the difference reaches past the
+    // origin (overlap), as in oracle/drc_oracle.c:gjk
+    if (dup) {
+      g.intersect = dot(v, w.w) <= 0;
+      break;
+    }
     SV2 nw;
     nw.w = w.w;
     nw.a = w.a;
@@ -279,10 +288,16 @@ DRC_HD __forceinline__ void gjk_run(const Shape& A, const Shape& B, GjkState& g)
       S[i].a = v3(here ? nw.a.x : S[i].a.x, here ? nw.a.y : S[i].a.y, here ? nw.a.z : S[i].a.z);
     }
     ++n;
+#ifdef DRC_NARROW_DEBUG
+    printf("gjk it %d add w %.17g %.17g %.17g (n=%d) vv %.6g vw %.6g\n", it, w.w.x, w.w.y, w.w.z, n, vv, dot(v, w.w));
+#endif
     if (n == 1) n = closest_n<1>(S, &v, g.lam);
     else if (n == 2) n = closest_n<2>(S, &v, g.lam);
     else if (n == 3) n = closest_n<3>(S, &v, g.lam);
     else n = closest_n<4>(S, &v, g.lam);
+#ifdef DRC_NARROW_DEBUG
+    printf("   -> n %d v %.6g %.6g %.6g |v| %.6g\n", n, v.x, v.y, v.z, sqrt(dot(v, v)));
+#endif
     if (n == 4 || dot(v, v) < 1e-24) {
       g.intersect = 1;
       break;
@@ -321,18 +336,47 @@ DRC_HD __noinline__ GjkDist gjk(const Shape A, const Shape B) {
 // (explicit DFS stack, same visiting order as the recursive oracle), so the
 // horizon is a single loop and the polytope stays a closed 2-manifold even
 // when flat features (cylinder caps, box faces) make the support mapping
-// degenerate.  The polytope lives in a per-workgroup L2-resident buffer; the closest-face scan is spread
-// over the wave, the expansion is lane-0 serial.  Same caps and decisions as
-// oracle/drc_oracle.c:epa.
-constexpr int kEpaMaxV = 128, kEpaMaxF = 256;
+// degenerate.  The polytope lives in LDS.  Per step the wave computes the
+// closest face, the support point, the stop tests and the visibility of
+// every face (one bit per face); one lane then walks the horizon with the
+// visited/visible bits in registers and packed adjacency (one LDS word per
+// edge).  Same caps and decisions as oracle/drc_oracle.c:epa.
+// caps: hpp-fcl's GJKSolver defaults (epa_max_vertex_num 64,
+// epa_max_face_num 128, epa_max_iterations 255), mirrored by the oracle
+constexpr int kEpaMaxV = 64, kEpaMaxF = 128;
+static_assert(kEpaMaxF == 128, "face bit masks are two 64-bit words");
 struct EpaPoly {
   double vw[kEpaMaxV][3], va[kEpaMaxV][3];
   double fn[kEpaMaxF][3], fd[kEpaMaxF];
   double out[6];
-  int16_t fv[kEpaMaxF][3], ff[kEpaMaxF][3], fpass[kEpaMaxF], stk_f[kEpaMaxF];
+  int32_t adj[kEpaMaxF][3];  // neighbour across edge e: face | (its edge << 16)
+  int32_t stk[kEpaMaxF];     // DFS stack: face | edge << 16 | state << 24
+  int16_t fv[kEpaMaxF][3];
   int16_t freel[kEpaMaxF], deadl[kEpaMaxF], newl[kEpaMaxF];  // recycled slots; this pass's kills / births
-  int8_t fe[kEpaMaxF][3], alive[kEpaMaxF], stk_e[kEpaMaxF], stk_s[kEpaMaxF];
-  int nv, nf, pass, hcf, hff, hnf, fail, stop, nfree, ndead, nnew;
+  int8_t alive[kEpaMaxF];
+  int nv, nf, hcf, hff, hnf, fail, stop, nfree, ndead, nnew;
+  double fdmin;  // distance of the face being expanded: new faces may not undercut it
+};
+// scalar state of a step, kept in registers while one lane grows the hull
+struct EpaCtl {
+  int nv, nf, hcf, hff, hnf, fail, nfree, ndead, nnew;
+  double fdmin;
+  DRC_HD __forceinline__ void load(const EpaPoly* E) {
+    nv = E->nv; nf = E->nf; hcf = E->hcf; hff = E->hff; hnf = E->hnf; fail = E->fail;
+    nfree = E->nfree; ndead = E->ndead; nnew = E->nnew; fdmin = E->fdmin;
+  }
+  DRC_HD __forceinline__ void store(EpaPoly* E) const {
+    E->nv = nv; E->nf = nf; E->hcf = hcf; E->hff = hff; E->hnf = hnf; E->fail = fail;
+    E->nfree = nfree; E->ndead = ndead; E->nnew = nnew; E->fdmin = fdmin;
+  }
+};
+struct FaceMask {
+  uint64_t lo, hi;
+  DRC_HD __forceinline__ bool has(int f) const { return f < 64 ? (lo >> f) & 1ull : (hi >> (f - 64)) & 1ull; }
+  DRC_HD __forceinline__ void set(int f) {
+    if (f < 64) lo |= 1ull << f;
+    else hi |= 1ull << (f - 64);
+  }
 };
 DRC_HD __forceinline__ V3 epa_vw(const EpaPoly* E, int i) { return v3(E->vw[i][0], E->vw[i][1], E->vw[i][2]); }
 DRC_HD __forceinline__ V3 epa_va(const EpaPoly* E, int i) { return v3(E->va[i][0], E->va[i][1], E->va[i][2]); }
@@ -341,85 +385,92 @@ DRC_HD __forceinline__ void epa_addv(EpaPoly* E, V3 w, V3 a) {
   st3(E->va[E->nv], a);
   E->nv++;
 }
-DRC_HD __forceinline__ int epa_newface(EpaPoly* E, int a, int b, int c) {
+// "face f sees w": the oracle's visibility test (not (n.w - d < -1e-12))
+DRC_HD __forceinline__ bool epa_sees(const EpaPoly* E, int f, V3 w) {
+  return !(dot(ld3(E->fn[f]), w) - E->fd[f] < -1e-12);
+}
+DRC_HD __forceinline__ int epa_newface(EpaPoly* E, EpaCtl& C, int a, int b, int c) {
   int f;
-  if (E->nfree > 0) {
-    f = E->freel[--E->nfree];
-  } else if (E->nf < kEpaMaxF) {
-    f = E->nf++;
+  if (C.nfree > 0) {
+    f = E->freel[--C.nfree];
+  } else if (C.nf < kEpaMaxF) {
+    f = C.nf++;
   } else {
-    E->fail = 1;
+    C.fail = 1;
     return -1;
   }
-  E->newl[E->nnew++] = f;
+  E->newl[C.nnew++] = f;
   E->fv[f][0] = a;
   E->fv[f][1] = b;
   E->fv[f][2] = c;
-  E->alive[f] = 1;
-  E->fpass[f] = 0;
-  V3 nn = cross(epa_vw(E, b) - epa_vw(E, a), epa_vw(E, c) - epa_vw(E, a));
+  const V3 va_ = epa_vw(E, a);
+  V3 nn = cross(epa_vw(E, b) - va_, epa_vw(E, c) - va_);
   const double L = sqrt(dot(nn, nn));
   if (!(L > 1e-300)) {
-    E->fail = 1;
+    C.fail = 1;
     E->alive[f] = 0;
     return -1;
   }
-  nn = (1.0 / L) * nn;
+  nn = v3(nn.x / L, nn.y / L, nn.z / L);  // same rounding as the oracle
+  const double fd = dot(nn, va_);
   st3(E->fn[f], nn);
-  E->fd[f] = dot(nn, epa_vw(E, a));
+  E->fd[f] = fd;
+  // the origin must stay inside (Bullet's EPA_INSIDE_EPS test): a face that
+  // sees it from outside means the hull went non-convex numerically.  And
+  // EPA's lower bound never decreases: a new face closer to the origin than
+  // the face it replaces is a rounding artefact of a near-coplanar support
+  if (fd < -1e-12 || fd < C.fdmin - 1e-12) {
+    C.fail = 1;
+    E->alive[f] = 0;
+    return -1;
+  }
+  E->alive[f] = 1;
   return f;
 }
 DRC_HD __forceinline__ void epa_bind(EpaPoly* E, int f0, int e0, int f1, int e1) {
-  E->ff[f0][e0] = f1;
-  E->fe[f0][e0] = e1;
-  E->ff[f1][e1] = f0;
-  E->fe[f1][e1] = e0;
+  E->adj[f0][e0] = f1 | (e1 << 16);
+  E->adj[f1][e1] = f0 | (e0 << 16);
 }
-// iterative form of btGjkEpa2::expand over the three edges of `best`
-DRC_HD inline bool epa_expand_all(EpaPoly* E, int w, int best) {
-  const V3 ww = epa_vw(E, w);
+// iterative form of btGjkEpa2::expand over the three edges of `best`; `vis`
+// holds epa_sees() of every face for the new vertex w (computed up front)
+DRC_HD __forceinline__ bool epa_expand_all(EpaPoly* E, EpaCtl& C, int w, int best, FaceMask vis) {
+  FaceMask done{0, 0};  // oracle: fpass[f] == pass
+  done.set(best);
   for (int j = 0; j < 3; ++j) {
-    E->stk_f[0] = E->ff[best][j];
-    E->stk_e[0] = E->fe[best][j];
-    E->stk_s[0] = 0;
+    E->stk[0] = E->adj[best][j];
     int sp = 1;
     while (sp > 0) {
-      const int f = E->stk_f[sp - 1], e = E->stk_e[sp - 1], st = E->stk_s[sp - 1];
+      const int ent = E->stk[sp - 1];
+      const int f = ent & 0xffff, e = (ent >> 16) & 0xff, st = ent >> 24;
       if (st == 0) {
-        if (E->fpass[f] == E->pass) {
+        if (done.has(f)) {
           --sp;
           continue;
         }
         const int e1 = e == 2 ? 0 : e + 1;
-        if (dot(ld3(E->fn[f]), ww) - E->fd[f] < -1e-12) {
-          const int nf = epa_newface(E, E->fv[f][e1], E->fv[f][e], w);
+        if (!vis.has(f)) {  // horizon edge: new face on (f's e1 vertex, e vertex, w)
+          const int nf = epa_newface(E, C, E->fv[f][e1], E->fv[f][e], w);
           if (nf < 0) return false;
           epa_bind(E, nf, 0, f, e);
-          if (E->hcf >= 0) epa_bind(E, E->hcf, 1, nf, 2);
-          else E->hff = nf;
-          E->hcf = nf;
-          ++E->hnf;
+          if (C.hcf >= 0) epa_bind(E, C.hcf, 1, nf, 2);
+          else C.hff = nf;
+          C.hcf = nf;
+          ++C.hnf;
           --sp;
           continue;
         }
-        E->fpass[f] = E->pass;
-        E->stk_s[sp - 1] = 1;
+        done.set(f);
+        E->stk[sp - 1] = f | (e << 16) | (1 << 24);
         if (sp >= kEpaMaxF) return false;
-        E->stk_f[sp] = E->ff[f][e1];
-        E->stk_e[sp] = E->fe[f][e1];
-        E->stk_s[sp] = 0;
-        ++sp;
+        E->stk[sp++] = E->adj[f][e1];
       } else if (st == 1) {
         const int e2 = e == 0 ? 2 : e - 1;
-        E->stk_s[sp - 1] = 2;
+        E->stk[sp - 1] = f | (e << 16) | (2 << 24);
         if (sp >= kEpaMaxF) return false;
-        E->stk_f[sp] = E->ff[f][e2];
-        E->stk_e[sp] = E->fe[f][e2];
-        E->stk_s[sp] = 0;
-        ++sp;
+        E->stk[sp++] = E->adj[f][e2];
       } else {
         E->alive[f] = 0;
-        E->deadl[E->ndead++] = f;
+        E->deadl[C.ndead++] = f;
         --sp;
       }
     }
@@ -428,15 +479,18 @@ DRC_HD inline bool epa_expand_all(EpaPoly* E, int w, int best) {
 }
 // rerun GJK and build the initial tetrahedron from its final simplex
 // (lane-serial)
-DRC_HD __noinline__ void epa_init(const Shape A, const Shape B, EpaPoly* E) {
+DRC_HD __forceinline__ void epa_init(const Shape A, const Shape B, EpaPoly* E) {
   GjkState g;
   gjk_run(A, B, g);
   E->nv = 0;
   E->nf = 0;
-  E->pass = 0;
   E->fail = 0;
   E->nfree = 0;
   E->nnew = 0;
+  E->ndead = 0;
+  E->hcf = E->hff = -1;
+  E->hnf = 0;
+  E->fdmin = -1e300;
   for (int i = 0; i < 4; ++i)
     if (i < g.n) epa_addv(E, g.S[i].w, g.S[i].a);
   for (int di = 0; di < 6 && E->nv < 4; ++di) {
@@ -463,8 +517,11 @@ DRC_HD __noinline__ void epa_init(const Shape A, const Shape B, EpaPoly* E) {
       }
     }
   }
-  const int t0 = epa_newface(E, 0, 1, 2), t1 = epa_newface(E, 1, 0, 3), t2 = epa_newface(E, 2, 1, 3),
-            t3 = epa_newface(E, 0, 2, 3);
+  EpaCtl C;
+  C.load(E);
+  const int t0 = epa_newface(E, C, 0, 1, 2), t1 = epa_newface(E, C, 1, 0, 3), t2 = epa_newface(E, C, 2, 1, 3),
+            t3 = epa_newface(E, C, 0, 2, 3);
+  C.store(E);
   if (!E->fail) {
     epa_bind(E, t0, 0, t1, 0);
     epa_bind(E, t0, 1, t2, 0);
@@ -475,45 +532,63 @@ DRC_HD __noinline__ void epa_init(const Shape A, const Shape B, EpaPoly* E) {
   }
   E->stop = E->fail;
 }
-// one expansion step from face `best` (lane-serial); sets E->stop when done
-DRC_HD __noinline__ void epa_step(const Shape A, const Shape B, EpaPoly* E, int best) {
-  const V3 bn = ld3(E->fn[best]);
-  const SV w = sup_md(A, B, bn);
-  if (dot(bn, w.w) - E->fd[best] <= 1e-12 || E->nv >= kEpaMaxV) {
+// stop tests of one expansion step from face `best`, given the support point
+// w in direction n_best: support gap below tolerance or vertex cap reached.
+// The duplicate-vertex test is separate so a wave can spread it over lanes.
+DRC_HD __forceinline__ bool epa_gap_stop(const EpaPoly* E, int best, const SV& w) {
+  return dot(ld3(E->fn[best]), w.w) - E->fd[best] <= 1e-12 || E->nv >= kEpaMaxV;
+}
+DRC_HD __forceinline__ bool epa_is_dup(const EpaPoly* E, int i, const SV& w) {
+  const V3 d = w.w - epa_vw(E, i);
+  return fabs(d.x) <= 1e-14 && fabs(d.y) <= 1e-14 && fabs(d.z) <= 1e-14;
+}
+// grow the polytope by w from face `best` (lane-serial; vis from the wave);
+// sets E->stop when the expansion is inconsistent (rolled back to the last
+// closed polytope)
+DRC_HD __forceinline__ void epa_grow(EpaPoly* E, const SV w, int best, FaceMask vis) {
+  EpaCtl C;
+  C.load(E);
+  const int wi = C.nv;
+  st3(E->vw[wi], w.w);
+  st3(E->va[wi], w.a);
+  C.nv++;
+  C.hcf = -1;
+  C.hff = -1;
+  C.hnf = 0;
+  C.ndead = 0;
+  C.nnew = 0;
+  C.fdmin = E->fd[best];
+  const bool valid = epa_expand_all(E, C, wi, best, vis);
+  if (!valid || C.hnf < 3 || C.fail) {  // roll back to the last closed polytope
+    for (int i = 0; i < C.nnew; ++i) E->alive[E->newl[i]] = 0;
+    for (int i = 0; i < C.ndead; ++i) E->alive[E->deadl[i]] = 1;
+    C.nv--;
+    C.store(E);
     E->stop = 1;
     return;
   }
-  for (int i = 0; i < E->nv; ++i) {  // support point already a vertex: cannot expand
-    const V3 d = w.w - epa_vw(E, i);
-    if (fabs(d.x) <= 1e-14 && fabs(d.y) <= 1e-14 && fabs(d.z) <= 1e-14) {
-      E->stop = 1;
-      return;
-    }
-  }
-  const int wi = E->nv;
-  epa_addv(E, w.w, w.a);
-  E->pass++;
-  E->hcf = -1;
-  E->hff = -1;
-  E->hnf = 0;
-  E->ndead = 0;
-  E->nnew = 0;
-  E->fpass[best] = E->pass;
-  const bool valid = epa_expand_all(E, wi, best);
-  if (!valid || E->hnf < 3 || E->fail) {  // roll back to the last closed polytope
-    for (int i = 0; i < E->nnew; ++i) E->alive[E->newl[i]] = 0;
-    for (int i = 0; i < E->ndead; ++i) E->alive[E->deadl[i]] = 1;
-    E->nv--;
-    E->stop = 1;
-    return;
-  }
-  epa_bind(E, E->hcf, 1, E->hff, 2);
+  epa_bind(E, C.hcf, 1, C.hff, 2);
   E->alive[best] = 0;
-  for (int i = 0; i < E->ndead; ++i) E->freel[E->nfree++] = E->deadl[i];
-  E->freel[E->nfree++] = best;
+  for (int i = 0; i < C.ndead; ++i) E->freel[C.nfree++] = E->deadl[i];
+  E->freel[C.nfree++] = best;
+  C.store(E);
+}
+// one expansion step (lane-serial form, host harness)
+DRC_HD inline void epa_step(const Shape& A, const Shape& B, EpaPoly* E, int best) {
+  const SV w = sup_md(A, B, ld3(E->fn[best]));
+  bool stop = epa_gap_stop(E, best, w);
+  for (int i = 0; !stop && i < E->nv; ++i) stop = epa_is_dup(E, i, w);
+  if (stop) {
+    E->stop = 1;
+    return;
+  }
+  FaceMask vis{0, 0};
+  for (int f = 0; f < E->nf; ++f)
+    if (epa_sees(E, f, w.w)) vis.set(f);
+  epa_grow(E, w, best, vis);
 }
 // witness points on the closest face (lane-serial); returns -depth
-DRC_HD __noinline__ double epa_finish(EpaPoly* E, int best) {
+DRC_HD __forceinline__ double epa_finish(EpaPoly* E, int best) {
   const double bd = E->fd[best];
   const V3 bn = ld3(E->fn[best]);
   const int i0 = E->fv[best][0], i1 = E->fv[best][1], i2 = E->fv[best][2];
@@ -541,7 +616,17 @@ DRC_HD inline int epa_best_serial(const EpaPoly* E) {
 // lane-serial driver (host harness and single-lane use)
 DRC_HD inline double epa_serial(const Shape& A, const Shape& B, EpaPoly* E) {
   epa_init(A, B, E);
-  for (int it = 0; it < 255 && !E->stop; ++it) epa_step(A, B, E, epa_best_serial(E));
+  for (int it = 0; it < 255 && !E->stop; ++it) {
+#ifdef DRC_NARROW_DEBUG
+    const int bb = epa_best_serial(E);
+    const SV ww = sup_md(A, B, ld3(E->fn[bb]));
+    printf("epa it %d best %d fd %.12g gap %.3g nv %d nf %d\n", it, bb, E->fd[bb], dot(ld3(E->fn[bb]), ww.w) - E->fd[bb], E->nv, E->nf);
+#endif
+    epa_step(A, B, E, epa_best_serial(E));
+  }
+#ifdef DRC_NARROW_DEBUG
+  printf("epa end stop %d fail %d nv %d\n", E->stop, E->fail, E->nv);
+#endif
   return epa_finish(E, epa_best_serial(E));
 }
 

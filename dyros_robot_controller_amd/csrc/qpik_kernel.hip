@@ -43,14 +43,14 @@ struct KParams {
   int oP, oG, oQ, oAB, oL, oU, oD, oE, oRho, oX, oZ, oY, oDY, oXT, oZT, oT1, oT2, oRed, oSc;
   // union region (kinematics | K^-1 | polish)
   int oU0;
-  int kT, kZ, kTe, kJ, kTg, kq, kqd, kA6, kAi, kW, kPart, kPd, kPf, kxdd, kmg, kdg, kJt, kSv, kScr;
+  int kT, kZ, kTe, kJ, kTg, kq, kqd, kA6, kAi, kW, kPart, kPd, kPf, kxdd, kmg, kdg, kJt, kSv, kScr, kEpa;
   int lds_doubles;
 };
 
 
 // ---- diagnostic phase stamps (built only with -DDRC_PHASE_TIMING) ---------
 #ifdef DRC_PHASE_TIMING
-__device__ unsigned long long g_phase_cycles[32];
+__device__ unsigned long long g_phase_cycles[64];
 #define PH_DECL unsigned long long ph_prev = __builtin_amdgcn_s_memtime(), ph_acc[16] = {0};
 #define PH(k)                                              \
   do {                                                     \
@@ -63,10 +63,22 @@ __device__ unsigned long long g_phase_cycles[32];
     if (lane_id() == 0)                                                           \
       for (int k_ = 0; k_ < 16; ++k_) atomicAdd(&g_phase_cycles[(base) + k_], ph_acc[k_]); \
   } while (0)
+// direct accumulation (functions without the kernel's stamp locals)
+#define PHG_DECL unsigned long long phg_t = __builtin_amdgcn_s_memtime();
+#define PHG(slot)                                                                  \
+  do {                                                                             \
+    unsigned long long t_ = __builtin_amdgcn_s_memtime();                          \
+    if (lane_id() == 0) atomicAdd(&g_phase_cycles[(slot)], t_ - phg_t);             \
+    phg_t = t_;                                                                    \
+  } while (0)
+#define PHG_RESET() do { phg_t = __builtin_amdgcn_s_memtime(); } while (0)
 #else
 #define PH_DECL
 #define PH(k) do {} while (0)
 #define PH_FLUSH(base) do {} while (0)
+#define PHG_DECL
+#define PHG(slot) do {} while (0)
+#define PHG_RESET() do {} while (0)
 #endif
 
 // scalar slots in the oSc region
@@ -405,6 +417,58 @@ __device__ __forceinline__ void factor_kinv(const KParams& kp, double* S) {
   }
 }
 
+// Register form for compile-time shapes: lane l assembles row l of K and the
+// Gauss-Jordan sweep runs on registers, the pivot row moving by v_readlane.
+// Same operation sequence as factor_kinv's LDS sweep (bit-identical).
+__device__ __forceinline__ double bcast(double v, int lane);
+template <class QD>
+__device__ __noinline__ void factor_kinv_regs(const KParams& kp, double* S) {
+  constexpr int NX = QD::nx, NG = QD::ng, NP = QD::np;
+  const int l = lane_id();
+  const double *P = S + kp.oP, *G = S + kp.oG, *ab = S + kp.oAB, *rho = S + kp.oRho;
+  double* K = S + kp.oU0;
+  if (l < NX) {  // row l of K = P + sigma I + A^T diag(rho) A (LDS, as factor_kinv)
+    for (int c = 0; c < NX; ++c) {
+      double s = (l < NP && c < NP) ? P[l * NP + c] : 0.0;
+      if (c == l) s += kp.s.sigma + ab[l] * ab[l] * rho[l];
+      for (int i = 0; i < NG; ++i) s += G[i * NX + l] * rho[NX + i] * G[i * NX + c];
+      K[l * NX + c] = s;
+    }
+  }
+  wsync();
+  const int lr = l < NX ? l : 0;
+  double Kr[NX];
+#pragma unroll
+  for (int c = 0; c < NX; ++c) Kr[c] = K[lr * NX + c];
+#pragma unroll
+  for (int k = 0; k < NX; ++k) {
+    if (l == k) {
+      const double p = 1.0 / Kr[k];
+      Kr[k] = 1.0;
+#pragma unroll
+      for (int j = 0; j < NX; ++j) Kr[j] *= p;
+    }
+    const double f = Kr[k];
+    if (l != k) Kr[k] = 0.0;
+#pragma unroll
+    for (int j = 0; j < NX; ++j) {
+      const double rkj = bcast(Kr[j], k);
+      if (l != k) Kr[j] -= f * rkj;
+    }
+  }
+  if (l < NX) {
+#pragma unroll
+    for (int c = 0; c < NX; ++c) K[l * NX + c] = Kr[c];
+  }
+  wsync();
+}
+
+template <class QD>
+__device__ __forceinline__ void factor_any(const KParams& kp, double* S) {
+  if constexpr (QD::nx > 0) factor_kinv_regs<QD>(kp, S);
+  else factor_kinv<QD>(kp, S);
+}
+
 template <class QD>
 __device__ __forceinline__ void set_rho(const KParams& kp, double* S, double rho) {
   const int l = lane_id(), nx = DNX, ng = DNG;
@@ -507,21 +571,45 @@ __device__ __forceinline__ void load_admm_regs(const KParams& kp, const double* 
 // line (runs every check_termination iterations).  Works on the published
 // LDS iterate.  Returns 0 = continue, 1 = continue after reloading the
 // registers (K^-1 or rho changed, or the iterate was touched), 2 = stop.
+#ifdef DRC_PHASE_TIMING
+#define CK_T0() unsigned long long ck_t = __builtin_amdgcn_s_memtime()
+#define CK_T(slot)                                                              \
+  do {                                                                          \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime();                 \
+    if (lane_id() == 0) atomicAdd(&g_phase_cycles[(slot)], t_ - ck_t);          \
+    ck_t = t_;                                                                  \
+  } while (0)
+#define CK_N(slot) do { if (lane_id() == 0) atomicAdd(&g_phase_cycles[(slot)], 1ull); } while (0)
+#else
+#define CK_T0() do {} while (0)
+#define CK_T(slot) do {} while (0)
+#define CK_N(slot) do {} while (0)
+#endif
 template <class QD>
 __device__ __noinline__ int admm_check(const KParams& kp, double* S, int it, int check, int adapt, int* status) {
   double *x = S + kp.oX, *z = S + kp.oZ, *y = S + kp.oY, *sc = S + kp.oSc;
   int reload = 0;
+  CK_T0();
   residuals<QD>(kp, S, x, z, y, kp.s.eps_abs, kp.s.eps_rel);
+  CK_T(32);
+  CK_N(33);
   if (check) {
     const bool conv = sc[SC_PRI] < sc[SC_EPSP] && sc[SC_DUA] < sc[SC_EPSD];
     // parity mode: a certified polish is exact whatever the ADMM residual,
-    // so also try it every 4th check (slow-ADMM vertices)
-    if (kp.s.exact && !conv && it % (4 * kp.s.check_termination) == 0) {
-      if (polish<QD>(kp, S, true)) {
+    // so try it at every check (the active set settles long before OSQP's
+    // eps_rel termination)
+    if (kp.s.exact && !conv) {
+      CK_T(34);
+      const bool ok_ = polish<QD>(kp, S, true);
+      CK_T(35);
+      CK_N(36);
+      if (ok_) {
+        CK_N(37);
         *status = DRC_STATUS_SOLVED;
         return 2;
       }
-      factor_kinv<QD>(kp, S);  // polish used the union region
+      factor_any<QD>(kp, S);
+      CK_T(38);  // polish used the union region
       residuals<QD>(kp, S, x, z, y, kp.s.eps_abs, kp.s.eps_rel);
       reload = 1;
     }
@@ -530,11 +618,17 @@ __device__ __noinline__ int admm_check(const KParams& kp, double* S, int it, int
         *status = DRC_STATUS_SOLVED;
         return 2;
       }
-      if (polish<QD>(kp, S, true)) {
+      CK_T(34);
+      const bool ok_ = polish<QD>(kp, S, true);
+      CK_T(35);
+      CK_N(36);
+      if (ok_) {
+        CK_N(37);
         *status = DRC_STATUS_SOLVED;
         return 2;
       }
-      factor_kinv<QD>(kp, S);
+      factor_any<QD>(kp, S);
+      CK_T(38);
       residuals<QD>(kp, S, x, z, y, kp.s.eps_fallback, kp.s.eps_fallback);
       if (sc[SC_PRI] < sc[SC_EPSP] && sc[SC_DUA] < sc[SC_EPSD]) {
         *status = DRC_STATUS_SOLVED;
@@ -554,7 +648,8 @@ __device__ __noinline__ int admm_check(const KParams& kp, double* S, int it, int
     rn = fmin(fmax(rn, kRhoMin), kRhoMax);
     if (rn > rho * kp.s.adaptive_rho_tolerance || rn < rho / kp.s.adaptive_rho_tolerance) {
       set_rho<QD>(kp, S, rn);
-      factor_kinv<QD>(kp, S);
+      factor_any<QD>(kp, S);
+      CK_T(38);
       reload = 1;
     }
   }
@@ -898,7 +993,6 @@ struct IO {
   int32_t* st_pair;
   double* rec;  // product path: per-instance task record [B][rec_stride] (coalesced)
   int64_t rec_stride;
-  EpaPoly* epa_ws;
 };
 
 // Occupancy target of the task kernel (waves per SIMD): the lane-serial
@@ -911,12 +1005,18 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRC_TAS
   const int l = lane_id();
   const int nv = kp.nv;
   const int64_t B = io.B;
-  EpaPoly* ews = io.epa_ws + blockIdx.x;
+  EpaPoly* ews = reinterpret_cast<EpaPoly*>(S + kp.kEpa);  // LDS-resident polytope
   PH_DECL
   const InstSeq seq(B, kp.xcd_map);
   for (int64_t j = seq.j0; j < seq.n; j += seq.step) {
     const int64_t b = seq.at(j);
     if (b >= B) continue;
+#ifdef DRC_PHASE_TIMING
+    const unsigned long long inst_t0 = __builtin_amdgcn_s_memtime();
+    unsigned long long ph_snap[8];
+    for (int k_ = 0; k_ < 8; ++k_) ph_snap[k_] = ph_acc[k_];
+    unsigned long long epa_calls = 0, epa_steps = 0, epa_maxsteps = 0, epa_t[3] = {0, 0, 0};
+#endif
     // re-derive the model pointer each instance: keeps LICM from hoisting
     // model-constant loads out of the instance loop into spilled registers
     const DevModel* M = M0;
@@ -1225,20 +1325,43 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRC_TAS
     }
     wsync();
     PH(4);
-    // EPA: one penetrating pair at a time; the owning lane expands the
-    // polytope, the whole wave scans for the closest face
-    for (int p0 = 0; p0 < M->npairs; p0 += 64) {
-      unsigned long long need = __ballot(p0 + l < M->npairs && pf[p0 + l] == 2.0);
-      while (need) {
-        const int ln = __ffsll(static_cast<long long>(need)) - 1;
-        need &= need - 1;
-        const int p = p0 + ln, ga = M->pair_a[p], gb = M->pair_b[p];
+    // EPA, best-first with bounds: the swept-core bound pd[p] <= d(p) also
+    // caps the penetration depth, so pairs are expanded in increasing pd and
+    // the search stops once no remaining pair can undercut the running
+    // minimum (same argmin and tie rule as computing every pair).  The owning
+    // lane expands the polytope, the whole wave scans for the closest face.
+    {
+      double gbd = bestd;
+      int gbi = besti;
+      wave_argmin(gbd, gbi);
+      for (;;) {
+        double cpd = 1.7976931348623157e308;
+        int cp = 0x7fffffff;
+        for (int p = l; p < M->npairs; p += 64)
+          if (pf[p] == 2.0 && pd[p] < cpd) {
+            cpd = pd[p];
+            cp = p;
+          }
+        wave_argmin(cpd, cp);
+        if (cp == 0x7fffffff || cpd > gbd || (cpd == gbd && cp > gbi)) break;
+        const int p = cp, ln = p & 63, ga = M->pair_a[p], gb = M->pair_b[p];
         const Shape A{M->gtype[ga], Tg + 12 * ga, M->gparam[ga][0], M->gparam[ga][1], M->gparam[ga][2]};
         const Shape Bs{M->gtype[gb], Tg + 12 * gb, M->gparam[gb][0], M->gparam[gb][1], M->gparam[gb][2]};
         if (l == ln) epa_init(A, Bs, ews);
         wsync();
+        double dres = 0;
+#ifdef DRC_PHASE_TIMING
+        epa_calls++;
+#endif
         for (int it = 0; it <= 255; ++it) {
-          const int stop = ews->stop;
+#ifdef DRC_PHASE_TIMING
+          epa_steps++;
+          if ((unsigned long long)it > epa_maxsteps) epa_maxsteps = it;
+#endif
+#ifdef DRC_PHASE_TIMING
+          unsigned long long te0 = __builtin_amdgcn_s_memtime();
+#endif
+          bool stop = ews->stop || it == 255;
           double fdm = 1e300;
           int fb = 0x7fffffff;
           for (int f = l; f < ews->nf; f += 64)
@@ -1247,9 +1370,28 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRC_TAS
               fb = f;
             }
           wave_argmin(fdm, fb);
-          if (stop || it == 255) {
+          if (fb == 0x7fffffff) {  // no alive face (failed seed): oracle takes face 0
+            fb = 0;
+            stop = true;
+          }
+#ifdef DRC_PHASE_TIMING
+          unsigned long long te1 = __builtin_amdgcn_s_memtime();
+          epa_t[0] += te1 - te0;
+#endif
+          SV w;
+          if (!stop) {  // support, gap and duplicate tests on the whole wave
+            w = sup_md(A, Bs, ld3(ews->fn[fb]));
+            stop = epa_gap_stop(ews, fb, w);
+            if (!stop) {
+              bool dup = false;
+              for (int i = l; i < ews->nv; i += 64) dup |= epa_is_dup(ews, i, w);
+              stop = __any(dup);
+            }
+          }
+          if (stop) {
             if (l == ln) {
-              const double d = epa_finish(ews, fb == 0x7fffffff ? 0 : fb);
+              const double d = epa_finish(ews, fb);
+              dres = d;
               if (d < bestd || (d == bestd && p < besti)) {
                 bestd = d;
                 besti = p;
@@ -1259,9 +1401,25 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRC_TAS
             }
             break;
           }
-          if (l == ln) epa_step(A, Bs, ews, fb);
+#ifdef DRC_PHASE_TIMING
+          unsigned long long te2 = __builtin_amdgcn_s_memtime();
+          epa_t[1] += te2 - te1;
+#endif
+          FaceMask vis;  // visibility of every face for w, one bit per face
+          vis.lo = __ballot(l < ews->nf && epa_sees(ews, l, w.w));
+          vis.hi = __ballot(l + 64 < ews->nf && epa_sees(ews, l + 64, w.w));
+          if (l == ln) epa_grow(ews, w, fb, vis);
           wsync();
+#ifdef DRC_PHASE_TIMING
+          epa_t[2] += __builtin_amdgcn_s_memtime() - te2;
+#endif
         }
+        const double dall = __shfl(dres, ln, 64);
+        if (dall < gbd || (dall == gbd && p < gbi)) {
+          gbd = dall;
+          gbi = p;
+        }
+        if (l == ln) pf[p] = 1.0;
         wsync();
       }
     }
@@ -1301,6 +1459,22 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRC_TAS
     }
     wsync();
     PH(7);
+#ifdef DRC_PHASE_TIMING
+    if (l == 0) {  // straggler census: max instance cycles, count above 2M
+      const unsigned long long dt = __builtin_amdgcn_s_memtime() - inst_t0;
+      atomicMax(&g_phase_cycles[30], dt);
+      if (dt > 2000000ull) atomicAdd(&g_phase_cycles[31], 1ull);
+      if (dt > 2000000ull) atomicAdd(&g_phase_cycles[29], dt);
+      if (dt > 2000000ull) {
+        for (int k_ = 0; k_ < 8; ++k_) atomicAdd(&g_phase_cycles[8 + k_], ph_acc[k_] - ph_snap[k_]);
+        atomicAdd(&g_phase_cycles[22], epa_calls);
+        atomicAdd(&g_phase_cycles[23], epa_steps);
+        atomicMax(&g_phase_cycles[28], epa_maxsteps);
+        atomicAdd(&g_phase_cycles[18], epa_t[0] + epa_t[1]);  // (qp kernel leaves 18, 20 free)
+        atomicAdd(&g_phase_cycles[20], epa_t[2]);
+      }
+    }
+#endif
     // ---------------- task data out -----------------------------------------
     if (io.rec) {  // product path: one coalesced record per instance
       double* rec = io.rec + b * io.rec_stride;
@@ -1541,8 +1715,10 @@ __device__ __forceinline__ int qp_admm(const KParams& kp, const KParams& kpl, do
   double* sc = S + kp.oSc;
   int status = DRC_STATUS_MAX_ITER;
   (void)G;
+  PHG_DECL
   set_rho<QD>(kp, S, kp.s.rho);
-  factor_kinv<QD>(kp, S);
+  factor_any<QD>(kpl, S);
+  PHG(24);
   if (l < nx) x[l] = 0.0;
   for (int row = l; row < m; row += 64) z[row] = y[row] = 0.0;
   wsync();
@@ -1558,6 +1734,10 @@ __device__ __forceinline__ int qp_admm(const KParams& kp, const KParams& kpl, do
     double Gc[NG], Kr[NX], GKr[NX];
     prep_admm_mats<QD>(kpl, S);
     load_admm_regs<QD>(kp, S, Gc, Kr, GKr);
+    PHG(25);
+#ifdef DRC_PHASE_TIMING
+    unsigned long long tchk = 0;
+#endif
     const bool hb = l < NX, hg = l < NG;
     const int lb_ = hb ? l : 0, lg_ = hg ? NX + l : 0;
     const double ab_l = ab[lb_], q_l = qq[lb_], lo_b = lo[lb_], up_b = up[lb_], lo_g = lo[lg_], up_g = up[lg_];
@@ -1620,7 +1800,13 @@ __device__ __forceinline__ int qp_admm(const KParams& kp, const KParams& kpl, do
       }
       wsync();
       if (!(check || adapt)) continue;  // last iteration: published for the output
+#ifdef DRC_PHASE_TIMING
+      const unsigned long long tc0 = __builtin_amdgcn_s_memtime();
+#endif
       const int act = admm_check<QD>(kpl, S, it, check, adapt, &status);
+#ifdef DRC_PHASE_TIMING
+      tchk += __builtin_amdgcn_s_memtime() - tc0;
+#endif
       if (act == 2) break;
       const bool reload = act == 1;
       if (reload) {
@@ -1638,6 +1824,13 @@ __device__ __forceinline__ int qp_admm(const KParams& kp, const KParams& kpl, do
         }
       }
     }
+#ifdef DRC_PHASE_TIMING
+    PHG(26);
+    if (l == 0) {
+      atomicAdd(&g_phase_cycles[27], tchk);
+      atomicAdd(&g_phase_cycles[26], 0ull - tchk);
+    }
+#endif
   } else {
     for (it = 1; it <= kp.s.max_iter; ++it) {
       for (int row = l; row < m; row += 64) w[row] = rv[row] * z[row] - y[row];
@@ -1701,7 +1894,7 @@ __device__ __forceinline__ int qp_admm(const KParams& kp, const KParams& kpl, do
         const bool conv = sc[SC_PRI] < sc[SC_EPSP] && sc[SC_DUA] < sc[SC_EPSD];
         // parity mode: a certified polish is exact whatever the ADMM
         // residual, so also try it every 4th check (slow-ADMM vertices)
-        if (kp.s.exact && !conv && it % (4 * kp.s.check_termination) == 0) {
+        if (kp.s.exact && !conv) {
           if (polish<QD>(kp, S, true)) {
             status = DRC_STATUS_SOLVED;
             break;
@@ -1805,8 +1998,6 @@ struct drc_model_impl {
   drc_kinematic_param kparam{};
   drc_joint_index jidx{};
   drc_actuator_index aidx{};
-  EpaPoly* epa_ws = nullptr;
-  int64_t epa_count = 0;
   void* pool = nullptr;  // task data when the caller does not keep it
   int64_t pool_bytes = 0;
   int timing = 0;                 // drc_debug_kernel_timing: HIP events around each launch
@@ -1985,6 +2176,7 @@ static int plan_layout(const DevModel& M, KParams* k, bool task_only) {
   k->kJt = takeu(6 * np);
   k->kSv = takeu(3 * kMaxWheels);
   k->kScr = takeu(96);
+  k->kEpa = task_only ? takeu(static_cast<int>((sizeof(EpaPoly) + 7) / 8)) : 0;
   int kin_end = u;
   int kinv_end = k->oU0 + nx * nx + nx * ng;  // K^-1 and G K^-1
   const int N = nx + ng;
@@ -2078,7 +2270,7 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
   // grid-stride launches; the task kernel's grid is capped so its per-wave
   // EPA workspaces (~60 KB each) stay modest
   const int64_t grid = B < 8192 ? B : 8192;
-  const int64_t grid_task = B < 4096 ? B : 4096;
+  const int64_t grid_task = B < 8192 ? B : 8192;
   // product path: per-instance task records (rLen doubles padded to whole
   // 128-B lines) in a model-owned pool; the stage API writes [field][B]
   const int64_t stride = (kt.rLen + 15) & ~int64_t(15);
@@ -2086,12 +2278,6 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
   double* rec = nullptr;
   {
     std::lock_guard<std::mutex> g(m->mu);
-    if (m->epa_count < grid_task) {
-      if (m->epa_ws) HIP_TRY(hipFree(m->epa_ws));
-      m->epa_ws = nullptr;
-      HIP_TRY(hipMalloc(&m->epa_ws, sizeof(EpaPoly) * grid_task));
-      m->epa_count = grid_task;
-    }
     if (!stages) {
       if (m->pool_bytes < stride * B * 8) {
         if (m->pool) HIP_TRY(hipFree(m->pool));
@@ -2104,7 +2290,7 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
   }
   // XCD-aware order needs grids that are multiples of 8 (both are, from 16 Ki up)
   kt.xcd_map = kq.xcd_map = B >= 16384 ? 1 : 0;
-  IO io{B, q, qdot, xt, xdt, xi, xdi, out, status, iters, pose, jac, man, dist, xdd, pair, rec, stride, m->epa_ws};
+  IO io{B, q, qdot, xt, xdt, xi, xdi, out, status, iters, pose, jac, man, dist, xdd, pair, rec, stride};
   hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
   if (m->timing && !stages) {
     for (auto& e : ev) HIP_TRY(hipEventCreate(&e));
@@ -2190,10 +2376,10 @@ int drc_debug_kernel_times(drc_model* m, double* task_ms, double* qp_ms, int* ca
 #ifdef DRC_PHASE_TIMING
 // diagnostic build only: accumulated per-phase s_memtime cycles (32 slots)
 int drc_debug_phase_cycles(unsigned long long* out, int reset) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(drc_amd::g_phase_cycles), sizeof(unsigned long long) * 32) != hipSuccess)
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(drc_amd::g_phase_cycles), sizeof(unsigned long long) * 64) != hipSuccess)
     return DRC_ERR_HIP;
   if (reset) {
-    unsigned long long z[32] = {0};
+    unsigned long long z[64] = {0};
     if (hipMemcpyToSymbol(HIP_SYMBOL(drc_amd::g_phase_cycles), z, sizeof(z)) != hipSuccess) return DRC_ERR_HIP;
   }
   return DRC_OK;
@@ -2273,7 +2459,6 @@ void drc_model_destroy(drc_model* m) {
   if (!m) return;
   (void)hipSetDevice(m->device);
   if (m->d_model) (void)hipFree(m->d_model);
-  if (m->epa_ws) (void)hipFree(m->epa_ws);
   if (m->pool) (void)hipFree(m->pool);
   delete m;
 }

@@ -374,6 +374,9 @@ static int closest_simplex(SV* S, int n, double* v, double* lam_out) {
         double p[3] = {0, 0, 0};
         for (int i = 0; i < k; ++i) for (int c = 0; c < 3; ++c) p[c] += lam[i] * S[idx[i]].w[c];
         double dv = dot3(p, p);
+        /* a tetrahedron spans R^3, so its candidate must be the origin itself;
+         * a nonzero p means a flat, ill-conditioned tetrahedron: reject it */
+        if (k == 4 && dv > 1e-20) continue;
         if (bmask == 0 || dv < best - 1e-18) {
             best = dv; bmask = mask;
             memcpy(v, p, sizeof(p));
@@ -401,7 +404,10 @@ static int gjk(const Shape* A, const Shape* B, SV* S, int* ns, double* lam, doub
         if (n > 0 && vv - dot3(v, w.w) <= 1e-12 * sqrt(vv)) break;
         int dup = 0;
         for (int i = 0; i < n; ++i) if (S[i].w[0] == w.w[0] && S[i].w[1] == w.w[1] && S[i].w[2] == w.w[2]) dup = 1;
-        if (dup) break;
+        /* a repeated support point before the gap test passed: the simplex
+         * stalled numerically.  The support in -v then tells the side: v.w <= 0
+         * means the Minkowski difference reaches past the origin (overlap). */
+        if (dup) { if (dot3(v, w.w) <= 0) { *ns = n; return 1; } break; }
         S[n++] = w;
         n = closest_simplex(S, n, v, lam);
         if (n == 4 || dot3(v, v) < 1e-24) { *ns = n; return 1; }
@@ -410,8 +416,9 @@ static int gjk(const Shape* A, const Shape* B, SV* S, int* ns, double* lam, doub
     return 0;
 }
 
-#define EPA_MAXV 128
-#define EPA_MAXF 256
+/* hpp-fcl GJKSolver defaults (epa_max_vertex_num, epa_max_face_num) */
+#define EPA_MAXV 64
+#define EPA_MAXF 128
 /* Expanding polytope with face adjacency (Bullet/libccd style): the visible
  * region is flood-filled from the closest face across shared edges, so the
  * horizon is always a single loop and the polytope stays a valid closed
@@ -424,6 +431,7 @@ typedef struct Epa {
     double fn[EPA_MAXF][3], fd[EPA_MAXF];
     int freel[EPA_MAXF], deadl[EPA_MAXF], newl[EPA_MAXF];  /* recycled slots; this pass's kills / births */
     int hcf, hff, hnf, fail, nfree, ndead, nnew;
+    double fdmin;  /* distance of the face being expanded: new faces may not undercut it */
 } Epa;
 
 static int epa_newface(Epa* E, int a, int b, int c) {
@@ -442,6 +450,12 @@ static int epa_newface(Epa* E, int a, int b, int c) {
     if (!(L > 1e-300)) { E->fail = 1; E->alive[f] = 0; return -1; }
     for (int k = 0; k < 3; ++k) E->fn[f][k] = nn[k] / L;
     E->fd[f] = dot3(E->fn[f], E->V[a].w);
+    /* the origin must stay inside (Bullet's EPA_INSIDE_EPS test): a face
+     * that sees it from outside means the hull went non-convex numerically */
+    if (E->fd[f] < -1e-12) { E->fail = 1; E->alive[f] = 0; return -1; }
+    /* EPA's lower bound never decreases: a new face closer to the origin than
+     * the face it replaces is a rounding artefact of a near-coplanar support */
+    if (E->fd[f] < E->fdmin - 1e-12) { E->fail = 1; E->alive[f] = 0; return -1; }
     return f;
 }
 static void epa_bind(Epa* E, int f0, int e0, int f1, int e1) {
@@ -475,7 +489,7 @@ static int epa_expand(Epa* E, int w, int f, int e) {
 static double epa(const Shape* A, const Shape* B, SV* S, int ns, double* pA, double* pB) {
     static const double dirs[6][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}, {-1, 0, 0}, {0, -1, 0}, {0, 0, -1}};
     static __thread Epa E;
-    E.nv = ns; E.nf = 0; E.pass = 0; E.fail = 0; E.nfree = 0; E.nnew = 0;
+    E.nv = ns; E.nf = 0; E.pass = 0; E.fail = 0; E.nfree = 0; E.nnew = 0; E.fdmin = -INFINITY;
     for (int i = 0; i < ns; ++i) E.V[i] = S[i];
     for (int di = 0; di < 6 && E.nv < 4; ++di) {
         SV w;
@@ -517,7 +531,7 @@ static double epa(const Shape* A, const Shape* B, SV* S, int ns, double* pA, dou
             int wi = E.nv;
             E.V[E.nv++] = w;
             E.pass++;
-            E.hcf = -1; E.hff = -1; E.hnf = 0; E.ndead = 0; E.nnew = 0;
+            E.hcf = -1; E.hff = -1; E.hnf = 0; E.ndead = 0; E.nnew = 0; E.fdmin = E.fd[best];
             E.fpass[best] = E.pass;
             int valid = 1;
             for (int j = 0; j < 3 && valid; ++j) valid = epa_expand(&E, wi, E.ff[best][j], E.fe[best][j]);
@@ -1108,8 +1122,9 @@ int oracle_solve_qp(int n, int m, const double* P, const double* qv, const doubl
         if (check) {
             int conv = w.pri_res < w.eps_pri && w.dua_res < w.eps_dua;
             /* parity mode: a certified polish is exact whatever the ADMM
-             * residual, so also try it every 4th check (slow-ADMM vertices) */
-            if (s->exact && !conv && it % (4 * s->check_termination) == 0 && qp_polish(&w, s, 1)) {
+             * residual, so try it at every check (the active set settles
+             * long before OSQP's eps_rel termination) */
+            if (s->exact && !conv && qp_polish(&w, s, 1)) {
                 status = ORC_SOLVED; pol = 1; break;
             }
             if (conv) {

@@ -14,7 +14,7 @@ ctrl = manipulator.RobotController(0.001, rd)
 link = "fr3_link8" if robot == "fr3" else "tool0"
 args = [torch.as_tensor(a, device=dev) for a in (q, qd, xt, xdt)]
 ctrl.QPIK_step_batch(*args, link); torch.cuda.synchronize()
-buf = (C.c_ulonglong * 32)()
+buf = (C.c_ulonglong * 64)()
 _capi.lib().drc_debug_phase_cycles(buf, 1)
 ctrl.QPIK_step_batch(*args, link); torch.cuda.synchronize()
 _capi.lib().drc_debug_phase_cycles(buf, 0)
@@ -22,7 +22,16 @@ v = np.array(buf[:], dtype=np.float64)
 names_t = ["fk+geoms", "J+taskvel", "manip", "broad+sphere", "gjk cand", "epa", "argmin+witness", "grad"]
 names_q = ["load+assemble", "scaling", "-", "rho+factor+admm+checks", "-", "output"]
 tt, tq = v[:8], v[16:22]
+ta = v[24:28]
 print("task kernel cycles/instance: %.0f" % (tt.sum() / B))
 for n, x in zip(names_t, tt): print("  %-16s %6.1f%%  %8.0f cyc/inst" % (n, 100 * x / tt.sum(), x / B))
 print("qp kernel cycles/instance: %.0f" % (tq.sum() / B))
 for n, x in zip(names_q, tq): print("  %-16s %6.1f%%  %8.0f cyc/inst" % (n, 100 * x / tq.sum(), x / B))
+names_a = ["set_rho+factor", "prep+load regs", "admm iterations (+publish)", "admm_check (residuals/polish/refactor)"]
+print("inside rho+factor+admm+checks:")
+for n, x in zip(names_a, ta): print("  %-40s %8.0f cyc/inst" % (n, x / B))
+print("task stragglers: max instance %.0f cycles, %d instances > 2M cycles (%.1f%% of task cycles)" % (v[30], v[31], 100 * v[29] / max(tt.sum(), 1)))
+print("straggler phase split: " + ", ".join("%s %.0f%%" % (n, 100 * x / max(v[8:16].sum(), 1)) for n, x in zip(names_t, v[8:16])))
+print("stragglers: %d EPA calls, %d EPA steps, max %d steps in one call" % (v[22], v[23], v[28]))
+print("straggler EPA step split: scan+support+tests %.0f, grow %.0f cycles/step" % (v[18] / max(v[23], 1), v[20] / max(v[23], 1)))
+print("admm_check: residuals %.0f cyc/inst (%d calls), polish %.0f cyc/inst (%d attempts, %d accepted), refactor after polish %.0f cyc/inst" % (v[32] / B, v[33], v[35] / B, v[36], v[37], v[38] / B))
