@@ -2207,12 +2207,18 @@ static int make_kparams(const drc_model_impl* mm, const drc_qpik_params* p, int 
   k->t = p->t;
   k->t0 = p->t0;
   k->duration = p->duration;
-  if (p->frame_id < 0 || p->frame_id >= M.nframes)
-    return set_err(DRC_ERR_UNKNOWN_LINK, "params.frame_id does not name a link of the model");
-  if (M.frame_joint[p->frame_id] == 0)
-    return set_err(DRC_ERR_UNKNOWN_LINK, "task frame is attached to the universe (no joint moves it)");
-  k->frame_joint = M.frame_joint[p->frame_id];
-  std::memcpy(k->frame_place, M.frame_place[p->frame_id], sizeof(k->frame_place));
+  if (stages && p->frame_id == -1) {  // stage outputs without a task frame: last joint
+    k->frame_joint = M.nv;
+    static const double eye[12] = {1, 0, 0, 0, 1, 0, 0, 0, 1, 0, 0, 0};
+    std::memcpy(k->frame_place, eye, sizeof(k->frame_place));
+  } else {
+    if (p->frame_id < 0 || p->frame_id >= M.nframes)
+      return set_err(DRC_ERR_UNKNOWN_LINK, "params.frame_id does not name a link of the model");
+    if (M.frame_joint[p->frame_id] == 0)
+      return set_err(DRC_ERR_UNKNOWN_LINK, "task frame is attached to the universe (no joint moves it)");
+    k->frame_joint = M.frame_joint[p->frame_id];
+    std::memcpy(k->frame_place, M.frame_place[p->frame_id], sizeof(k->frame_place));
+  }
   if (p->mode < DRC_MODE_QPIK || p->mode > DRC_MODE_QPIK_CUBIC) return set_err(DRC_ERR_INVALID_ARGUMENT, "bad mode");
   k->mode = p->mode;
   k->stages = stages;

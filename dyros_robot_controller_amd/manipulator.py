@@ -122,7 +122,8 @@ class RobotData:
 
     # -- task-space getters through the kernel's stage outputs ---------------
     def _stages(self, q, qdot, link_name):
-        p = QPIKParamsBuilder(self.model, exact=True).params(link_name, mode=_capi.MODE_QPIK)
+        pb = QPIKParamsBuilder(self.model, exact=True)
+        p = pb.params(link_name, mode=_capi.MODE_QPIK) if link_name else pb.params_no_frame(_capi.MODE_QPIK)
         dq = _batch.as_device(np.asarray(q, float).reshape(-1, 1), self.device)
         dqd = _batch.as_device(np.asarray(qdot, float).reshape(-1, 1), self.device)
         z6 = _batch.as_device(np.zeros((6, 1)), self.device)
@@ -158,15 +159,7 @@ class RobotData:
     def getMinDistance(self, with_grad=True, with_graddot=False, verbose=False):
         if with_graddot:
             raise NotImplementedError("grad_dot is outside the QPIK hot path (SURVEY §8f)")
-        link = None
-        for cand in ("fr3_link8", "tool0"):
-            try:
-                self.model.frame_id(cand)
-                link = cand
-                break
-            except _capi.DrcError:
-                pass
-        st = self._stages(self.q_, self.qdot_, link)
+        st = self._stages(self.q_, self.qdot_, None)  # no task frame needed
         return MinDistResult(st["dist"][0], st["dist"][1:] if with_grad else np.zeros(self.getDof()))
 
     get_pose, get_jacobian, get_velocity = getPose, getJacobian, getVelocity
@@ -199,6 +192,14 @@ class QPIKParamsBuilder:
         self.model = model
         self.base = _capi.QPIKParams()
         _capi.check(_capi.lib().drc_default_qpik_params(model.handle, C.c_int(1 if exact else 0), C.byref(self.base)))
+
+    def params_no_frame(self, mode):
+        """Stage-only parameters without a task frame (frame_id = -1)."""
+        p = _capi.QPIKParams()
+        C.pointer(p)[0] = self.base
+        p.frame_id = -1
+        p.mode = mode
+        return p
 
     def params(self, link_name, mode, kp=None, kv=None, t=0.0, t0=0.0, duration=1.0):
         p = _capi.QPIKParams()

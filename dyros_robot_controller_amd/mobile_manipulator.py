@@ -1,0 +1,314 @@
+"""``drc.mobile_manipulator`` mirror: RobotData + RobotController (QPIK).
+
+Mirrors the reference's Python interface for the whole-body QP-IK path
+(drc/mobile_manipulator/robot_data.py:16-44, robot_controller.py:188-249;
+src/mobile_manipulator/robot_data.cpp:7-144,407-496; QP_IK.cpp:7-128;
+robot_controller.cpp:147-197) and the types of drc/type_define.py:6-91.
+
+=====================================================  ==========================================
+reference                                              here
+=====================================================  ==========================================
+``KinematicParam / JointIndex / ActuatorIndex``        same classes (``DriveType`` enum)
+``RobotData(param, joint_idx, actuator_idx, urdf,      same (+ ``device``)
+srdf, packages)``
+``update_state(q_virtual, q_mobile, q_mani, qdot_*)``  same
+``get_dof / get_actuator_dof / get_manipulator_dof /   same
+get_mobile_dof / get_joint_index / ...``
+``get_mobile_FK_jacobian``                             same (model build, HIP library)
+``RobotController(dt, robot_data)``                    same
+``QPIK / QPIK_step / QPIK_cubic -> (qdot_mobile,       same
+qdot_mani)``
+(none)                                                 ``QPIK_batch`` / ``QPIK_step_batch`` /
+                                                       ``QPIK_cubic_batch`` over [field][B]
+                                                       device tensors -> (eta [A][B], status)
+=====================================================  ==========================================
+
+Every result comes from ``libdrc_amd.so``; the single-instance calls are
+B = 1 launches of the batched kernel.
+"""
+import sys
+from enum import IntEnum
+
+import numpy as np
+
+from . import _batch, _capi
+from ._capi import C
+from .manipulator import QPIKParamsBuilder, _ModelHandle, _default_device, pose_to12
+
+
+class DriveType(IntEnum):
+    """drc/type_define.py:6-9 (Caster bases are not supported by the kernel)."""
+    Differential = _capi.DRIVE_DIFFERENTIAL
+    Mecanum = _capi.DRIVE_MECANUM
+    Caster = _capi.DRIVE_CASTER
+
+
+class KinematicParam:
+    """drc/type_define.py:11-54 (include/dyros_robot_controller/type_define.h:58-120)."""
+
+    def __init__(self, type, wheel_radius, max_lin_speed=2.0, max_ang_speed=2.0, max_lin_acc=2.0,
+                 max_ang_acc=2.0, base_width=None, roller_angles=None, base2wheel_positions=None,
+                 base2wheel_angles=None, wheel_offset=None):
+        self.type = DriveType(type)
+        self.wheel_radius = float(wheel_radius)
+        self.max_lin_speed, self.max_ang_speed = float(max_lin_speed), float(max_ang_speed)
+        self.max_lin_acc, self.max_ang_acc = float(max_lin_acc), float(max_ang_acc)
+        self.base_width = base_width
+        self.roller_angles = roller_angles
+        self.base2wheel_positions = base2wheel_positions
+        self.base2wheel_angles = base2wheel_angles
+        self.wheel_offset = wheel_offset
+        if self.type == DriveType.Differential and base_width is None:
+            raise ValueError("Differential drive requires base_width")
+        if self.type == DriveType.Mecanum and (roller_angles is None or base2wheel_positions is None
+                                               or base2wheel_angles is None):
+            raise ValueError("Mecanum drive requires roller_angles, base2wheel_positions, base2wheel_angles")
+
+    def c_struct(self):
+        p = _capi.KinematicParam()
+        p.type = int(self.type)
+        p.wheel_radius = self.wheel_radius
+        p.max_lin_speed, p.max_ang_speed = self.max_lin_speed, self.max_ang_speed
+        p.max_lin_acc, p.max_ang_acc = self.max_lin_acc, self.max_ang_acc
+        p.base_width = float(self.base_width) if self.base_width is not None else 0.0
+        n = 2
+        if self.type == DriveType.Mecanum:
+            n = len(self.roller_angles)
+            if n > _capi.MAX_WHEELS:
+                raise ValueError("at most %d wheels" % _capi.MAX_WHEELS)
+            for i in range(n):
+                p.roller_angles[i] = float(self.roller_angles[i])
+                p.base2wheel_positions[i][0] = float(self.base2wheel_positions[i][0])
+                p.base2wheel_positions[i][1] = float(self.base2wheel_positions[i][1])
+                p.base2wheel_angles[i] = float(self.base2wheel_angles[i])
+        p.n_wheels = n
+        p.wheel_offset = float(self.wheel_offset) if self.wheel_offset is not None else 0.0
+        return p
+
+
+class JointIndex:
+    """drc/type_define.py:56-74."""
+
+    def __init__(self, virtual_start, mani_start, mobi_start):
+        self.virtual_start, self.mani_start, self.mobi_start = int(virtual_start), int(mani_start), int(mobi_start)
+
+    def c_struct(self):
+        j = _capi.JointIndex()
+        j.virtual_start, j.mani_start, j.mobi_start = self.virtual_start, self.mani_start, self.mobi_start
+        return j
+
+
+class ActuatorIndex:
+    """drc/type_define.py:76-91."""
+
+    def __init__(self, mani_start, mobi_start):
+        self.mani_start, self.mobi_start = int(mani_start), int(mobi_start)
+
+    def c_struct(self):
+        a = _capi.ActuatorIndex()
+        a.mani_start, a.mobi_start = self.mani_start, self.mobi_start
+        return a
+
+
+class RobotData:
+    """MobileManipulator::RobotData (mobile_manipulator/robot_data.h:55)."""
+
+    def __init__(self, mobile_param, joint_idx, actuator_idx, urdf_path, srdf_path="", packages_path="",
+                 device=None):
+        import torch
+        self.device = torch.device(device) if device is not None else _default_device()
+        self._param, self._jidx, self._aidx = mobile_param, joint_idx, actuator_idx
+        kp, ji, ai = mobile_param.c_struct(), joint_idx.c_struct(), actuator_idx.c_struct()
+        h = C.c_void_p()
+        _capi.check(_capi.lib().drc_model_create_mobile_manipulator(
+            C.byref(kp), C.byref(ji), C.byref(ai), urdf_path.encode(), (srdf_path or "").encode(),
+            (packages_path or "").encode(), C.c_int(self.device.index or 0), C.byref(h)))
+        self.model = _ModelHandle(h, self.device)
+        n = self.model.dof
+        self._lims = [np.zeros(n) for _ in range(4)]
+        _capi.check(_capi.lib().drc_model_limits(h, *(a.ctypes.data_as(C.POINTER(C.c_double)) for a in self._lims)))
+        self._Jm = np.zeros((3, self.model.mobi_dof))
+        Jm = np.zeros(3 * _capi.MAX_WHEELS)
+        _capi.check(_capi.lib().drc_model_mobile_fk_jacobian(h, Jm.ctypes.data_as(C.POINTER(C.c_double))))
+        self._Jm = Jm[:3 * self.model.mobi_dof].reshape(3, self.model.mobi_dof)
+        self.q_ = np.zeros(n)
+        self.qdot_ = np.zeros(n)
+
+    # -- sizes and indices -----------------------------------------------------
+    def get_dof(self):
+        return self.model.dof
+
+    def get_actuator_dof(self):
+        return self.model.actuated_dof
+
+    def get_manipulator_dof(self):
+        return self.model.mani_dof
+
+    def get_mobile_dof(self):
+        return self.model.mobi_dof
+
+    def get_joint_index(self):
+        return self._jidx
+
+    def get_actuator_index(self):
+        return self._aidx
+
+    def get_mobile_FK_jacobian(self):
+        return self._Jm.copy()
+
+    compute_mobile_FK_jacobian = lambda self, q_mobile=None: self.get_mobile_FK_jacobian()  # noqa: E731
+
+    def get_joint_position_limit(self):
+        return self._lims[0].copy(), self._lims[1].copy()
+
+    def get_joint_velocity_limit(self):
+        return self._lims[2].copy(), self._lims[3].copy()
+
+    # -- state -----------------------------------------------------------------
+    def joint_vector(self, q_virtual, q_mobile, q_mani):
+        """getJointVector (robot_data.cpp:418-427): place the blocks by JointIndex."""
+        q = np.zeros(self.get_dof())
+        ji = self._jidx
+        q[ji.virtual_start:ji.virtual_start + 3] = np.asarray(q_virtual, float).reshape(-1)
+        q[ji.mobi_start:ji.mobi_start + self.get_mobile_dof()] = np.asarray(q_mobile, float).reshape(-1)
+        q[ji.mani_start:ji.mani_start + self.get_manipulator_dof()] = np.asarray(q_mani, float).reshape(-1)
+        return q
+
+    def update_state(self, q_virtual, q_mobile, q_mani, qdot_virtual, qdot_mobile, qdot_mani):
+        self.q_ = self.joint_vector(q_virtual, q_mobile, q_mani)
+        self.qdot_ = self.joint_vector(qdot_virtual, qdot_mobile, qdot_mani)
+        return True
+
+    updateState = update_state
+
+    def get_joint_position(self):
+        return self.q_.copy()
+
+    def get_joint_velocity(self):
+        return self.qdot_.copy()
+
+    # -- task-space values through the kernel's stage outputs ----------------
+    def _stages(self, link_name):
+        pb = QPIKParamsBuilder(self.model, exact=True)
+        p = pb.params(link_name, mode=_capi.MODE_QPIK) if link_name else pb.params_no_frame(_capi.MODE_QPIK)
+        dev = self.device
+        st = _batch.stages_batch(self.model, p, _batch.as_device(self.q_.reshape(-1, 1), dev),
+                                 _batch.as_device(self.qdot_.reshape(-1, 1), dev), None,
+                                 _batch.as_device(np.zeros((6, 1)), dev))
+        return {k: v.cpu().numpy() for k, v in st.items()}
+
+    def get_pose(self, link_name):
+        from .manipulator import pose_from12
+        return pose_from12(self._stages(link_name)["pose"][:, 0])
+
+    def get_jacobian(self, link_name):
+        return self._stages(link_name)["jac"][:, 0].reshape(6, self.get_dof())
+
+    def get_manipulability(self, with_grad, with_graddot, link_name):
+        from .manipulator import ManipulabilityResult
+        m = self._stages(link_name)["man"][:, 0]
+        return ManipulabilityResult(m[0], m[1:] if with_grad else None)
+
+    def get_min_distance(self, with_grad, with_graddot, verbose=False):
+        from .manipulator import MinDistResult
+        d = self._stages(None)["dist"][:, 0]
+        return MinDistResult(d[0], d[1:] if with_grad else None)
+
+
+class RobotController:
+    """MobileManipulator::RobotController QPIK entries
+    (src/mobile_manipulator/robot_controller.cpp:7-22,147-197): xdot_des =
+    Kp (x) e + xdot_target with Kp = 400 (no Kv term), eta split by
+    ActuatorIndex into (qdot_mobile, qdot_mani); zeros on failure."""
+
+    def __init__(self, dt, robot_data, solver_mode="exact"):
+        if not isinstance(robot_data, RobotData):
+            raise TypeError("robot_data must be a mobile_manipulator.RobotData")
+        self.dt_ = float(dt)
+        self.robot_data_ = robot_data
+        self.Kp_task_ = np.full(6, 400.0)
+        self.Kv_task_ = np.full(6, 0.0)
+        self.set_solver_mode(solver_mode)
+
+    def set_solver_mode(self, mode):
+        if mode not in ("exact", "osqp_default"):
+            raise ValueError("solver_mode must be 'exact' or 'osqp_default'")
+        self.solver_mode = mode
+        self._pb = QPIKParamsBuilder(self.robot_data_.model, exact=(mode == "exact"))
+
+    def set_task_gain(self, kp, kv):
+        kp, kv = np.asarray(kp, float).reshape(-1), np.asarray(kv, float).reshape(-1)
+        if kp.size != 6 or kv.size != 6:
+            raise RuntimeError("Kp and Kv must be of size 6.")
+        self.Kp_task_, self.Kv_task_ = kp, kv
+
+    def set_task_kp_gain(self, kp):
+        kp = np.asarray(kp, float).reshape(-1)
+        if kp.size != 6:
+            raise RuntimeError("Kp must be of size 6.")
+        self.Kp_task_ = kp
+
+    def set_task_kv_gain(self, kv):
+        kv = np.asarray(kv, float).reshape(-1)
+        if kv.size != 6:
+            raise RuntimeError("Kv must be of size 6.")
+        self.Kv_task_ = kv
+
+    setTaskGain, setTaskKpGain, setTaskKvGain = set_task_gain, set_task_kp_gain, set_task_kv_gain
+
+    # -- batched entries (device tensors, [field][B]; q is the full joint vector)
+    def _run(self, mode, link_name, q, qdot, x_target, xdot_target, x_init=None, xdot_init=None,
+             t=0.0, t0=0.0, duration=1.0, iters=None):
+        p = self._pb.params(link_name, mode, self.Kp_task_, self.Kv_task_, t, t0, duration)
+        dev = self.robot_data_.device
+        return _batch.qpik_batch(self.robot_data_.model, p, _batch.as_device(q, dev), _batch.as_device(qdot, dev),
+                                 _batch.as_device(x_target, dev), _batch.as_device(xdot_target, dev),
+                                 _batch.as_device(x_init, dev), _batch.as_device(xdot_init, dev), iters=iters)
+
+    def QPIK_batch(self, q, qdot, xdot_target, link_name):
+        return self._run(_capi.MODE_QPIK, link_name, q, qdot, None, xdot_target)
+
+    def QPIK_step_batch(self, q, qdot, x_target, xdot_target, link_name, iters=None):
+        return self._run(_capi.MODE_QPIK_STEP, link_name, q, qdot, x_target, xdot_target, iters=iters)
+
+    def QPIK_cubic_batch(self, q, qdot, x_target, xdot_target, x_init, xdot_init, current_time, init_time,
+                         duration, link_name):
+        return self._run(_capi.MODE_QPIK_CUBIC, link_name, q, qdot, x_target, xdot_target, x_init, xdot_init,
+                         current_time, init_time, duration)
+
+    def split_actuated(self, eta):
+        """eta [A] -> (qdot_mobile [W], qdot_mani [n]) by ActuatorIndex."""
+        a = self.robot_data_.get_actuator_index()
+        W, n = self.robot_data_.get_mobile_dof(), self.robot_data_.get_manipulator_dof()
+        return eta[a.mobi_start:a.mobi_start + W].copy(), eta[a.mani_start:a.mani_start + n].copy()
+
+    # -- single-instance entries (reference signatures; B = 1 launches) -------
+    def _one(self, out_status):
+        out, status = out_status
+        eta, st = out.cpu().numpy()[:, 0], int(status.cpu().numpy()[0])
+        if st != _capi.STATUS_SOLVED:
+            print("QP IK failed to compute optimal joint velocity.", file=sys.stderr)
+            eta = np.zeros(self.robot_data_.get_actuator_dof())
+        return self.split_actuated(eta)
+
+    def _state(self):
+        rd = self.robot_data_
+        return rd.q_.reshape(-1, 1), rd.qdot_.reshape(-1, 1)
+
+    def QPIK(self, xdot_target, link_name):
+        q, qd = self._state()
+        return self._one(self.QPIK_batch(q, qd, np.asarray(xdot_target, float).reshape(6, 1), link_name))
+
+    def QPIK_step(self, x_target, xdot_target, link_name):
+        q, qd = self._state()
+        return self._one(self.QPIK_step_batch(q, qd, pose_to12(x_target).reshape(12, 1),
+                                              np.asarray(xdot_target, float).reshape(6, 1), link_name))
+
+    def QPIK_cubic(self, x_target, xdot_target, x_init, xdot_init, current_time, init_time, duration, link_name):
+        q, qd = self._state()
+        return self._one(self.QPIK_cubic_batch(
+            q, qd, pose_to12(x_target).reshape(12, 1), np.asarray(xdot_target, float).reshape(6, 1),
+            pose_to12(x_init).reshape(12, 1), np.asarray(xdot_init, float).reshape(6, 1),
+            current_time, init_time, duration, link_name))
+
+    QPIKStep, QPIKCubic = QPIK_step, QPIK_cubic

@@ -173,7 +173,9 @@ int drc_qpik_batch(const drc_model* model, const drc_qpik_params* params, int64_
  *   man  [1+mani][B] (manipulability, grad)  (getManipulability(true,false)),
  *   dist [1+dof][B]  (distance, grad)        (getMinDistance(true,false,false)),
  *   pair [B] (argmin collision pair), xdot_des [6][B] (the QP's task velocity).
- * Any output pointer may be NULL. */
+ * Any output pointer may be NULL.  params->frame_id == -1 selects no task
+ * frame (pose/jac/man/xdot_des then refer to the last joint's frame), for
+ * callers that only need the distance stage (getMinDistance). */
 int drc_qpik_stages_batch(const drc_model* model, const drc_qpik_params* params, int64_t B,
                           const double* q, const double* qdot, const double* x_target,
                           const double* xdot_target, const double* x_init,

@@ -120,7 +120,7 @@ def pinv_cod(A, thr=1e-6):
         return np.zeros(A.T.shape)
     r = int(np.sum(d > thr * d[0]))
     # minimum-norm pseudo-inverse restricted to the numerical rank
-    U, s, Vt = np.linalg.svd(A)
+    U, s, Vt = np.linalg.svd(A, full_matrices=False)
     s_inv = np.zeros_like(s)
     s_inv[:r] = 1.0 / s[:r]
     return (Vt.T * s_inv) @ U.T

@@ -1,0 +1,89 @@
+"""GPU parity for the mobile-manipulator whole-body QP-IK (SURVEY §8a
+a18-a22): Husky-FR3 (differential, A = 9) and XLS-FR3 (mecanum, A = 11) vs
+the oracle restatement, through the C-ABI.
+
+Tolerances as tests/test_gpu_parity.py.  The MoMa QP has no slack variables
+(QP_IK.cpp:85-128), so instances can be primal infeasible: the status must
+match the oracle's and such instances return zeros (QP_IK.cpp:56-61)."""
+import numpy as np
+import pytest
+
+import oracle as O
+from _common import LINK, make_moma, moma_step_inputs, nonsmooth_min_distance, oracle_batch, stage_pose
+from dyros_robot_controller_amd import mobile_manipulator as MM
+
+pytestmark = pytest.mark.gpu
+ROBOTS = ["husky_fr3", "xls_fr3"]
+
+
+@pytest.mark.parametrize("robot", ROBOTS)
+def test_moma_model_and_mobile_jacobian(cuda, robot):
+    rd = make_moma(robot, cuda)
+    pm, om, spec = O.load(robot)
+    assert rd.get_dof() == om.nv
+    assert rd.get_manipulator_dof() == 7 and rd.get_mobile_dof() == spec["n_wheel"]
+    assert rd.get_actuator_dof() == 7 + spec["n_wheel"]
+    np.testing.assert_allclose(rd.get_mobile_FK_jacobian(), spec["J_mobile"](), atol=1e-12)
+
+
+@pytest.mark.parametrize("robot", ROBOTS)
+def test_moma_stages_match_oracle(cuda, robot):
+    rd = make_moma(robot, cuda)
+    B = 128
+    q, qd, xt, xdt = moma_step_inputs(rd, robot, 1, B, cuda)
+    st = stage_pose(rd.model, cuda, q, qd, LINK[robot])
+    pm, om, spec = O.load(robot)
+    n = om.nv
+    for b in range(B):
+        pose, J = O.fk_pose(om, q[:, b])
+        np.testing.assert_allclose(st["pose"][:9, b], pose[:9].reshape(3, 3).T.reshape(-1), atol=1e-12)
+        np.testing.assert_allclose(st["pose"][9:, b], pose[9:], atol=1e-12)
+        np.testing.assert_allclose(st["jac"][:, b].reshape(6, n), J, atol=1e-12)
+        m, mg = O.manipulability(om, q[:, b])
+        assert abs(st["man"][0, b] - m) <= 1e-10 * max(1.0, m)
+        np.testing.assert_allclose(st["man"][1:, b], mg, atol=1e-8)
+        d, dg, pair = O.min_distance(om, q[:, b])
+        assert abs(st["dist"][0, b] - d) <= (1e-9 if d > 0 else 1e-6), (b, st["dist"][0, b], d)
+        if st["pair"][b] == pair and np.max(np.abs(st["dist"][1:, b] - dg)) > (1e-5 if d > 0 else 1e-3):
+            assert nonsmooth_min_distance(om, q[:, b]), b
+
+
+@pytest.mark.parametrize("robot", ROBOTS)
+def test_moma_qpik_step_exact_matches_oracle(cuda, robot):
+    rd = make_moma(robot, cuda)
+    ctrl = MM.RobotController(0.001, rd, solver_mode="exact")
+    B = 512
+    q, qd, xt, xdt = moma_step_inputs(rd, robot, 2, B, cuda)
+    out, status = ctrl.QPIK_step_batch(q, qd, xt, xdt, LINK[robot])
+    out, status = out.cpu().numpy(), status.cpu().numpy()
+    ref, rstat, _, om = oracle_batch(robot, q, qd, xt, xdt, exact=True)
+    assert np.array_equal(status, rstat)
+    assert np.all(out[:, status != 1] == 0)
+    err = np.abs(out - ref).max(axis=0)
+    assert np.median(err) <= 1e-9
+    off = [b for b in range(B) if err[b] > 1e-4 and not nonsmooth_min_distance(om, q[:, b])]
+    print("%s: %d/%d instances outside 1e-4, %d not solved" % (robot, len(off), B, int(np.sum(status != 1))))
+    assert len(off) <= 0.05 * B, off
+
+
+def test_moma_single_instance_split(cuda):
+    """QPIK_step returns (qdot_mobile, qdot_mani) split by ActuatorIndex
+    (mobile_manipulator/robot_controller.cpp:182-196)."""
+    robot = "xls_fr3"
+    rd = make_moma(robot, cuda)
+    ctrl = MM.RobotController(0.001, rd)
+    q, qd, xt, xdt = moma_step_inputs(rd, robot, 5, 1, cuda)
+    ji = rd.get_joint_index()
+    W = rd.get_mobile_dof()
+    rd.update_state(q[ji.virtual_start:ji.virtual_start + 3, 0], q[ji.mobi_start:ji.mobi_start + W, 0],
+                    q[ji.mani_start:ji.mani_start + 7, 0], qd[ji.virtual_start:ji.virtual_start + 3, 0],
+                    qd[ji.mobi_start:ji.mobi_start + W, 0], qd[ji.mani_start:ji.mani_start + 7, 0])
+    from dyros_robot_controller_amd.manipulator import pose_from12
+    vm, va = ctrl.QPIK_step(pose_from12(xt[:, 0]), xdt[:, 0], LINK[robot])
+    eta, st = ctrl.QPIK_step_batch(q, qd, xt, xdt, LINK[robot])
+    eta = eta.cpu().numpy()[:, 0]
+    a = rd.get_actuator_index()
+    if int(st.cpu().numpy()[0]) == 1:
+        np.testing.assert_array_equal(vm, eta[a.mobi_start:a.mobi_start + W])
+        np.testing.assert_array_equal(va, eta[a.mani_start:a.mani_start + 7])
+    assert vm.shape == (W,) and va.shape == (7,)
