@@ -98,26 +98,27 @@ def main():
     ap.add_argument("--batch", type=int, default=65536, help="instances per GPU")
     ap.add_argument("--robot", default="fr3", choices=sorted(LINKS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--chunks", type=int, default=2, help="concurrent sub-batches per call")
     args = ap.parse_args()
 
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    from dyros_robot_controller_amd import dist as ddist
+    rank, world, local = ddist.env_rank()
+    backend = os.environ.get("DRC_DIST_BACKEND", "nccl")   # gloo: rehearse N ranks on one GPU
     if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+        torch.cuda.set_device(local % max(torch.cuda.device_count(), 1))
+        ddist.init(backend, torch.device("cuda", local) if backend == "nccl" else None)
+    dev = torch.device("cuda", local % max(torch.cuda.device_count(), 1))
     torch.cuda.set_device(dev)
 
     from dyros_robot_controller_amd import manipulator, robot_path
     robot, B = args.robot, args.batch
     rd = manipulator.RobotData(robot_path(robot), robot_path(robot, "srdf"), device=dev)
     ctrl = manipulator.RobotController(0.001, rd, solver_mode="exact")
-    q, qd, xt, xdt, dq, dqd, dxt, dxdt = make_inputs(rd, robot, B, 12345, rank * B, dev)
+    offset, _ = ddist.shard(rank, B)   # contiguous instance range of this rank
+    q, qd, xt, xdt, dq, dqd, dxt, dxdt = make_inputs(rd, robot, B, 12345, offset, dev)
     iters = torch.zeros(B, dtype=torch.int32, device=dev)
     link = LINKS[robot]
 
@@ -127,6 +128,7 @@ def main():
     from dyros_robot_controller_amd import _capi
     import ctypes as C
     handle = rd.model.handle
+    _capi.check(_capi.lib().drc_set_concurrency(handle, args.chunks))
     for _ in range(args.warmup):
         out, status = step()
     torch.cuda.synchronize()
@@ -148,20 +150,16 @@ def main():
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     step_event_ms = ev0.elapsed_time(ev1) / args.steps   # HIP events on the launch stream
-    tk, tq, nc = C.c_double(), C.c_double(), C.c_int()
-    _capi.check(_capi.lib().drc_debug_kernel_times(handle, C.byref(tk), C.byref(tq), C.byref(nc)))
+    tw, tk, tq, nc = C.c_double(), C.c_double(), C.c_double(), C.c_int()
+    _capi.check(_capi.lib().drc_debug_kernel_times(handle, C.byref(tw), C.byref(tk), C.byref(tq), C.byref(nc)))
     _capi.check(_capi.lib().drc_debug_kernel_timing(handle, 0))
-    task_ms, qp_ms = tk.value / max(nc.value, 1), tq.value / max(nc.value, 1)
-    kernel_ms = task_ms + qp_ms
-    t = torch.tensor([wall], dtype=torch.float64, device=dev)
-    n_bad = torch.tensor([float((status != 1).sum().item())], dtype=torch.float64, device=dev)
-    it_mean = torch.tensor([float(iters.double().mean().item())], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dist.all_reduce(n_bad, op=dist.ReduceOp.SUM)
-        dist.all_reduce(it_mean, op=dist.ReduceOp.SUM)
-        it_mean /= world
-    wall = t.item()
+    ncall = max(nc.value, 1)
+    # kernel_ms: one drc_qpik_batch call on its stream (fork -> join of the
+    # concurrent sub-batches); task/qp: summed per-sub-batch kernel durations
+    kernel_ms, task_ms, qp_ms = tw.value / ncall, tk.value / ncall, tq.value / ncall
+    wall, n_bad, it_mean = ddist.reduce_stats(wall, float((status != 1).sum().item()),
+                                              float(iters.double().mean().item()), world,
+                                              dev if backend == "nccl" else "cpu")
 
     if rank == 0:
         nv = rd.getDof()
@@ -171,7 +169,7 @@ def main():
         per_launch_bytes = algorithmic_bytes(nv) * B
         achieved = per_launch_bytes / (kernel_ms * 1e-3) / 1e9
         traffic = load_traffic(robot, B)
-        fl = flops_per_solve(nv, it_mean.item()) * B / (kernel_ms * 1e-3) / 1e12
+        fl = flops_per_solve(nv, it_mean) * B / (kernel_ms * 1e-3) / 1e12
         line = {
             "metric": "QP-IK solves/s (FR3 7-DoF, batch 65k) + achieved HBM GB/s vs peak",
             "value": value, "unit": "solves/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -183,14 +181,15 @@ def main():
                        "parallelism": "dp%d (instances sharded, no data-path collective)" % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "drc_qpik_batch = task_kernel + qp_kernel (one stream, one launch each)",
+                         "kernel": "drc_qpik_batch call (task_kernel + qp_kernel per sub-batch, %d concurrent "
+                                   "sub-batches)" % args.chunks,
                          "bytes_per_solve": algorithmic_bytes(nv), "bytes_per_launch": per_launch_bytes,
-                         "kernel_ms": kernel_ms, "task_kernel_ms": task_ms, "qp_kernel_ms": qp_ms,
+                         "kernel_ms": kernel_ms, "task_kernel_ms_sum": task_ms, "qp_kernel_ms_sum": qp_ms,
                          "step_event_ms": step_event_ms,
                          "fp64_valu_estimate": {"achieved_tflops": fl, "peak_tflops": FP64_VECTOR_PEAK_TFS,
                                                 "frac": fl / FP64_VECTOR_PEAK_TFS,
-                                                "flops_per_solve": flops_per_solve(nv, it_mean.item())}},
-            "non_solved": int(n_bad.item()), "admm_iters_mean": it_mean.item(),
+                                                "flops_per_solve": flops_per_solve(nv, it_mean)}},
+            "non_solved": int(n_bad), "admm_iters_mean": it_mean,
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(robot, q, qd, xt, xdt)

@@ -985,7 +985,8 @@ struct InstSeq {
 };
 
 struct IO {
-  int64_t B;
+  int64_t B;       // instances of this launch
+  int64_t b0, ld;  // global offset of instance 0, row stride of the [field][B] arrays
   const double *q, *qdot, *xt, *xdt, *xi, *xdi;
   double* out;
   int32_t *status, *iters;
@@ -1011,6 +1012,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRC_TAS
   for (int64_t j = seq.j0; j < seq.n; j += seq.step) {
     const int64_t b = seq.at(j);
     if (b >= B) continue;
+    const int64_t gb = io.b0 + b, LD = io.ld;  // position in the caller's [field][B] arrays
 #ifdef DRC_PHASE_TIMING
     const unsigned long long inst_t0 = __builtin_amdgcn_s_memtime();
     unsigned long long ph_snap[8];
@@ -1025,8 +1027,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRC_TAS
     double* qv = S + kp.kq;
     double* qd = S + kp.kqd;
     if (l < nv) {
-      qv[l] = io.q[l * B + b];
-      qd[l] = io.qdot[l * B + b];
+      qv[l] = io.q[l * LD + gb];
+      qd[l] = io.qdot[l * LD + gb];
     }
     wsync();
     // ---------------- FK: local joint transforms, then the chain ------------
@@ -1106,15 +1108,15 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRC_TAS
     double* xdd = S + kp.kxdd;
     if (l == 0) {
       if (kp.mode == DRC_MODE_QPIK) {
-        for (int i = 0; i < 6; ++i) xdd[i] = io.xdt[i * B + b];
+        for (int i = 0; i < 6; ++i) xdd[i] = io.xdt[i * LD + gb];
       } else {
         double xt[12], xdt[6];
-        for (int i = 0; i < 12; ++i) xt[i] = io.xt[i * B + b];
-        for (int i = 0; i < 6; ++i) xdt[i] = io.xdt[i * B + b];
+        for (int i = 0; i < 12; ++i) xt[i] = io.xt[i * LD + gb];
+        for (int i = 0; i < 6; ++i) xdt[i] = io.xdt[i * LD + gb];
         if (kp.mode == DRC_MODE_QPIK_CUBIC) {  // getTaskSpaceCubic (math_type_define.h:647)
           double xi[12], xdi[6], Rt[9], Ri[9];
-          for (int i = 0; i < 12; ++i) xi[i] = io.xi[i * B + b];
-          for (int i = 0; i < 6; ++i) xdi[i] = io.xdi[i * B + b];
+          for (int i = 0; i < 12; ++i) xi[i] = io.xi[i * LD + gb];
+          for (int i = 0; i < 6; ++i) xdi[i] = io.xdi[i * LD + gb];
           for (int r = 0; r < 3; ++r)
             for (int c = 0; c < 3; ++c) {
               Rt[3 * r + c] = xt[3 * c + r];
@@ -1493,20 +1495,20 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRC_TAS
       if (io.st_pose && l < 12) {
         // R row-major -> column-major storage, then p
         double v = l < 9 ? Te[(l % 3) * 3 + l / 3] : Te[l];
-        io.st_pose[l * B + b] = v;
+        io.st_pose[l * LD + gb] = v;
       }
       if (io.st_jac)
-        for (int e = l; e < 6 * nv; e += 64) io.st_jac[(int64_t)e * B + b] = J[e];
+        for (int e = l; e < 6 * nv; e += 64) io.st_jac[(int64_t)e * LD + gb] = J[e];
       if (io.st_man) {
-        if (l == 0) io.st_man[b] = S[kp.oSc + SC_MAN];
-        if (l < narm) io.st_man[(int64_t)(1 + l) * B + b] = mg[l];
+        if (l == 0) io.st_man[gb] = S[kp.oSc + SC_MAN];
+        if (l < narm) io.st_man[(int64_t)(1 + l) * LD + gb] = mg[l];
       }
       if (io.st_dist) {
-        if (l == 0) io.st_dist[b] = bestd;
-        if (l < nv) io.st_dist[(int64_t)(1 + l) * B + b] = dgv[l];
+        if (l == 0) io.st_dist[gb] = bestd;
+        if (l < nv) io.st_dist[(int64_t)(1 + l) * LD + gb] = dgv[l];
       }
-      if (io.st_pair && l == 0) io.st_pair[b] = besti < M->npairs ? besti : -1;
-      if (io.st_xdd && l < 6) io.st_xdd[l * B + b] = xdd[l];
+      if (io.st_pair && l == 0) io.st_pair[gb] = besti < M->npairs ? besti : -1;
+      if (io.st_xdd && l < 6) io.st_xdd[l * LD + gb] = xdd[l];
     }
     wsync();
   }
@@ -1963,6 +1965,7 @@ qp_kernel(const DevModel* __restrict__ M0, const KParams kp, const IO io) {
   for (int64_t j = seq.j0; j < seq.n; j += seq.step) {
     const int64_t b = seq.at(j);
     if (b >= B) continue;
+    const int64_t gb = io.b0 + b, LD = io.ld;  // position in the caller's [field][B] arrays
     const DevModel* M = M0;
     asm volatile("" : "+s"(M));
     qp_assemble<QD>(M, kp, S, io, b);
@@ -1973,10 +1976,10 @@ qp_kernel(const DevModel* __restrict__ M0, const KParams kp, const IO io) {
     PH(3);
     // ---------------- outputs (zero on failure, QP_IK.cpp:56-61) ------------
     const double *D = S + kp.oD, *x = S + kp.oX;
-    if (l < kp.na) io.out[(int64_t)l * B + b] = status == DRC_STATUS_SOLVED ? D[l] * x[l] : 0.0;
+    if (l < kp.na) io.out[(int64_t)l * LD + gb] = status == DRC_STATUS_SOLVED ? D[l] * x[l] : 0.0;
     if (l == 0) {
-      io.status[b] = status;
-      if (io.iters) io.iters[b] = iters;
+      io.status[gb] = status;
+      if (io.iters) io.iters[gb] = iters;
     }
     wsync();
     PH(5);
@@ -2000,8 +2003,17 @@ struct drc_model_impl {
   drc_actuator_index aidx{};
   void* pool = nullptr;  // task data when the caller does not keep it
   int64_t pool_bytes = 0;
-  int timing = 0;                 // drc_debug_kernel_timing: HIP events around each launch
-  std::vector<hipEvent_t> events;  // 3 per timed call: before task, between, after qp
+  int timing = 0;  // drc_debug_kernel_timing: HIP events around each launch
+  // timed calls: {caller-stream start, caller-stream end, per chunk: task start, task end, qp end}
+  std::vector<std::vector<hipEvent_t>> events;
+  // concurrent sub-batches: the batch is cut into `chunks` contiguous ranges
+  // run on internal streams forked from / joined to the caller's stream, so
+  // one range's task kernel overlaps another's QP kernel and the straggler
+  // tails of the kernels interleave
+  int chunks = 2;
+  std::vector<hipStream_t> lanes;
+  std::vector<hipEvent_t> joins;
+  hipEvent_t fork = nullptr;
   std::mutex mu;
 };
 
@@ -2294,38 +2306,88 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
       rec = reinterpret_cast<double*>(m->pool);
     }
   }
-  // XCD-aware order needs grids that are multiples of 8 (both are, from 16 Ki up)
-  kt.xcd_map = kq.xcd_map = B >= 16384 ? 1 : 0;
-  IO io{B, q, qdot, xt, xdt, xi, xdi, out, status, iters, pose, jac, man, dist, xdd, pair, rec, stride};
-  hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
-  if (m->timing && !stages) {
-    for (auto& e : ev) HIP_TRY(hipEventCreate(&e));
+  // sub-batches: whole multiples of 16 Ki instances per chunk (each keeps the
+  // XCD-aware order, whose grids must be multiples of 8)
+  int S = 1;
+  if (!stages)
+    for (int c = m->chunks; c > 1; --c)
+      if (B / c >= 16384) {
+        S = c;
+        break;
+      }
+  const bool timed = m->timing && !stages;
+  std::vector<hipEvent_t> tev;
+  auto mkev = [&](hipEvent_t* e) -> int {
+    HIP_TRY(hipEventCreate(e));
+    tev.push_back(*e);
+    return DRC_OK;
+  };
+  {
     std::lock_guard<std::mutex> g(m->mu);
-    for (auto& e : ev) m->events.push_back(e);
+    while (static_cast<int>(m->lanes.size()) < S) {
+      hipStream_t ls;
+      hipEvent_t je;
+      HIP_TRY(hipStreamCreateWithFlags(&ls, hipStreamNonBlocking));
+      HIP_TRY(hipEventCreateWithFlags(&je, hipEventDisableTiming));
+      m->lanes.push_back(ls);
+      m->joins.push_back(je);
+    }
+    if (!m->fork) HIP_TRY(hipEventCreateWithFlags(&m->fork, hipEventDisableTiming));
   }
-  if (ev[0]) HIP_TRY(hipEventRecord(ev[0], st));
-  hipLaunchKernelGGL(task_kernel, dim3(static_cast<unsigned>(grid_task)), dim3(64),
-                     static_cast<size_t>(kt.lds_doubles) * sizeof(double), st, m->d_model, kt, io);
-  HIP_TRY(hipGetLastError());
-  if (ev[1]) HIP_TRY(hipEventRecord(ev[1], st));
-  if (!stages) {
-    const size_t lds = static_cast<size_t>(kq.lds_doubles) * sizeof(double);
-    const dim3 g(static_cast<unsigned>(grid)), blk(64);
-    // compile-time QP shapes of the bundled robots; anything else runs the
-    // runtime-sized instantiation
-    if (kq.nx == 23 && kq.ng == 16 && kq.np == 7)
-      hipLaunchKernelGGL((qp_kernel<Dims<23, 16, 7>>), g, blk, lds, st, m->d_model, kq, io);  // FR3
-    else if (kq.nx == 20 && kq.ng == 14 && kq.np == 6)
-      hipLaunchKernelGGL((qp_kernel<Dims<20, 14, 6>>), g, blk, lds, st, m->d_model, kq, io);  // UR5e
-    else if (kq.nx == 9 && kq.ng == 16 && kq.np == 9)
-      hipLaunchKernelGGL((qp_kernel<Dims<9, 16, 9>>), g, blk, lds, st, m->d_model, kq, io);  // Husky-FR3
-    else if (kq.nx == 11 && kq.ng == 16 && kq.np == 11)
-      hipLaunchKernelGGL((qp_kernel<Dims<11, 16, 11>>), g, blk, lds, st, m->d_model, kq, io);  // XLS-FR3
-    else
-      hipLaunchKernelGGL((qp_kernel<Dims<0, 0, 0>>), g, blk, lds, st, m->d_model, kq, io);
+  hipEvent_t e_start = nullptr, e_end = nullptr;
+  if (timed) {
+    if (int r = mkev(&e_start)) return r;
+    if (int r = mkev(&e_end)) return r;
+    HIP_TRY(hipEventRecord(e_start, st));
+  }
+  if (S > 1) HIP_TRY(hipEventRecord(m->fork, st));
+  for (int c = 0; c < S; ++c) {
+    const int64_t b0 = B * c / S, b1 = B * (c + 1) / S, Bc = b1 - b0;
+    hipStream_t cs = S > 1 ? m->lanes[c] : st;
+    if (S > 1) HIP_TRY(hipStreamWaitEvent(cs, m->fork, 0));
+    KParams kt_c = kt, kq_c = kq;
+    kt_c.xcd_map = kq_c.xcd_map = Bc >= 16384 ? 1 : 0;
+    const int64_t gq = Bc < 8192 ? Bc : 8192, gt = Bc < 8192 ? Bc : 8192;
+    IO io{Bc, b0, B, q, qdot, xt, xdt, xi, xdi, out, status, iters, pose, jac, man, dist, xdd, pair,
+          rec ? rec + b0 * stride : nullptr, stride};
+    hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr;
+    if (timed) {
+      if (int r = mkev(&e0)) return r;
+      if (int r = mkev(&e1)) return r;
+      if (int r = mkev(&e2)) return r;
+      HIP_TRY(hipEventRecord(e0, cs));
+    }
+    hipLaunchKernelGGL(task_kernel, dim3(static_cast<unsigned>(gt)), dim3(64),
+                       static_cast<size_t>(kt_c.lds_doubles) * sizeof(double), cs, m->d_model, kt_c, io);
     HIP_TRY(hipGetLastError());
+    if (timed) HIP_TRY(hipEventRecord(e1, cs));
+    if (!stages) {
+      const size_t lds = static_cast<size_t>(kq_c.lds_doubles) * sizeof(double);
+      const dim3 g(static_cast<unsigned>(gq)), blk(64);
+      // compile-time QP shapes of the bundled robots; anything else runs the
+      // runtime-sized instantiation
+      if (kq_c.nx == 23 && kq_c.ng == 16 && kq_c.np == 7)
+        hipLaunchKernelGGL((qp_kernel<Dims<23, 16, 7>>), g, blk, lds, cs, m->d_model, kq_c, io);  // FR3
+      else if (kq_c.nx == 20 && kq_c.ng == 14 && kq_c.np == 6)
+        hipLaunchKernelGGL((qp_kernel<Dims<20, 14, 6>>), g, blk, lds, cs, m->d_model, kq_c, io);  // UR5e
+      else if (kq_c.nx == 9 && kq_c.ng == 16 && kq_c.np == 9)
+        hipLaunchKernelGGL((qp_kernel<Dims<9, 16, 9>>), g, blk, lds, cs, m->d_model, kq_c, io);  // Husky-FR3
+      else if (kq_c.nx == 11 && kq_c.ng == 16 && kq_c.np == 11)
+        hipLaunchKernelGGL((qp_kernel<Dims<11, 16, 11>>), g, blk, lds, cs, m->d_model, kq_c, io);  // XLS-FR3
+      else
+        hipLaunchKernelGGL((qp_kernel<Dims<0, 0, 0>>), g, blk, lds, cs, m->d_model, kq_c, io);
+      HIP_TRY(hipGetLastError());
+    }
+    if (timed) HIP_TRY(hipEventRecord(e2, cs));
+    if (S > 1) HIP_TRY(hipEventRecord(m->joins[c], cs));
   }
-  if (ev[2]) HIP_TRY(hipEventRecord(ev[2], st));
+  if (S > 1)
+    for (int c = 0; c < S; ++c) HIP_TRY(hipStreamWaitEvent(st, m->joins[c], 0));
+  if (timed) {
+    HIP_TRY(hipEventRecord(e_end, st));
+    std::lock_guard<std::mutex> g(m->mu);
+    m->events.push_back(tev);
+  }
   return DRC_OK;
 }
 
@@ -2357,25 +2419,38 @@ int drc_debug_kernel_timing(drc_model* m, int enable) {
   return DRC_OK;
 }
 
-int drc_debug_kernel_times(drc_model* m, double* task_ms, double* qp_ms, int* calls) {
-  if (!m || !task_ms || !qp_ms || !calls) return drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "null argument");
+int drc_debug_kernel_times(drc_model* m, double* wall_ms, double* task_ms, double* qp_ms, int* calls) {
+  if (!m || !wall_ms || !task_ms || !qp_ms || !calls) return drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "null argument");
   std::lock_guard<std::mutex> g(m->mu);
-  double t0 = 0, t1 = 0;
-  const int n = static_cast<int>(m->events.size() / 3);
-  for (int i = 0; i < n; ++i) {
-    hipEvent_t* e = &m->events[3 * i];
-    if (hipEventSynchronize(e[2]) != hipSuccess) return drc_amd::set_err(DRC_ERR_HIP, "hipEventSynchronize");
-    float a = 0, b = 0;
-    if (hipEventElapsedTime(&a, e[0], e[1]) != hipSuccess || hipEventElapsedTime(&b, e[1], e[2]) != hipSuccess)
-      return drc_amd::set_err(DRC_ERR_HIP, "hipEventElapsedTime");
-    t0 += a;
-    t1 += b;
+  double tw = 0, t0 = 0, t1 = 0;
+  for (auto& ev : m->events) {  // {start, end, [task start, task end, qp end] per chunk}
+    float a = 0;
+    if (hipEventSynchronize(ev[1]) != hipSuccess) return drc_amd::set_err(DRC_ERR_HIP, "hipEventSynchronize");
+    if (hipEventElapsedTime(&a, ev[0], ev[1]) != hipSuccess) return drc_amd::set_err(DRC_ERR_HIP, "hipEventElapsedTime");
+    tw += a;
+    for (size_t c = 2; c + 2 < ev.size(); c += 3) {
+      float x = 0, y = 0;
+      if (hipEventElapsedTime(&x, ev[c], ev[c + 1]) != hipSuccess ||
+          hipEventElapsedTime(&y, ev[c + 1], ev[c + 2]) != hipSuccess)
+        return drc_amd::set_err(DRC_ERR_HIP, "hipEventElapsedTime");
+      t0 += x;
+      t1 += y;
+    }
   }
-  for (hipEvent_t e : m->events) (void)hipEventDestroy(e);
+  *calls = static_cast<int>(m->events.size());
+  for (auto& ev : m->events)
+    for (hipEvent_t e : ev) (void)hipEventDestroy(e);
   m->events.clear();
+  *wall_ms = tw;
   *task_ms = t0;
   *qp_ms = t1;
-  *calls = n;
+  return DRC_OK;
+}
+
+int drc_set_concurrency(drc_model* m, int chunks) {
+  if (!m || chunks < 1 || chunks > 16) return drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "chunks must be 1..16");
+  std::lock_guard<std::mutex> g(m->mu);
+  m->chunks = chunks;
   return DRC_OK;
 }
 
@@ -2464,8 +2539,14 @@ int drc_model_create_mobile_manipulator(const drc_kinematic_param* param, const 
 void drc_model_destroy(drc_model* m) {
   if (!m) return;
   (void)hipSetDevice(m->device);
+  for (hipStream_t ls : m->lanes) (void)hipStreamSynchronize(ls);
   if (m->d_model) (void)hipFree(m->d_model);
   if (m->pool) (void)hipFree(m->pool);
+  for (hipStream_t ls : m->lanes) (void)hipStreamDestroy(ls);
+  for (hipEvent_t e : m->joins) (void)hipEventDestroy(e);
+  if (m->fork) (void)hipEventDestroy(m->fork);
+  for (auto& ev : m->events)
+    for (hipEvent_t e : ev) (void)hipEventDestroy(e);
   delete m;
 }
 

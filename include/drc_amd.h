@@ -187,7 +187,16 @@ int drc_qpik_stages_batch(const drc_model* model, const drc_qpik_params* params,
  * drc_debug_kernel_times waits for them and returns the summed durations
  * (ms) and the number of timed calls since the last query. */
 int drc_debug_kernel_timing(drc_model* model, int enable);
-int drc_debug_kernel_times(drc_model* model, double* task_ms, double* qp_ms, int* calls);
+/* wall_ms: summed caller-stream time of the timed calls (fork to join);
+ * task_ms / qp_ms: summed durations of the task / QP kernels of every
+ * sub-batch (they overlap in time when a call runs several sub-batches). */
+int drc_debug_kernel_times(drc_model* model, double* wall_ms, double* task_ms, double* qp_ms, int* calls);
+
+/* Concurrency of drc_qpik_batch: the batch is split into up to `chunks`
+ * contiguous sub-batches (each >= 16384 instances) that run on internal
+ * streams forked from and joined back to the caller's stream (default 2).
+ * Results do not depend on it. */
+int drc_set_concurrency(drc_model* model, int chunks);
 
 const char* drc_error_string(int code);
 /* Thread-local detail of the last failing call (parse position, HIP error). */
