@@ -1810,21 +1810,17 @@ __device__ __forceinline__ int qp_admm(const KParams& kp, const KParams& kpl, do
       tchk += __builtin_amdgcn_s_memtime() - tc0;
 #endif
       if (act == 2) break;
-      const bool reload = act == 1;
-      if (reload) {
-        load_admm_regs<QD>(kp, S, Gc, Kr, GKr);
-        rb = rv[lb_];
-        rg = rv[lg_];
-        if (hb) {
-          xl = x[l];
-          zb = z[l];
-          yb = y[l];
-        }
-        if (hg) {
-          zg = z[NX + l];
-          yg = y[NX + l];
-        }
-      }
+      // Always re-read the register state from LDS (published above, or
+      // updated by the check): nothing large stays live across the call, so
+      // the out-of-line block costs no spill traffic.
+      load_admm_regs<QD>(kp, S, Gc, Kr, GKr);
+      rb = rv[lb_];
+      rg = rv[lg_];
+      xl = x[lb_];
+      zb = z[lb_];
+      yb = y[lb_];
+      zg = z[lg_];
+      yg = y[lg_];
     }
 #ifdef DRC_PHASE_TIMING
     PHG(26);
