@@ -36,7 +36,8 @@ EXPORTED_SYMBOLS = (
     "drc_model_create_manipulator", "drc_model_create_mobile_manipulator", "drc_model_destroy",
     "drc_model_info", "drc_model_limits", "drc_model_find_frame", "drc_model_mobile_fk_jacobian",
     "drc_default_qpik_params", "drc_qpik_batch", "drc_qpik_stages_batch", "drc_debug_kernel_timing",
-    "drc_debug_kernel_times", "drc_set_concurrency", "drc_error_string", "drc_last_error",
+    "drc_debug_kernel_times", "drc_set_concurrency", "drc_qpik_host", "drc_qpik_stages_host",
+    "drc_error_string", "drc_last_error",
 )
 
 
@@ -123,6 +124,9 @@ def _load():
     lib.drc_debug_kernel_timing.argtypes = [vp, C.c_int]
     lib.drc_debug_kernel_times.argtypes = [vp, dp, dp, dp, ip]
     lib.drc_set_concurrency.argtypes = [vp, C.c_int]
+    lib.drc_qpik_host.argtypes = [vp, C.POINTER(QPIKParams), C.c_int64, dp, dp, dp, dp, dp, dp, dp, ip, ip]
+    lib.drc_qpik_stages_host.argtypes = [vp, C.POINTER(QPIKParams), C.c_int64, dp, dp, dp, dp, dp, dp,
+                                         dp, dp, dp, dp, ip, dp]
     for name in EXPORTED_SYMBOLS:
         if name not in ("drc_model_destroy", "drc_error_string", "drc_last_error"):
             getattr(lib, name).restype = C.c_int

@@ -11,7 +11,7 @@ namespace drc_amd {
 
 constexpr int kMaxJoints = 16;    // 1-DoF joints (XLS-FR3 needs 14)
 constexpr int kMaxGeoms = 64;
-constexpr int kMaxPairs = 512;
+constexpr int kMaxPairs = 1024;
 constexpr int kMaxFrames = 64;
 constexpr int kMaxWheels = 8;
 

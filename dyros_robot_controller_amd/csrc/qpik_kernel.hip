@@ -2010,6 +2010,11 @@ struct drc_model_impl {
   std::vector<hipStream_t> lanes;
   std::vector<hipEvent_t> joins;
   hipEvent_t fork = nullptr;
+  // host-buffer entry points: device staging + an internal stream
+  std::mutex host_mu;
+  void* stage = nullptr;
+  int64_t stage_bytes = 0;
+  hipStream_t hstream = nullptr;
   std::mutex mu;
 };
 
@@ -2539,6 +2544,8 @@ void drc_model_destroy(drc_model* m) {
   if (m->d_model) (void)hipFree(m->d_model);
   if (m->pool) (void)hipFree(m->pool);
   for (hipStream_t ls : m->lanes) (void)hipStreamDestroy(ls);
+  if (m->hstream) (void)hipStreamSynchronize(m->hstream), (void)hipStreamDestroy(m->hstream);
+  if (m->stage) (void)hipFree(m->stage);
   for (hipEvent_t e : m->joins) (void)hipEventDestroy(e);
   if (m->fork) (void)hipEventDestroy(m->fork);
   for (auto& ev : m->events)
@@ -2642,6 +2649,99 @@ int drc_qpik_stages_batch(const drc_model* m, const drc_qpik_params* p, int64_t 
                           double* xdd, void* stream) {
   return drc_amd::launch(m, p, 1, B, q, qdot, xt, xdt, xi, xdi, nullptr, nullptr, nullptr, pose, jac, man, dist,
                          pair, xdd, stream);
+}
+
+
+// ---- host-buffer entry points (synchronous; staged through device memory) --
+namespace {
+struct HostIO {
+  const double* src[6];  // q, qdot, xt, xdt, xi, xdi
+  int64_t rows[6];
+};
+}  // namespace
+
+static int host_call(drc_model* m, const drc_qpik_params* p, int stages, int64_t B, const HostIO& in,
+                     double** outs, const int64_t* out_rows, int nouts, int32_t** iouts, int niouts) {
+  if (!m || !p) return drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "null model/params");
+  if (B <= 0) return B == 0 ? DRC_OK : drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "negative batch");
+  std::lock_guard<std::mutex> g(m->host_mu);
+  if (hipSetDevice(m->device) != hipSuccess) return drc_amd::set_err(DRC_ERR_HIP, "hipSetDevice");
+  int64_t words = 0;
+  for (int i = 0; i < 6; ++i) words += in.src[i] ? in.rows[i] * B : 0;
+  for (int i = 0; i < nouts; ++i) words += outs[i] ? out_rows[i] * B : 0;
+  words += niouts * ((B + 1) / 2);
+  const int64_t bytes = words * 8;
+  if (m->stage_bytes < bytes) {
+    if (m->stage) (void)hipFree(m->stage);
+    m->stage = nullptr;
+    m->stage_bytes = 0;
+    if (hipMalloc(&m->stage, bytes) != hipSuccess) return drc_amd::set_err(DRC_ERR_HIP, "hipMalloc (staging)");
+    m->stage_bytes = bytes;
+  }
+  if (!m->hstream && hipStreamCreateWithFlags(&m->hstream, hipStreamNonBlocking) != hipSuccess)
+    return drc_amd::set_err(DRC_ERR_HIP, "hipStreamCreate");
+  double* d = reinterpret_cast<double*>(m->stage);
+  const double* din[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  for (int i = 0; i < 6; ++i)
+    if (in.src[i]) {
+      if (hipMemcpyAsync(d, in.src[i], in.rows[i] * B * 8, hipMemcpyHostToDevice, m->hstream) != hipSuccess)
+        return drc_amd::set_err(DRC_ERR_HIP, "hipMemcpyAsync H2D");
+      din[i] = d;
+      d += in.rows[i] * B;
+    }
+  double* dout[8] = {nullptr};
+  for (int i = 0; i < nouts; ++i)
+    if (outs[i]) {
+      dout[i] = d;
+      d += out_rows[i] * B;
+    }
+  int32_t* diout[2] = {nullptr, nullptr};
+  for (int i = 0; i < niouts; ++i)
+    if (iouts[i]) {
+      diout[i] = reinterpret_cast<int32_t*>(d);
+      d += (B + 1) / 2;
+    }
+  int rc;
+  if (!stages)
+    rc = drc_amd::launch(m, p, 0, B, din[0], din[1], din[2], din[3], din[4], din[5], dout[0], diout[0], diout[1],
+                         nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, m->hstream);
+  else
+    rc = drc_amd::launch(m, p, 1, B, din[0], din[1], din[2], din[3], din[4], din[5], nullptr, nullptr, nullptr,
+                         dout[0], dout[1], dout[2], dout[3], diout[0], dout[4], m->hstream);
+  if (rc) return rc;
+  for (int i = 0; i < nouts; ++i)
+    if (outs[i] && hipMemcpyAsync(outs[i], dout[i], out_rows[i] * B * 8, hipMemcpyDeviceToHost, m->hstream) != hipSuccess)
+      return drc_amd::set_err(DRC_ERR_HIP, "hipMemcpyAsync D2H");
+  for (int i = 0; i < niouts; ++i)
+    if (iouts[i] && hipMemcpyAsync(iouts[i], diout[i], B * 4, hipMemcpyDeviceToHost, m->hstream) != hipSuccess)
+      return drc_amd::set_err(DRC_ERR_HIP, "hipMemcpyAsync D2H");
+  if (hipStreamSynchronize(m->hstream) != hipSuccess) return drc_amd::set_err(DRC_ERR_HIP, "hipStreamSynchronize");
+  return DRC_OK;
+}
+
+int drc_qpik_host(drc_model* m, const drc_qpik_params* p, int64_t B, const double* q, const double* qdot,
+                  const double* xt, const double* xdt, const double* xi, const double* xdi, double* out,
+                  int32_t* status, int32_t* iters) {
+  if (!m) return drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "null model");
+  if (!out || !status) return drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "qdot_out and status are required");
+  const int64_t n = m->hm.dev.nv, a = m->hm.dev.kind == 1 ? m->hm.dev.n_arm + m->hm.dev.n_wheel : n;
+  HostIO in{{q, qdot, xt, xdt, xi, xdi}, {n, n, 12, 6, 12, 6}};
+  double* outs[1] = {out};
+  const int64_t rows[1] = {a};
+  int32_t* iouts[2] = {status, iters};
+  return host_call(m, p, 0, B, in, outs, rows, 1, iouts, 2);
+}
+
+int drc_qpik_stages_host(drc_model* m, const drc_qpik_params* p, int64_t B, const double* q, const double* qdot,
+                         const double* xt, const double* xdt, const double* xi, const double* xdi, double* pose,
+                         double* jac, double* man, double* dist, int32_t* pair, double* xdd) {
+  if (!m) return drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "null model");
+  const int64_t n = m->hm.dev.nv, na = m->hm.dev.kind == 1 ? m->hm.dev.n_arm : n;
+  HostIO in{{q, qdot, xt, xdt, xi, xdi}, {n, n, 12, 6, 12, 6}};
+  double* outs[5] = {pose, jac, man, dist, xdd};
+  const int64_t rows[5] = {12, 6 * n, 1 + na, 1 + n, 6};
+  int32_t* iouts[1] = {pair};
+  return host_call(m, p, 1, B, in, outs, rows, 5, iouts, 1);
 }
 
 }  // extern "C"

@@ -182,6 +182,22 @@ int drc_qpik_stages_batch(const drc_model* model, const drc_qpik_params* params,
                           const double* xdot_init, double* pose, double* jac, double* man,
                           double* dist, int32_t* pair, double* xdot_des, void* stream);
 
+/* Host-buffer forms of drc_qpik_batch / drc_qpik_stages_batch: same
+ * arguments, but every array is a HOST array ([field][B], row stride B).  The
+ * call stages them through model-owned device memory on an internal stream
+ * and returns when the outputs are back on the host (PCIe-inclusive).  Calls
+ * on one model are serialised.  Used by the C++ facade (include/drc_amd.hpp)
+ * for the reference's single-robot signatures (B = 1). */
+int drc_qpik_host(drc_model* model, const drc_qpik_params* params, int64_t B,
+                  const double* q, const double* qdot, const double* x_target,
+                  const double* xdot_target, const double* x_init, const double* xdot_init,
+                  double* qdot_out, int32_t* status, int32_t* iters);
+int drc_qpik_stages_host(drc_model* model, const drc_qpik_params* params, int64_t B,
+                         const double* q, const double* qdot, const double* x_target,
+                         const double* xdot_target, const double* x_init,
+                         const double* xdot_init, double* pose, double* jac, double* man,
+                         double* dist, int32_t* pair, double* xdot_des);
+
 /* Diagnostics (no reference counterpart): when enabled, drc_qpik_batch
  * records HIP events on its stream around the task and QP kernels;
  * drc_debug_kernel_times waits for them and returns the summed durations
