@@ -1707,6 +1707,109 @@ __device__ __forceinline__ int qp_scale(const KParams& kp, double* S) {
   return status;
 }
 
+// Register form of qp_scale for compile-time shapes: lane l holds row l of P
+// (= column l: P is symmetric bit for bit), column l and row l of G; the
+// Ruiz factors move by v_readlane.  Same operations in the same order as
+// qp_scale (bit-identical results); P, G, q, D, E written back at the end.
+template <class QD>
+__device__ __noinline__ int qp_scale_regs(const KParams& kp, double* S) {
+  constexpr int NX = QD::nx, NG = QD::ng, NP = QD::np, M = NX + NG;
+  const int l = lane_id();
+  double *P = S + kp.oP, *G = S + kp.oG, *qq = S + kp.oQ, *ab = S + kp.oAB, *lo = S + kp.oL, *up = S + kp.oU;
+  double *D = S + kp.oD, *E = S + kp.oE, *sc = S + kp.oSc;
+  {
+    bool finite = true;
+    for (int e = l; e < NP * NP; e += 64) finite &= isfinite(P[e]);
+    for (int e = l; e < NG * NX; e += 64) finite &= isfinite(G[e]);
+    if (l < NX) finite &= isfinite(qq[l]);
+    for (int row = l; row < M; row += 64) finite &= !isnan(lo[row]) && !isnan(up[row]);
+    if (!__all(finite)) return DRC_STATUS_NONFINITE;
+  }
+  const bool hx = l < NX, hg = l < NG, hp = l < NP;
+  const int lx = hx ? l : 0, lg = hg ? l : 0, lp = hp ? l : 0;
+  double Prow[NP], Gcol[NG], Grow[NX];
+#pragma unroll
+  for (int c = 0; c < NP; ++c) Prow[c] = P[lp * NP + c];
+#pragma unroll
+  for (int i = 0; i < NG; ++i) Gcol[i] = G[i * NX + lx];
+#pragma unroll
+  for (int j = 0; j < NX; ++j) Grow[j] = G[lg * NX + j];
+  double abl = ab[lx], ql = qq[lx], Dl = 1.0, El = 1.0, EGl = 1.0, cs = 1.0;
+  auto clampf = [](double v) { return v < kMinScaling ? 1.0 : (v > kMaxScaling ? kMaxScaling : v); };
+  for (int it = 0; it < kp.s.scaling; ++it) {
+    double s = fabs(abl);
+    if (hp)
+#pragma unroll
+      for (int i = 0; i < NP; ++i) s = fmax(s, fabs(Prow[i]));
+#pragma unroll
+    for (int i = 0; i < NG; ++i) s = fmax(s, fabs(Gcol[i]));
+    const double Dt = 1.0 / sqrt(clampf(s));
+    const double Et = 1.0 / sqrt(clampf(fabs(abl)));
+    double sg = 0;
+#pragma unroll
+    for (int j = 0; j < NX; ++j) sg = fmax(sg, fabs(Grow[j]));
+    const double EtG = 1.0 / sqrt(clampf(sg));
+    double DtA[NX], EtGA[NG];
+#pragma unroll
+    for (int c = 0; c < NX; ++c) DtA[c] = bcast(Dt, c);
+#pragma unroll
+    for (int i = 0; i < NG; ++i) EtGA[i] = bcast(EtG, i);
+    if (hp)
+#pragma unroll
+      for (int c = 0; c < NP; ++c) Prow[c] *= Dt * DtA[c];
+    if (hx)
+#pragma unroll
+      for (int i = 0; i < NG; ++i) Gcol[i] *= EtGA[i] * Dt;
+    if (hg)
+#pragma unroll
+      for (int j = 0; j < NX; ++j) Grow[j] *= EtG * DtA[j];
+    if (hx) {
+      abl *= Et * Dt;
+      ql *= Dt;
+      Dl *= Dt;
+      El *= Et;
+    }
+    if (hg) EGl *= EtG;
+    // cost scaling: mean column norm of P vs |q|_inf
+    double cn = 0, qn = 0;
+    if (hp)
+#pragma unroll
+      for (int i = 0; i < NP; ++i) cn = fmax(cn, fabs(Prow[i]));
+    if (hx) qn = fabs(ql);
+    cn = wave_sum(cn) / NX;
+    qn = wave_max(qn);
+    qn = clampf(qn);
+    double ct = clampf(fmax(cn, qn));
+    ct = 1.0 / ct;
+    if (hp)
+#pragma unroll
+      for (int c = 0; c < NP; ++c) Prow[c] *= ct;
+    if (hx) ql *= ct;
+    cs *= ct;
+  }
+  if (hp)
+#pragma unroll
+    for (int c = 0; c < NP; ++c) P[l * NP + c] = Prow[c];
+  if (hg)
+#pragma unroll
+    for (int j = 0; j < NX; ++j) G[l * NX + j] = Grow[j];
+  if (hx) {
+    ab[l] = abl;
+    qq[l] = ql;
+    D[l] = Dl;
+    E[l] = El;
+  }
+  if (hg) E[NX + l] = EGl;
+  if (l == 0) sc[SC_C] = cs;
+  wsync();
+  for (int row = l; row < M; row += 64) {
+    lo[row] = fmax(lo[row], -kInf) * E[row];
+    up[row] = fmin(up[row], kInf) * E[row];
+  }
+  wsync();
+  return DRC_STATUS_MAX_ITER;
+}
+
 // rho, K^-1 and the ADMM iterations (+ polish); returns the status
 template <class QD>
 __device__ __forceinline__ int qp_admm(const KParams& kp, const KParams& kpl, double* S, int* iters_out) {
@@ -1966,7 +2069,9 @@ qp_kernel(const DevModel* __restrict__ M0, const KParams kp, const IO io) {
     asm volatile("" : "+s"(M));
     qp_assemble<QD>(M, kp, S, io, b);
     PH(0);
-    int status = qp_scale<QD>(kp, S), iters = 0;
+    int status, iters = 0;
+    if constexpr (QD::nx > 0) status = qp_scale_regs<QD>(kpl, S);
+    else status = qp_scale<QD>(kp, S);
     PH(1);
     if (status != DRC_STATUS_NONFINITE) status = qp_admm<QD>(kp, kpl, S, &iters);
     PH(3);

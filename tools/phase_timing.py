@@ -11,6 +11,7 @@ B = int(sys.argv[2]) if len(sys.argv) > 2 else 65536
 rd = make_manipulator(robot, dev)
 q, qd, xt, xdt = step_inputs(rd, robot, 7, B, dev)
 ctrl = manipulator.RobotController(0.001, rd)
+_capi.lib().drc_set_concurrency(rd.model.handle, 1)  # one sub-batch: per-instance cycles without overlap
 link = "fr3_link8" if robot == "fr3" else "tool0"
 args = [torch.as_tensor(a, device=dev) for a in (q, qd, xt, xdt)]
 ctrl.QPIK_step_batch(*args, link); torch.cuda.synchronize()
