@@ -76,3 +76,47 @@ def stages_batch(model, params, q, qdot, x_target=None, xdot_target=None, x_init
         _ptr(x_init), _ptr(xdot_init), _ptr(pose), _ptr(jac), _ptr(man), _ptr(dist), _ptr(pair), _ptr(xdd),
         C.c_void_p(stream)))
     return dict(pose=pose, jac=jac, man=man, dist=dist, pair=pair, xdot_des=xdd)
+
+
+DYN_FIELDS = ("M", "Minv", "g", "nle", "c")
+
+
+def dynamics_batch(model, q, qdot=None, actuated=False, fields=DYN_FIELDS, stream=None):
+    """Launch ``drc_dynamics_batch`` on device tensors
+    [dof][B]; returns {name: tensor} with M, Minv as [n][n][B] and the vectors
+    as [n][B] (n = actuated dof when ``actuated``)."""
+    torch = _torch()
+    dev = q.device
+    B = q.shape[1]
+    check_shapes(model.dof, B, q=q, qdot=qdot)
+    n = model.actuated_dof if actuated else model.dof
+    out = {}
+    for k in fields:
+        rows = n * n if k in ("M", "Minv") else n
+        out[k] = torch.empty((rows, B), dtype=torch.float64, device=dev)
+    if stream is None:
+        stream = torch.cuda.current_stream(dev).cuda_stream
+    _capi.check(_capi.lib().drc_dynamics_batch(
+        model.handle, C.c_int(1 if actuated else 0), C.c_int64(B), _ptr(q), _ptr(qdot),
+        _ptr(out.get("M")), _ptr(out.get("Minv")), _ptr(out.get("g")), _ptr(out.get("nle")), _ptr(out.get("c")),
+        C.c_void_p(stream)))
+    for k in ("M", "Minv"):
+        if k in out:
+            out[k] = out[k].view(n, n, B)
+    return out
+
+
+def dynamics_host(model, q, qdot=None, actuated=False):
+    """``drc_dynamics_host`` on numpy arrays [dof][B] (synchronous)."""
+    q = np.ascontiguousarray(q, dtype=np.float64)
+    B = q.shape[1]
+    qd = None if qdot is None else np.ascontiguousarray(qdot, dtype=np.float64)
+    n = model.actuated_dof if actuated else model.dof
+    M, Mi = np.zeros((n, n, B)), np.zeros((n, n, B))
+    g = np.zeros((n, B))
+    nle = np.zeros((n, B)) if qd is not None else None
+    c = np.zeros((n, B)) if qd is not None else None
+    dp = lambda a: a.ctypes.data_as(C.POINTER(C.c_double)) if a is not None else None
+    _capi.check(_capi.lib().drc_dynamics_host(model.handle, C.c_int(1 if actuated else 0), C.c_int64(B), dp(q),
+                                              dp(qd), dp(M), dp(Mi), dp(g), dp(nle), dp(c)))
+    return dict(M=M, Minv=Mi, g=g, nle=nle, c=c)

@@ -269,6 +269,45 @@ struct Builder {
       geom_link.push_back(lname);
       ++m.ngeom;
     }
+    if (const XmlNode* ie = ln->child("inertial")) {
+      // URDF <inertial>: mass, com origin, inertia about the com in the origin's
+      // rotated frame; rotate into the joint frame and merge (parallel axis)
+      const XmlNode* ms = ie->child("mass");
+      const XmlNode* it = ie->child("inertia");
+      double mass = 0;
+      if (ms && ms->get("value") && !parse_vec(ms->get("value"), 1, &mass)) return fail("bad mass in link " + lname);
+      double Il[6] = {0, 0, 0, 0, 0, 0};  // xx yy zz xy xz yz
+      static const char* kI[6] = {"ixx", "iyy", "izz", "ixy", "ixz", "iyz"};
+      for (int k2 = 0; k2 < 6; ++k2)
+        if (it && it->get(kI[k2]) && !parse_vec(it->get(kI[k2]), 1, &Il[k2])) return fail("bad inertia in link " + lname);
+      const SE3 T = mul(place, origin_of(ie));
+      const double L[9] = {Il[0], Il[3], Il[4], Il[3], Il[1], Il[5], Il[4], Il[5], Il[2]};
+      double RI[9], I[9];
+      for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) RI[3 * r + c] = T.R[3 * r] * L[c] + T.R[3 * r + 1] * L[3 + c] + T.R[3 * r + 2] * L[6 + c];
+      for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) I[3 * r + c] = RI[3 * r] * T.R[3 * c] + RI[3 * r + 1] * T.R[3 * c + 1] + RI[3 * r + 2] * T.R[3 * c + 2];
+      double* b = m.inertia[jid];
+      const double m0 = b[0], m1 = m0 + mass;
+      double c0[3] = {b[1], b[2], b[3]}, c1[3];
+      for (int i = 0; i < 3; ++i) c1[i] = m1 > 0 ? (m0 * c0[i] + mass * T.p[i]) / m1 : 0.0;
+      // I_new(about c1) = I0 + m0 (|d0|^2 E - d0 d0^T) + I + mass (|d|^2 E - d d^T)
+      double Inew[9];
+      for (int i = 0; i < 9; ++i) Inew[i] = 0;
+      const double I0[9] = {b[4], b[7], b[8], b[7], b[5], b[9], b[8], b[9], b[6]};
+      auto add = [&](const double* Ib, double mb, const double* cb) {
+        const double d[3] = {cb[0] - c1[0], cb[1] - c1[1], cb[2] - c1[2]};
+        const double dd = d[0] * d[0] + d[1] * d[1] + d[2] * d[2];
+        for (int r = 0; r < 3; ++r)
+          for (int c = 0; c < 3; ++c) Inew[3 * r + c] += Ib[3 * r + c] + mb * ((r == c ? dd : 0.0) - d[r] * d[c]);
+      };
+      add(I0, m0, c0);
+      add(I, mass, T.p);
+      b[0] = m1;
+      for (int i = 0; i < 3; ++i) b[1 + i] = c1[i];
+      b[4] = Inew[0]; b[5] = Inew[4]; b[6] = Inew[8];
+      b[7] = Inew[1]; b[8] = Inew[2]; b[9] = Inew[5];
+    }
     return true;
   }
 

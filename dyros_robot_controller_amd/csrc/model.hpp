@@ -40,6 +40,11 @@ struct DevModel {
   double gbound[kMaxGeoms];        // conservative core/bounding radius for the broad phase
   int16_t pair_a[kMaxPairs], pair_b[kMaxPairs];
   double J_mobile[3][kMaxWheels];  // base twist = J_mobile * wheel velocity
+  // rigid-body inertia carried by each joint (links behind fixed joints merged,
+  // Pinocchio appendBodyToJoint), in the joint frame:
+  // {mass, com x, y, z, Ixx, Iyy, Izz, Ixy, Ixz, Iyz} with I about the com
+  double inertia[kMaxJoints + 1][10];
+  int dyn_origin;                  // joint whose origin the dynamics kernel takes as spatial reference (0 = world)
 };
 
 struct HostModel {

@@ -312,7 +312,7 @@ struct GjkDist {
   double dist;
   V3 pA, pB;
 };
-DRC_HD __noinline__ GjkDist gjk(const Shape A, const Shape B) {
+DRC_HD inline __noinline__ GjkDist gjk(const Shape A, const Shape B) {
   GjkState g;
   gjk_run(A, B, g);
   GjkDist o;

@@ -23,7 +23,9 @@
 #include <vector>
 
 #include "../../include/drc_amd.h"
+#include "dynamics.hpp"
 #include "model.hpp"
+#include "pinv_cod.hpp"
 #include "qpik_device.hpp"
 
 namespace drc_amd {
@@ -200,57 +202,8 @@ __device__ void pinv_cod6(const double* A, double* X, double* ws) {
     }
     return;
   }
-  // rank-deficient: Moore-Penrose via symmetric Jacobi on the top-r modes
-  double *M = ws, *V = ws + 36, *w = ws + 72, *idx = ws + 78;
-  for (int i = 0; i < 36; ++i) {
-    M[i] = A[i];
-    V[i] = (i % 7 == 0) ? 1.0 : 0.0;
-  }
-  for (int sweep = 0; sweep < 60; ++sweep) {
-    double off = 0;
-    for (int i = 0; i < 6; ++i)
-      for (int j = i + 1; j < 6; ++j) off += M[i * 6 + j] * M[i * 6 + j];
-    if (off < 1e-300) break;
-    for (int p = 0; p < 6; ++p)
-      for (int q = p + 1; q < 6; ++q) {
-        if (fabs(M[p * 6 + q]) < 1e-300) continue;
-        double th = (M[q * 6 + q] - M[p * 6 + p]) / (2 * M[p * 6 + q]);
-        double t = (th >= 0 ? 1 : -1) / (fabs(th) + sqrt(th * th + 1));
-        double c = 1 / sqrt(t * t + 1), s = t * c;
-        for (int k = 0; k < 6; ++k) {
-          double a = M[k * 6 + p], b = M[k * 6 + q];
-          M[k * 6 + p] = c * a - s * b;
-          M[k * 6 + q] = s * a + c * b;
-        }
-        for (int k = 0; k < 6; ++k) {
-          double a = M[p * 6 + k], b = M[q * 6 + k];
-          M[p * 6 + k] = c * a - s * b;
-          M[q * 6 + k] = s * a + c * b;
-        }
-        for (int k = 0; k < 6; ++k) {
-          double a = V[k * 6 + p], b = V[k * 6 + q];
-          V[k * 6 + p] = c * a - s * b;
-          V[k * 6 + q] = s * a + c * b;
-        }
-      }
-  }
-  for (int i = 0; i < 6; ++i) {
-    w[i] = M[i * 7];
-    idx[i] = i;
-  }
-  for (int i = 0; i < 6; ++i)
-    for (int j = i + 1; j < 6; ++j)
-      if (fabs(w[(int)idx[j]]) > fabs(w[(int)idx[i]])) {
-        double t = idx[i];
-        idx[i] = idx[j];
-        idx[j] = t;
-      }
-  for (int i = 0; i < 36; ++i) X[i] = 0;
-  for (int kk = 0; kk < r; ++kk) {
-    int e2 = (int)idx[kk];
-    for (int i = 0; i < 6; ++i)
-      for (int j = 0; j < 6; ++j) X[i * 6 + j] += V[i * 6 + e2] * V[j * 6 + e2] / w[e2];
-  }
+  // rank-deficient (or not numerically PD): Eigen's COD pseudo-inverse
+  pinv_cod_serial(A, 6, 1, X, ws);
 }
 
 __device__ double cubic(double t, double t0, double tf, double x0, double xf, double xd0, double xdf) {
@@ -2120,6 +2073,9 @@ struct drc_model_impl {
   void* stage = nullptr;
   int64_t stage_bytes = 0;
   hipStream_t hstream = nullptr;
+  // drc_dynamics_batch: queue of instances whose M_inv needs the serial COD
+  int* dyn_list = nullptr;
+  int64_t dyn_list_cap = 0;
   std::mutex mu;
 };
 
@@ -2624,6 +2580,7 @@ int drc_model_create_mobile_manipulator(const drc_kinematic_param* param, const 
   d.mobi_start = ji->mobi_start;
   d.act_mani_start = ai->mani_start;
   d.act_mobi_start = ai->mobi_start;
+  d.dyn_origin = ji->virtual_start + 3;  // the base (yaw joint) origin: keeps spatial moments small
   if (d.n_arm < 1 || d.n_arm > 8 || ji->virtual_start + 3 > d.nv || ji->mani_start + d.n_arm > d.nv ||
       ji->mobi_start + W > d.nv || ai->mani_start + d.n_arm > d.n_arm + W || ai->mobi_start + W > d.n_arm + W) {
     delete m;
@@ -2648,6 +2605,7 @@ void drc_model_destroy(drc_model* m) {
   for (hipStream_t ls : m->lanes) (void)hipStreamSynchronize(ls);
   if (m->d_model) (void)hipFree(m->d_model);
   if (m->pool) (void)hipFree(m->pool);
+  if (m->dyn_list) (void)hipFree(m->dyn_list);
   for (hipStream_t ls : m->lanes) (void)hipStreamDestroy(ls);
   if (m->hstream) (void)hipStreamSynchronize(m->hstream), (void)hipStreamDestroy(m->hstream);
   if (m->stage) (void)hipFree(m->stage);
@@ -2847,6 +2805,85 @@ int drc_qpik_stages_host(drc_model* m, const drc_qpik_params* p, int64_t B, cons
   const int64_t rows[5] = {12, 6 * n, 1 + na, 1 + n, 6};
   int32_t* iouts[1] = {pair};
   return host_call(m, p, 1, B, in, outs, rows, 5, iouts, 1);
+}
+
+
+// ---- joint-space dynamics ------------------------------
+int drc_dynamics_batch(drc_model* m, int actuated, int64_t B, const double* q, const double* qdot, double* M,
+                       double* M_inv, double* g, double* nle, double* c, void* stream) {
+  using drc_amd::set_err;
+  if (!m) return drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "null model");
+  if (B < 0) return drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "negative batch");
+  if (B == 0) return DRC_OK;
+  if (!q) return drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "q is required");
+  if ((nle || c) && !qdot) return drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "qdot is required for nle / c");
+  if (actuated && m->hm.dev.kind != 1)
+    return drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "actuated dynamics need a mobile-manipulator model");
+  if (B > 0x7ffffff0) return drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "batch too large");
+  HIP_TRY(hipSetDevice(m->device));
+  int* list = nullptr;
+  if (M_inv) {
+    std::lock_guard<std::mutex> lk(m->mu);
+    if (m->dyn_list_cap < B + 1) {
+      if (m->dyn_list) HIP_TRY(hipFree(m->dyn_list));
+      m->dyn_list = nullptr;
+      m->dyn_list_cap = 0;
+      HIP_TRY(hipMalloc(&m->dyn_list, (B + 1) * sizeof(int)));
+      m->dyn_list_cap = B + 1;
+    }
+    list = m->dyn_list;
+  }
+  const int rc = drc_amd::launch_dynamics(m->d_model, m->hm.dev, actuated != 0, B, q, qdot, M, M_inv, g, nle, c,
+                                          list, reinterpret_cast<hipStream_t>(stream));
+  if (rc == 1) return drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "batch too large");
+  if (rc) return drc_amd::set_err(DRC_ERR_HIP, std::string("dynamics launch: ") + hipGetErrorString(hipGetLastError()));
+  return DRC_OK;
+}
+
+int drc_dynamics_host(drc_model* m, int actuated, int64_t B, const double* q, const double* qdot, double* M,
+                      double* M_inv, double* g, double* nle, double* c) {
+  using drc_amd::set_err;
+  if (!m) return drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "null model");
+  if (B <= 0) return B == 0 ? DRC_OK : drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "negative batch");
+  if (!q) return drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "q is required");
+  const drc_amd::DevModel& d = m->hm.dev;
+  const int64_t n = d.nv, no = actuated ? d.n_arm + d.n_wheel : n;
+  std::lock_guard<std::mutex> lk(m->host_mu);
+  HIP_TRY(hipSetDevice(m->device));
+  double* outs[5] = {M, M_inv, g, nle, c};
+  const int64_t rows[5] = {no * no, no * no, no, no, no};
+  int64_t words = (qdot ? 2 : 1) * n * B;
+  for (int i = 0; i < 5; ++i) words += outs[i] ? rows[i] * B : 0;
+  if (m->stage_bytes < words * 8) {
+    if (m->stage) (void)hipFree(m->stage);
+    m->stage = nullptr;
+    m->stage_bytes = 0;
+    HIP_TRY(hipMalloc(&m->stage, words * 8));
+    m->stage_bytes = words * 8;
+  }
+  if (!m->hstream) HIP_TRY(hipStreamCreateWithFlags(&m->hstream, hipStreamNonBlocking));
+  double* dp = reinterpret_cast<double*>(m->stage);
+  double* dq = dp;
+  dp += n * B;
+  HIP_TRY(hipMemcpyAsync(dq, q, n * B * 8, hipMemcpyHostToDevice, m->hstream));
+  double* dqd = nullptr;
+  if (qdot) {
+    dqd = dp;
+    dp += n * B;
+    HIP_TRY(hipMemcpyAsync(dqd, qdot, n * B * 8, hipMemcpyHostToDevice, m->hstream));
+  }
+  double* dout[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+  for (int i = 0; i < 5; ++i)
+    if (outs[i]) {
+      dout[i] = dp;
+      dp += rows[i] * B;
+    }
+  int rc = drc_dynamics_batch(m, actuated, B, dq, dqd, dout[0], dout[1], dout[2], dout[3], dout[4], m->hstream);
+  if (rc) return rc;
+  for (int i = 0; i < 5; ++i)
+    if (outs[i]) HIP_TRY(hipMemcpyAsync(outs[i], dout[i], rows[i] * B * 8, hipMemcpyDeviceToHost, m->hstream));
+  HIP_TRY(hipStreamSynchronize(m->hstream));
+  return DRC_OK;
 }
 
 }  // extern "C"

@@ -92,6 +92,7 @@ class RobotData:
         _capi.check(_capi.lib().drc_model_limits(h, *(a.ctypes.data_as(C.POINTER(C.c_double)) for a in self._lims)))
         self.q_ = np.zeros(n)
         self.qdot_ = np.zeros(n)
+        self._dyn_cache = None
 
     # -- state ---------------------------------------------------------------
     def updateState(self, q, qdot):
@@ -99,6 +100,7 @@ class RobotData:
         if q.size != self.getDof() or qdot.size != self.getDof():
             raise ValueError("q and qdot must have size dof")
         self.q_, self.qdot_ = q.copy(), qdot.copy()
+        self._dyn_cache = None
         return True
 
     update_state = updateState
@@ -165,6 +167,55 @@ class RobotData:
     get_pose, get_jacobian, get_velocity = getPose, getJacobian, getVelocity
     get_manipulability, get_min_distance = getManipulability, getMinDistance
     compute_pose, compute_jacobian, compute_velocity = computePose, computeJacobian, computeVelocity
+
+    # -- joint-space dynamics (robot_data.cpp:109-124; getters robot_data.h:176-198) ----
+    def _dynamics(self, q, qdot, actuated=False):
+        dq = _batch.as_device(np.asarray(q, float).reshape(-1, 1), self.device)
+        dqd = _batch.as_device(np.asarray(qdot, float).reshape(-1, 1), self.device)
+        d = _batch.dynamics_batch(self.model, dq, dqd, actuated=actuated)
+        return {k: v.cpu().numpy()[..., 0] for k, v in d.items()}
+
+    def _cached_dynamics(self):
+        if self._dyn_cache is None:
+            self._dyn_cache = self._dynamics(self.q_, self.qdot_)
+        return self._dyn_cache
+
+    def getMassMatrix(self):
+        return self._cached_dynamics()["M"].copy()
+
+    def getMassMatrixInv(self):
+        return self._cached_dynamics()["Minv"].copy()
+
+    def getGravity(self):
+        return self._cached_dynamics()["g"].copy()
+
+    def getCoriolis(self):
+        return self._cached_dynamics()["c"].copy()
+
+    def getNonlinearEffects(self):
+        return self._cached_dynamics()["nle"].copy()
+
+    def computeMassMatrix(self, q):
+        return self._dynamics(q, np.zeros_like(np.asarray(q, float)))["M"]
+
+    def computeGravity(self, q):
+        return self._dynamics(q, np.zeros_like(np.asarray(q, float)))["g"]
+
+    def computeCoriolis(self, q, qdot):
+        return self._dynamics(q, qdot)["c"]
+
+    def computeNonlinearEffects(self, q, qdot):
+        return self._dynamics(q, qdot)["nle"]
+
+    def dynamics_batch(self, q, qdot=None, fields=_batch.DYN_FIELDS):
+        """Batched updateDynamics on device tensors [dof][B]; see _batch.dynamics_batch."""
+        return _batch.dynamics_batch(self.model, _batch.as_device(q, self.device),
+                                     _batch.as_device(qdot, self.device), fields=fields)
+
+    get_mass_matrix, get_mass_matrix_inv, get_gravity = getMassMatrix, getMassMatrixInv, getGravity
+    get_coriolis, get_nonlinear_effects = getCoriolis, getNonlinearEffects
+    compute_mass_matrix, compute_gravity = computeMassMatrix, computeGravity
+    compute_coriolis, compute_nonlinear_effects = computeCoriolis, computeNonlinearEffects
 
 
 class ManipulabilityResult:

@@ -133,6 +133,7 @@ class RobotData:
         self._Jm = Jm[:3 * self.model.mobi_dof].reshape(3, self.model.mobi_dof)
         self.q_ = np.zeros(n)
         self.qdot_ = np.zeros(n)
+        self._dyn_cache = {}
 
     # -- sizes and indices -----------------------------------------------------
     def get_dof(self):
@@ -177,6 +178,7 @@ class RobotData:
     def update_state(self, q_virtual, q_mobile, q_mani, qdot_virtual, qdot_mobile, qdot_mani):
         self.q_ = self.joint_vector(q_virtual, q_mobile, q_mani)
         self.qdot_ = self.joint_vector(qdot_virtual, qdot_mobile, qdot_mani)
+        self._dyn_cache = {}
         return True
 
     updateState = update_state
@@ -213,6 +215,88 @@ class RobotData:
         from .manipulator import MinDistResult
         d = self._stages(None)["dist"][:, 0]
         return MinDistResult(d[0], d[1:] if with_grad else None)
+
+    # -- dynamics (robot_data.cpp:126-144; getters robot_data.h:425-445) --------
+    def _dynamics(self, q, qdot, actuated):
+        dq = _batch.as_device(np.asarray(q, float).reshape(-1, 1), self.device)
+        dqd = _batch.as_device(np.asarray(qdot, float).reshape(-1, 1), self.device)
+        d = _batch.dynamics_batch(self.model, dq, dqd, actuated=actuated)
+        return {k: v.cpu().numpy()[..., 0] for k, v in d.items()}
+
+    def _cached(self, actuated):
+        if actuated not in self._dyn_cache:
+            self._dyn_cache[actuated] = self._dynamics(self.q_, self.qdot_, actuated)
+        return self._dyn_cache[actuated]
+
+    def get_mass_matrix(self):
+        return self._cached(False)["M"].copy()
+
+    def get_mass_matrix_inv(self):
+        return self._cached(False)["Minv"].copy()
+
+    def get_gravity(self):
+        return self._cached(False)["g"].copy()
+
+    def get_coriolis(self):
+        return self._cached(False)["c"].copy()
+
+    def get_nonlinear_effects(self):
+        return self._cached(False)["nle"].copy()
+
+    def get_mass_matrix_actuated(self):
+        return self._cached(True)["M"].copy()
+
+    def get_mass_matrix_actuated_inv(self):
+        return self._cached(True)["Minv"].copy()
+
+    def get_gravity_actuated(self):
+        return self._cached(True)["g"].copy()
+
+    def get_coriolis_actuated(self):
+        return self._cached(True)["c"].copy()
+
+    def get_nonlinear_effects_actuated(self):
+        return self._cached(True)["nle"].copy()
+
+    def _blocks(self, q_virtual, q_mobile, q_mani, qdot_virtual=None, qdot_mobile=None, qdot_mani=None):
+        q = self.joint_vector(q_virtual, q_mobile, q_mani)
+        qd = (np.zeros_like(q) if qdot_virtual is None
+              else self.joint_vector(qdot_virtual, qdot_mobile, qdot_mani))
+        return q, qd
+
+    def compute_mass_matrix(self, q_virtual, q_mobile, q_mani):
+        return self._dynamics(*self._blocks(q_virtual, q_mobile, q_mani), False)["M"]
+
+    def compute_gravity(self, q_virtual, q_mobile, q_mani):
+        return self._dynamics(*self._blocks(q_virtual, q_mobile, q_mani), False)["g"]
+
+    def compute_coriolis(self, q_virtual, q_mobile, q_mani, qdot_virtual, qdot_mobile, qdot_mani):
+        return self._dynamics(*self._blocks(q_virtual, q_mobile, q_mani, qdot_virtual, qdot_mobile, qdot_mani),
+                              False)["c"]
+
+    def compute_nonlinear_effects(self, q_virtual, q_mobile, q_mani, qdot_virtual, qdot_mobile, qdot_mani):
+        return self._dynamics(*self._blocks(q_virtual, q_mobile, q_mani, qdot_virtual, qdot_mobile, qdot_mani),
+                              False)["nle"]
+
+    def compute_mass_matrix_actuated(self, q_virtual, q_mobile, q_mani):
+        return self._dynamics(*self._blocks(q_virtual, q_mobile, q_mani), True)["M"]
+
+    def compute_gravity_actuated(self, q_virtual, q_mobile, q_mani):
+        return self._dynamics(*self._blocks(q_virtual, q_mobile, q_mani), True)["g"]
+
+    def compute_coriolis_actuated(self, q_virtual, q_mobile, q_mani, qdot_virtual, qdot_mobile, qdot_mani):
+        return self._dynamics(*self._blocks(q_virtual, q_mobile, q_mani, qdot_virtual, qdot_mobile, qdot_mani),
+                              True)["c"]
+
+    def compute_nonlinear_effects_actuated(self, q_virtual, q_mobile, q_mani, qdot_virtual, qdot_mobile,
+                                           qdot_mani):
+        return self._dynamics(*self._blocks(q_virtual, q_mobile, q_mani, qdot_virtual, qdot_mobile, qdot_mani),
+                              True)["nle"]
+
+    def dynamics_batch(self, q, qdot=None, actuated=False, fields=_batch.DYN_FIELDS):
+        """Batched updateDynamics on device tensors [dof][B] (full joint vectors)."""
+        return _batch.dynamics_batch(self.model, _batch.as_device(q, self.device),
+                                     _batch.as_device(qdot, self.device), actuated=actuated, fields=fields)
 
 
 class RobotController:

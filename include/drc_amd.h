@@ -218,6 +218,29 @@ const char* drc_error_string(int code);
 /* Thread-local detail of the last failing call (parse position, HIP error). */
 const char* drc_last_error(void);
 
+/* ---- joint-space dynamics --------------------
+ * drc_dynamics_batch: for B robots, the quantities RobotData::updateState caches
+ * after updateDynamics:
+ *   actuated = 0:  Manipulator::RobotData::updateDynamics (src/manipulator/robot_data.cpp:109-124)
+ *                  M = crba (symmetric), M_inv = DyrosMath::PinvCOD(M), g = computeGeneralizedGravity,
+ *                  nle = nonLinearEffects, c = nle - g;  n = dof.  Getters getMassMatrix / getMassMatrixInv /
+ *                  getGravity / getNonlinearEffects / getCoriolis (robot_data.h:176-198); computeMassMatrix /
+ *                  computeGravity / computeCoriolis / computeNonlinearEffects (robot_data.h:70-92) are the
+ *                  same call with the fields they return.
+ *   actuated = 1:  MobileManipulator::RobotData::updateDynamics (src/mobile_manipulator/robot_data.cpp:126-144)
+ *                  S^T M S, PinvCOD(S^T M S), S^T g, S^T nle, S^T (nle - g) with the selection matrix of
+ *                  robot_data.cpp:22-25,115-120;  n = actuated dof.  (getMassMatrixActuated etc.,
+ *                  mobile_manipulator/robot_data.h:425-445; compute*Actuated :151-187.)
+ * q, qdot: [dof][B] full joint vectors (JointIndex order for mobile manipulators); qdot may be NULL when
+ * nle and c are NULL (treated as zero).  Outputs, any of which may be NULL: M, M_inv [n*n][B] (entry (i,j) at
+ * field i*n + j), g, nle, c [n][B].  Gravity is Pinocchio's default (0, 0, -9.81).  Asynchronous on `stream`;
+ * a second, usually empty, launch re-solves M_inv by a serial COD where the kernel cannot certify full rank. */
+int drc_dynamics_batch(drc_model* model, int actuated, int64_t B, const double* q, const double* qdot,
+                       double* M, double* M_inv, double* g, double* nle, double* c, void* stream);
+/* Same contract with HOST buffers; synchronous (PCIe-inclusive). */
+int drc_dynamics_host(drc_model* model, int actuated, int64_t B, const double* q, const double* qdot,
+                      double* M, double* M_inv, double* g, double* nle, double* c);
+
 #ifdef __cplusplus
 }
 #endif

@@ -198,37 +198,91 @@ static int rank_cpqr(const double* A, int n, double thr) {
     return r;
 }
 
-/* symmetric Jacobi eigen-decomposition (for the rank-deficient pinv) */
-static void jacobi_eig(const double* A, int n, double* w, double* V) {
-    double M[64];
-    memcpy(M, A, n * n * sizeof(double));
-    for (int i = 0; i < n * n; ++i) V[i] = 0;
-    for (int i = 0; i < n; ++i) V[i * n + i] = 1;
-    for (int sweep = 0; sweep < 60; ++sweep) {
-        double off = 0;
-        for (int i = 0; i < n; ++i) for (int j = i + 1; j < n; ++j) off += M[i * n + j] * M[i * n + j];
-        if (off < 1e-300) break;
-        for (int p = 0; p < n; ++p)
-            for (int q = p + 1; q < n; ++q) {
-                if (fabs(M[p * n + q]) < 1e-300) continue;
-                double th = (M[q * n + q] - M[p * n + p]) / (2 * M[p * n + q]);
-                double t = (th >= 0 ? 1 : -1) / (fabs(th) + sqrt(th * th + 1));
-                double c = 1 / sqrt(t * t + 1), s = t * c;
-                for (int k = 0; k < n; ++k) {
-                    double mkp = M[k * n + p], mkq = M[k * n + q];
-                    M[k * n + p] = c * mkp - s * mkq; M[k * n + q] = s * mkp + c * mkq;
-                }
-                for (int k = 0; k < n; ++k) {
-                    double mpk = M[p * n + k], mqk = M[q * n + k];
-                    M[p * n + k] = c * mpk - s * mqk; M[q * n + k] = s * mpk + c * mqk;
-                }
-                for (int k = 0; k < n; ++k) {
-                    double vkp = V[k * n + p], vkq = V[k * n + q];
-                    V[k * n + p] = c * vkp - s * vkq; V[k * n + q] = s * vkp + c * vkq;
-                }
+/* Moore-Penrose inverse of the QR-truncated matrix Q_r [R11 R12] P^T: what
+   Eigen's CompleteOrthogonalDecomposition::pseudoInverse() returns with the
+   rank cut |R_ii| > thr * max|R_ii| (math_type_define.h:563-570).
+   X = P W^T (W W^T)^-1 Q_r^T with W = R[:r, :].  n <= 16. */
+static void pinv_qr_trunc(const double* A, int n, double thr, double* X) {
+    double R[256], G[256], Y[256], beta[16], v0[16], cn[16];
+    int perm[16];
+    memcpy(R, A, (size_t)n * n * sizeof(double));
+    for (int j = 0; j < n; ++j) perm[j] = j;
+    double maxpiv = 0;
+    for (int k = 0; k < n; ++k) {
+        int p = k;
+        for (int j = k; j < n; ++j) {
+            double s = 0;
+            for (int i = k; i < n; ++i) s += R[i * n + j] * R[i * n + j];
+            cn[j] = s;
+            if (s > cn[p]) p = j;
+        }
+        if (p != k) {
+            for (int i = 0; i < n; ++i) { double t = R[i * n + k]; R[i * n + k] = R[i * n + p]; R[i * n + p] = t; }
+            int t = perm[k]; perm[k] = perm[p]; perm[p] = t;
+            double c = cn[k]; cn[k] = cn[p]; cn[p] = c;
+        }
+        double nrm = sqrt(cn[k]);
+        beta[k] = 0; v0[k] = 0;
+        if (nrm > 0) {
+            double x0 = R[k * n + k], alpha = x0 > 0 ? -nrm : nrm, w0 = x0 - alpha, vn = w0 * w0;
+            for (int i = k + 1; i < n; ++i) vn += R[i * n + k] * R[i * n + k];
+            double bt = vn > 0 ? 2.0 / vn : 0.0;
+            for (int j = k + 1; j < n; ++j) {
+                double s = w0 * R[k * n + j];
+                for (int i = k + 1; i < n; ++i) s += R[i * n + k] * R[i * n + j];
+                s *= bt;
+                R[k * n + j] -= s * w0;
+                for (int i = k + 1; i < n; ++i) R[i * n + j] -= s * R[i * n + k];
             }
+            R[k * n + k] = alpha;
+            beta[k] = bt; v0[k] = w0;
+        }
+        if (fabs(R[k * n + k]) > maxpiv) maxpiv = fabs(R[k * n + k]);
     }
-    for (int i = 0; i < n; ++i) w[i] = M[i * n + i];
+    int r = 0;
+    for (int k = 0; k < n; ++k) if (fabs(R[k * n + k]) > thr * maxpiv) ++r;
+    memset(X, 0, (size_t)n * n * sizeof(double));
+    if (r == 0) return;
+    for (int i = 0; i < r; ++i)
+        for (int j = 0; j <= i; ++j) {
+            double s = 0;
+            for (int k = i; k < n; ++k) s += R[i * n + k] * R[j * n + k];
+            G[i * r + j] = s;
+        }
+    for (int j = 0; j < r; ++j) {
+        double s = G[j * r + j];
+        for (int k = 0; k < j; ++k) s -= G[j * r + k] * G[j * r + k];
+        double d = sqrt(s > 1e-300 ? s : 1e-300);
+        G[j * r + j] = d;
+        for (int i = j + 1; i < r; ++i) {
+            double t = G[i * r + j];
+            for (int k = 0; k < j; ++k) t -= G[i * r + k] * G[j * r + k];
+            G[i * r + j] = t / d;
+        }
+    }
+    for (int c = 0; c < n; ++c) {
+        double* y = Y + c * r;
+        for (int i = 0; i < r; ++i) y[i] = c >= i ? R[i * n + c] : 0.0;
+        for (int i = 0; i < r; ++i) { double t = y[i]; for (int k = 0; k < i; ++k) t -= G[i * r + k] * y[k]; y[i] = t / G[i * r + i]; }
+        for (int i = r - 1; i >= 0; --i) { double t = y[i]; for (int k = i + 1; k < r; ++k) t -= G[k * r + i] * y[k]; y[i] = t / G[i * r + i]; }
+    }
+    for (int col = 0; col < n; ++col) {
+        double u[16];
+        for (int i = 0; i < n; ++i) u[i] = i == col ? 1.0 : 0.0;
+        for (int k = 0; k < n; ++k) {
+            if (beta[k] == 0) continue;
+            double s = v0[k] * u[k];
+            for (int i = k + 1; i < n; ++i) s += R[i * n + k] * u[i];
+            s *= beta[k];
+            u[k] -= s * v0[k];
+            for (int i = k + 1; i < n; ++i) u[i] -= s * R[i * n + k];
+        }
+        for (int c = 0; c < n; ++c) {
+            double s = 0;
+            for (int i = 0; i < r; ++i) s += Y[c * r + i] * u[i];
+            X[perm[c] * n + col] = s;
+        }
+    }
 }
 
 /* Cholesky LL^T in place (lower), returns 0 on failure */
@@ -268,16 +322,7 @@ static void pinv_cod_sym(const double* A, int n, double* X) {
             return;
         }
     }
-    double w[8], V[64];
-    int idx[8];
-    jacobi_eig(A, n, w, V);
-    for (int i = 0; i < n; ++i) idx[i] = i;
-    for (int i = 0; i < n; ++i) for (int j = i + 1; j < n; ++j) if (fabs(w[idx[j]]) > fabs(w[idx[i]])) { int t = idx[i]; idx[i] = idx[j]; idx[j] = t; }
-    memset(X, 0, n * n * sizeof(double));
-    for (int kk = 0; kk < r; ++kk) {
-        int e = idx[kk];
-        for (int i = 0; i < n; ++i) for (int j = 0; j < n; ++j) X[i * n + j] += V[i * n + e] * V[j * n + e] / w[e];
-    }
+    pinv_qr_trunc(A, n, 1e-6, X);
 }
 
 /* ------------------------------------------------------------------------ */

@@ -110,20 +110,25 @@ def frame_jacobian_dq(m, oMi, link):
 
 
 def pinv_cod(A, thr=1e-6):
-    """DyrosMath::PinvCOD (math_type_define.h:563-570): Moore-Penrose inverse
-    with the rank decided by column-pivoted QR, |R_ii| > thr*|R_00|."""
+    """DyrosMath::PinvCOD (math_type_define.h:563-570): Eigen's
+    CompleteOrthogonalDecomposition with setThreshold(1e-6).  The rank is the
+    number of column-pivoted QR pivots with |R_ii| > thr*|R_00|; the result is
+    the Moore-Penrose inverse of the QR-truncated matrix Q_r [R11 R12] P^T
+    (what cod.pseudoInverse() returns; unique, so independent of the Z chosen)."""
     A = np.asarray(A, float)
     import scipy.linalg as sla
-    Q, R, P = sla.qr(A, pivoting=True)
+    if A.size == 0:
+        return np.zeros(A.T.shape)
+    Q, R, P = sla.qr(A, pivoting=True, mode="economic")
     d = np.abs(np.diag(R))
-    if d.size == 0 or d[0] == 0:
+    if d[0] == 0:
         return np.zeros(A.T.shape)
     r = int(np.sum(d > thr * d[0]))
-    # minimum-norm pseudo-inverse restricted to the numerical rank
-    U, s, Vt = np.linalg.svd(A, full_matrices=False)
-    s_inv = np.zeros_like(s)
-    s_inv[:r] = 1.0 / s[:r]
-    return (Vt.T * s_inv) @ U.T
+    W = R[:r, :]                                  # [R11 R12], full row rank
+    Wp = W.T @ np.linalg.inv(W @ W.T)             # pinv of W
+    X = np.zeros((A.shape[1], A.shape[0]))
+    X[P, :] = Wp @ Q[:, :r].T
+    return X
 
 
 def manipulability(m, q, link, arm_cols=None):
@@ -426,6 +431,126 @@ def task_space_cubic(x_target, xdot_target, x_init, xdot_init, t, t0, T):
         rd = np.zeros(3)
     xdd[3:] = rd
     return xd, xdd
+
+
+# ----------------------------------------------------------------------------
+# Dynamics  (robot_data.cpp:109-124: crba, computeGeneralizedGravity,
+#            nonLinearEffects, PinvCOD; MoMa robot_data.cpp:126-144)
+# Two formulations that share nothing but the model, so each pins the other:
+#   * mass_matrix: kinetic-energy definition, sum over bodies of the COM
+#     Jacobian quadratic forms (what CRBA computes).
+#   * rnea: Luh-Walker-Paul Newton-Euler in the world frame about each body's
+#     COM (what nonLinearEffects / computeGeneralizedGravity compute with
+#     qdd = 0 / qd = qdd = 0).
+# ----------------------------------------------------------------------------
+GRAVITY = np.array([0.0, 0.0, -9.81])   # pinocchio::Model::gravity981 default
+
+
+def body_inertias(m):
+    """Per joint: merged (mass, com, I about com) in the joint frame —
+    Pinocchio's appendBodyToJoint for links behind fixed joints."""
+    out = [(0.0, np.zeros(3), np.zeros((3, 3)))]
+    for j in range(1, m.nv + 1):
+        parts = m.inertia[j]
+        mass = sum(p[0] for p in parts)
+        if mass <= 0:
+            out.append((0.0, np.zeros(3), sum((p[2] for p in parts), np.zeros((3, 3)))))
+            continue
+        com = sum(p[0] * p[1] for p in parts) / mass
+        I = np.zeros((3, 3))
+        for mk, ck, Ik in parts:
+            d = ck - com
+            I += Ik + mk * (d @ d * np.eye(3) - np.outer(d, d))
+        out.append((mass, com, I))
+    return out
+
+
+def mass_matrix(m, q):
+    """M(q) = sum_k m_k Jv_k^T Jv_k + Jw_k^T I_k Jw_k (full symmetric M of
+    crba + selfadjointView<Upper>, robot_data.cpp:111,116)."""
+    oMi = fk(m, q)
+    M = np.zeros((m.nv, m.nv))
+    for j, (mass, com, I) in enumerate(body_inertias(m)):
+        if j == 0:
+            continue
+        R, p = oMi[j][:3, :3], oMi[j][:3, 3]
+        J = point_jacobian(m, oMi, j, R @ com + p)
+        Jv, Jw = J[:3], J[3:]
+        M += mass * Jv.T @ Jv + Jw.T @ (R @ I @ R.T) @ Jw
+    return M
+
+
+def rnea(m, q, qd, qdd, gravity=GRAVITY):
+    """Inverse dynamics tau = M qdd + C(q,qd) qd + g(q)."""
+    n = m.nv
+    oMi = fk(m, q)
+    bi = body_inertias(m)
+    w = [np.zeros(3)] * (n + 1)
+    wd = [np.zeros(3)] * (n + 1)
+    a = [-np.asarray(gravity, float)] + [None] * n      # origin acceleration of each joint frame
+    F, N, c = [None] * (n + 1), [None] * (n + 1), [None] * (n + 1)
+    for j in range(1, n + 1):
+        pj = m.jparent[j]
+        z = oMi[j][:3, :3] @ m.jaxis[j]
+        r = oMi[j][:3, 3] - oMi[pj][:3, 3]
+        aj = a[pj] + np.cross(wd[pj], r) + np.cross(w[pj], np.cross(w[pj], r))
+        if m.jtype[j] == REVOLUTE:
+            w[j] = w[pj] + z * qd[j - 1]
+            wd[j] = wd[pj] + z * qdd[j - 1] + np.cross(w[pj], z) * qd[j - 1]
+        else:
+            w[j], wd[j] = w[pj], wd[pj]
+            aj = aj + z * qdd[j - 1] + 2.0 * np.cross(w[pj], z) * qd[j - 1]
+        a[j] = aj
+        mass, com, I = bi[j]
+        R = oMi[j][:3, :3]
+        c[j] = R @ com + oMi[j][:3, 3]
+        rc = c[j] - oMi[j][:3, 3]
+        ac = aj + np.cross(wd[j], rc) + np.cross(w[j], np.cross(w[j], rc))
+        Iw = R @ I @ R.T
+        F[j] = mass * ac
+        N[j] = Iw @ wd[j] + np.cross(w[j], Iw @ w[j])
+    f = [np.zeros(3) for _ in range(n + 1)]
+    nm = [np.zeros(3) for _ in range(n + 1)]     # moment about the joint-frame origin
+    tau = np.zeros(n)
+    for j in range(n, 0, -1):
+        pj_ = oMi[j][:3, 3]
+        f[j] = f[j] + F[j]
+        nm[j] = nm[j] + N[j] + np.cross(c[j] - pj_, F[j])
+        z = oMi[j][:3, :3] @ m.jaxis[j]
+        tau[j - 1] = z @ nm[j] if m.jtype[j] == REVOLUTE else z @ f[j]
+        pp = m.jparent[j]
+        if pp > 0:
+            f[pp] = f[pp] + f[j]
+            nm[pp] = nm[pp] + nm[j] + np.cross(pj_ - oMi[pp][:3, 3], f[j])
+    return tau
+
+
+def dynamics(m, q, qd):
+    """RobotData::updateDynamics (robot_data.cpp:109-124): M, M+, g, nle, c."""
+    M = mass_matrix(m, q)
+    g = rnea(m, q, np.zeros(m.nv), np.zeros(m.nv))
+    nle = rnea(m, q, qd, np.zeros(m.nv))
+    return dict(M=M, Minv=pinv_cod(M), g=g, nle=nle, c=nle - g)
+
+
+def selection_matrix(nv, n_arm, n_wheel, joint_index, actuator_index, J_mobile, yaw):
+    """MobileManipulator S (D x A): identity on the arm and wheel blocks
+    (robot_data.cpp:22-25), Rz(yaw) J_mobile on the virtual block (:115-120)."""
+    vs, ms, ws = joint_index
+    am, aw = actuator_index
+    S = np.zeros((nv, n_arm + n_wheel))
+    S[ms:ms + n_arm, am:am + n_arm] = np.eye(n_arm)
+    S[ws:ws + n_wheel, aw:aw + n_wheel] = np.eye(n_wheel)
+    c, s = np.cos(yaw), np.sin(yaw)
+    S[vs:vs + 3, aw:aw + n_wheel] = np.array([[c, -s, 0], [s, c, 0], [0, 0, 1]]) @ J_mobile
+    return S
+
+
+def dynamics_actuated(m, q, qd, S):
+    """MobileManipulator::RobotData::updateDynamics (robot_data.cpp:136-142)."""
+    d = dynamics(m, q, qd)
+    Ma = S.T @ d["M"] @ S
+    return dict(M=Ma, Minv=pinv_cod(Ma), g=S.T @ d["g"], nle=S.T @ d["nle"], c=S.T @ d["c"])
 
 
 # ----------------------------------------------------------------------------

@@ -3,7 +3,7 @@
 set -e
 cd "$(dirname "$0")/.."
 HIPCC=${HIPCC:-/opt/rocm/bin/hipcc}
-SRC="dyros_robot_controller_amd/csrc/qpik_kernel.hip dyros_robot_controller_amd/csrc/model.cpp"
+SRC="dyros_robot_controller_amd/csrc/qpik_kernel.hip dyros_robot_controller_amd/csrc/dynamics.hip dyros_robot_controller_amd/csrc/model.cpp"
 for w in ${WAVES:-1 2 3 4}; do
   $HIPCC --offload-arch=gfx950 -O3 -fPIC -shared -std=c++17 -DDRC_TASK_WAVES=$w $SRC \
     -o dyros_robot_controller_amd/libdrc_amd_w$w.so -Wl,-rpath,/opt/rocm/lib &
