@@ -120,3 +120,27 @@ def dynamics_host(model, q, qdot=None, actuated=False):
     _capi.check(_capi.lib().drc_dynamics_host(model.handle, C.c_int(1 if actuated else 0), C.c_int64(B), dp(q),
                                               dp(qd), dp(M), dp(Mi), dp(g), dp(nle), dp(c)))
     return dict(M=M, Minv=Mi, g=g, nle=nle, c=c)
+
+
+def joint_torque_step_batch(model, q, qdot=None, q_target=None, qdot_target=None, qddot_target=None, dt=0.0,
+                            kp=None, kv=None, stream=None):
+    """``drc_joint_torque_step_batch`` on device tensors: tau [nb][B] for the
+    controlled block (all joints, or the arm of a mobile manipulator)."""
+    torch = _torch()
+    dev = q.device
+    B = q.shape[1]
+    check_shapes(model.dof, B, q=q, qdot=qdot)
+    nb = model.mani_dof
+    for name, t in (("q_target", q_target), ("qdot_target", qdot_target), ("qddot_target", qddot_target)):
+        if t is not None and tuple(t.shape) != (nb, B):
+            raise ValueError("%s must be [%d][B=%d], got %s" % (name, nb, B, tuple(t.shape)))
+    tau = torch.empty((nb, B), dtype=torch.float64, device=dev)
+    gain = lambda g: None if g is None else np.ascontiguousarray(np.broadcast_to(np.asarray(g, float), (nb,)))
+    kp, kv = gain(kp), gain(kv)
+    dp = lambda a: a.ctypes.data_as(C.POINTER(C.c_double)) if a is not None else None
+    if stream is None:
+        stream = torch.cuda.current_stream(dev).cuda_stream
+    _capi.check(_capi.lib().drc_joint_torque_step_batch(
+        model.handle, C.c_int64(B), _ptr(q), _ptr(qdot), _ptr(q_target), _ptr(qdot_target), _ptr(qddot_target),
+        C.c_double(dt), dp(kp), dp(kv), _ptr(tau), C.c_void_p(stream)))
+    return tau

@@ -37,7 +37,8 @@ EXPORTED_SYMBOLS = (
     "drc_model_info", "drc_model_limits", "drc_model_find_frame", "drc_model_mobile_fk_jacobian",
     "drc_default_qpik_params", "drc_qpik_batch", "drc_qpik_stages_batch", "drc_debug_kernel_timing",
     "drc_debug_kernel_times", "drc_set_concurrency", "drc_qpik_host", "drc_qpik_stages_host",
-    "drc_dynamics_batch", "drc_dynamics_host", "drc_error_string", "drc_last_error",
+    "drc_dynamics_batch", "drc_dynamics_host", "drc_joint_torque_step_batch", "drc_joint_torque_step_host",
+    "drc_error_string", "drc_last_error",
 )
 
 
@@ -129,6 +130,8 @@ def _load():
                                          dp, dp, dp, dp, ip, dp]
     lib.drc_dynamics_batch.argtypes = [vp, C.c_int, C.c_int64, vp, vp, vp, vp, vp, vp, vp, vp]
     lib.drc_dynamics_host.argtypes = [vp, C.c_int, C.c_int64, dp, dp, dp, dp, dp, dp, dp]
+    lib.drc_joint_torque_step_batch.argtypes = [vp, C.c_int64, vp, vp, vp, vp, vp, C.c_double, dp, dp, vp, vp]
+    lib.drc_joint_torque_step_host.argtypes = [vp, C.c_int64, dp, dp, dp, dp, dp, C.c_double, dp, dp, dp]
     for name in EXPORTED_SYMBOLS:
         if name not in ("drc_model_destroy", "drc_error_string", "drc_last_error"):
             getattr(lib, name).restype = C.c_int

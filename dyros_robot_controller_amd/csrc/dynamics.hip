@@ -155,10 +155,19 @@ struct DynIO {
   const double* qd;
   double *M, *Minv, *g, *nle, *c;
   int* list;      // fallback queue (count at list[0], entries from list[1])
+  // joint torque step (kTorque): controlled block [bs, bs + bn) of the joints
+  const double *qt, *qdt, *qddt;
+  double dt;
+  int bs, bn;
+  double kp[kMaxJoints], kv[kMaxJoints];
+  double* tau;
 };
 
-template <bool ACT, bool FALLBACK>
+enum DynMode { kDyn = 0, kDynActuated = 1, kTorque = 2 };
+
+template <int MODE, bool FALLBACK>
 __global__ void __launch_bounds__(kDT) __attribute__((amdgpu_waves_per_eu(4, 8))) dyn_kernel(const DevModel* __restrict__ M0, const DynIO io) {
+  constexpr bool ACT = MODE == kDynActuated, TQ = MODE == kTorque;
   extern __shared__ double lds[];
   const int tid = threadIdx.x, g = tid >> 4, j = tid & 15, J = j + 1;
   const int n = M0->nv;
@@ -191,6 +200,27 @@ __global__ void __launch_bounds__(kDT) __attribute__((amdgpu_waves_per_eu(4, 8))
       const bool in = b0 + t < B;
       sq[idx] = in ? io.q[f * B + b0 + t] : 0.0;
       sqd[idx] = (in && io.qd) ? io.qd[f * B + b0 + t] : 0.0;
+    }
+  }
+  double* svec = lds + L.vec;
+  if (TQ) {
+    __syncthreads();  // q, qd staged by other lanes
+    // joint-space acceleration command of the controlled block -> svec row n + j
+    // (moveJointTorqueStep robot_controller.cpp:115-125; MoMa arm block
+    // mobile_manipulator/robot_controller.cpp:103-118)
+    if (j < io.bn) {
+      const int jj = io.bs + j;
+      double acc = 0;
+      if (b >= 0) {
+        if (io.qddt) {
+          acc = io.qddt[j * B + b];
+        } else {
+          const double qv = sq[jj * kDI + g], qdv = sqd[jj * kDI + g], qdt = io.qdt[j * B + b];
+          const double qt = io.qt ? io.qt[j * B + b] : qv + io.dt * qdt;   // fr3_controller.cpp:133
+          acc = io.kp[j] * (qt - qv) + io.kv[j] * (qdt - qdv);
+        }
+      }
+      svec[(n + j) * kDI + g] = acc;
     }
   }
   __syncthreads();
@@ -281,7 +311,7 @@ __global__ void __launch_bounds__(kDT) __attribute__((amdgpu_waves_per_eu(4, 8))
   const V3 ag = v3(0, 0, 9.81);  // -pinocchio::Model::gravity981
   double* sf = lds + L.f + (g * n) * 6;
   double* sF = lds + L.F + (g * n) * 6;
-  {
+  if (!TQ) {
     Sp V{v3(0, 0, 0), v3(0, 0, 0)}, A{v3(0, 0, 0), ag};
     for (int k = 1; k <= n; ++k) {
       if ((ancJ >> (k - 1)) & 1u) {
@@ -307,20 +337,23 @@ __global__ void __launch_bounds__(kDT) __attribute__((amdgpu_waves_per_eu(4, 8))
       Ic.h = Ic.h + ld3(bk + 1);
 #pragma unroll
       for (int i = 0; i < 6; ++i) Ic.I[i] += bk[4 + i];
-      const Sp fk = sp_ld(sf + 6 * (k - 1));
-      Fs = Sp{Fs.a + fk.a, Fs.b + fk.b};
+      if (!TQ) {
+        const Sp fk = sp_ld(sf + 6 * (k - 1));
+        Fs = Sp{Fs.a + fk.a, Fs.b + fk.b};
+      }
     }
   }
   const double nleJ = sp_dot(SJ, Fs);
   const double gJ = sp_dot(SJ, Sp{cross(Ic.h, ag), Ic.m * ag});
   const Sp FJ = inertia_mul(Ic, SJ);
-  double* svec = lds + L.vec;
   __syncthreads();  // every lane is done reading sf before sF (aliased region) is written
   if (on) {
     sp_st(sF + 6 * j, FJ);
-    svec[(0 * n + j) * kDI + g] = gJ;
-    svec[(1 * n + j) * kDI + g] = nleJ;
-    svec[(2 * n + j) * kDI + g] = nleJ - gJ;
+    if (!TQ) {
+      svec[(0 * n + j) * kDI + g] = gJ;
+      svec[(1 * n + j) * kDI + g] = nleJ;
+      svec[(2 * n + j) * kDI + g] = nleJ - gJ;
+    }
   }
   __syncthreads();
   // ---- M column J: M_IJ = S_I . (Ic_J S_J) for I ancestor-or-self of J,
@@ -335,6 +368,24 @@ __global__ void __launch_bounds__(kDT) __attribute__((amdgpu_waves_per_eu(4, 8))
       else if ((M0->anc[i + 1] >> j) & 1u)
         a[i] = sp_dot(SJ, sp_ld(sF + 6 * i));
     }
+  }
+  if (TQ) {
+    // tau_J = sum_I M_JI acc_I + g_J over the block (M symmetric: column J = row J)
+    const int s0 = io.bs, bn = io.bn;
+    if (on && j >= s0 && j < s0 + bn) {
+      double t = gJ;
+#pragma unroll
+      for (int i = 0; i < kMaxJoints; ++i)
+        if (i >= s0 && i < s0 + bn) t = fma(a[i], svec[(n + i - s0) * kDI + g], t);
+      svec[(2 * n + j - s0) * kDI + g] = t;
+    }
+    __syncthreads();
+    const int64_t b0 = static_cast<int64_t>(blockIdx.x) * kDI;
+    for (int idx = tid; idx < bn * kDI; idx += kDT) {
+      const int f = idx >> 4, t = idx & 15;
+      if (b0 + t < B) io.tau[f * B + b0 + t] = svec[2 * n * kDI + idx];
+    }
+    return;
   }
   __syncthreads();  // phase A dead: phase B overwrites the union
   double* sM = lds + L.M;
@@ -471,27 +522,28 @@ __global__ void __launch_bounds__(kDT) __attribute__((amdgpu_waves_per_eu(4, 8))
   store(io.c, vsrc + 2 * no * kDI, no);
 }
 
-template <bool ACT, bool FB>
+template <int MODE, bool FB>
 int launch_one(const DevModel* d_model, const DynLayout& L, int64_t blocks, const DynIO& io, hipStream_t st) {
   const size_t lds = static_cast<size_t>(L.total) * sizeof(double);
   if (lds > 65536 &&
-      hipFuncSetAttribute(reinterpret_cast<const void*>(&dyn_kernel<ACT, FB>),
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&dyn_kernel<MODE, FB>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)) != hipSuccess)
     return 2;
-  hipLaunchKernelGGL((dyn_kernel<ACT, FB>), dim3(static_cast<unsigned>(blocks)), dim3(kDT), lds, st, d_model, io);
+  hipLaunchKernelGGL((dyn_kernel<MODE, FB>), dim3(static_cast<unsigned>(blocks)), dim3(kDT), lds, st, d_model, io);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
-template <bool ACT>
+template <int MODE>
 int launch_pair(const DevModel* d_model, int n, int na, int64_t B, const DynIO& io, hipStream_t st) {
   const int64_t blocks = (B + kDI - 1) / kDI;
   if (blocks > 0x7fffffff) return 1;
   if (io.Minv && hipMemsetAsync(io.list, 0, sizeof(int), st) != hipSuccess) return 2;
-  if (int rc = launch_one<ACT, false>(d_model, dyn_layout(n, na, ACT, false), blocks, io, st)) return rc;
+  constexpr bool ACT = MODE == kDynActuated;
+  if (int rc = launch_one<MODE, false>(d_model, dyn_layout(n, na, ACT, false), blocks, io, st)) return rc;
   // re-solve the uncertified instances (queued by the first kernel); blocks
   // past the queue length exit at once
   if (io.Minv)
-    if (int rc = launch_one<ACT, true>(d_model, dyn_layout(n, na, ACT, true), blocks, io, st)) return rc;
+    if (int rc = launch_one<MODE, true>(d_model, dyn_layout(n, na, ACT, true), blocks, io, st)) return rc;
   return 0;
 }
 
@@ -504,9 +556,29 @@ int dyn_lds_bytes(int n, int na, bool act, bool fallback) {
 int launch_dynamics(const DevModel* d_model, const DevModel& host, bool act, int64_t B, const double* q,
                     const double* qd, double* M, double* Minv, double* g, double* nle, double* c, int* list,
                     hipStream_t st) {
-  DynIO io{B, q, qd, M, Minv, g, nle, c, list};
+  DynIO io{};
+  io.B = B; io.q = q; io.qd = qd;
+  io.M = M; io.Minv = Minv; io.g = g; io.nle = nle; io.c = c; io.list = list;
   const int n = host.nv, na = act ? host.n_arm + host.n_wheel : host.nv;
-  return act ? launch_pair<true>(d_model, n, na, B, io, st) : launch_pair<false>(d_model, n, na, B, io, st);
+  return act ? launch_pair<kDynActuated>(d_model, n, na, B, io, st) : launch_pair<kDyn>(d_model, n, na, B, io, st);
+}
+
+int launch_torque_step(const DevModel* d_model, const DevModel& host, int64_t B, const double* q, const double* qd,
+                       const double* q_target, const double* qdot_target, const double* qddot_target, double dt,
+                       const double* kp, const double* kv, double* tau, hipStream_t st) {
+  DynIO io{};
+  io.B = B; io.q = q; io.qd = qd;
+  io.qt = q_target; io.qdt = qdot_target; io.qddt = qddot_target; io.dt = dt;
+  io.bs = host.kind == 1 ? host.mani_start : 0;
+  io.bn = host.kind == 1 ? host.n_arm : host.nv;
+  for (int i = 0; i < kMaxJoints; ++i) {
+    io.kp[i] = i < io.bn ? kp[i] : 0.0;
+    io.kv[i] = i < io.bn ? kv[i] : 0.0;
+  }
+  io.tau = tau;
+  const int64_t blocks = (B + kDI - 1) / kDI;
+  if (blocks > 0x7fffffff) return 1;
+  return launch_one<kTorque, false>(d_model, dyn_layout(host.nv, host.nv, false, false), blocks, io, st);
 }
 
 }  // namespace drc_amd

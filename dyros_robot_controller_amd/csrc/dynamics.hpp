@@ -20,4 +20,12 @@ int launch_dynamics(const DevModel* d_model, const DevModel& host, bool act, int
                     const double* qd, double* M, double* Minv, double* g, double* nle, double* c, int* list,
                     hipStream_t st);
 
+// Joint torque step for the controlled block (all joints of a manipulator, the
+// arm of a mobile manipulator): tau = M_b acc + g_b with acc = qddot_target or
+// kp (q_target - q_b) + kv (qdot_target - qdot_b); q_target == nullptr means
+// q_b + dt qdot_target.  kp, kv: host arrays of the block size.
+int launch_torque_step(const DevModel* d_model, const DevModel& host, int64_t B, const double* q, const double* qd,
+                       const double* q_target, const double* qdot_target, const double* qddot_target, double dt,
+                       const double* kp, const double* kv, double* tau, hipStream_t st);
+
 }  // namespace drc_amd

@@ -2886,4 +2886,68 @@ int drc_dynamics_host(drc_model* m, int actuated, int64_t B, const double* q, co
   return DRC_OK;
 }
 
+// ---- joint torque step ---------------------------------
+int drc_joint_torque_step_batch(drc_model* m, int64_t B, const double* q, const double* qdot, const double* q_target,
+                                const double* qdot_target, const double* qddot_target, double dt, const double* kp,
+                                const double* kv, double* tau, void* stream) {
+  using drc_amd::set_err;
+  if (!m) return set_err(DRC_ERR_INVALID_ARGUMENT, "null model");
+  if (B < 0) return set_err(DRC_ERR_INVALID_ARGUMENT, "negative batch");
+  if (B == 0) return DRC_OK;
+  if (!q || !tau) return set_err(DRC_ERR_INVALID_ARGUMENT, "q and tau are required");
+  if (!qddot_target && (!qdot || !qdot_target))
+    return set_err(DRC_ERR_INVALID_ARGUMENT, "qdot and qdot_target are required without qddot_target");
+  const drc_amd::DevModel& d = m->hm.dev;
+  const int nb = d.kind == 1 ? d.n_arm : d.nv;
+  double kpv[drc_amd::kMaxJoints], kvv[drc_amd::kMaxJoints];
+  for (int i = 0; i < nb; ++i) {  // robot_controller.cpp:14-15 (MoMa :17-18): 400 / 40
+    kpv[i] = kp ? kp[i] : 400.0;
+    kvv[i] = kv ? kv[i] : 40.0;
+  }
+  HIP_TRY(hipSetDevice(m->device));
+  const int rc = drc_amd::launch_torque_step(m->d_model, d, B, q, qdot, q_target, qdot_target, qddot_target, dt, kpv,
+                                             kvv, tau, reinterpret_cast<hipStream_t>(stream));
+  if (rc == 1) return set_err(DRC_ERR_INVALID_ARGUMENT, "batch too large");
+  if (rc) return set_err(DRC_ERR_HIP, std::string("torque step launch: ") + hipGetErrorString(hipGetLastError()));
+  return DRC_OK;
+}
+
+int drc_joint_torque_step_host(drc_model* m, int64_t B, const double* q, const double* qdot, const double* q_target,
+                               const double* qdot_target, const double* qddot_target, double dt, const double* kp,
+                               const double* kv, double* tau) {
+  using drc_amd::set_err;
+  if (!m) return set_err(DRC_ERR_INVALID_ARGUMENT, "null model");
+  if (B <= 0) return B == 0 ? DRC_OK : set_err(DRC_ERR_INVALID_ARGUMENT, "negative batch");
+  if (!q || !tau) return set_err(DRC_ERR_INVALID_ARGUMENT, "q and tau are required");
+  const drc_amd::DevModel& d = m->hm.dev;
+  const int64_t n = d.nv, nb = d.kind == 1 ? d.n_arm : d.nv;
+  std::lock_guard<std::mutex> lk(m->host_mu);
+  HIP_TRY(hipSetDevice(m->device));
+  const double* src[5] = {q, qdot, q_target, qdot_target, qddot_target};
+  const int64_t rows[5] = {n, n, nb, nb, nb};
+  int64_t words = nb * B;
+  for (int i = 0; i < 5; ++i) words += src[i] ? rows[i] * B : 0;
+  if (m->stage_bytes < words * 8) {
+    if (m->stage) (void)hipFree(m->stage);
+    m->stage = nullptr;
+    m->stage_bytes = 0;
+    HIP_TRY(hipMalloc(&m->stage, words * 8));
+    m->stage_bytes = words * 8;
+  }
+  if (!m->hstream) HIP_TRY(hipStreamCreateWithFlags(&m->hstream, hipStreamNonBlocking));
+  double* dp = reinterpret_cast<double*>(m->stage);
+  const double* din[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+  for (int i = 0; i < 5; ++i)
+    if (src[i]) {
+      HIP_TRY(hipMemcpyAsync(dp, src[i], rows[i] * B * 8, hipMemcpyHostToDevice, m->hstream));
+      din[i] = dp;
+      dp += rows[i] * B;
+    }
+  int rc = drc_joint_torque_step_batch(m, B, din[0], din[1], din[2], din[3], din[4], dt, kp, kv, dp, m->hstream);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(tau, dp, nb * B * 8, hipMemcpyDeviceToHost, m->hstream));
+  HIP_TRY(hipStreamSynchronize(m->hstream));
+  return DRC_OK;
+}
+
 }  // extern "C"

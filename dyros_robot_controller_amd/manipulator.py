@@ -282,6 +282,8 @@ class RobotController:
         self.dof_ = robot_data.getDof()
         self.Kp_task_ = np.full(6, 100.0)
         self.Kv_task_ = np.full(6, 20.0)
+        self.Kp_joint_ = np.full(self.dof_, 400.0)    # robot_controller.cpp:14-15
+        self.Kv_joint_ = np.full(self.dof_, 40.0)
         self.set_solver_mode(solver_mode)
 
     def set_solver_mode(self, mode):
@@ -309,6 +311,52 @@ class RobotController:
         self.Kv_task_ = Kv
 
     set_task_gain, set_task_kp_gain, set_task_kv_gain = setTaskGain, setTaskKpGain, setTaskKvGain
+
+    def setJointGain(self, Kp, Kv):
+        Kp, Kv = np.asarray(Kp, float).reshape(-1), np.asarray(Kv, float).reshape(-1)
+        if Kp.size != self.dof_ or Kv.size != self.dof_:
+            raise RuntimeError("Kp and Kv must be of size dof_.")
+        self.Kp_joint_, self.Kv_joint_ = Kp, Kv
+
+    def setJointKpGain(self, Kp):
+        Kp = np.asarray(Kp, float).reshape(-1)
+        if Kp.size != self.dof_:
+            raise RuntimeError("Kp must be of size dof_.")
+        self.Kp_joint_ = Kp
+
+    def setJointKvGain(self, Kv):
+        Kv = np.asarray(Kv, float).reshape(-1)
+        if Kv.size != self.dof_:
+            raise RuntimeError("Kv must be of size dof_.")
+        self.Kv_joint_ = Kv
+
+    set_joint_gain, set_joint_kp_gain, set_joint_kv_gain = setJointGain, setJointKpGain, setJointKvGain
+
+    # -- joint torque step (robot_controller.cpp:115-125) -----------------------
+    def moveJointTorqueStep_batch(self, q, qdot, q_target=None, qdot_target=None, qddot_target=None, dt=None):
+        """tau [dof][B]; q_target None -> q + dt * qdot_target (fr3_controller.cpp:133)."""
+        dev = self.robot_data_.device
+        a = lambda t: _batch.as_device(t, dev)
+        return _batch.joint_torque_step_batch(self.robot_data_.model, a(q), a(qdot), a(q_target), a(qdot_target),
+                                              a(qddot_target), self.dt_ if dt is None else dt,
+                                              self.Kp_joint_, self.Kv_joint_)
+
+    def moveJointTorqueStep(self, *args):
+        """moveJointTorqueStep(qddot_target) or moveJointTorqueStep(q_target, qdot_target)."""
+        q, qd = self._state()
+        col = lambda v: np.asarray(v, float).reshape(-1, 1)
+        if len(args) == 1:
+            tau = self.moveJointTorqueStep_batch(q, qd, qddot_target=col(args[0]))
+        else:
+            tau = self.moveJointTorqueStep_batch(q, qd, q_target=col(args[0]), qdot_target=col(args[1]))
+        return tau.cpu().numpy()[:, 0]
+
+    def move_joint_torque_step(self, q_target=None, qdot_target=None, qddot_target=None):
+        if qddot_target is not None:
+            return self.moveJointTorqueStep(qddot_target)
+        if q_target is not None and qdot_target is not None:
+            return self.moveJointTorqueStep(q_target, qdot_target)
+        return None
 
     # -- batched entries (device tensors, [field][B]) --------------------------
     def _run(self, mode, link_name, q, qdot, x_target, xdot_target, x_init=None, xdot_init=None,

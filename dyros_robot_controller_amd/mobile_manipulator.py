@@ -312,6 +312,9 @@ class RobotController:
         self.robot_data_ = robot_data
         self.Kp_task_ = np.full(6, 400.0)
         self.Kv_task_ = np.full(6, 0.0)
+        n = robot_data.get_manipulator_dof()
+        self.Kp_mani_joint_ = np.full(n, 400.0)   # mobile_manipulator/robot_controller.cpp:17-18
+        self.Kv_mani_joint_ = np.full(n, 40.0)
         self.set_solver_mode(solver_mode)
 
     def set_solver_mode(self, mode):
@@ -339,6 +342,51 @@ class RobotController:
         self.Kv_task_ = kv
 
     setTaskGain, setTaskKpGain, setTaskKvGain = set_task_gain, set_task_kp_gain, set_task_kv_gain
+
+    def _mani_vec(self, v, what):
+        v = np.asarray(v, float).reshape(-1)
+        if v.size != self.robot_data_.get_manipulator_dof():
+            raise RuntimeError("%s must be of size mani_dof_." % what)
+        return v
+
+    def set_manipulator_joint_gain(self, kp, kv):
+        self.Kp_mani_joint_, self.Kv_mani_joint_ = self._mani_vec(kp, "Kp"), self._mani_vec(kv, "Kv")
+
+    def set_manipulator_joint_kp_gain(self, kp):
+        self.Kp_mani_joint_ = self._mani_vec(kp, "Kp")
+
+    def set_manipulator_joint_kv_gain(self, kv):
+        self.Kv_mani_joint_ = self._mani_vec(kv, "Kv")
+
+    setManipulatorJointGain = set_manipulator_joint_gain
+    setManipulatorJointKpGain, setManipulatorJointKvGain = set_manipulator_joint_kp_gain, set_manipulator_joint_kv_gain
+
+    # -- arm joint torque step (mobile_manipulator/robot_controller.cpp:103-118) --
+    def move_manipulator_joint_torque_step_batch(self, q, qdot, q_mani_target=None, qdot_mani_target=None,
+                                                 qddot_mani_target=None, dt=None):
+        """tau_mani [n_arm][B] from full states q, qdot [dof][B]."""
+        dev = self.robot_data_.device
+        a = lambda t: _batch.as_device(t, dev)
+        return _batch.joint_torque_step_batch(self.robot_data_.model, a(q), a(qdot), a(q_mani_target),
+                                              a(qdot_mani_target), a(qddot_mani_target),
+                                              self.dt_ if dt is None else dt, self.Kp_mani_joint_, self.Kv_mani_joint_)
+
+    def moveManipulatorJointTorqueStep(self, *args):
+        rd = self.robot_data_
+        q, qd = rd.q_.reshape(-1, 1), rd.qdot_.reshape(-1, 1)
+        col = lambda v: np.asarray(v, float).reshape(-1, 1)
+        if len(args) == 1:
+            tau = self.move_manipulator_joint_torque_step_batch(q, qd, qddot_mani_target=col(args[0]))
+        else:
+            tau = self.move_manipulator_joint_torque_step_batch(q, qd, col(args[0]), col(args[1]))
+        return tau.cpu().numpy()[:, 0]
+
+    def move_manipulator_joint_torque_step(self, q_mani_target=None, qdot_mani_target=None, qddot_mani_target=None):
+        if qddot_mani_target is not None:
+            return self.moveManipulatorJointTorqueStep(qddot_mani_target)
+        if q_mani_target is not None and qdot_mani_target is not None:
+            return self.moveManipulatorJointTorqueStep(q_mani_target, qdot_mani_target)
+        return None
 
     # -- batched entries (device tensors, [field][B]; q is the full joint vector)
     def _run(self, mode, link_name, q, qdot, x_target, xdot_target, x_init=None, xdot_init=None,

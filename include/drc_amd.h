@@ -241,6 +241,27 @@ int drc_dynamics_batch(drc_model* model, int actuated, int64_t B, const double* 
 int drc_dynamics_host(drc_model* model, int actuated, int64_t B, const double* q, const double* qdot,
                       double* M, double* M_inv, double* g, double* nle, double* c);
 
+/* ---- joint torque step ------------------------
+ * Manipulator::RobotController::moveJointTorqueStep (src/manipulator/robot_controller.cpp:115-125) for B
+ * robots, computing M and g in the same launch (robot_data.cpp:111-112):
+ *   tau = M qddot_target + g                                     when qddot_target != NULL
+ *   tau = M (kp .* (q_target - q) + kv .* (qdot_target - qdot)) + g   otherwise,
+ * with q_target == NULL meaning q + dt * qdot_target: the Euler step that follows QPIK in the reference's
+ * FR3 control loop (examples/C++/src/fr3_controller.cpp:132-134), so
+ *   drc_qpik_batch(...qdot_out...) ; drc_joint_torque_step_batch(..., NULL, qdot_out, NULL, dt, ...)
+ * is that whole cycle on the device.  Mobile manipulators: the arm block, as
+ * MobileManipulator::RobotController::moveManipulatorJointTorqueStep (mobile_manipulator/robot_controller.cpp:103-118).
+ * q, qdot: [dof][B]; q_target, qdot_target, qddot_target, tau: [nb][B] with nb = dof (manipulator) or the arm
+ * dof (mobile manipulator).  kp, kv: HOST arrays [nb] or NULL for the reference defaults 400 / 40
+ * (robot_controller.cpp:14-15). */
+int drc_joint_torque_step_batch(drc_model* model, int64_t B, const double* q, const double* qdot,
+                                const double* q_target, const double* qdot_target, const double* qddot_target,
+                                double dt, const double* kp, const double* kv, double* tau, void* stream);
+/* Same contract with HOST buffers; synchronous. */
+int drc_joint_torque_step_host(drc_model* model, int64_t B, const double* q, const double* qdot,
+                               const double* q_target, const double* qdot_target, const double* qddot_target,
+                               double dt, const double* kp, const double* kv, double* tau);
+
 #ifdef __cplusplus
 }
 #endif

@@ -118,3 +118,51 @@ def test_host_entry_and_getters(cuda):
     np.testing.assert_allclose(rd.computeGravity(q[:, 2]), ref["g"], atol=1e-11)
     # empty batch is a no-op
     assert _batch.dynamics_batch(rd.model, _batch.as_device(np.zeros((7, 0)), cuda))["M"].shape == (7, 7, 0)
+
+
+def _torque_ref(d, q, qd, qt, qdt, kp, kv, s, n):
+    acc = kp * (qt - q[s:s + n]) + kv * (qdt - qd[s:s + n])
+    return d["M"][s:s + n, s:s + n] @ acc + d["g"][s:s + n]
+
+
+@pytest.mark.parametrize("robot", ["fr3", "xls_fr3"])
+def test_joint_torque_step_matches_oracle(cuda, robot):
+    """moveJointTorqueStep (robot_controller.cpp:115-125) / the MoMa arm block
+    (mobile_manipulator/robot_controller.cpp:103-118), including the QPIK
+    example's Euler target q + dt qdot* (fr3_controller.cpp:133)."""
+    pm, _, spec = O.load(robot)
+    moma = spec["kind"] == 1
+    rd = make_moma(robot, cuda) if moma else make_manipulator(robot, cuda)
+    B = 45
+    if moma:
+        q, qd = workload.mobile_states(np.array(pm.lower), np.array(pm.upper), np.array(pm.vel),
+                                       spec["joint_index"], spec["n_arm"], spec["n_wheel"], 3, B, 0)
+        s, n = spec["joint_index"][1], spec["n_arm"]
+    else:
+        q, qd = _states(pm, B, 12)
+        s, n = 0, pm.nv
+    rng = np.random.default_rng(13)
+    qt, qdt, qddt = rng.uniform(-1, 1, (n, B)), rng.uniform(-1, 1, (n, B)), rng.uniform(-3, 3, (n, B))
+    kp, kv = rng.uniform(100, 500, n), rng.uniform(10, 50, n)
+    dt = 0.001
+    A = lambda t: _batch.as_device(t, cuda)
+    t1 = _batch.joint_torque_step_batch(rd.model, A(q), A(qd), A(qt), A(qdt), None, dt, kp, kv).cpu().numpy()
+    t2 = _batch.joint_torque_step_batch(rd.model, A(q), A(qd), None, A(qdt), None, dt, kp, kv).cpu().numpy()
+    t3 = _batch.joint_torque_step_batch(rd.model, A(q), A(qd), None, None, A(qddt), dt).cpu().numpy()
+    t4 = _batch.joint_torque_step_batch(rd.model, A(q), A(qd), A(qt), A(qdt), None, dt).cpu().numpy()
+    for b in range(B):
+        d = R.dynamics(pm, q[:, b], qd[:, b])
+        scale = lambda r: 1e-11 * max(1.0, np.abs(r).max())
+        r1 = _torque_ref(d, q[:, b], qd[:, b], qt[:, b], qdt[:, b], kp, kv, s, n)
+        r2 = _torque_ref(d, q[:, b], qd[:, b], q[s:s + n, b] + dt * qdt[:, b], qdt[:, b], kp, kv, s, n)
+        r3 = d["M"][s:s + n, s:s + n] @ qddt[:, b] + d["g"][s:s + n]
+        r4 = _torque_ref(d, q[:, b], qd[:, b], qt[:, b], qdt[:, b], 400.0, 40.0, s, n)
+        for t, r in ((t1, r1), (t2, r2), (t3, r3), (t4, r4)):
+            np.testing.assert_allclose(t[:, b], r, atol=scale(r))
+    # single-instance mirror signatures
+    if not moma:
+        ctrl = manipulator.RobotController(dt, rd)
+        rd.updateState(q[:, 0], qd[:, 0])
+        ctrl.setJointGain(kp, kv)
+        np.testing.assert_allclose(ctrl.move_joint_torque_step(q_target=qt[:, 0], qdot_target=qdt[:, 0]), t1[:, 0],
+                                   rtol=0, atol=1e-12 * max(1, np.abs(t1[:, 0]).max()))
