@@ -7,6 +7,7 @@ $HIPCC --offload-arch=gfx950 -O3 -fPIC -shared -std=c++17 -Wall -Wno-unused-func
   dyros_robot_controller_amd/csrc/qpik_kernel.hip dyros_robot_controller_amd/csrc/dynamics.hip dyros_robot_controller_amd/csrc/model.cpp \
   -o dyros_robot_controller_amd/libdrc_amd.so -Wl,-rpath,/opt/rocm/lib
 make -s -C oracle
+mkdir -p dyros_robot_controller_amd/python
 # C++ facade + pybind11 module with the reference's module/class names (host code only)
 PYEXT=$(python3 -c "import sysconfig; print(sysconfig.get_config_var('EXT_SUFFIX'))")
 PYINC=$(python3 -c "import pybind11, sysconfig; print('-I' + pybind11.get_include() + ' -I' + sysconfig.get_paths()['include'])")
