@@ -1996,8 +1996,11 @@ __device__ __forceinline__ int qp_admm(const KParams& kp, const KParams& kpl, do
 
 // QP kernel: assembles and solves the QP of each instance from the task
 // record written by task_kernel.
+#ifndef DRC_QP_WAVES
+#define DRC_QP_WAVES 2
+#endif
 template <class QD>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 8)))
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRC_QP_WAVES, 8)))
 qp_kernel(const DevModel* __restrict__ M0, const KParams kp, const IO io) {
   extern __shared__ __attribute__((aligned(16))) double S[];
   // LDS copy of the parameters for the out-of-line (rare) ADMM blocks: a

@@ -701,7 +701,14 @@ static void make_shape(const OracleModel* m, const Kin* k, int g, Shape* s) {
 }
 
 /* RobotData::getMinDistance(true,false,false)  robot_data.cpp:424-494 */
+static void min_distance_w(const OracleModel* m, const Kin* k, double* dist, double* grad, int* pair_out,
+                           double* wA, double* wB);
 static void min_distance(const OracleModel* m, const Kin* k, double* dist, double* grad, int* pair_out) {
+    double wA[3], wB[3];
+    min_distance_w(m, k, dist, grad, pair_out, wA, wB);
+}
+static void min_distance_w(const OracleModel* m, const Kin* k, double* dist, double* grad, int* pair_out,
+                           double* wA, double* wB) {
     Shape sh[ORC_MAXG];
     for (int g = 0; g < m->ngeom; ++g) make_shape(m, k, g, &sh[g]);
     double best = 1.7976931348623157e308, bpA[3] = {0}, bpB[3] = {0};
@@ -713,6 +720,8 @@ static void min_distance(const OracleModel* m, const Kin* k, double* dist, doubl
     }
     *dist = best;
     *pair_out = bi;
+    memcpy(wA, bpA, sizeof(bpA));
+    memcpy(wB, bpB, sizeof(bpB));
     int nv = m->nv;
     memset(grad, 0, nv * sizeof(double));
     if (bi < 0) return;  /* reference indexes pair -1; we return zero gradient */
@@ -728,6 +737,134 @@ static void min_distance(const OracleModel* m, const Kin* k, double* dist, doubl
         double s = 0;
         for (int i = 0; i < 3; ++i) s += n[i] * (JB[i * nv + c] - JA[i * nv + c]);
         grad[c] = best < 0 ? -s : s;
+    }
+}
+
+/* ------------------------------------------------------------------------ */
+/* Jacobian time variation and the grad_dot terms of QPID                   */
+/* ------------------------------------------------------------------------ */
+#define ORC_ALL_JOINTS 0xffffffffu
+/* velocity of a point p rigidly attached to the body of joint X, from the
+ * joints a on its support path whose bit (a-1) is set in mask */
+static void point_velocity(const OracleModel* m, const Kin* k, int X, const double* p, const double* qd,
+                           uint32_t mask, double* v) {
+    v[0] = v[1] = v[2] = 0;
+    for (int a = X; a > 0; a = m->parent[a]) {
+        if (!(mask & (1u << (a - 1)))) continue;
+        double c[3];
+        if (m->jtype[a] == 0) { double r[3]; sub3(p, k->T[a] + 9, r); cross3(k->z[a], r, c); }
+        else memcpy(c, k->z[a], sizeof(c));
+        for (int i = 0; i < 3; ++i) v[i] += qd[a - 1] * c[i];
+    }
+}
+
+/* d/dt of the 6 x nv LWA Jacobian of a point p attached to joint X
+ * (pinocchio computeJointJacobiansTimeVariation + get{Joint,Frame}Jacobian-
+ * TimeVariation(LOCAL_WORLD_ALIGNED), robot_data.cpp:109,414,476-477) with the
+ * joint velocities restricted to `mask`.  Column c (revolute):
+ * [zdot_c x (p - o_c) + z_c x (pdot - odot_c); zdot_c], zdot_c = w_parent(c) x z_c;
+ * (prismatic): [zdot_c; 0]. */
+static void point_jacobian_dot(const OracleModel* m, const Kin* k, int X, const double* p, const double* qd,
+                               uint32_t mask, double* Jd) {
+    int nv = m->nv;
+    memset(Jd, 0, 6 * nv * sizeof(double));
+    double pdot[3];
+    point_velocity(m, k, X, p, qd, mask, pdot);
+    for (int c = X; c > 0; c = m->parent[c]) {
+        double w[3] = {0, 0, 0};
+        for (int a = m->parent[c]; a > 0; a = m->parent[a])
+            if (m->jtype[a] == 0 && (mask & (1u << (a - 1))))
+                for (int i = 0; i < 3; ++i) w[i] += qd[a - 1] * k->z[a][i];
+        double zd[3];
+        cross3(w, k->z[c], zd);
+        if (m->jtype[c] == 0) {
+            double od[3], r[3], t1[3], dv[3], t2[3];
+            point_velocity(m, k, c, k->T[c] + 9, qd, mask, od);
+            sub3(p, k->T[c] + 9, r);
+            cross3(zd, r, t1);
+            sub3(pdot, od, dv);
+            cross3(k->z[c], dv, t2);
+            for (int i = 0; i < 3; ++i) { Jd[i * nv + c - 1] = t1[i] + t2[i]; Jd[(3 + i) * nv + c - 1] = zd[i]; }
+        } else {
+            for (int i = 0; i < 3; ++i) Jd[i * nv + c - 1] = zd[i];
+        }
+    }
+}
+
+/* getManipulability(true, true, link) grad_dot, literally
+ * (robot_data.cpp:555-569; MoMa :477-492 on the arm block c0..c0+nc):
+ *   mani_dot = m tr(Jd J^T Ai), Ai_dot = -Ai (2 Jd J^T) Ai,
+ *   grad_dot_i = mani_dot tr(dJ_i J^T Ai) + m tr(dJ_i Jd^T Ai + dJ_i J^T Ai_dot)
+ * with dJ_i = the frame Jacobian time variation at qdot = e_(c0+i). */
+static void manip_graddot(const OracleModel* m, const Kin* k, const double* J, int c0, int nc, const double* qd,
+                          double man, double* gd) {
+    int nv = m->nv;
+    double Jr[6 * ORC_MAXJ], Jdf[6 * ORC_MAXJ], Jd[6 * ORC_MAXJ], A[36], Ai[36], JJd[36], T1[36], Aid[36];
+    for (int i = 0; i < 6; ++i) for (int c = 0; c < nc; ++c) Jr[i * nc + c] = J[i * nv + c0 + c];
+    for (int i = 0; i < 6; ++i) for (int j = 0; j < 6; ++j) { double s = 0; for (int c = 0; c < nc; ++c) s += Jr[i * nc + c] * Jr[j * nc + c]; A[i * 6 + j] = s; }
+    pinv_cod_sym(A, 6, Ai);
+    point_jacobian_dot(m, k, m->ee_joint, k->pe, qd, ORC_ALL_JOINTS, Jdf);
+    for (int i = 0; i < 6; ++i) for (int c = 0; c < nc; ++c) Jd[i * nc + c] = Jdf[i * nv + c0 + c];
+    /* JJt_dot = 2 Jd J^T (robot_data.cpp:562, as written: not symmetrised) */
+    for (int i = 0; i < 6; ++i) for (int j = 0; j < 6; ++j) { double s = 0; for (int c = 0; c < nc; ++c) s += Jd[i * nc + c] * Jr[j * nc + c]; JJd[i * 6 + j] = 2 * s; }
+    for (int i = 0; i < 6; ++i) for (int j = 0; j < 6; ++j) { double s = 0; for (int a = 0; a < 6; ++a) s += Ai[i * 6 + a] * JJd[a * 6 + j]; T1[i * 6 + j] = s; }
+    for (int i = 0; i < 6; ++i) for (int j = 0; j < 6; ++j) { double s = 0; for (int a = 0; a < 6; ++a) s += T1[i * 6 + a] * Ai[a * 6 + j]; Aid[i * 6 + j] = -s; }
+    /* tr(X Y^T Z) = sum_{a,c,b} X[a][c] Y[b][c] Z[b][a] */
+    #define TR3(X, Y, Z) ({ double t_ = 0; for (int a_ = 0; a_ < 6; ++a_) for (int b_ = 0; b_ < 6; ++b_) { double u_ = 0; \
+        for (int c_ = 0; c_ < nc; ++c_) { u_ += (X)[a_ * nc + c_] * (Y)[b_ * nc + c_]; } t_ += u_ * (Z)[b_ * 6 + a_]; } t_; })
+    double mani_dot = man * TR3(Jd, Jr, Ai);
+    double* dJ = (double*)malloc((size_t)nv * 6 * nv * sizeof(double));
+    frame_jacobian_dq(m, k, dJ);
+    for (int i = 0; i < nc; ++i) {
+        const double* D = dJ + (size_t)(c0 + i) * 6 * nv;
+        double Db[6 * ORC_MAXJ];
+        for (int a = 0; a < 6; ++a) for (int c = 0; c < nc; ++c) Db[a * nc + c] = D[a * nv + c0 + c];
+        gd[i] = mani_dot * TR3(Db, Jr, Ai) + man * (TR3(Db, Jd, Ai) + TR3(Db, Jr, Aid));
+    }
+    #undef TR3
+    free(dJ);
+}
+
+/* getMinDistance(.., with_graddot = true, ..) grad_dot, literally
+ * (robot_data.cpp:496-512): JX_dot = J_jX_dot.top - (skew(rX_dot) J_jX.bottom
+ * + skew(rX) J_jX_dot.bottom), rX_dot = JX qdot - J_jX.top qdot;
+ * grad_dot = n^T (JB_dot - JA_dot) (n_dot neglected; no sign flip). */
+static void mindist_graddot(const OracleModel* m, const Kin* k, int pair, const double* pA, const double* pB,
+                            const double* qd, double* gd) {
+    int nv = m->nv;
+    memset(gd, 0, nv * sizeof(double));
+    if (pair < 0) return;
+    double n[3];
+    sub3(pB, pA, n);
+    double L = norm3(n);
+    n[0] /= L; n[1] /= L; n[2] /= L;
+    double JXd[2][3 * ORC_MAXJ];
+    for (int s = 0; s < 2; ++s) {
+        int jX = m->gparent[s == 0 ? m->pair_a[pair] : m->pair_b[pair]];
+        const double* pX = s == 0 ? pA : pB;
+        const double* oX = k->T[jX] + 9;
+        double Jj[6 * ORC_MAXJ], Jjd[6 * ORC_MAXJ], r[3], vt[3] = {0, 0, 0}, pd[3] = {0, 0, 0}, rd[3];
+        point_jacobian(m, k, jX, oX, Jj);
+        point_jacobian_dot(m, k, jX, oX, qd, ORC_ALL_JOINTS, Jjd);
+        sub3(pX, oX, r);
+        for (int c = 0; c < nv; ++c) {
+            double top[3] = {Jj[0 * nv + c], Jj[1 * nv + c], Jj[2 * nv + c]}, bot[3] = {Jj[3 * nv + c], Jj[4 * nv + c], Jj[5 * nv + c]}, rb[3];
+            cross3(r, bot, rb);
+            for (int i = 0; i < 3; ++i) { pd[i] += (top[i] - rb[i]) * qd[c]; vt[i] += top[i] * qd[c]; }
+        }
+        sub3(pd, vt, rd);
+        for (int c = 0; c < nv; ++c) {
+            double bot[3] = {Jj[3 * nv + c], Jj[4 * nv + c], Jj[5 * nv + c]}, botd[3] = {Jjd[3 * nv + c], Jjd[4 * nv + c], Jjd[5 * nv + c]};
+            double t1[3], t2[3];
+            cross3(rd, bot, t1);
+            cross3(r, botd, t2);
+            for (int i = 0; i < 3; ++i) JXd[s][i * nv + c] = Jjd[i * nv + c] - (t1[i] + t2[i]);
+        }
+    }
+    for (int c = 0; c < nv; ++c) {
+        double t = 0;
+        for (int i = 0; i < 3; ++i) t += n[i] * (JXd[1][i * nv + c] - JXd[0][i * nv + c]);
+        gd[c] = t;
     }
 }
 
@@ -821,6 +958,13 @@ static void limit_scaling(double* v, int n) {
     for (int i = 0; i < n; ++i) { if (v[i] < MIN_SCALING) v[i] = 1.0; else if (v[i] > MAX_SCALING) v[i] = MAX_SCALING; }
 }
 
+/* residuals and tolerances of one iterate (scaled problem) */
+typedef struct Res {
+    double pri_res, dua_res, pri_res_s, dua_res_s;
+    double nAx_s, nz_s, nPx_s, nAty_s, nq_s;
+    double eps_pri, eps_dua;
+} Res;
+
 typedef struct QPW {
     int n, m;
     double P[ORC_MAXX * ORC_MAXX], q[ORC_MAXX], A[ORC_MAXC * ORC_MAXX], l[ORC_MAXC], u[ORC_MAXC];
@@ -829,9 +973,7 @@ typedef struct QPW {
     int ctype[ORC_MAXC];  /* -1 loose, 0 ineq, 1 eq */
     double L[ORC_MAXX * ORC_MAXX];
     double x[ORC_MAXX], z[ORC_MAXC], y[ORC_MAXC], dy[ORC_MAXC];
-    double pri_res, dua_res, pri_res_s, dua_res_s;
-    double nAx_s, nz_s, nPx_s, nAty_s, nq_s;
-    double eps_pri, eps_dua;
+    Res r;
 } QPW;
 
 static void qp_factor(QPW* w, double sigma) {
@@ -892,7 +1034,7 @@ static void qp_scale(QPW* w, int iters) {
 }
 
 /* residuals at the current iterate (scaled and unscaled) */
-static void qp_residuals(QPW* w, const double* x, const double* z, const double* y, double eps_abs, double eps_rel) {
+static void qp_residuals(const QPW* w, Res* o, const double* x, const double* z, const double* y, double eps_abs, double eps_rel) {
     int n = w->n, m = w->m;
     double Ax[ORC_MAXC], Px[ORC_MAXX], Aty[ORC_MAXX];
     for (int i = 0; i < m; ++i) { double s = 0; for (int j = 0; j < n; ++j) s += w->A[i * n + j] * x[j]; Ax[i] = s; }
@@ -919,13 +1061,13 @@ static void qp_residuals(QPW* w, const double* x, const double* z, const double*
         nAtys = fmax(nAtys, fabs(Aty[i]));
         nqs = fmax(nqs, fabs(w->q[i]));
     }
-    w->pri_res = pr;
-    w->dua_res = dr / w->c;
-    w->pri_res_s = prs;
-    w->dua_res_s = drs;
-    w->nAx_s = nAxs; w->nz_s = nzs; w->nPx_s = nPxs; w->nAty_s = nAtys; w->nq_s = nqs;
-    w->eps_pri = eps_abs + eps_rel * fmax(nAx, nz);
-    w->eps_dua = eps_abs + eps_rel * fmax(fmax(nPx, nAty), nq) / w->c;
+    o->pri_res = pr;
+    o->dua_res = dr / w->c;
+    o->pri_res_s = prs;
+    o->dua_res_s = drs;
+    o->nAx_s = nAxs; o->nz_s = nzs; o->nPx_s = nPxs; o->nAty_s = nAtys; o->nq_s = nqs;
+    o->eps_pri = eps_abs + eps_rel * fmax(nAx, nz);
+    o->eps_dua = eps_abs + eps_rel * fmax(fmax(nPx, nAty), nq) / w->c;
 }
 
 static int qp_primal_infeasible(QPW* w, double eps) {
@@ -1025,8 +1167,8 @@ static int qp_polish(QPW* w, const OracleSettings* s, int strict) {
     int flag[ORC_MAXC];  /* -1 lower-active, +1 upper-active, 0 inactive */
     for (int i = 0; i < m; ++i)
         flag[i] = (w->z[i] - w->l[i] < -w->y[i]) ? -1 : ((w->u[i] - w->z[i] < w->y[i]) ? 1 : 0);
-    const double pr0 = w->pri_res, dr0 = w->dua_res;
-    static __thread QPW tmp;
+    const double pr0 = w->r.pri_res, dr0 = w->r.dua_res;
+    Res tmp;
     double xp[ORC_MAXX], yp[ORC_MAXC], zp[ORC_MAXC], ax[ORC_MAXC], xc[ORC_MAXX];
     int have_feasible = 0;
     for (int it = 0; it < (strict ? POLISH_FEAS_ATTEMPTS + POLISH_AS_ITERS : 1); ++it) {
@@ -1060,8 +1202,7 @@ static int qp_polish(QPW* w, const OracleSettings* s, int strict) {
             ax[i] = t;
             zp[i] = t < w->l[i] ? w->l[i] : (t > w->u[i] ? w->u[i] : t);
         }
-        memcpy(&tmp, w, sizeof(QPW));
-        qp_residuals(&tmp, xp, zp, yp, s->eps_exact, s->eps_exact);
+        qp_residuals(w, &tmp, xp, zp, yp, s->eps_exact, s->eps_exact);
         int ok = (tmp.pri_res < pr0 && tmp.dua_res < dr0) || (tmp.pri_res < pr0 && dr0 < 1e-10) || (tmp.dua_res < dr0 && pr0 < 1e-10);
         int worst = -1;
         double wv = 0;
@@ -1084,8 +1225,8 @@ static int qp_polish(QPW* w, const OracleSettings* s, int strict) {
             memcpy(w->x, xp, n * sizeof(double));
             memcpy(w->y, yp, m * sizeof(double));
             memcpy(w->z, zp, m * sizeof(double));
-            w->pri_res = tmp.pri_res;
-            w->dua_res = tmp.dua_res;
+            w->r.pri_res = tmp.pri_res;
+            w->r.dua_res = tmp.dua_res;
             return 1;
         }
         if (!strict) return 0;
@@ -1163,9 +1304,9 @@ int oracle_solve_qp(int n, int m, const double* P, const double* qv, const doubl
         }
         int check = s->check_termination > 0 && it % s->check_termination == 0;
         int adapt = s->adaptive_rho && s->adaptive_rho_interval > 0 && it % s->adaptive_rho_interval == 0;
-        if (check || adapt) qp_residuals(&w, w.x, w.z, w.y, s->eps_abs, s->eps_rel);
+        if (check || adapt) qp_residuals(&w, &w.r, w.x, w.z, w.y, s->eps_abs, s->eps_rel);
         if (check) {
-            int conv = w.pri_res < w.eps_pri && w.dua_res < w.eps_dua;
+            int conv = w.r.pri_res < w.r.eps_pri && w.r.dua_res < w.r.eps_dua;
             /* parity mode: a certified polish is exact whatever the ADMM
              * residual, so try it at every check (the active set settles
              * long before OSQP's eps_rel termination) */
@@ -1176,9 +1317,8 @@ int oracle_solve_qp(int n, int m, const double* P, const double* qv, const doubl
                 if (!s->exact) { status = ORC_SOLVED; break; }
                 if (qp_polish(&w, s, 1)) { status = ORC_SOLVED; pol = 1; break; }
                 /* tight ADMM-only fallback */
-                static __thread QPW t2;
-                memcpy(&t2, &w, sizeof(QPW));
-                qp_residuals(&t2, w.x, w.z, w.y, s->eps_fallback, s->eps_fallback);
+                Res t2;
+                qp_residuals(&w, &t2, w.x, w.z, w.y, s->eps_fallback, s->eps_fallback);
                 if (t2.pri_res < t2.eps_pri && t2.dua_res < t2.eps_dua) { status = ORC_SOLVED; break; }
             } else if (qp_primal_infeasible(&w, s->eps_prim_inf)) {
                 status = ORC_PRIMAL_INFEASIBLE;
@@ -1186,8 +1326,8 @@ int oracle_solve_qp(int n, int m, const double* P, const double* qv, const doubl
             }
         }
         if (adapt) {
-            double pr = w.pri_res_s / (fmax(w.nAx_s, w.nz_s) + DIVISION_TOL);
-            double dr = w.dua_res_s / (fmax(fmax(w.nq_s, w.nAty_s), w.nPx_s) + DIVISION_TOL);
+            double pr = w.r.pri_res_s / (fmax(w.r.nAx_s, w.r.nz_s) + DIVISION_TOL);
+            double dr = w.r.dua_res_s / (fmax(fmax(w.r.nq_s, w.r.nAty_s), w.r.nPx_s) + DIVISION_TOL);
             double rn = w.rho * sqrt(pr / (dr + DIVISION_TOL));
             rn = fmin(fmax(rn, RHO_MIN), RHO_MAX);
             if (rn > w.rho * s->adaptive_rho_tolerance || rn < w.rho / s->adaptive_rho_tolerance) {
@@ -1366,6 +1506,224 @@ int oracle_qpik_one(const OracleModel* m, const OracleParams* p, const double* q
         diag->polished = pol;
     }
     return st;
+}
+
+/* ------------------------------------------------------------------------ */
+/* controller entry: QPID / QPIDStep / QPIDCubic                            */
+/* ------------------------------------------------------------------------ */
+void oracle_default_qpid_params(int kind, OracleParams* p, int exact) {
+    oracle_default_params(kind, p, exact);
+    for (int i = 0; i < 6; ++i) {
+        p->kp[i] = kind == 0 ? 100 : 400;   /* robot_controller.cpp:12-13 / MoMa :15-16 */
+        p->kv[i] = kind == 0 ? 20 : 40;     /* MoMa QPIDStep uses Kv (:230)            */
+    }
+    p->w_reg = 0;                           /* QP_ID.cpp:102 regulariser commented out */
+    /* P = 2 J^T J is singular on null(J) (no regulariser) and the cost
+     * scaling (slack weight 1000) leaves eigenvalues of the scaled reduced KKT
+     * near OSQP's delta = 1e-6, where 3 refinement steps cannot certify at
+     * eps_exact: parity mode regularises the polish with delta = 1e-10 */
+    if (exact) p->solver.delta = 1e-10;
+}
+
+/* Manipulator::QPID (src/manipulator/QP_ID.cpp:7-193) and MobileManipulator::
+ * QPID (src/mobile_manipulator/QP_ID.cpp:7-184) through the controllers'
+ * QPID / QPIDStep / QPIDCubic (robot_controller.cpp:319-361; MoMa :199-250).
+ * M, g: the (actuated, for MoMa) mass matrix and gravity the QP's equality
+ * rows use (getMassMatrix / getGravity, or the *Actuated getters), row-major
+ * na x na and na; g_full: the full joint-order gravity (MoMa failure path,
+ * robot_controller.cpp:211,218 — the reference slices the joint-order vector
+ * at actuator offsets; restated as written).  Outputs qdd[na], tau[na]:
+ * non-Solved -> qdd = 0, tau = g (manipulator :335) / g_full[0..na) (MoMa). */
+int oracle_qpid_one(const OracleModel* m, const OracleParams* p, const double* q, const double* qdot,
+                    const double* x_target, const double* xdot_target, const double* x_init,
+                    const double* xdot_init, const double* Mq, const double* gq, const double* g_full,
+                    double* qdd, double* tau, OracleDiag* diag) {
+    int nv = m->nv;
+    Kin k;
+    kin_fk(m, q, &k);
+    double J[6 * ORC_MAXJ];
+    point_jacobian(m, &k, m->ee_joint, k.pe, J);
+    int moma = m->kind == 1;
+    int na = moma ? m->n_wheel + m->n_arm : nv;
+    double S[ORC_MAXJ * ORC_MAXJ];
+    double eta[ORC_MAXJ], v[ORC_MAXJ];   /* eta = qdot_actuated, v = S eta */
+    if (moma) {
+        memset(S, 0, sizeof(double) * nv * na);
+        for (int i = 0; i < m->n_arm; ++i) S[(m->mani_start + i) * na + m->act_mani_start + i] = 1;
+        for (int i = 0; i < m->n_wheel; ++i) S[(m->mobi_start + i) * na + m->act_mobi_start + i] = 1;
+        double yaw = q[m->virtual_start + 2], cy = cos(yaw), sy = sin(yaw);
+        double Rz[9] = {cy, -sy, 0, sy, cy, 0, 0, 0, 1};
+        for (int r = 0; r < 3; ++r)
+            for (int wc = 0; wc < m->n_wheel; ++wc) {
+                double t = 0;
+                for (int c = 0; c < 3; ++c) t += Rz[3 * r + c] * m->J_mobile[c][wc];
+                S[(m->virtual_start + r) * na + m->act_mobi_start + wc] = t;
+            }
+        for (int i = 0; i < m->n_arm; ++i) eta[m->act_mani_start + i] = qdot[m->mani_start + i];
+        for (int i = 0; i < m->n_wheel; ++i) eta[m->act_mobi_start + i] = qdot[m->mobi_start + i];
+        for (int j = 0; j < nv; ++j) { double t = 0; for (int a = 0; a < na; ++a) t += S[j * na + a] * eta[a]; v[j] = t; }
+    } else {
+        memcpy(v, qdot, nv * sizeof(double));
+    }
+    /* desired task acceleration */
+    double xdd[6];
+    if (p->mode == 0) memcpy(xdd, xdot_target, sizeof(xdd));   /* QPID(xddot_target) */
+    else {
+        double xt[12], xdt[6];
+        if (p->mode == 2) task_space_cubic(x_target, xdot_target, x_init, xdot_init, p->t, p->t0, p->duration, xt, xdt);
+        else { memcpy(xt, x_target, sizeof(xt)); memcpy(xdt, xdot_target, sizeof(xdt)); }
+        double Rt[9], pt[3], xd[6], e[6], phi[3] = {0, 0, 0};
+        pose_unpack(xt, Rt, pt);
+        for (int i = 0; i < 6; ++i) { double t = 0; for (int c = 0; c < nv; ++c) t += J[i * nv + c] * qdot[c]; xd[i] = t; }
+        for (int i = 0; i < 3; ++i) e[i] = pt[i] - k.pe[i];
+        for (int i = 0; i < 3; ++i) {
+            double a[3] = {Rt[i], Rt[3 + i], Rt[6 + i]}, b[3] = {k.Te[i], k.Te[3 + i], k.Te[6 + i]}, c[3];
+            cross3(a, b, c);
+            phi[0] += c[0]; phi[1] += c[1]; phi[2] += c[2];
+        }
+        for (int i = 0; i < 3; ++i) e[3 + i] = -0.5 * phi[i];
+        /* QPIDStep: Kp e + Kv (xdot_target - xdot) (robot_controller.cpp:347; MoMa :230) */
+        for (int i = 0; i < 6; ++i) xdd[i] = p->kp[i] * e[i] + p->kv[i] * (xdt[i] - xd[i]);
+    }
+    /* Jdot (frame, full qdot) and its product with S eta / qdot */
+    double Jd[6 * ORC_MAXJ], bias[6];
+    point_jacobian_dot(m, &k, m->ee_joint, k.pe, qdot, ORC_ALL_JOINTS, Jd);
+    for (int i = 0; i < 6; ++i) { double t = 0; for (int c = 0; c < nv; ++c) t += Jd[i * nv + c] * v[c]; bias[i] = t; }
+    /* manipulability (+grad, grad_dot) and min distance (+grad, grad_dot) */
+    int c0 = moma ? m->mani_start : 0, n = moma ? m->n_arm : nv;
+    double man, mgrad[ORC_MAXJ], mgd[ORC_MAXJ], dist, dgrad[ORC_MAXJ], dgd[ORC_MAXJ], wA[3], wB[3];
+    int pair;
+    manip(m, &k, J, c0, n, &man, mgrad);
+    manip_graddot(m, &k, J, c0, n, qdot, man, mgd);
+    min_distance_w(m, &k, &dist, dgrad, &pair, wA, wB);
+    mindist_graddot(m, &k, pair, wA, wB, qdot, dgd);
+    const double* qa = q + c0;      /* arm joint positions / velocities */
+    const double* qda = qdot + c0;
+    double man_gd = 0, dist_gd = 0, mg_qd = 0, dg_qd = 0;
+    for (int i = 0; i < n; ++i) {
+        man_gd += mgd[i] * qda[i];
+        dist_gd += dgd[c0 + i] * qda[i];
+        mg_qd += mgrad[i] * qda[i];
+        dg_qd += dgrad[c0 + i] * qda[i];
+    }
+    /* task Jacobian over the QP's task variables */
+    double Jt[6 * ORC_MAXJ];
+    if (moma) {
+        for (int r = 0; r < 6; ++r)
+            for (int c = 0; c < na; ++c) { double t = 0; for (int j = 0; j < nv; ++j) t += J[r * nv + j] * S[j * na + c]; Jt[r * na + c] = t; }
+    } else {
+        memcpy(Jt, J, 6 * nv * sizeof(double));
+    }
+    /* QP assembly */
+    static __thread double P[ORC_MAXX * ORC_MAXX], A[ORC_MAXC * ORC_MAXX];
+    double qv[ORC_MAXX], l[ORC_MAXC], u[ORC_MAXC];
+    const double a = p->alpha_cbf;
+    const int nb = moma ? 0 : 1;                    /* bound rows present (nbc = nx or 0) */
+    const int nx = moma ? 2 * na : 6 * n + 2;       /* QP_ID.cpp:48-56 / MoMa :22 */
+    const int nineq = 4 * n + 2, neq = na, nc = nb * nx + nineq + neq;
+    const int as = moma ? m->act_mani_start : 0;    /* QP column of arm joint 0 */
+    memset(P, 0, sizeof(double) * nx * nx);
+    memset(A, 0, sizeof(double) * nc * nx);
+    for (int i = 0; i < nx; ++i) qv[i] = 0;
+    for (int i = 0; i < na; ++i)
+        for (int j = 0; j < na; ++j) {
+            double t = 0;
+            for (int r = 0; r < 6; ++r) t += Jt[r * na + i] * Jt[r * na + j];
+            P[i * nx + j] = 2 * t + (i == j ? p->w_reg : 0);
+        }
+    for (int i = 0; i < na; ++i) { double t = 0; for (int r = 0; r < 6; ++r) t += Jt[r * na + i] * (xdd[r] - bias[r]); qv[i] = -2 * t; }
+    int row = 0;
+    if (nb) {   /* setBoundConstraint (QP_ID.cpp:112-120): slacks >= 0, the rest free */
+        for (int i = 0; i < nx; ++i) { A[i * nx + i] = 1; l[i] = i < 2 * n ? -INFTY : 0; u[i] = INFTY; }
+        for (int i = 2 * n; i < nx; ++i) qv[i] = p->slack_w;
+        row = nx;
+    }
+    double* G = A + row * nx;
+    double* lg = l + row;
+    double* ug = u + row;
+    for (int i = 0; i < nineq; ++i) ug[i] = INFTY;
+    for (int i = 0; i < n; ++i) {
+        const int j = c0 + i;
+        G[i * nx + as + i] = 1;               lg[i] = -2 * a * qda[i] - a * a * (qa[i] - m->lower[j]);
+        G[(n + i) * nx + as + i] = -1;        lg[n + i] = 2 * a * qda[i] - a * a * (m->upper[j] - qa[i]);
+        G[(2 * n + i) * nx + as + i] = 1;     lg[2 * n + i] = -a * (qda[i] + m->vel[j]);
+        G[(3 * n + i) * nx + as + i] = -1;    lg[3 * n + i] = -a * (m->vel[j] - qda[i]);
+        if (!moma) {
+            G[i * nx + 2 * n + i] = 1; G[(n + i) * nx + 3 * n + i] = 1;
+            G[(2 * n + i) * nx + 4 * n + i] = 1; G[(3 * n + i) * nx + 5 * n + i] = 1;
+        }
+    }
+    for (int c = 0; c < n; ++c) { G[(4 * n) * nx + as + c] = mgrad[c]; G[(4 * n + 1) * nx + as + c] = dgrad[c0 + c]; }
+    if (!moma) { G[(4 * n) * nx + 6 * n] = 1; G[(4 * n + 1) * nx + 6 * n + 1] = 1; }
+    lg[4 * n] = -man_gd - 2 * a * mg_qd - a * a * (man - p->man_min);
+    lg[4 * n + 1] = -dist_gd - 2 * a * dg_qd - a * a * (dist - p->dist_min);
+    /* setEqConstraint: [M -I][qdd; tau] = -g (QP_ID.cpp:176-192) */
+    double* Ge = G + nineq * nx;
+    for (int i = 0; i < na; ++i) {
+        for (int j = 0; j < na; ++j) Ge[i * nx + j] = Mq[i * na + j];
+        Ge[i * nx + na + i] = -1;
+        lg[nineq + i] = ug[nineq + i] = -gq[i];
+    }
+    double x[ORC_MAXX], y[ORC_MAXC];
+    int iters = 0, pol = 0;
+    int st = oracle_solve_qp(nx, nc, P, qv, A, l, u, &p->solver, x, y, &iters, &pol);
+    for (int i = 0; i < na; ++i) {
+        qdd[i] = st == ORC_SOLVED ? x[i] : 0.0;
+        tau[i] = st == ORC_SOLVED ? x[na + i] : (moma ? g_full[i] : gq[i]);
+    }
+    if (diag) {
+        for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) diag->pose[3 * r + c] = k.Te[3 * r + c];
+        memcpy(diag->pose + 9, k.pe, 3 * sizeof(double));
+        memcpy(diag->J, J, 6 * nv * sizeof(double));
+        memcpy(diag->xdot_des, xdd, sizeof(xdd));
+        diag->man = man;
+        memcpy(diag->man_grad, mgrad, n * sizeof(double));
+        diag->dist = dist;
+        memcpy(diag->dist_grad, dgrad, nv * sizeof(double));
+        diag->pair = pair;
+        diag->iters = iters;
+        diag->polished = pol;
+        memcpy(diag->jdot_v, bias, sizeof(bias));
+        memcpy(diag->man_graddot, mgd, n * sizeof(double));
+        memcpy(diag->dist_graddot, dgd, nv * sizeof(double));
+        diag->man_gd = man_gd;
+        diag->dist_gd = dist_gd;
+        memcpy(diag->Jdot, Jd, 6 * nv * sizeof(double));
+    }
+    return st;
+}
+
+/* stage helper: frame Jacobian time variation (getJacobianTimeVariation,
+ * robot_data.cpp:404-417) and the QPID grad_dot vectors at (q, qdot) */
+void oracle_qpid_stages(const OracleModel* m, const double* q, const double* qdot, double* Jdot,
+                        double* man_graddot, double* dist_graddot) {
+    Kin k;
+    kin_fk(m, q, &k);
+    double J[6 * ORC_MAXJ], man, mg[ORC_MAXJ], dist, dg[ORC_MAXJ], wA[3], wB[3];
+    int pair, c0 = m->kind == 1 ? m->mani_start : 0, n = m->kind == 1 ? m->n_arm : m->nv;
+    point_jacobian(m, &k, m->ee_joint, k.pe, J);
+    point_jacobian_dot(m, &k, m->ee_joint, k.pe, qdot, ORC_ALL_JOINTS, Jdot);
+    manip(m, &k, J, c0, n, &man, mg);
+    manip_graddot(m, &k, J, c0, n, qdot, man, man_graddot);
+    min_distance_w(m, &k, &dist, dg, &pair, wA, wB);
+    mindist_graddot(m, &k, pair, wA, wB, qdot, dist_graddot);
+}
+
+/* joint-frame Jacobian time variation of joint jid at a world point p moving
+ * rigidly with that joint's body (for finite-difference tests) */
+void oracle_point_jacobian_dot(const OracleModel* m, const double* q, const double* qdot, int jid,
+                               const double* p, double* J, double* Jdot) {
+    Kin k;
+    kin_fk(m, q, &k);
+    if (J) point_jacobian(m, &k, jid, p, J);
+    if (Jdot) point_jacobian_dot(m, &k, jid, p, qdot, ORC_ALL_JOINTS, Jdot);
+}
+
+/* joint placement (oMi, R row-major + p) for the tests */
+void oracle_joint_placement(const OracleModel* m, const double* q, int jid, double* T12) {
+    Kin k;
+    kin_fk(m, q, &k);
+    memcpy(T12, k.T[jid], 12 * sizeof(double));
 }
 
 /* ------------------------------------------------------------------------ */

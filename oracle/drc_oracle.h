@@ -31,8 +31,8 @@
 #define ORC_MAXJ 32
 #define ORC_MAXG 96
 #define ORC_MAXP 1024
-#define ORC_MAXX 32
-#define ORC_MAXC 64
+#define ORC_MAXX 64
+#define ORC_MAXC 128
 
 typedef struct OracleModel {
     int nv;                          /* number of 1-DoF joints              */
@@ -89,6 +89,12 @@ typedef struct OracleDiag {
     int pair;
     int iters;
     int polished;
+    /* QPID stage data (oracle_qpid_one) */
+    double jdot_v[6];                /* Jdot * qdot (MoMa: Jdot * S * eta)  */
+    double man_graddot[ORC_MAXJ];    /* getManipulability grad_dot (arm)    */
+    double dist_graddot[ORC_MAXJ];   /* getMinDistance grad_dot (full dof)  */
+    double man_gd, dist_gd;          /* grad_dot . qdot_arm used in the rows */
+    double Jdot[6 * ORC_MAXJ];       /* frame Jacobian time variation        */
 } OracleDiag;
 
 enum { ORC_SOLVED = 1, ORC_MAX_ITER = -2, ORC_PRIMAL_INFEASIBLE = -3, ORC_NONFINITE = -10 };
@@ -113,6 +119,21 @@ int64_t oracle_qpik_batch(const OracleModel* m, const OracleParams* p, int64_t B
                           const double* x_target, const double* xdot_target,
                           const double* x_init, const double* xdot_init,
                           double* out, int32_t* status, int32_t* iters, int nthreads);
+
+/* QPID / QPIDStep / QPIDCubic for one instance (mode 0 takes the task
+ * acceleration in xdot_target).  M, g: na x na (row-major) and na, the
+ * matrices of the QP's equality rows (MoMa: S^T M S, S^T g); g_full: full
+ * joint-order gravity (MoMa failure path).  Outputs qdd[na], tau[na]. */
+void oracle_default_qpid_params(int kind, OracleParams* p, int exact);
+int oracle_qpid_one(const OracleModel* m, const OracleParams* p, const double* q, const double* qdot,
+                    const double* x_target, const double* xdot_target, const double* x_init,
+                    const double* xdot_init, const double* M, const double* g, const double* g_full,
+                    double* qdd, double* tau, OracleDiag* diag);
+void oracle_qpid_stages(const OracleModel* m, const double* q, const double* qdot, double* Jdot,
+                        double* man_graddot, double* dist_graddot);
+void oracle_point_jacobian_dot(const OracleModel* m, const double* q, const double* qdot, int jid,
+                               const double* p, double* J, double* Jdot);
+void oracle_joint_placement(const OracleModel* m, const double* q, int jid, double* T12);
 
 /* stage helpers exposed for tests */
 void oracle_fk_pose(const OracleModel* m, const double* q, double* pose12, double* J6xn);

@@ -88,6 +88,10 @@ class OracleDiag(C.Structure):
         ("man", C.c_double), ("man_grad", C.c_double * MAXJ),
         ("dist", C.c_double), ("dist_grad", C.c_double * MAXJ),
         ("pair", C.c_int), ("iters", C.c_int), ("polished", C.c_int),
+        ("jdot_v", C.c_double * 6),
+        ("man_graddot", C.c_double * MAXJ), ("dist_graddot", C.c_double * MAXJ),
+        ("man_gd", C.c_double), ("dist_gd", C.c_double),
+        ("Jdot", C.c_double * (6 * MAXJ)),
     ]
 
 
@@ -275,3 +279,65 @@ def solve_qp(P, qv, A, l, u, settings):
     st = lib().oracle_solve_qp(C.c_int(n), C.c_int(m), *[_ptr(a) for a in arrs], C.byref(settings),
                                _ptr(x), _ptr(y), C.byref(it), C.byref(pol))
     return st, x, y, it.value, pol.value
+
+
+# ---------------------------------------------------------------------------
+# QPID (torque-level QP) — manipulator/QP_ID.cpp, mobile_manipulator/QP_ID.cpp
+# ---------------------------------------------------------------------------
+def default_qpid_params(kind, exact=True):
+    p = OracleParams()
+    lib().oracle_default_qpid_params(C.c_int(kind), C.byref(p), C.c_int(1 if exact else 0))
+    return p
+
+
+def qpid_dynamics(pm, om, spec, q, qdot):
+    """(M, g, g_full) the QPID equality rows use, from the numpy restatement
+    (pyref.dynamics): manipulator M, g; MoMa S^T M S, S^T g and the full g."""
+    import pyref
+    d = pyref.dynamics(pm, q, qdot)
+    if om.kind == 0:
+        return d["M"], d["g"], d["g"]
+    Jm = np.array([[om.J_mobile[r][c] for c in range(om.n_wheel)] for r in range(3)])
+    S = pyref.selection_matrix(om.nv, om.n_arm, om.n_wheel, (om.virtual_start, om.mani_start, om.mobi_start),
+                               (om.act_mani_start, om.act_mobi_start), Jm, q[om.virtual_start + 2])
+    return S.T @ d["M"] @ S, S.T @ d["g"], d["g"]
+
+
+def qpid_one(om, params, q, qdot, M, g, g_full, x_target=None, xdot_target=None, x_init=None, xdot_init=None):
+    na = om.n_wheel + om.n_arm if om.kind == 1 else om.nv
+    f = lambda a, n: np.ascontiguousarray(a if a is not None else np.zeros(n), float)
+    q, qdot = f(q, om.nv), f(qdot, om.nv)
+    xt, xdt, xi, xdi = f(x_target, 12), f(xdot_target, 6), f(x_init, 12), f(xdot_init, 6)
+    M, g, gf = f(M, na * na), f(g, na), f(g_full, om.nv)
+    qdd, tau = np.zeros(na), np.zeros(na)
+    dg = OracleDiag()
+    st = lib().oracle_qpid_one(C.byref(om), C.byref(params), _ptr(q), _ptr(qdot), _ptr(xt), _ptr(xdt), _ptr(xi),
+                               _ptr(xdi), _ptr(M), _ptr(g), _ptr(gf), _ptr(qdd), _ptr(tau), C.byref(dg))
+    return st, qdd, tau, dg
+
+
+def qpid_stages(om, q, qdot):
+    """(Jdot 6 x nv, manipulability grad_dot, min-distance grad_dot)."""
+    nv = om.nv
+    n = om.n_arm if om.kind == 1 else nv
+    Jd, mgd, dgd = np.zeros(6 * nv), np.zeros(n), np.zeros(nv)
+    lib().oracle_qpid_stages(C.byref(om), _ptr(np.ascontiguousarray(q, float)), _ptr(np.ascontiguousarray(qdot, float)),
+                             _ptr(Jd), _ptr(mgd), _ptr(dgd))
+    return Jd.reshape(6, nv), mgd, dgd
+
+
+def point_jacobian_dot(om, q, qdot, jid, p):
+    J, Jd = np.zeros(6 * om.nv), np.zeros(6 * om.nv)
+    lib().oracle_point_jacobian_dot(C.byref(om), _ptr(np.ascontiguousarray(q, float)),
+                                    _ptr(np.ascontiguousarray(qdot, float)), C.c_int(jid),
+                                    _ptr(np.ascontiguousarray(p, float)), _ptr(J), _ptr(Jd))
+    return J.reshape(6, om.nv), Jd.reshape(6, om.nv)
+
+
+def joint_placement(om, q, jid):
+    T = np.zeros(12)
+    lib().oracle_joint_placement(C.byref(om), _ptr(np.ascontiguousarray(q, float)), C.c_int(jid), _ptr(T))
+    out = np.eye(4)
+    out[:3, :3] = T[:9].reshape(3, 3)
+    out[:3, 3] = T[9:]
+    return out

@@ -632,6 +632,57 @@ def build_qp_moma(m, q, S, xdot_des, link, mani_start_j, mani_start_a, n_arm, ma
     return P, qv, A, l, u
 
 
+def build_qp_qpid(m, q, qd, Jt, xdd, jdot_v, M, g, man, dist, arm, arm_col, slacks):
+    """QPID's QP (manipulator/QP_ID.cpp:85-192 with slacks; MoMa QP_ID.cpp:
+    66-184 without).  Jt: 6 x na task Jacobian over the QP's task variables,
+    jdot_v: its time variation times the actuated velocity, man/dist:
+    (value, grad[arm], graddot . qdot_arm), arm: joint ids (0-based) of the
+    arm, arm_col: QP column of arm joint 0."""
+    na = Jt.shape[1]
+    n = len(arm)
+    nx = 2 * na + (4 * n + 2 if slacks else 0)
+    P = np.zeros((nx, nx))
+    qv = np.zeros(nx)
+    P[:na, :na] = 2.0 * Jt.T @ Jt
+    qv[:na] = -2.0 * Jt.T @ (xdd - jdot_v)
+    if slacks:
+        qv[2 * na:] = 1000.0
+    nineq = 4 * n + 2
+    G = np.zeros((nineq, nx))
+    lg = np.zeros(nineq)
+    qa, qda = q[arm], qd[arm]
+    lo, hi, vm = m.lower[arm], m.upper[arm], m.vel[arm]
+    a = ALPHA
+    for i in range(n):
+        c = arm_col + i
+        G[i, c] = 1.0; lg[i] = -2 * a * qda[i] - a * a * (qa[i] - lo[i])
+        G[n + i, c] = -1.0; lg[n + i] = 2 * a * qda[i] - a * a * (hi[i] - qa[i])
+        G[2 * n + i, c] = 1.0; lg[2 * n + i] = -a * (qda[i] + vm[i])
+        G[3 * n + i, c] = -1.0; lg[3 * n + i] = -a * (vm[i] - qda[i])
+        if slacks:
+            for k in range(4):
+                G[k * n + i, 2 * na + k * n + i] = 1.0
+    mval, mgrad, mgd = man
+    dval, dgrad, dgd = dist
+    G[4 * n, arm_col:arm_col + n] = mgrad
+    lg[4 * n] = -mgd - 2 * a * mgrad @ qda - a * a * (mval - 0.01)
+    G[4 * n + 1, arm_col:arm_col + n] = dgrad
+    lg[4 * n + 1] = -dgd - 2 * a * dgrad @ qda - a * a * (dval - 0.05)
+    if slacks:
+        G[4 * n, 2 * na + 4 * n] = 1.0
+        G[4 * n + 1, 2 * na + 4 * n + 1] = 1.0
+    Ge = np.zeros((na, nx))
+    Ge[:, :na] = M
+    Ge[:, na:2 * na] = -np.eye(na)
+    rows = [G, Ge]
+    l = [lg, -g]
+    u = [np.full(nineq, OSQP_INFTY), -g]
+    if slacks:
+        lb = np.concatenate([np.full(2 * na, -OSQP_INFTY), np.zeros(nx - 2 * na)])
+        rows.insert(0, np.eye(nx)); l.insert(0, lb); u.insert(0, np.full(nx, OSQP_INFTY))
+    return P, qv, np.vstack(rows), np.concatenate(l), np.concatenate(u)
+
+
 # ----------------------------------------------------------------------------
 # Exact QP solution (independent of the ADMM restatement): primal-dual
 # interior point + active-set refinement + KKT certificate.
