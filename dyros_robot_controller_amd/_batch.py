@@ -60,6 +60,48 @@ def qpik_batch(model, params, q, qdot, x_target=None, xdot_target=None, x_init=N
     return out, status
 
 
+def qpid_batch(model, params, q, qdot, x_target=None, xdot_target=None, x_init=None, xdot_init=None,
+               qddot=None, tau=None, status=None, iters=None, stream=None):
+    """Launch ``drc_qpid_batch``: returns (qddot [na][B],
+    tau [na][B], status [B]) device tensors."""
+    torch = _torch()
+    dev = q.device
+    B = q.shape[1]
+    check_shapes(model.dof, B, q=q, qdot=qdot, x_target=x_target, xdot_target=xdot_target,
+                 x_init=x_init, xdot_init=xdot_init)
+    na = model.actuated_dof
+    if qddot is None:
+        qddot = torch.empty((na, B), dtype=torch.float64, device=dev)
+    if tau is None:
+        tau = torch.empty((na, B), dtype=torch.float64, device=dev)
+    if status is None:
+        status = torch.empty(B, dtype=torch.int32, device=dev)
+    if stream is None:
+        stream = torch.cuda.current_stream(dev).cuda_stream
+    _capi.check(_capi.lib().drc_qpid_batch(
+        model.handle, C.byref(params), C.c_int64(B), _ptr(q), _ptr(qdot), _ptr(x_target), _ptr(xdot_target),
+        _ptr(x_init), _ptr(xdot_init), _ptr(qddot), _ptr(tau), _ptr(status), _ptr(iters), C.c_void_p(stream)))
+    return qddot, tau, status
+
+
+def qpid_stages_batch(model, params, q, qdot, x_target=None, xdot_target=None, x_init=None, xdot_init=None):
+    """QPID stage outputs: the QPIK stage fields plus jdot [6*nv][B] and
+    qpid_terms [8][B] = (Jdot v, man grad_dot . qdot_arm, dist grad_dot . qdot_arm)."""
+    torch = _torch()
+    dev = q.device
+    B = q.shape[1]
+    nv = model.dof
+    f = lambda r: torch.zeros((r, B), dtype=torch.float64, device=dev)
+    pose, jac, man, dist, xdd, jdot, terms = f(12), f(6 * nv), f(1 + model.mani_dof), f(1 + nv), f(6), f(6 * nv), f(8)
+    pair = torch.zeros(B, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    _capi.check(_capi.lib().drc_qpid_stages_batch(
+        model.handle, C.byref(params), C.c_int64(B), _ptr(q), _ptr(qdot), _ptr(x_target), _ptr(xdot_target),
+        _ptr(x_init), _ptr(xdot_init), _ptr(pose), _ptr(jac), _ptr(man), _ptr(dist), _ptr(pair), _ptr(xdd),
+        _ptr(jdot), _ptr(terms), C.c_void_p(stream)))
+    return dict(pose=pose, jac=jac, man=man, dist=dist, pair=pair, xddot_des=xdd, jdot=jdot, qpid_terms=terms)
+
+
 def stages_batch(model, params, q, qdot, x_target=None, xdot_target=None, x_init=None, xdot_init=None):
     """Stage outputs (pose, J, manipulability, min distance, task velocity)."""
     torch = _torch()

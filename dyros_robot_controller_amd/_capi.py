@@ -27,6 +27,7 @@ STATUS_PRIMAL_INFEASIBLE = -3
 STATUS_NONFINITE = -10
 # modes
 MODE_QPIK, MODE_QPIK_STEP, MODE_QPIK_CUBIC = 0, 1, 2
+MODE_QPID, MODE_QPID_STEP, MODE_QPID_CUBIC = 0, 1, 2
 # drive types
 DRIVE_DIFFERENTIAL, DRIVE_MECANUM, DRIVE_CASTER = 0, 1, 2
 MAX_WHEELS = 8
@@ -38,6 +39,7 @@ EXPORTED_SYMBOLS = (
     "drc_default_qpik_params", "drc_qpik_batch", "drc_qpik_stages_batch", "drc_debug_kernel_timing",
     "drc_debug_kernel_times", "drc_set_concurrency", "drc_qpik_host", "drc_qpik_stages_host",
     "drc_dynamics_batch", "drc_dynamics_host", "drc_joint_torque_step_batch", "drc_joint_torque_step_host",
+    "drc_default_qpid_params", "drc_qpid_batch", "drc_qpid_stages_batch", "drc_qpid_host",
     "drc_error_string", "drc_last_error",
 )
 
@@ -132,6 +134,11 @@ def _load():
     lib.drc_dynamics_host.argtypes = [vp, C.c_int, C.c_int64, dp, dp, dp, dp, dp, dp, dp]
     lib.drc_joint_torque_step_batch.argtypes = [vp, C.c_int64, vp, vp, vp, vp, vp, C.c_double, dp, dp, vp, vp]
     lib.drc_joint_torque_step_host.argtypes = [vp, C.c_int64, dp, dp, dp, dp, dp, C.c_double, dp, dp, dp]
+    lib.drc_default_qpid_params.argtypes = [vp, C.c_int, C.POINTER(QPIKParams)]
+    lib.drc_qpid_batch.argtypes = [vp, C.POINTER(QPIKParams), C.c_int64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    lib.drc_qpid_stages_batch.argtypes = [vp, C.POINTER(QPIKParams), C.c_int64, vp, vp, vp, vp, vp, vp,
+                                          vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    lib.drc_qpid_host.argtypes = [vp, C.POINTER(QPIKParams), C.c_int64, dp, dp, dp, dp, dp, dp, dp, dp, ip, ip]
     for name in EXPORTED_SYMBOLS:
         if name not in ("drc_model_destroy", "drc_error_string", "drc_last_error"):
             getattr(lib, name).restype = C.c_int

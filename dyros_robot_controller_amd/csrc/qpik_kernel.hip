@@ -40,12 +40,16 @@ struct KParams {
   int nv, nx, ng, np, na, m, narm, c0;
   int xcd_map;                         // XCD-aware instance order (grid % 8 == 0)
   int rJac, rMan, rDist, rXdd, rQ, rLen;  // per-instance task record (doubles)
+  int problem;                         // 0 QPIK, 1 QPID (torque-level QP)
+  int rQd, rBias, rMgd, rDgd;          // QPID extras of the task record
+  int nbuf;                            // polish work-vector stride (64, or 128 when nx + ng > 64)
   drc_solver_settings s;
   // persistent QP region
   int oP, oG, oQ, oAB, oL, oU, oD, oE, oRho, oX, oZ, oY, oDY, oXT, oZT, oT1, oT2, oRed, oSc;
   // union region (kinematics | K^-1 | polish)
   int oU0;
   int kT, kZ, kTe, kJ, kTg, kq, kqd, kA6, kAi, kW, kPart, kPd, kPf, kxdd, kmg, kdg, kJt, kSv, kScr, kEpa;
+  int kJd, kDa, kVf, kX6, kBias, kMq, kGq;  // QPID: Jdot, arm-only Jdot, S eta, 6x6 scratch, bias | M, g
   int lds_doubles;
 };
 
@@ -654,12 +658,13 @@ __device__ __forceinline__ bool eqp(const KParams& kp, double* S, int actb, int 
   double* U = S + kp.oU0;
   int* Fidx = reinterpret_cast<int*>(U);  // 64 ints
   int* Ridx = Fidx + 64;                   // 64 ints
+  const int nb = kp.nbuf;                   // >= N
   double* rhs = U + 64 + 64 + 128;         // [N]  (xx, yy live at U+64 / U+128)
-  double* sol = rhs + 64;
-  double* res = sol + 64;
-  double* vv = res + 64;
-  double* dg = vv + 64;
-  double* L = dg + 64;  // packed lower triangle N(N+1)/2
+  double* sol = rhs + nb;
+  double* res = sol + nb;
+  double* vv = res + nb;
+  double* dg = vv + nb;
+  double* L = dg + nb;  // packed lower triangle N(N+1)/2
   if (l < nx && actb == 0) Fidx[__popcll(freeMask & ((1ull << l) - 1))] = l;
   if (l < ng && actg != 0) Ridx[__popcll(rowMask & ((1ull << l) - 1))] = l;
   if (l < nx) xx[l] = actb == 0 ? 0.0 : (actb < 0 ? lo[l] : up[l]) / ab[l];
@@ -947,13 +952,198 @@ struct IO {
   int32_t* st_pair;
   double* rec;  // product path: per-instance task record [B][rec_stride] (coalesced)
   int64_t rec_stride;
+  // QPID: dynamics of the equality rows ([na*na][B], [na][B]; MoMa also the
+  // joint-order gravity [nv][B]), torque output, and the QPID stage outputs
+  const double *dM, *dG, *dGf;
+  double* out2;
+  double *st_jdot, *st_qpid;  // [6*nv][B] Jdot; [8][B] bias(6), man_gd, dist_gd
 };
+
+// ------------------------------------------------------------------------
+// QPID stage data.  Pinocchio's LOCAL_WORLD_ALIGNED
+// Jacobian time variation is d/dt of the LWA Jacobian (robot_data.cpp:109,
+// 414, 476-477).  Column c of the Jacobian of a point p carried by a body,
+// differentiated with the joint velocities restricted to `mask`:
+//   revolute c:  [zd x (p - o_c) + z_c x (pdot - od_c); zd],  zd = w_par(c) x z_c
+//   prismatic c: [zd; 0]
+// with w_par(c) the angular velocity of c's parent body and od_c the velocity
+// of c's origin.  One lane per column, O(nv) per lane.
+// ------------------------------------------------------------------------
+__device__ __forceinline__ void col_dot(const DevModel* M, const double* T, const double* Zw, const double* qd, int nv,
+                                        int c, V3 p, V3 pdot, uint32_t mask, V3* lin, V3* ang) {
+  const V3 oc = v3(T[12 * c + 9], T[12 * c + 10], T[12 * c + 11]), zc = ld3(Zw + 3 * c);
+  V3 w = v3(0, 0, 0), od = v3(0, 0, 0);
+  const uint32_t ac = M->anc[c] & mask;
+  for (int a = 1; a <= nv; ++a) {
+    if (!(ac & (1u << (a - 1)))) continue;
+    const V3 za = ld3(Zw + 3 * a);
+    if (M->jtype[a] == kRevolute) {
+      if (a != c) w = w + qd[a - 1] * za;
+      od = od + qd[a - 1] * cross(za, oc - v3(T[12 * a + 9], T[12 * a + 10], T[12 * a + 11]));
+    } else {
+      od = od + qd[a - 1] * za;
+    }
+  }
+  const V3 zd = cross(w, zc);
+  if (M->jtype[c] == kRevolute) {
+    *lin = cross(zd, p - oc) + cross(zc, pdot - od);
+    *ang = zd;
+  } else {
+    *lin = zd;
+    *ang = v3(0, 0, 0);
+  }
+}
+
+// velocity and angular velocity of the body of joint X (point p on it)
+__device__ __forceinline__ void body_velocity(const DevModel* M, const double* T, const double* Zw, const double* qd,
+                                              int nv, int X, V3 p, V3* v, V3* w) {
+  *v = v3(0, 0, 0);
+  *w = v3(0, 0, 0);
+  if (X <= 0) return;
+  const uint32_t ax = M->anc[X];
+  for (int a = 1; a <= nv; ++a) {
+    if (!(ax & (1u << (a - 1)))) continue;
+    const V3 za = ld3(Zw + 3 * a);
+    if (M->jtype[a] == kRevolute) {
+      *w = *w + qd[a - 1] * za;
+      *v = *v + qd[a - 1] * cross(za, p - v3(T[12 * a + 9], T[12 * a + 10], T[12 * a + 11]));
+    } else {
+      *v = *v + qd[a - 1] * za;
+    }
+  }
+}
+
+// Fills kBias = [Jdot v (6), man_gd, dist_gd] and kJd (6 x nv frame Jdot):
+//   v = qdot (manipulator) or S eta (MoMa, getJacobianActuatedTimeVariation *
+//       eta, mobile_manipulator/robot_data.cpp:412-415, Sdot neglected);
+//   man_gd  = getManipulability(true,true).grad_dot . qdot_arm, contracted:
+//       sum_i qdot_i dJ_i = Da (arm-only Jdot), so with W = Ja^T Ai
+//       man_gd = mdot tr(Da W) + m [tr(Da Jda^T Ai) - 2 tr((Da W)(Jda W))],
+//       mdot = m tr(Jda W)           (robot_data.cpp:555-569, MoMa :477-492);
+//   dist_gd = getMinDistance(..,true,..).grad_dot . qdot_arm
+//       = sum_{c in arm} qdot_c n.(JB_dot - JA_dot)[:, c]   (robot_data.cpp:496-512).
+__device__ __noinline__ void qpid_task_extras(const DevModel* M, const KParams& kp, double* S, double bestd,
+                                              int besti) {
+  const int l = lane_id(), nv = kp.nv, narm = kp.narm, c0 = kp.c0;
+  const double *T = S + kp.kT, *Zw = S + kp.kZ, *J = S + kp.kJ, *qd = S + kp.kqd, *Te = S + kp.kTe,
+               *red = S + kp.oRed, *W = S + kp.kW, *Ai = S + kp.kAi, *qv = S + kp.kq;
+  double *Jd = S + kp.kJd, *Da = S + kp.kDa, *vf = S + kp.kVf, *X = S + kp.kX6, *out = S + kp.kBias;
+  const uint32_t all = 0xffffffffu, arm = ((1u << narm) - 1) << c0;
+  const uint32_t anc_e = M->anc[kp.frame_joint];
+  const V3 pe = v3(Te[9], Te[10], Te[11]);
+  V3 ve = v3(0, 0, 0), va = v3(0, 0, 0);  // frame-point velocity: full / arm joints only
+  for (int c = 0; c < nv; ++c) {
+    const V3 jc = v3(J[c], J[nv + c], J[2 * nv + c]);
+    ve = ve + qd[c] * jc;
+    if (arm & (1u << c)) va = va + qd[c] * jc;
+  }
+  double dsum = 0;
+  if (l < nv) {
+    const int j = l + 1;
+    V3 lin = v3(0, 0, 0), ang = v3(0, 0, 0), lina = v3(0, 0, 0), anga = v3(0, 0, 0);
+    if (anc_e & (1u << l)) {
+      col_dot(M, T, Zw, qd, nv, j, pe, ve, all, &lin, &ang);
+      if (arm & (1u << l)) col_dot(M, T, Zw, qd, nv, j, pe, va, arm, &lina, &anga);
+    }
+    Jd[0 * nv + l] = lin.x; Jd[1 * nv + l] = lin.y; Jd[2 * nv + l] = lin.z;
+    Jd[3 * nv + l] = ang.x; Jd[4 * nv + l] = ang.y; Jd[5 * nv + l] = ang.z;
+    if (arm & (1u << l)) {
+      const int c = l - c0;
+      Da[0 * narm + c] = lina.x; Da[1 * narm + c] = lina.y; Da[2 * narm + c] = lina.z;
+      Da[3 * narm + c] = anga.x; Da[4 * narm + c] = anga.y; Da[5 * narm + c] = anga.z;
+    }
+    // actuated velocity mapped to the joints: S eta (MoMa robot_data.cpp:115-120)
+    double v = qd[l];
+    if (M->kind == 1 && l >= M->virtual_start && l < M->virtual_start + 3) {
+      const int r = l - M->virtual_start;
+      const double yaw = qv[M->virtual_start + 2], cy = cos(yaw), sy = sin(yaw);
+      v = 0;
+      for (int w = 0; w < M->n_wheel; ++w) {
+        const double j0 = M->J_mobile[0][w], j1 = M->J_mobile[1][w], j2 = M->J_mobile[2][w];
+        const double sw = r == 0 ? cy * j0 - sy * j1 : (r == 1 ? sy * j0 + cy * j1 : j2);
+        v += sw * qd[M->mobi_start + w];
+      }
+    }
+    vf[l] = v;
+    // self-collision grad_dot term of this column
+    if (besti < M->npairs && (arm & (1u << l))) {
+      const V3 pA = ld3(red), pB = ld3(red + 3);
+      V3 n = pB - pA;
+      n = (1.0 / sqrt(dot(n, n))) * n;
+      V3 jdx[2];
+      for (int s_ = 0; s_ < 2; ++s_) {
+        const int jX = M->gparent[s_ == 0 ? M->pair_a[besti] : M->pair_b[besti]];
+        jdx[s_] = v3(0, 0, 0);
+        if (jX <= 0 || !(M->anc[jX] & (1u << l))) continue;
+        const V3 oX = v3(T[12 * jX + 9], T[12 * jX + 10], T[12 * jX + 11]);
+        const V3 pX = s_ == 0 ? pA : pB, zj = ld3(Zw + 3 * j);
+        V3 cl, ca;  // column of the joint Jacobian of jX at oX
+        if (M->jtype[j] == kRevolute) {
+          cl = cross(zj, oX - v3(T[12 * j + 9], T[12 * j + 10], T[12 * j + 11]));
+          ca = zj;
+        } else {
+          cl = zj;
+          ca = v3(0, 0, 0);
+        }
+        V3 vX, wX, ld, ad;
+        body_velocity(M, T, Zw, qd, nv, jX, oX, &vX, &wX);
+        col_dot(M, T, Zw, qd, nv, j, oX, vX, all, &ld, &ad);
+        const V3 r = pX - oX, rd = cross(wX, r);
+        jdx[s_] = ld - (cross(rd, ca) + cross(r, ad));
+      }
+      dsum = qd[l] * dot(n, jdx[1] - jdx[0]);
+    }
+  }
+  const double dist_gd = wave_sum(dsum);
+  (void)bestd;
+  wsync();
+  // 6x6 products for the manipulability term (lanes (a, b))
+  double t1 = 0, t2 = 0, t3 = 0;
+  if (l < 36) {
+    const int a = l / 6, b = l % 6;
+    double x1 = 0, x2 = 0, x3 = 0;
+    for (int c = 0; c < narm; ++c) {
+      const double dac = Da[a * narm + c], jac = Jd[a * nv + c0 + c];
+      x1 += dac * W[c * 6 + b];
+      x2 += jac * W[c * 6 + b];
+      x3 += dac * Jd[b * nv + c0 + c];
+    }
+    X[l] = x1;
+    X[36 + l] = x2;
+    if (a == b) {
+      t1 = x2;
+      t2 = x1;
+    }
+    t3 = x3 * Ai[b * 6 + a];
+  }
+  wsync();
+  double t4 = 0;
+  if (l < 36) t4 = X[l] * X[36 + (l % 6) * 6 + l / 6];
+  t1 = wave_sum(t1);
+  t2 = wave_sum(t2);
+  t3 = wave_sum(t3);
+  t4 = wave_sum(t4);
+  const double m = S[kp.oSc + SC_MAN], mdot = m * t1;
+  if (l < 6) {
+    double s = 0;
+    for (int c = 0; c < nv; ++c) s += Jd[l * nv + c] * vf[c];
+    out[l] = s;
+  }
+  if (l == 0) {
+    out[6] = mdot * t2 + m * (t3 - 2.0 * t4);
+    out[7] = dist_gd;
+  }
+  wsync();
+}
 
 // Occupancy target of the task kernel (waves per SIMD): the lane-serial
 // narrow phase and task-velocity code would otherwise take all 512 registers.
 #ifndef DRC_TASK_WAVES
 #define DRC_TASK_WAVES 2
 #endif
+// PROBLEM 0: QPIK stage data; 1: also the QPID extras (a separate
+// instantiation, so the QPIK kernel carries no call frame for them)
+template <int PROBLEM>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRC_TASK_WAVES, 8))) task_kernel(const DevModel* __restrict__ M0, const KParams kp, const IO io) {
   extern __shared__ __attribute__((aligned(16))) double S[];
   const int l = lane_id();
@@ -1413,6 +1603,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRC_TAS
       dgv[l] = g;
     }
     wsync();
+    if constexpr (PROBLEM == 1) qpid_task_extras(M, kp, S, bestd, besti);
     PH(7);
 #ifdef DRC_PHASE_TIMING
     if (l == 0) {  // straggler census: max instance cycles, count above 2M
@@ -1441,7 +1632,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRC_TAS
         else if (e == kp.rDist) v = bestd;
         else if (e < kp.rXdd) v = dgv[e - kp.rDist - 1];
         else if (e < kp.rQ) v = xdd[e - kp.rXdd];
-        else v = qv[e - kp.rQ];
+        else if (PROBLEM == 0 || e < kp.rQd) v = qv[e - kp.rQ];
+        else if (e < kp.rBias) v = qd[e - kp.rQd];
+        else v = S[kp.kBias + e - kp.rBias];  // QPID: Jdot v (6), man_gd, dist_gd
         rec[e] = v;
       }
     } else {  // stage outputs, [field][B]
@@ -1462,6 +1655,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRC_TAS
       }
       if (io.st_pair && l == 0) io.st_pair[gb] = besti < M->npairs ? besti : -1;
       if (io.st_xdd && l < 6) io.st_xdd[l * LD + gb] = xdd[l];
+      if constexpr (PROBLEM == 1) {
+        if (io.st_jdot)
+          for (int e = l; e < 6 * nv; e += 64) io.st_jdot[(int64_t)e * LD + gb] = S[kp.kJd + e];
+        if (io.st_qpid && l < 8) io.st_qpid[l * LD + gb] = S[kp.kBias + l];
+      }
     }
     wsync();
   }
@@ -2044,6 +2242,181 @@ qp_kernel(const DevModel* __restrict__ M0, const KParams kp, const IO io) {
   PH_FLUSH(16);
 }
 
+// ------------------------------------------------------------------------
+// QPID: the torque-level QP.
+//   manipulator  (src/manipulator/QP_ID.cpp:7-193):
+//     x = [qdd(n) | tau(n) | s_qmin | s_qmax | s_qdmin | s_qdmax (n each) | s_sing | s_col]
+//     P[qdd,qdd] = 2 J^T J, q[qdd] = -2 J^T (xdd - Jdot qdot), q[slacks] = 1000
+//     bounds: slacks >= 0, the rest free
+//   mobile manipulator (src/mobile_manipulator/QP_ID.cpp:7-184):
+//     x = [eta_dot(A) | tau(A)], P = 2 J~^T J~, q = -2 J~^T (xdd - J~dot eta), no bound rows
+//   rows (arm joints i, alpha = 50):
+//     qdd_i (+s) >= -2a qdot_i - a^2 (q_i - q_min)     -qdd_i (+s) >= 2a qdot_i - a^2 (q_max - q_i)
+//     qdd_i (+s) >= -a (qdot_i - qdot_min)             -qdd_i (+s) >= -a (qdot_max - qdot_i)
+//     grad_m . qdd (+s) >= -gd_m - 2a grad_m . qdot - a^2 (m - 0.01)
+//     grad_d . qdd (+s) >= -gd_d - 2a grad_d . qdot - a^2 (d - 0.05)
+//     [M -I] [qdd; tau] = -g                           (equality rows)
+// Runs the generic (runtime-sized, LDS) OSQP path: nx = 6n+2 / 2A, ng = 4n+2+A.
+// ------------------------------------------------------------------------
+__device__ __forceinline__ void qpid_assemble(const DevModel* M, const KParams& kp, double* S, const IO& io,
+                                              int64_t b) {
+  const int l = lane_id();
+  const int nv = kp.nv, narm = kp.narm, na = kp.na;
+  const int64_t gb = io.b0 + b, LD = io.ld;
+  double *qv = S + kp.kq, *qdl = S + kp.kqd, *J = S + kp.kJ, *xdd = S + kp.kxdd, *mg = S + kp.kmg, *dgv = S + kp.kdg,
+         *bias = S + kp.kBias, *Mq = S + kp.kMq, *Gq = S + kp.kGq;
+  {
+    const double* rec = io.rec + b * io.rec_stride;
+    for (int e = l; e < kp.rLen; e += 64) {
+      const double v = rec[e];
+      if (e < kp.rMan) J[e] = v;
+      else if (e == kp.rMan) S[kp.oSc + SC_MAN] = v;
+      else if (e < kp.rDist) mg[e - kp.rMan - 1] = v;
+      else if (e == kp.rDist) S[kp.oSc + SC_DIST] = v;
+      else if (e < kp.rXdd) dgv[e - kp.rDist - 1] = v;
+      else if (e < kp.rQ) xdd[e - kp.rXdd] = v;
+      else if (e < kp.rQd) qv[e - kp.rQ] = v;
+      else if (e < kp.rBias) qdl[e - kp.rQd] = v;
+      else bias[e - kp.rBias] = v;
+    }
+    for (int e = l; e < na * na; e += 64) Mq[e] = io.dM[(int64_t)e * LD + gb];
+    if (l < na) Gq[l] = io.dG[(int64_t)l * LD + gb];
+  }
+  wsync();
+  const int nx = kp.nx, ng = kp.ng, np = kp.np;
+  double *P = S + kp.oP, *G = S + kp.oG, *qq = S + kp.oQ, *ab = S + kp.oAB, *lo = S + kp.oL, *up = S + kp.oU;
+  const double a = kp.alpha_cbf, man = S[kp.oSc + SC_MAN], dist = S[kp.oSc + SC_DIST];
+  double* Jt = S + kp.kJt;  // 6 x na
+  if (M->kind == 0) {
+    for (int e = l; e < 6 * np; e += 64) Jt[e] = J[(e / np) * nv + e % np];
+  } else {  // J~ = J S (robot_data.cpp:407-410)
+    const double yaw = qv[M->virtual_start + 2], cy = cos(yaw), sy = sin(yaw);
+    for (int e = l; e < 6 * np; e += 64) {
+      const int r = e / np, c = e % np;
+      double v = 0;
+      const int am = c - M->act_mani_start, aw = c - M->act_mobi_start;
+      if (am >= 0 && am < M->n_arm) {
+        v = J[r * nv + M->mani_start + am];
+      } else if (aw >= 0 && aw < M->n_wheel) {
+        const double s0 = cy * M->J_mobile[0][aw] - sy * M->J_mobile[1][aw];
+        const double s1 = sy * M->J_mobile[0][aw] + cy * M->J_mobile[1][aw];
+        const double s2 = M->J_mobile[2][aw];
+        const int vs = M->virtual_start;
+        v = J[r * nv + M->mobi_start + aw] + J[r * nv + vs] * s0 + J[r * nv + vs + 1] * s1 + J[r * nv + vs + 2] * s2;
+      }
+      Jt[e] = v;
+    }
+  }
+  wsync();
+  for (int e = l; e < np * np; e += 64) {
+    const int i = e / np, j = e % np;
+    double s = 0;
+    for (int r = 0; r < 6; ++r) s += Jt[r * np + i] * Jt[r * np + j];
+    P[e] = 2.0 * s + (i == j ? kp.w_reg : 0.0);
+  }
+  for (int e = l; e < ng * nx; e += 64) G[e] = 0.0;
+  const bool slacks = M->kind == 0;
+  if (l < nx) {
+    double qi = 0;
+    if (l < np) {
+      double s = 0;
+      for (int r = 0; r < 6; ++r) s += Jt[r * np + l] * (xdd[r] - bias[r]);
+      qi = -2.0 * s;
+    } else if (l >= 2 * na) {
+      qi = kp.slack_w;
+    }
+    qq[l] = qi;
+    ab[l] = slacks ? 1.0 : 0.0;  // MoMa: nbc = 0 -> zero rows, equivalent to no bound rows
+    lo[l] = (slacks && l >= 2 * na) ? 0.0 : -kInf;
+    up[l] = kInf;
+  }
+  wsync();
+  if (l < ng) {
+    const int n = narm, row = nx + l;
+    const int vo = M->kind == 0 ? 0 : M->act_mani_start;  // QP column of arm joint 0
+    const int qo = M->kind == 0 ? 0 : M->mani_start;      // joint index of arm joint 0
+    double* Gr = G + l * nx;
+    double lval, uval = kInf;
+    if (l < 4 * n) {
+      const int k = l / n, i = l % n, jq = qo + i;
+      const double qi = qv[jq], qdi = qdl[jq];
+      Gr[vo + i] = (k & 1) ? -1.0 : 1.0;
+      if (slacks) Gr[2 * na + k * n + i] = 1.0;
+      if (k == 0) lval = -2 * a * qdi - a * a * (qi - M->lower[jq]);
+      else if (k == 1) lval = 2 * a * qdi - a * a * (M->upper[jq] - qi);
+      else if (k == 2) lval = -a * (qdi + M->vel[jq]);
+      else lval = -a * (M->vel[jq] - qdi);
+    } else if (l == 4 * n) {
+      double gq = 0;
+      for (int c = 0; c < n; ++c) {
+        Gr[vo + c] = mg[c];
+        gq += mg[c] * qdl[qo + c];
+      }
+      if (slacks) Gr[2 * na + 4 * n] = 1.0;
+      lval = -bias[6] - 2 * a * gq - a * a * (man - kp.man_min);
+    } else if (l == 4 * n + 1) {
+      double gq = 0;
+      for (int c = 0; c < n; ++c) {
+        Gr[vo + c] = dgv[qo + c];
+        gq += dgv[qo + c] * qdl[qo + c];
+      }
+      if (slacks) Gr[2 * na + 4 * n + 1] = 1.0;
+      lval = -bias[7] - 2 * a * gq - a * a * (dist - kp.dist_min);
+    } else {  // [M -I][qdd; tau] = -g (QP_ID.cpp:176-192)
+      const int i = l - (4 * n + 2);
+      for (int c = 0; c < na; ++c) Gr[c] = Mq[i * na + c];
+      Gr[na + i] = -1.0;
+      lval = uval = -Gq[i];
+    }
+    lo[row] = lval;
+    up[row] = uval;
+  }
+  wsync();
+}
+
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 8)))
+qpid_kernel(const DevModel* __restrict__ M0, const KParams kp, const IO io) {
+  using QD = Dims<0, 0, 0>;
+  extern __shared__ __attribute__((aligned(16))) double S[];
+  __shared__ KParams kpl;
+  const int l = lane_id();
+  {
+    const uint64_t* src = reinterpret_cast<const uint64_t*>(&kp);
+    uint64_t* dst = reinterpret_cast<uint64_t*>(&kpl);
+    for (int e = l; e < static_cast<int>(sizeof(KParams) / 8); e += 64) dst[e] = src[e];
+    wsync();
+  }
+  const int64_t B = io.B;
+  const InstSeq seq(B, kp.xcd_map);
+  for (int64_t j = seq.j0; j < seq.n; j += seq.step) {
+    const int64_t b = seq.at(j);
+    if (b >= B) continue;
+    const int64_t gb = io.b0 + b, LD = io.ld;
+    const DevModel* M = M0;
+    asm volatile("" : "+s"(M));
+    qpid_assemble(M, kp, S, io, b);
+    int status, iters = 0;
+    status = qp_scale<QD>(kp, S);
+    if (status != DRC_STATUS_NONFINITE) status = qp_admm<QD>(kp, kpl, S, &iters);
+    // outputs: QP_ID.cpp:74-83 getOptJoint; failure -> qdd = 0, tau = gravity
+    // (robot_controller.cpp:333-336; MoMa :208-213 slices the joint-order
+    // gravity at actuator offsets — restated as written)
+    const double *D = S + kp.oD, *x = S + kp.oX;
+    const int na = kp.na;
+    const bool ok = status == DRC_STATUS_SOLVED;
+    if (l < na) {
+      io.out[(int64_t)l * LD + gb] = ok ? D[l] * x[l] : 0.0;
+      const double gfail = M->kind == 0 ? io.dG[(int64_t)l * LD + gb] : io.dGf[(int64_t)l * LD + gb];
+      io.out2[(int64_t)l * LD + gb] = ok ? D[na + l] * x[na + l] : gfail;
+    }
+    if (l == 0) {
+      io.status[gb] = status;
+      if (io.iters) io.iters[gb] = iters;
+    }
+    wsync();
+  }
+}
+
 }  // namespace drc_amd
 
 // ==========================================================================
@@ -2253,11 +2626,21 @@ static int plan_layout(const DevModel& M, KParams* k, bool task_only) {
   k->kJt = takeu(6 * np);
   k->kSv = takeu(3 * kMaxWheels);
   k->kScr = takeu(96);
+  if (k->problem == 1) {  // QPID stage data (task kernel) and dynamics (QP kernel)
+    k->kJd = takeu(6 * nv);
+    k->kDa = takeu(6 * k->narm);
+    k->kVf = takeu(nv);
+    k->kX6 = takeu(72);
+    k->kBias = takeu(8);
+    k->kMq = takeu(k->na * k->na);
+    k->kGq = takeu(k->na);
+  }
   k->kEpa = task_only ? takeu(static_cast<int>((sizeof(EpaPoly) + 7) / 8)) : 0;
   int kin_end = u;
   int kinv_end = k->oU0 + nx * nx + nx * ng;  // K^-1 and G K^-1
   const int N = nx + ng;
-  int pol_end = k->oU0 + 64 + 64 + 128 + 64 * 5 + N * (N + 1) / 2;
+  k->nbuf = N > 64 ? 128 : 64;
+  int pol_end = k->oU0 + 64 + 64 + 128 + k->nbuf * 5 + N * (N + 1) / 2;
   int end = kin_end;
   if (!task_only) {
     end = end > kinv_end ? end : kinv_end;
@@ -2268,9 +2651,11 @@ static int plan_layout(const DevModel& M, KParams* k, bool task_only) {
   return DRC_OK;
 }
 
-static int make_kparams(const drc_model_impl* mm, const drc_qpik_params* p, int stages, KParams* k) {
+static int make_kparams(const drc_model_impl* mm, const drc_qpik_params* p, int stages, KParams* k,
+                        int problem = 0) {
   const DevModel& M = mm->hm.dev;
   std::memset(k, 0, sizeof(*k));
+  k->problem = problem;
   for (int i = 0; i < 6; ++i) {
     k->kp[i] = p->kp[i];
     k->kv[i] = p->kv[i];
@@ -2315,15 +2700,23 @@ static int make_kparams(const drc_model_impl* mm, const drc_qpik_params* p, int 
     k->na = k->np;
   }
   k->ng = 2 * k->narm + 2;
+  if (problem == 1) {  // QPID: QP_ID.cpp:11-63 / MoMa QP_ID.cpp:11-33
+    k->nx = M.kind == 0 ? 6 * M.nv + 2 : 2 * k->na;
+    k->ng = 4 * k->narm + 2 + k->na;
+  }
   k->m = k->nx + k->ng;
   k->rJac = 0;
   k->rMan = 6 * M.nv;
   k->rDist = k->rMan + 1 + k->narm;
   k->rXdd = k->rDist + 1 + M.nv;
   k->rQ = k->rXdd + 6;
-  k->rLen = k->rQ + M.nv;
+  k->rQd = k->rQ + M.nv;
+  k->rBias = k->rQd + M.nv;
+  k->rMgd = k->rBias + 6;
+  k->rDgd = k->rMgd + 1;
+  k->rLen = problem == 1 ? k->rDgd + 1 : k->rQd;
   k->xcd_map = 0;
-  if (k->nx > 64 || k->ng > 64 || k->narm > 8)
+  if (k->nx > 64 || k->ng > 64 || k->narm > 8 || k->m > 128)
     return set_err(DRC_ERR_UNSUPPORTED, "QP larger than one wavefront's row mapping");
   if (k->s.max_iter < 1 || k->s.check_termination < 0) return set_err(DRC_ERR_INVALID_ARGUMENT, "bad solver settings");
   return plan_layout(M, k, stages != 0);
@@ -2422,7 +2815,7 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
       if (int r = mkev(&e2)) return r;
       HIP_TRY(hipEventRecord(e0, cs));
     }
-    hipLaunchKernelGGL(task_kernel, dim3(static_cast<unsigned>(gt)), dim3(64),
+    hipLaunchKernelGGL(task_kernel<0>, dim3(static_cast<unsigned>(gt)), dim3(64),
                        static_cast<size_t>(kt_c.lds_doubles) * sizeof(double), cs, m->d_model, kt_c, io);
     HIP_TRY(hipGetLastError());
     if (timed) HIP_TRY(hipEventRecord(e1, cs));
@@ -2452,6 +2845,79 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
     HIP_TRY(hipEventRecord(e_end, st));
     std::lock_guard<std::mutex> g(m->mu);
     m->events.push_back(tev);
+  }
+  return DRC_OK;
+}
+
+// QPID pipeline for one call: dynamics launch(es) -> task kernel (QPID stage
+// data into the records) -> QPID kernel; or, with stages, the task kernel
+// writing the stage outputs.  Model-owned scratch holds the records and the
+// dynamics ([na*na][B] M, [na][B] g, MoMa also [nv][B] joint-order g).
+static int launch_qpid(const drc_model_impl* cm, const drc_qpik_params* params, int stages, int64_t B,
+                       const double* q, const double* qdot, const double* xt, const double* xdt, const double* xi,
+                       const double* xdi, double* qdd, double* tau, int32_t* status, int32_t* iters, double* pose,
+                       double* jac, double* man, double* dist, int32_t* pair, double* xdd, double* jdot,
+                       double* qpid_st, void* stream) {
+  drc_model_impl* m = const_cast<drc_model_impl*>(cm);
+  if (!m || !params) return set_err(DRC_ERR_INVALID_ARGUMENT, "null model/params");
+  if (B < 0) return set_err(DRC_ERR_INVALID_ARGUMENT, "negative batch");
+  if (B == 0) return DRC_OK;
+  if (B > 0x7ffffff0) return set_err(DRC_ERR_INVALID_ARGUMENT, "batch too large");
+  if (!q || !qdot || !xdt) return set_err(DRC_ERR_INVALID_ARGUMENT, "q, qdot and xdot_target are required");
+  if (params->mode != DRC_MODE_QPIK && !xt) return set_err(DRC_ERR_INVALID_ARGUMENT, "x_target required for QPIDStep/QPIDCubic");
+  if (params->mode == DRC_MODE_QPIK_CUBIC && (!xi || !xdi))
+    return set_err(DRC_ERR_INVALID_ARGUMENT, "x_init/xdot_init required for QPIDCubic");
+  if (!stages && (!qdd || !tau || !status)) return set_err(DRC_ERR_INVALID_ARGUMENT, "qddot_out, tau_out and status are required");
+  KParams kt, kq;
+  int rc = make_kparams(m, params, 1, &kt, 1);
+  if (rc) return rc;
+  if (!stages) {
+    rc = make_kparams(m, params, 0, &kq, 1);
+    if (rc) return rc;
+  }
+  const DevModel& d = m->hm.dev;
+  HIP_TRY(hipSetDevice(m->device));
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int64_t stride = (kt.rLen + 15) & ~int64_t(15);
+  const int na = kt.na, nv = d.nv;
+  const int64_t dyn_words = stages ? 0 : (int64_t(na) * na + na + (d.kind == 1 ? nv : 0)) * B;
+  double *rec = nullptr, *dM = nullptr, *dG = nullptr, *dGf = nullptr;
+  if (!stages) {
+    std::lock_guard<std::mutex> g(m->mu);
+    const int64_t bytes = (stride * B + dyn_words) * 8;
+    if (m->pool_bytes < bytes) {
+      if (m->pool) HIP_TRY(hipFree(m->pool));
+      m->pool = nullptr;
+      m->pool_bytes = 0;
+      HIP_TRY(hipMalloc(&m->pool, bytes));
+      m->pool_bytes = bytes;
+    }
+    rec = reinterpret_cast<double*>(m->pool);
+    dM = rec + stride * B;
+    dG = dM + int64_t(na) * na * B;
+    dGf = d.kind == 1 ? dG + int64_t(na) * B : nullptr;
+    // getMassMatrix / getGravity (or the *Actuated getters) the equality rows use
+    rc = launch_dynamics(m->d_model, d, d.kind == 1, B, q, qdot, dM, nullptr, dG, nullptr, nullptr, nullptr, st);
+    if (!rc && d.kind == 1) rc = launch_dynamics(m->d_model, d, false, B, q, qdot, nullptr, nullptr, dGf, nullptr, nullptr, nullptr, st);
+    if (rc) return set_err(DRC_ERR_HIP, std::string("dynamics launch: ") + hipGetErrorString(hipGetLastError()));
+  }
+  const int64_t grid = B < 8192 ? B : 8192;
+  KParams kt_c = kt, kq_c = kq;
+  kt_c.xcd_map = kq_c.xcd_map = B >= 16384 ? 1 : 0;
+  IO io{B, 0, B, q, qdot, xt, xdt, xi, xdi, qdd, status, iters, pose, jac, man, dist, xdd, pair, rec, stride};
+  io.dM = dM;
+  io.dG = dG;
+  io.dGf = dGf;
+  io.out2 = tau;
+  io.st_jdot = jdot;
+  io.st_qpid = qpid_st;
+  hipLaunchKernelGGL(task_kernel<1>, dim3(static_cast<unsigned>(grid)), dim3(64),
+                     static_cast<size_t>(kt_c.lds_doubles) * sizeof(double), st, m->d_model, kt_c, io);
+  HIP_TRY(hipGetLastError());
+  if (!stages) {
+    hipLaunchKernelGGL(qpid_kernel, dim3(static_cast<unsigned>(grid)), dim3(64),
+                       static_cast<size_t>(kq_c.lds_doubles) * sizeof(double), st, m->d_model, kq_c, io);
+    HIP_TRY(hipGetLastError());
   }
   return DRC_OK;
 }
@@ -2718,6 +3184,38 @@ int drc_qpik_stages_batch(const drc_model* m, const drc_qpik_params* p, int64_t 
 }
 
 
+// ---- QPID -------------------------------------------------
+int drc_default_qpid_params(const drc_model* m, int exact, drc_qpik_params* p) {
+  int rc = drc_default_qpik_params(m, exact, p);
+  if (rc) return rc;
+  const bool moma = m->hm.dev.kind == 1;
+  for (int i = 0; i < 6; ++i) {
+    p->kp[i] = moma ? 400 : 100;  // robot_controller.cpp:12-13; MoMa :15-16
+    p->kv[i] = moma ? 40 : 20;    // QPIDStep: Kp e + Kv (xdot_target - xdot) (:347; MoMa :230)
+  }
+  p->feedforward = 0;
+  p->w_reg = 0;  // QP_ID.cpp:102: the regulariser is commented out
+  // P is singular on null(J); OSQP's polish delta 1e-6 cannot certify at
+  // eps_exact there, so parity mode regularises the polish with 1e-10
+  if (exact) p->solver.delta = 1e-10;
+  return DRC_OK;
+}
+
+int drc_qpid_batch(const drc_model* m, const drc_qpik_params* p, int64_t B, const double* q, const double* qdot,
+                   const double* xt, const double* xdt, const double* xi, const double* xdi, double* qddot_out,
+                   double* tau_out, int32_t* status, int32_t* iters, void* stream) {
+  return drc_amd::launch_qpid(m, p, 0, B, q, qdot, xt, xdt, xi, xdi, qddot_out, tau_out, status, iters, nullptr,
+                              nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, stream);
+}
+
+int drc_qpid_stages_batch(const drc_model* m, const drc_qpik_params* p, int64_t B, const double* q,
+                          const double* qdot, const double* xt, const double* xdt, const double* xi,
+                          const double* xdi, double* pose, double* jac, double* man, double* dist, int32_t* pair,
+                          double* xddot_des, double* jdot, double* qpid_terms, void* stream) {
+  return drc_amd::launch_qpid(m, p, 1, B, q, qdot, xt, xdt, xi, xdi, nullptr, nullptr, nullptr, nullptr, pose, jac,
+                              man, dist, pair, xddot_des, jdot, qpid_terms, stream);
+}
+
 // ---- host-buffer entry points (synchronous; staged through device memory) --
 namespace {
 struct HostIO {
@@ -2810,6 +3308,51 @@ int drc_qpik_stages_host(drc_model* m, const drc_qpik_params* p, int64_t B, cons
   return host_call(m, p, 1, B, in, outs, rows, 5, iouts, 1);
 }
 
+
+int drc_qpid_host(drc_model* m, const drc_qpik_params* p, int64_t B, const double* q, const double* qdot,
+                  const double* xt, const double* xdt, const double* xi, const double* xdi, double* qdd, double* tau,
+                  int32_t* status, int32_t* iters) {
+  using drc_amd::set_err;
+  if (!m || !p) return set_err(DRC_ERR_INVALID_ARGUMENT, "null model/params");
+  if (B <= 0) return B == 0 ? DRC_OK : set_err(DRC_ERR_INVALID_ARGUMENT, "negative batch");
+  if (!qdd || !tau || !status) return set_err(DRC_ERR_INVALID_ARGUMENT, "qddot_out, tau_out and status are required");
+  const drc_amd::DevModel& d = m->hm.dev;
+  const int64_t n = d.nv, na = d.kind == 1 ? d.n_arm + d.n_wheel : n;
+  std::lock_guard<std::mutex> lk(m->host_mu);
+  HIP_TRY(hipSetDevice(m->device));
+  const double* src[6] = {q, qdot, xt, xdt, xi, xdi};
+  const int64_t rows[6] = {n, n, 12, 6, 12, 6};
+  int64_t words = 2 * na * B + B;  // outputs + status/iters
+  for (int i = 0; i < 6; ++i) words += src[i] ? rows[i] * B : 0;
+  if (m->stage_bytes < words * 8) {
+    if (m->stage) (void)hipFree(m->stage);
+    m->stage = nullptr;
+    m->stage_bytes = 0;
+    HIP_TRY(hipMalloc(&m->stage, words * 8));
+    m->stage_bytes = words * 8;
+  }
+  if (!m->hstream) HIP_TRY(hipStreamCreateWithFlags(&m->hstream, hipStreamNonBlocking));
+  double* dp = reinterpret_cast<double*>(m->stage);
+  const double* din[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  for (int i = 0; i < 6; ++i)
+    if (src[i]) {
+      HIP_TRY(hipMemcpyAsync(dp, src[i], rows[i] * B * 8, hipMemcpyHostToDevice, m->hstream));
+      din[i] = dp;
+      dp += rows[i] * B;
+    }
+  double* dqdd = dp;
+  double* dtau = dp + na * B;
+  int32_t* dst = reinterpret_cast<int32_t*>(dp + 2 * na * B);
+  int32_t* dit = iters ? dst + B : nullptr;
+  int rc = drc_qpid_batch(m, p, B, din[0], din[1], din[2], din[3], din[4], din[5], dqdd, dtau, dst, dit, m->hstream);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(qdd, dqdd, na * B * 8, hipMemcpyDeviceToHost, m->hstream));
+  HIP_TRY(hipMemcpyAsync(tau, dtau, na * B * 8, hipMemcpyDeviceToHost, m->hstream));
+  HIP_TRY(hipMemcpyAsync(status, dst, B * 4, hipMemcpyDeviceToHost, m->hstream));
+  if (iters) HIP_TRY(hipMemcpyAsync(iters, dit, B * 4, hipMemcpyDeviceToHost, m->hstream));
+  HIP_TRY(hipStreamSynchronize(m->hstream));
+  return DRC_OK;
+}
 
 // ---- joint-space dynamics ------------------------------
 int drc_dynamics_batch(drc_model* m, int actuated, int64_t B, const double* q, const double* qdot, double* M,

@@ -237,12 +237,14 @@ class MinDistResult:
 
 
 class QPIKParamsBuilder:
-    """Fills ``drc_qpik_params`` from the reference defaults of the model kind."""
+    """Fills ``drc_qpik_params`` from the reference defaults of the model kind
+    (``qpid``: the QPID defaults, drc_default_qpid_params)."""
 
-    def __init__(self, model, exact=True):
+    def __init__(self, model, exact=True, qpid=False):
         self.model = model
         self.base = _capi.QPIKParams()
-        _capi.check(_capi.lib().drc_default_qpik_params(model.handle, C.c_int(1 if exact else 0), C.byref(self.base)))
+        fn = _capi.lib().drc_default_qpid_params if qpid else _capi.lib().drc_default_qpik_params
+        _capi.check(fn(model.handle, C.c_int(1 if exact else 0), C.byref(self.base)))
 
     def params_no_frame(self, mode):
         """Stage-only parameters without a task frame (frame_id = -1)."""
@@ -291,6 +293,7 @@ class RobotController:
             raise ValueError("solver_mode must be 'exact' or 'osqp_default'")
         self.solver_mode = mode
         self._pb = QPIKParamsBuilder(self.robot_data_.model, exact=(mode == "exact"))
+        self._pbd = QPIKParamsBuilder(self.robot_data_.model, exact=(mode == "exact"), qpid=True)
 
     def setTaskGain(self, Kp, Kv):
         Kp, Kv = np.asarray(Kp, float).reshape(-1), np.asarray(Kv, float).reshape(-1)
@@ -408,3 +411,47 @@ class RobotController:
             current_time, init_time, duration, link_name))
 
     QPIK_step, QPIK_cubic = QPIKStep, QPIKCubic
+
+    # -- QPID / QPIDStep / QPIDCubic (robot_controller.cpp:319-361)
+    def _run_id(self, mode, link_name, q, qdot, x_target, xdot_target, x_init=None, xdot_init=None,
+                t=0.0, t0=0.0, duration=1.0, iters=None):
+        p = self._pbd.params(link_name, mode, self.Kp_task_, self.Kv_task_, t, t0, duration)
+        a = lambda v: _batch.as_device(v, self.robot_data_.device)
+        return _batch.qpid_batch(self.robot_data_.model, p, a(q), a(qdot), a(x_target), a(xdot_target), a(x_init),
+                                 a(xdot_init), iters=iters)
+
+    def QPID_batch(self, q, qdot, xddot_target, link_name):
+        """(qddot, tau, status) for B robots; tau = gravity where not solved."""
+        return self._run_id(_capi.MODE_QPID, link_name, q, qdot, None, xddot_target)
+
+    def QPID_step_batch(self, q, qdot, x_target, xdot_target, link_name, iters=None):
+        return self._run_id(_capi.MODE_QPID_STEP, link_name, q, qdot, x_target, xdot_target, iters=iters)
+
+    def QPID_cubic_batch(self, q, qdot, x_target, xdot_target, x_init, xdot_init, current_time, init_time,
+                         duration, link_name):
+        return self._run_id(_capi.MODE_QPID_CUBIC, link_name, q, qdot, x_target, xdot_target, x_init, xdot_init,
+                            current_time, init_time, duration)
+
+    def _one_id(self, res):
+        qdd, tau, status = res
+        if int(status.cpu().numpy()[0]) != _capi.STATUS_SOLVED:
+            print("QP ID failed to compute optimal joint torque.", file=sys.stderr)
+        return tau.cpu().numpy()[:, 0]   # already the gravity torque on failure (:333-336)
+
+    def QPID(self, xddot_target, link_name):
+        q, qd = self._state()
+        return self._one_id(self.QPID_batch(q, qd, np.asarray(xddot_target, float).reshape(6, 1), link_name))
+
+    def QPIDStep(self, x_target, xdot_target, link_name):
+        q, qd = self._state()
+        return self._one_id(self.QPID_step_batch(q, qd, pose_to12(x_target).reshape(12, 1),
+                                                 np.asarray(xdot_target, float).reshape(6, 1), link_name))
+
+    def QPIDCubic(self, x_target, xdot_target, x_init, xdot_init, current_time, init_time, duration, link_name):
+        q, qd = self._state()
+        return self._one_id(self.QPID_cubic_batch(
+            q, qd, pose_to12(x_target).reshape(12, 1), np.asarray(xdot_target, float).reshape(6, 1),
+            pose_to12(x_init).reshape(12, 1), np.asarray(xdot_init, float).reshape(6, 1),
+            current_time, init_time, duration, link_name))
+
+    QPID_step, QPID_cubic = QPIDStep, QPIDCubic

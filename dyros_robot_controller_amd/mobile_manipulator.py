@@ -310,8 +310,8 @@ class RobotController:
             raise TypeError("robot_data must be a mobile_manipulator.RobotData")
         self.dt_ = float(dt)
         self.robot_data_ = robot_data
-        self.Kp_task_ = np.full(6, 400.0)
-        self.Kv_task_ = np.full(6, 0.0)
+        self.Kp_task_ = np.full(6, 400.0)         # robot_controller.cpp:15-16
+        self.Kv_task_ = np.full(6, 40.0)          # used by QPID only (QPIKStep has no Kv term, :177)
         n = robot_data.get_manipulator_dof()
         self.Kp_mani_joint_ = np.full(n, 400.0)   # mobile_manipulator/robot_controller.cpp:17-18
         self.Kv_mani_joint_ = np.full(n, 40.0)
@@ -322,6 +322,7 @@ class RobotController:
             raise ValueError("solver_mode must be 'exact' or 'osqp_default'")
         self.solver_mode = mode
         self._pb = QPIKParamsBuilder(self.robot_data_.model, exact=(mode == "exact"))
+        self._pbd = QPIKParamsBuilder(self.robot_data_.model, exact=(mode == "exact"), qpid=True)
 
     def set_task_gain(self, kp, kv):
         kp, kv = np.asarray(kp, float).reshape(-1), np.asarray(kv, float).reshape(-1)
@@ -391,7 +392,7 @@ class RobotController:
     # -- batched entries (device tensors, [field][B]; q is the full joint vector)
     def _run(self, mode, link_name, q, qdot, x_target, xdot_target, x_init=None, xdot_init=None,
              t=0.0, t0=0.0, duration=1.0, iters=None):
-        p = self._pb.params(link_name, mode, self.Kp_task_, self.Kv_task_, t, t0, duration)
+        p = self._pb.params(link_name, mode, self.Kp_task_, np.zeros(6), t, t0, duration)   # no Kv in QPIKStep
         dev = self.robot_data_.device
         return _batch.qpik_batch(self.robot_data_.model, p, _batch.as_device(q, dev), _batch.as_device(qdot, dev),
                                  _batch.as_device(x_target, dev), _batch.as_device(xdot_target, dev),
@@ -444,3 +445,51 @@ class RobotController:
             current_time, init_time, duration, link_name))
 
     QPIKStep, QPIKCubic = QPIK_step, QPIK_cubic
+
+    # -- QPID / QPIDStep / QPIDCubic (robot_controller.cpp:199-250)
+    def _run_id(self, mode, link_name, q, qdot, x_target, xdot_target, x_init=None, xdot_init=None,
+                t=0.0, t0=0.0, duration=1.0, iters=None):
+        p = self._pbd.params(link_name, mode, self.Kp_task_, self.Kv_task_, t, t0, duration)
+        a = lambda v: _batch.as_device(v, self.robot_data_.device)
+        return _batch.qpid_batch(self.robot_data_.model, p, a(q), a(qdot), a(x_target), a(xdot_target), a(x_init),
+                                 a(xdot_init), iters=iters)
+
+    def QPID_batch(self, q, qdot, xddot_target, link_name):
+        """(eta_dot [A][B], tau [A][B], status [B]) in ActuatorIndex order."""
+        return self._run_id(_capi.MODE_QPID, link_name, q, qdot, None, xddot_target)
+
+    def QPID_step_batch(self, q, qdot, x_target, xdot_target, link_name, iters=None):
+        return self._run_id(_capi.MODE_QPID_STEP, link_name, q, qdot, x_target, xdot_target, iters=iters)
+
+    def QPID_cubic_batch(self, q, qdot, x_target, xdot_target, x_init, xdot_init, current_time, init_time,
+                         duration, link_name):
+        return self._run_id(_capi.MODE_QPID_CUBIC, link_name, q, qdot, x_target, xdot_target, x_init, xdot_init,
+                            current_time, init_time, duration)
+
+    def _one_id(self, res):
+        """-> (qddot_mobile [W], torque_manipulator [n]) (robot_controller.cpp:215-218)."""
+        qdd, tau, status = res
+        if int(status.cpu().numpy()[0]) != _capi.STATUS_SOLVED:
+            print("QP ID failed to compute optimal joint torque.", file=sys.stderr)
+        qdd, tau = qdd.cpu().numpy()[:, 0], tau.cpu().numpy()[:, 0]
+        a = self.robot_data_.get_actuator_index()
+        W, n = self.robot_data_.get_mobile_dof(), self.robot_data_.get_manipulator_dof()
+        return qdd[a.mobi_start:a.mobi_start + W].copy(), tau[a.mani_start:a.mani_start + n].copy()
+
+    def QPID(self, xddot_target, link_name):
+        q, qd = self._state()
+        return self._one_id(self.QPID_batch(q, qd, np.asarray(xddot_target, float).reshape(6, 1), link_name))
+
+    def QPID_step(self, x_target, xdot_target, link_name):
+        q, qd = self._state()
+        return self._one_id(self.QPID_step_batch(q, qd, pose_to12(x_target).reshape(12, 1),
+                                                 np.asarray(xdot_target, float).reshape(6, 1), link_name))
+
+    def QPID_cubic(self, x_target, xdot_target, x_init, xdot_init, current_time, init_time, duration, link_name):
+        q, qd = self._state()
+        return self._one_id(self.QPID_cubic_batch(
+            q, qd, pose_to12(x_target).reshape(12, 1), np.asarray(xdot_target, float).reshape(6, 1),
+            pose_to12(x_init).reshape(12, 1), np.asarray(xdot_init, float).reshape(6, 1),
+            current_time, init_time, duration, link_name))
+
+    QPIDStep, QPIDCubic = QPID_step, QPID_cubic

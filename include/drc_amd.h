@@ -262,6 +262,41 @@ int drc_joint_torque_step_host(drc_model* model, int64_t B, const double* q, con
                                const double* q_target, const double* qdot_target, const double* qddot_target,
                                double dt, const double* kp, const double* kv, double* tau);
 
+/* ---- QPID: the torque-level QP ----------------------
+ * Manipulator::RobotController::QPID / QPIDStep / QPIDCubic (src/manipulator/robot_controller.cpp:319-361) over
+ * Manipulator::QPID (src/manipulator/QP_ID.cpp:7-193), and the MobileManipulator twins
+ * (src/mobile_manipulator/robot_controller.cpp:199-250, QP_ID.cpp:7-184), for B robots.  Same params struct
+ * as QPIK: mode DRC_MODE_QPID* (0 = QPID(xddot_target) with the task acceleration in xdot_target,
+ * 1 = QPIDStep, 2 = QPIDCubic), kp/kv the task gains (defaults 100/20, MoMa 400/40).  Per call: M and g of the
+ * equality rows are computed on the device (drc_dynamics_batch's kernel), then the QPID stage data (frame
+ * Jacobian time variation, grad_dot terms of the singularity and self-collision CBF rows) and the QP.
+ *   qddot_out [na][B]: qddot (manipulator) / eta_dot in ActuatorIndex order (MoMa);
+ *   tau_out   [na][B]: joint torques / actuated torques;
+ *   status [B], iters [B] (may be NULL).
+ * Non-Solved: qddot = 0, tau = getGravity() (robot_controller.cpp:333-336); MoMa: tau[i] = the joint-order
+ * getGravity()[i] — the reference slices that vector at ActuatorIndex offsets (mobile_manipulator/
+ * robot_controller.cpp:211,218), restated as written. */
+enum { DRC_MODE_QPID = 0, DRC_MODE_QPID_STEP = 1, DRC_MODE_QPID_CUBIC = 2 };
+int drc_default_qpid_params(const drc_model* model, int exact, drc_qpik_params* params);
+int drc_qpid_batch(const drc_model* model, const drc_qpik_params* params, int64_t B,
+                   const double* q, const double* qdot, const double* x_target,
+                   const double* xdot_target, const double* x_init, const double* xdot_init,
+                   double* qddot_out, double* tau_out, int32_t* status, int32_t* iters, void* stream);
+/* Stage outputs of the QPID task stage: as drc_qpik_stages_batch (xddot_des = the QP's task
+ * acceleration), plus jdot [6*dof][B] (getJacobianTimeVariation, LWA, robot_data.cpp:404-417) and
+ * qpid_terms [8][B] = (Jdot v (6) with v = qdot or S eta, grad_dot_m . qdot_arm, grad_dot_d . qdot_arm).
+ * Any output may be NULL. */
+int drc_qpid_stages_batch(const drc_model* model, const drc_qpik_params* params, int64_t B,
+                          const double* q, const double* qdot, const double* x_target,
+                          const double* xdot_target, const double* x_init, const double* xdot_init,
+                          double* pose, double* jac, double* man, double* dist, int32_t* pair,
+                          double* xddot_des, double* jdot, double* qpid_terms, void* stream);
+/* Host-buffer form of drc_qpid_batch (synchronous, PCIe-inclusive). */
+int drc_qpid_host(drc_model* model, const drc_qpik_params* params, int64_t B,
+                  const double* q, const double* qdot, const double* x_target,
+                  const double* xdot_target, const double* x_init, const double* xdot_init,
+                  double* qddot_out, double* tau_out, int32_t* status, int32_t* iters);
+
 #ifdef __cplusplus
 }
 #endif
