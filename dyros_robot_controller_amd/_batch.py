@@ -93,13 +93,15 @@ def qpid_stages_batch(model, params, q, qdot, x_target=None, xdot_target=None, x
     nv = model.dof
     f = lambda r: torch.zeros((r, B), dtype=torch.float64, device=dev)
     pose, jac, man, dist, xdd, jdot, terms = f(12), f(6 * nv), f(1 + model.mani_dof), f(1 + nv), f(6), f(6 * nv), f(8)
+    gdv = f(model.mani_dof + nv)
     pair = torch.zeros(B, dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream(dev).cuda_stream
     _capi.check(_capi.lib().drc_qpid_stages_batch(
         model.handle, C.byref(params), C.c_int64(B), _ptr(q), _ptr(qdot), _ptr(x_target), _ptr(xdot_target),
         _ptr(x_init), _ptr(xdot_init), _ptr(pose), _ptr(jac), _ptr(man), _ptr(dist), _ptr(pair), _ptr(xdd),
-        _ptr(jdot), _ptr(terms), C.c_void_p(stream)))
-    return dict(pose=pose, jac=jac, man=man, dist=dist, pair=pair, xddot_des=xdd, jdot=jdot, qpid_terms=terms)
+        _ptr(jdot), _ptr(terms), _ptr(gdv), C.c_void_p(stream)))
+    return dict(pose=pose, jac=jac, man=man, dist=dist, pair=pair, xddot_des=xdd, jdot=jdot, qpid_terms=terms,
+                man_graddot=gdv[:model.mani_dof], dist_graddot=gdv[model.mani_dof:])
 
 
 def stages_batch(model, params, q, qdot, x_target=None, xdot_target=None, x_init=None, xdot_init=None):

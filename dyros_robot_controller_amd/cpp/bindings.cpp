@@ -7,7 +7,8 @@
 // The reference's drc/ Python package subclasses these classes
 // (drc/manipulator/robot_data.py, robot_controller.py, ...).  Besides the
 // reference methods, each controller has QPIKBatch / QPIKStepBatch /
-// QPIKCubicBatch over [field][B] numpy arrays.
+// QPIKCubicBatch and QPIDBatch / QPIDStepBatch / QPIDCubicBatch over
+// [field][B] numpy arrays.
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
@@ -96,8 +97,37 @@ py::tuple batch(const ControllerBase& self, int A, int mode, const Arr& q, const
   return py::make_tuple(out, status);
 }
 
+// [field][B] numpy QPID batch -> (qddot [A][B], tau [A][B], status [B])
+py::tuple batch_id(const ControllerBase& self, int A, int mode, const Arr& q, const Arr& qdot, const Arr* xt,
+                   const Arr& xdt, const Arr* xi, const Arr* xdi, double t, double t0, double T,
+                   const std::string& link) {
+  if (q.ndim() != 2) throw std::invalid_argument("q must be [dof][B]");
+  const int64_t B = q.shape(1);
+  py::array_t<double> qdd({static_cast<py::ssize_t>(A), static_cast<py::ssize_t>(B)});
+  py::array_t<double> tau({static_cast<py::ssize_t>(A), static_cast<py::ssize_t>(B)});
+  py::array_t<int32_t> status(static_cast<py::ssize_t>(B));
+  {
+    py::gil_scoped_release nogil;
+    self.QPIDBatch(mode, B, q.data(), qdot.data(), xt ? xt->data() : nullptr, xdt.data(), xi ? xi->data() : nullptr,
+                   xdi ? xdi->data() : nullptr, t, t0, T, link, qdd.mutable_data(), tau.mutable_data(),
+                   status.mutable_data(), false);
+  }
+  return py::make_tuple(qdd, tau, status);
+}
+
 template <class RC, class RD>
 void add_controller_common(py::class_<RC>& c) {
+  c.def("QPIDBatch", [](const RC& s, const Arr& q, const Arr& qd, const Arr& xdd, const std::string& l) {
+     return batch_id(s, s.actuatedDof(), DRC_MODE_QPID, q, qd, nullptr, xdd, nullptr, nullptr, 0, 0, 1, l);
+   })
+      .def("QPIDStepBatch", [](const RC& s, const Arr& q, const Arr& qd, const Arr& xt, const Arr& xdt,
+                               const std::string& l) {
+        return batch_id(s, s.actuatedDof(), DRC_MODE_QPID_STEP, q, qd, &xt, xdt, nullptr, nullptr, 0, 0, 1, l);
+      })
+      .def("QPIDCubicBatch", [](const RC& s, const Arr& q, const Arr& qd, const Arr& xt, const Arr& xdt,
+                                const Arr& xi, const Arr& xdi, double t, double t0, double T, const std::string& l) {
+        return batch_id(s, s.actuatedDof(), DRC_MODE_QPID_CUBIC, q, qd, &xt, xdt, &xi, &xdi, t, t0, T, l);
+      });
   c.def("setTaskGain", [](RC& s, const Arr& kp, const Arr& kv) { s.setTaskGain(to_vec(kp), to_vec(kv)); })
       .def("setTaskKpGain", [](RC& s, const Arr& kp) { s.setTaskKpGain(to_vec(kp)); })
       .def("setTaskKvGain", [](RC& s, const Arr& kv) { s.setTaskKvGain(to_vec(kv)); })
@@ -190,7 +220,13 @@ PYBIND11_MODULE(dyros_robot_controller_cpp_wrapper, m) {
       .def("getVelocity", [](const MN_RD& s, const std::string& l) { return to_arr(s.getVelocity(l)); })
       .def("getManipulability", &MN_RD::getManipulability)
       .def("getMinDistance", &MN_RD::getMinDistance, py::arg("with_grad"), py::arg("with_graddot"),
-           py::arg("verbose") = false);
+           py::arg("verbose") = false)
+      .def("getJacobianTimeVariation", [](const MN_RD& s, const std::string& l) {
+        return to_mat(s.getJacobianTimeVariation(l), 6, s.getDof());
+      })
+      .def("computeJacobianTimeVariation", [](const MN_RD& s, const Arr& q, const Arr& qd, const std::string& l) {
+        return to_mat(s.computeJacobianTimeVariation(to_vec(q), to_vec(qd), l), 6, s.getDof());
+      });
 
   // ---- ManipulatorRobotController (bindings.cpp:398-426) --------------------
   py::class_<MN_RC> mnrc(m, "ManipulatorRobotController");
@@ -213,6 +249,14 @@ PYBIND11_MODULE(dyros_robot_controller_cpp_wrapper, m) {
       .def("QPIKCubicBatch", [](const MN_RC& s, const Arr& q, const Arr& qd, const Arr& xt, const Arr& xdt,
                                 const Arr& xi, const Arr& xdi, double t, double t0, double T, const std::string& l) {
         return batch(s, s.actuatedDof(), DRC_MODE_QPIK_CUBIC, q, qd, &xt, xdt, &xi, &xdi, t, t0, T, l);
+      })
+      .def("QPID", [](const MN_RC& s, const Arr& xdd, const std::string& l) { return to_arr(s.QPID(to_vec(xdd), l)); })
+      .def("QPIDStep", [](const MN_RC& s, const Arr& x, const Arr& xd, const std::string& l) {
+        return to_arr(s.QPIDStep(to_pose(x), to_vec(xd), l));
+      })
+      .def("QPIDCubic", [](const MN_RC& s, const Arr& xt, const Arr& xdt, const Arr& xi, const Arr& xdi, double t,
+                           double t0, double T, const std::string& l) {
+        return to_arr(s.QPIDCubic(to_pose(xt), to_vec(xdt), to_pose(xi), to_vec(xdi), t, t0, T, l));
       });
   add_controller_common<MN_RC, MN_RD>(mnrc);
 
@@ -243,7 +287,11 @@ PYBIND11_MODULE(dyros_robot_controller_cpp_wrapper, m) {
       .def("getPose", [](const MM_RD& s, const std::string& l) { return from_pose(s.getPose(l)); })
       .def("getJacobian", [](const MM_RD& s, const std::string& l) { return to_mat(s.getJacobian(l), 6, s.getDof()); })
       .def("getMinDistance", &MM_RD::getMinDistance, py::arg("with_grad"), py::arg("with_graddot"),
-           py::arg("verbose") = false);
+           py::arg("verbose") = false)
+      .def("getManipulability", &MM_RD::getManipulability)
+      .def("getJacobianTimeVariation", [](const MM_RD& s, const std::string& l) {
+        return to_mat(s.getJacobianTimeVariation(l), 6, s.getDof());
+      });
 
   // ---- MobileManipulatorRobotController (bindings.cpp:430-444) --------------
   py::class_<MM_RC> mmrc(m, "MobileManipulatorRobotController");
@@ -274,6 +322,22 @@ PYBIND11_MODULE(dyros_robot_controller_cpp_wrapper, m) {
       .def("QPIKCubicBatch", [](const MM_RC& s, const Arr& q, const Arr& qd, const Arr& xt, const Arr& xdt,
                                 const Arr& xi, const Arr& xdi, double t, double t0, double T, const std::string& l) {
         return batch(s, s.actuatedDof(), DRC_MODE_QPIK_CUBIC, q, qd, &xt, xdt, &xi, &xdi, t, t0, T, l);
+      })
+      .def("QPID", [](const MM_RC& s, const Arr& xdd, const std::string& l) {
+        Vec am, ta;
+        s.QPID(to_vec(xdd), l, am, ta);
+        return py::make_tuple(to_arr(am), to_arr(ta));
+      })
+      .def("QPIDStep", [](const MM_RC& s, const Arr& x, const Arr& xd, const std::string& l) {
+        Vec am, ta;
+        s.QPIDStep(to_pose(x), to_vec(xd), l, am, ta);
+        return py::make_tuple(to_arr(am), to_arr(ta));
+      })
+      .def("QPIDCubic", [](const MM_RC& s, const Arr& xt, const Arr& xdt, const Arr& xi, const Arr& xdi, double t,
+                           double t0, double T, const std::string& l) {
+        Vec am, ta;
+        s.QPIDCubic(to_pose(xt), to_vec(xdt), to_pose(xi), to_vec(xdi), t, t0, T, l, am, ta);
+        return py::make_tuple(to_arr(am), to_arr(ta));
       });
   add_controller_common<MM_RC, MM_RD>(mmrc);
 }

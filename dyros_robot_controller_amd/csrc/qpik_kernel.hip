@@ -50,6 +50,7 @@ struct KParams {
   int oU0;
   int kT, kZ, kTe, kJ, kTg, kq, kqd, kA6, kAi, kW, kPart, kPd, kPf, kxdd, kmg, kdg, kJt, kSv, kScr, kEpa;
   int kJd, kDa, kVf, kX6, kBias, kMq, kGq;  // QPID: Jdot, arm-only Jdot, S eta, 6x6 scratch, bias | M, g
+  int kGdv;                                 // QPID stage: grad_dot vectors
   int lds_doubles;
 };
 
@@ -957,6 +958,7 @@ struct IO {
   const double *dM, *dG, *dGf;
   double* out2;
   double *st_jdot, *st_qpid;  // [6*nv][B] Jdot; [8][B] bias(6), man_gd, dist_gd
+  double* st_gdv;             // [narm + nv][B] grad_dot vectors (manipulability | min distance)
 };
 
 // ------------------------------------------------------------------------
@@ -1022,8 +1024,10 @@ __device__ __forceinline__ void body_velocity(const DevModel* M, const double* T
 //       mdot = m tr(Jda W)           (robot_data.cpp:555-569, MoMa :477-492);
 //   dist_gd = getMinDistance(..,true,..).grad_dot . qdot_arm
 //       = sum_{c in arm} qdot_c n.(JB_dot - JA_dot)[:, c]   (robot_data.cpp:496-512).
+// full: also the reference's grad_dot VECTORS (stage outputs) into kGdv =
+//   [getManipulability grad_dot (narm) | getMinDistance grad_dot (nv)].
 __device__ __noinline__ void qpid_task_extras(const DevModel* M, const KParams& kp, double* S, double bestd,
-                                              int besti) {
+                                              int besti, bool full) {
   const int l = lane_id(), nv = kp.nv, narm = kp.narm, c0 = kp.c0;
   const double *T = S + kp.kT, *Zw = S + kp.kZ, *J = S + kp.kJ, *qd = S + kp.kqd, *Te = S + kp.kTe,
                *red = S + kp.oRed, *W = S + kp.kW, *Ai = S + kp.kAi, *qv = S + kp.kq;
@@ -1065,8 +1069,9 @@ __device__ __noinline__ void qpid_task_extras(const DevModel* M, const KParams& 
       }
     }
     vf[l] = v;
-    // self-collision grad_dot term of this column
-    if (besti < M->npairs && (arm & (1u << l))) {
+    // self-collision grad_dot of this column (robot_data.cpp:496-512)
+    double gcol = 0;
+    if (besti < M->npairs && (full || (arm & (1u << l)))) {
       const V3 pA = ld3(red), pB = ld3(red + 3);
       V3 n = pB - pA;
       n = (1.0 / sqrt(dot(n, n))) * n;
@@ -1091,8 +1096,10 @@ __device__ __noinline__ void qpid_task_extras(const DevModel* M, const KParams& 
         const V3 r = pX - oX, rd = cross(wX, r);
         jdx[s_] = ld - (cross(rd, ca) + cross(r, ad));
       }
-      dsum = qd[l] * dot(n, jdx[1] - jdx[0]);
+      gcol = dot(n, jdx[1] - jdx[0]);
+      if (arm & (1u << l)) dsum = qd[l] * gcol;
     }
+    if (full) S[kp.kGdv + narm + l] = gcol;
   }
   const double dist_gd = wave_sum(dsum);
   (void)bestd;
@@ -1132,6 +1139,56 @@ __device__ __noinline__ void qpid_task_extras(const DevModel* M, const KParams& 
   if (l == 0) {
     out[6] = mdot * t2 + m * (t3 - 2.0 * t4);
     out[7] = dist_gd;
+  }
+  if (full) {
+    // grad_dot_k = mdot tr(dJ_k Ja^T Ai) + m tr(dJ_k (Jda^T Ai + Ja^T Ai_dot)),
+    // Ja^T Ai_dot = -2 W (Jda W) = -2 W X2; lane per (k, c) builds dJ_k[:, c]
+    // (the manipulability gradient's closed form) and dots it with the rows.
+    double* Y = X + 72;  // narm x 6: Jda^T Ai - 2 W X2
+    for (int e = l; e < narm * 6; e += 64) {
+      const int c = e / 6, a = e % 6;
+      double y = 0;
+      for (int b_ = 0; b_ < 6; ++b_) y += Jd[b_ * nv + c0 + c] * Ai[b_ * 6 + a] - 2.0 * W[c * 6 + b_] * X[36 + b_ * 6 + a];
+      Y[e] = y;
+    }
+    wsync();
+    double* part = X + 72 + 6 * narm;  // narm x narm x 2
+    for (int e = l; e < narm * narm; e += 64) {
+      const int kk = e / narm, c = e % narm, jk = c0 + kk + 1, ji = c0 + c + 1;
+      double p1 = 0, p2 = 0;
+      if ((anc_e & (1u << (jk - 1))) && (anc_e & (1u << (ji - 1)))) {
+        const V3 zk = ld3(Zw + 3 * jk), zi = ld3(Zw + 3 * ji);
+        const V3 pk_ = v3(T[12 * jk + 9], T[12 * jk + 10], T[12 * jk + 11]);
+        const V3 pi_ = v3(T[12 * ji + 9], T[12 * ji + 10], T[12 * ji + 11]);
+        const bool krev = M->jtype[jk] == kRevolute;
+        const V3 dpe = krev ? cross(zk, pe - pk_) : zk;
+        const bool moves_i = jk != ji && (M->anc[ji] & (1u << (jk - 1)));
+        const V3 dzi = (moves_i && krev) ? cross(zk, zi) : v3(0, 0, 0);
+        const V3 dpi = moves_i ? (krev ? cross(zk, pi_ - pk_) : zk) : v3(0, 0, 0);
+        V3 lin, ang;
+        if (M->jtype[ji] == kRevolute) {
+          lin = cross(dzi, pe - pi_) + cross(zi, dpe - dpi);
+          ang = dzi;
+        } else {
+          lin = dzi;
+          ang = v3(0, 0, 0);
+        }
+        const double *w = W + c * 6, *y = Y + c * 6;
+        p1 = lin.x * w[0] + lin.y * w[1] + lin.z * w[2] + ang.x * w[3] + ang.y * w[4] + ang.z * w[5];
+        p2 = lin.x * y[0] + lin.y * y[1] + lin.z * y[2] + ang.x * y[3] + ang.y * y[4] + ang.z * y[5];
+      }
+      part[2 * e] = p1;
+      part[2 * e + 1] = p2;
+    }
+    wsync();
+    if (l < narm) {
+      double s1 = 0, s2 = 0;
+      for (int c = 0; c < narm; ++c) {
+        s1 += part[2 * (l * narm + c)];
+        s2 += part[2 * (l * narm + c) + 1];
+      }
+      S[kp.kGdv + l] = mdot * s1 + m * s2;
+    }
   }
   wsync();
 }
@@ -1603,7 +1660,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRC_TAS
       dgv[l] = g;
     }
     wsync();
-    if constexpr (PROBLEM == 1) qpid_task_extras(M, kp, S, bestd, besti);
+    if constexpr (PROBLEM == 1) qpid_task_extras(M, kp, S, bestd, besti, io.st_gdv != nullptr);
     PH(7);
 #ifdef DRC_PHASE_TIMING
     if (l == 0) {  // straggler census: max instance cycles, count above 2M
@@ -1659,6 +1716,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRC_TAS
         if (io.st_jdot)
           for (int e = l; e < 6 * nv; e += 64) io.st_jdot[(int64_t)e * LD + gb] = S[kp.kJd + e];
         if (io.st_qpid && l < 8) io.st_qpid[l * LD + gb] = S[kp.kBias + l];
+        if (io.st_gdv)
+          for (int e = l; e < narm + nv; e += 64) io.st_gdv[(int64_t)e * LD + gb] = S[kp.kGdv + e];
       }
     }
     wsync();
@@ -2630,7 +2689,8 @@ static int plan_layout(const DevModel& M, KParams* k, bool task_only) {
     k->kJd = takeu(6 * nv);
     k->kDa = takeu(6 * k->narm);
     k->kVf = takeu(nv);
-    k->kX6 = takeu(72);
+    k->kX6 = takeu(72 + 6 * k->narm + 2 * k->narm * k->narm);
+    k->kGdv = takeu(k->narm + nv);
     k->kBias = takeu(8);
     k->kMq = takeu(k->na * k->na);
     k->kGq = takeu(k->na);
@@ -2857,7 +2917,7 @@ static int launch_qpid(const drc_model_impl* cm, const drc_qpik_params* params, 
                        const double* q, const double* qdot, const double* xt, const double* xdt, const double* xi,
                        const double* xdi, double* qdd, double* tau, int32_t* status, int32_t* iters, double* pose,
                        double* jac, double* man, double* dist, int32_t* pair, double* xdd, double* jdot,
-                       double* qpid_st, void* stream) {
+                       double* qpid_st, double* gdv, void* stream) {
   drc_model_impl* m = const_cast<drc_model_impl*>(cm);
   if (!m || !params) return set_err(DRC_ERR_INVALID_ARGUMENT, "null model/params");
   if (B < 0) return set_err(DRC_ERR_INVALID_ARGUMENT, "negative batch");
@@ -2911,6 +2971,7 @@ static int launch_qpid(const drc_model_impl* cm, const drc_qpik_params* params, 
   io.out2 = tau;
   io.st_jdot = jdot;
   io.st_qpid = qpid_st;
+  io.st_gdv = gdv;
   hipLaunchKernelGGL(task_kernel<1>, dim3(static_cast<unsigned>(grid)), dim3(64),
                      static_cast<size_t>(kt_c.lds_doubles) * sizeof(double), st, m->d_model, kt_c, io);
   HIP_TRY(hipGetLastError());
@@ -3205,15 +3266,66 @@ int drc_qpid_batch(const drc_model* m, const drc_qpik_params* p, int64_t B, cons
                    const double* xt, const double* xdt, const double* xi, const double* xdi, double* qddot_out,
                    double* tau_out, int32_t* status, int32_t* iters, void* stream) {
   return drc_amd::launch_qpid(m, p, 0, B, q, qdot, xt, xdt, xi, xdi, qddot_out, tau_out, status, iters, nullptr,
-                              nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, stream);
+                              nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, stream);
 }
 
 int drc_qpid_stages_batch(const drc_model* m, const drc_qpik_params* p, int64_t B, const double* q,
                           const double* qdot, const double* xt, const double* xdt, const double* xi,
                           const double* xdi, double* pose, double* jac, double* man, double* dist, int32_t* pair,
-                          double* xddot_des, double* jdot, double* qpid_terms, void* stream) {
+                          double* xddot_des, double* jdot, double* qpid_terms, double* graddot, void* stream) {
   return drc_amd::launch_qpid(m, p, 1, B, q, qdot, xt, xdt, xi, xdi, nullptr, nullptr, nullptr, nullptr, pose, jac,
-                              man, dist, pair, xddot_des, jdot, qpid_terms, stream);
+                              man, dist, pair, xddot_des, jdot, qpid_terms, graddot, stream);
+}
+
+int drc_qpid_stages_host(drc_model* m, const drc_qpik_params* p, int64_t B, const double* q, const double* qdot,
+                         const double* xt, const double* xdt, const double* xi, const double* xdi, double* pose,
+                         double* jac, double* man, double* dist, int32_t* pair, double* xddot_des, double* jdot,
+                         double* qpid_terms, double* graddot) {
+  using drc_amd::set_err;
+  if (!m || !p) return set_err(DRC_ERR_INVALID_ARGUMENT, "null model/params");
+  if (B <= 0) return B == 0 ? DRC_OK : set_err(DRC_ERR_INVALID_ARGUMENT, "negative batch");
+  const drc_amd::DevModel& d = m->hm.dev;
+  const int64_t n = d.nv, na = d.kind == 1 ? d.n_arm : n;
+  std::lock_guard<std::mutex> lk(m->host_mu);
+  HIP_TRY(hipSetDevice(m->device));
+  const double* src[6] = {q, qdot, xt, xdt, xi, xdi};
+  const int64_t rin[6] = {n, n, 12, 6, 12, 6};
+  double* outs[8] = {pose, jac, man, dist, xddot_des, jdot, qpid_terms, graddot};
+  const int64_t rout[8] = {12, 6 * n, 1 + na, 1 + n, 6, 6 * n, 8, na + n};
+  int64_t words = (B + 1) / 2;
+  for (int i = 0; i < 6; ++i) words += src[i] ? rin[i] * B : 0;
+  for (int i = 0; i < 8; ++i) words += outs[i] ? rout[i] * B : 0;
+  if (m->stage_bytes < words * 8) {
+    if (m->stage) (void)hipFree(m->stage);
+    m->stage = nullptr;
+    m->stage_bytes = 0;
+    HIP_TRY(hipMalloc(&m->stage, words * 8));
+    m->stage_bytes = words * 8;
+  }
+  if (!m->hstream) HIP_TRY(hipStreamCreateWithFlags(&m->hstream, hipStreamNonBlocking));
+  double* dp = reinterpret_cast<double*>(m->stage);
+  const double* din[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  for (int i = 0; i < 6; ++i)
+    if (src[i]) {
+      HIP_TRY(hipMemcpyAsync(dp, src[i], rin[i] * B * 8, hipMemcpyHostToDevice, m->hstream));
+      din[i] = dp;
+      dp += rin[i] * B;
+    }
+  double* dout[8] = {nullptr};
+  for (int i = 0; i < 8; ++i)
+    if (outs[i]) {
+      dout[i] = dp;
+      dp += rout[i] * B;
+    }
+  int32_t* dpair = pair ? reinterpret_cast<int32_t*>(dp) : nullptr;
+  int rc = drc_qpid_stages_batch(m, p, B, din[0], din[1], din[2], din[3], din[4], din[5], dout[0], dout[1], dout[2],
+                                 dout[3], dpair, dout[4], dout[5], dout[6], dout[7], m->hstream);
+  if (rc) return rc;
+  for (int i = 0; i < 8; ++i)
+    if (outs[i]) HIP_TRY(hipMemcpyAsync(outs[i], dout[i], rout[i] * B * 8, hipMemcpyDeviceToHost, m->hstream));
+  if (pair) HIP_TRY(hipMemcpyAsync(pair, dpair, B * 4, hipMemcpyDeviceToHost, m->hstream));
+  HIP_TRY(hipStreamSynchronize(m->hstream));
+  return DRC_OK;
 }
 
 // ---- host-buffer entry points (synchronous; staged through device memory) --

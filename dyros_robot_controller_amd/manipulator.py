@@ -152,18 +152,47 @@ class RobotData:
     def getVelocity(self, link_name):
         return self.getJacobian(link_name) @ self.qdot_
 
+    def _qpid_stages(self, q, qdot, link_name):
+        """QPID stage outputs (Jdot, grad_dot vectors) at (q, qdot) for one robot."""
+        pb = QPIKParamsBuilder(self.model, exact=True, qpid=True)
+        p = pb.params(link_name, mode=_capi.MODE_QPID) if link_name else pb.params_no_frame(_capi.MODE_QPID)
+        dq = _batch.as_device(np.asarray(q, float).reshape(-1, 1), self.device)
+        dqd = _batch.as_device(np.asarray(qdot, float).reshape(-1, 1), self.device)
+        z6 = _batch.as_device(np.zeros((6, 1)), self.device)
+        st = _batch.qpid_stages_batch(self.model, p, dq, dqd, None, z6)
+        return {k: v.cpu().numpy()[..., 0] for k, v in st.items()}
+
     def getManipulability(self, with_grad=True, with_graddot=False, link_name=None):
+        """robot_data.cpp:519-573 (grad_dot: :555-569, through the QPID stage)."""
         if with_graddot:
-            raise NotImplementedError("grad_dot is outside the QPIK hot path (SURVEY §8f)")
+            st = self._qpid_stages(self.q_, self.qdot_, link_name)
+            r = ManipulabilityResult(st["man"][0], st["man"][1:])
+            r.grad_dot = st["man_graddot"].copy()
+            return r
         st = self._stages(self.q_, self.qdot_, link_name)
         return ManipulabilityResult(st["man"][0], st["man"][1:] if with_grad else np.zeros(self.getDof()))
 
     def getMinDistance(self, with_grad=True, with_graddot=False, verbose=False):
+        """robot_data.cpp:424-517 (grad_dot: :496-512, through the QPID stage)."""
         if with_graddot:
-            raise NotImplementedError("grad_dot is outside the QPIK hot path (SURVEY §8f)")
-        st = self._stages(self.q_, self.qdot_, None)  # no task frame needed
-        return MinDistResult(st["dist"][0], st["dist"][1:] if with_grad else np.zeros(self.getDof()))
+            st = self._qpid_stages(self.q_, self.qdot_, None)
+            r = MinDistResult(st["dist"][0], st["dist"][1:])
+            r.grad_dot = st["dist_graddot"].copy()
+        else:
+            st = self._stages(self.q_, self.qdot_, None)  # no task frame needed
+            r = MinDistResult(st["dist"][0], st["dist"][1:] if with_grad else np.zeros(self.getDof()))
+        if verbose:
+            print("[RobotDataBase] closest pair %d | distance = %g [m]" % (int(st["pair"]), r.distance))
+        return r
 
+    def computeJacobianTimeVariation(self, q, qdot, link_name):
+        """LOCAL_WORLD_ALIGNED dJ/dt (robot_data.cpp:404-417)."""
+        return self._qpid_stages(q, qdot, link_name)["jdot"].reshape(6, self.getDof())
+
+    def getJacobianTimeVariation(self, link_name):
+        return self.computeJacobianTimeVariation(self.q_, self.qdot_, link_name)
+
+    get_jacobian_time_variation, compute_jacobian_time_variation = getJacobianTimeVariation, computeJacobianTimeVariation
     get_pose, get_jacobian, get_velocity = getPose, getJacobian, getVelocity
     get_manipulability, get_min_distance = getManipulability, getMinDistance
     compute_pose, compute_jacobian, compute_velocity = computePose, computeJacobian, computeVelocity

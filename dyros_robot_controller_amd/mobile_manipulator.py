@@ -206,15 +206,61 @@ class RobotData:
     def get_jacobian(self, link_name):
         return self._stages(link_name)["jac"][:, 0].reshape(6, self.get_dof())
 
+    def _qpid_stages(self, link_name):
+        pb = QPIKParamsBuilder(self.model, exact=True, qpid=True)
+        p = pb.params(link_name, mode=_capi.MODE_QPID) if link_name else pb.params_no_frame(_capi.MODE_QPID)
+        dev = self.device
+        st = _batch.qpid_stages_batch(self.model, p, _batch.as_device(self.q_.reshape(-1, 1), dev),
+                                      _batch.as_device(self.qdot_.reshape(-1, 1), dev), None,
+                                      _batch.as_device(np.zeros((6, 1)), dev))
+        return {k: v.cpu().numpy()[..., 0] for k, v in st.items()}
+
     def get_manipulability(self, with_grad, with_graddot, link_name):
+        """Arm-block manipulability (robot_data.cpp:439-496)."""
         from .manipulator import ManipulabilityResult
+        n = self.get_manipulator_dof()
+        if with_graddot:
+            st = self._qpid_stages(link_name)
+            r = ManipulabilityResult(st["man"][0], st["man"][1:])
+            r.grad_dot = st["man_graddot"].copy()
+            return r
         m = self._stages(link_name)["man"][:, 0]
-        return ManipulabilityResult(m[0], m[1:] if with_grad else None)
+        return ManipulabilityResult(m[0], m[1:] if with_grad else np.zeros(n))
 
     def get_min_distance(self, with_grad, with_graddot, verbose=False):
         from .manipulator import MinDistResult
+        if with_graddot:
+            st = self._qpid_stages(None)
+            r = MinDistResult(st["dist"][0], st["dist"][1:])
+            r.grad_dot = st["dist_graddot"].copy()
+            return r
         d = self._stages(None)["dist"][:, 0]
-        return MinDistResult(d[0], d[1:] if with_grad else None)
+        return MinDistResult(d[0], d[1:] if with_grad else np.zeros(self.get_dof()))
+
+    def get_selection_matrix(self):
+        """S (dof x A): identity on the arm and wheel blocks, Rz(yaw) J_mobile
+        on the virtual block (robot_data.cpp:22-25,115-120)."""
+        ji, ai = self.get_joint_index(), self.get_actuator_index()
+        n, W = self.get_manipulator_dof(), self.get_mobile_dof()
+        S = np.zeros((self.get_dof(), n + W))
+        S[ji.mani_start:ji.mani_start + n, ai.mani_start:ai.mani_start + n] = np.eye(n)
+        S[ji.mobi_start:ji.mobi_start + W, ai.mobi_start:ai.mobi_start + W] = np.eye(W)
+        c, s_ = np.cos(self.q_[ji.virtual_start + 2]), np.sin(self.q_[ji.virtual_start + 2])
+        S[ji.virtual_start:ji.virtual_start + 3, ai.mobi_start:ai.mobi_start + W] = (
+            np.array([[c, -s_, 0], [s_, c, 0], [0, 0, 1]]) @ self.get_mobile_FK_jacobian())
+        return S
+
+    def get_jacobian_time_variation(self, link_name):
+        """LOCAL_WORLD_ALIGNED dJ/dt at the full (q, qdot) (robot_data.cpp:404-417)."""
+        return self._qpid_stages(link_name)["jdot"].reshape(6, self.get_dof())
+
+    def get_jacobian_actuated(self, link_name):
+        """J S (robot_data.cpp:407-410)."""
+        return self.get_jacobian(link_name) @ self.get_selection_matrix()
+
+    def get_jacobian_actuated_time_variation(self, link_name):
+        """Jdot S, Sdot neglected (robot_data.cpp:412-415)."""
+        return self.get_jacobian_time_variation(link_name) @ self.get_selection_matrix()
 
     # -- dynamics (robot_data.cpp:126-144; getters robot_data.h:425-445) --------
     def _dynamics(self, q, qdot, actuated):

@@ -283,14 +283,20 @@ int drc_qpid_batch(const drc_model* model, const drc_qpik_params* params, int64_
                    const double* xdot_target, const double* x_init, const double* xdot_init,
                    double* qddot_out, double* tau_out, int32_t* status, int32_t* iters, void* stream);
 /* Stage outputs of the QPID task stage: as drc_qpik_stages_batch (xddot_des = the QP's task
- * acceleration), plus jdot [6*dof][B] (getJacobianTimeVariation, LWA, robot_data.cpp:404-417) and
- * qpid_terms [8][B] = (Jdot v (6) with v = qdot or S eta, grad_dot_m . qdot_arm, grad_dot_d . qdot_arm).
- * Any output may be NULL. */
+ * acceleration), plus jdot [6*dof][B] (getJacobianTimeVariation, LWA, robot_data.cpp:404-417),
+ * qpid_terms [8][B] = (Jdot v (6) with v = qdot or S eta, grad_dot_m . qdot_arm, grad_dot_d . qdot_arm) and
+ * graddot [mani + dof][B] = the grad_dot vectors of getManipulability(true, true) (robot_data.cpp:555-569;
+ * MoMa :477-492) and getMinDistance(true, true) (:496-512).  Any output may be NULL. */
 int drc_qpid_stages_batch(const drc_model* model, const drc_qpik_params* params, int64_t B,
                           const double* q, const double* qdot, const double* x_target,
                           const double* xdot_target, const double* x_init, const double* xdot_init,
                           double* pose, double* jac, double* man, double* dist, int32_t* pair,
-                          double* xddot_des, double* jdot, double* qpid_terms, void* stream);
+                          double* xddot_des, double* jdot, double* qpid_terms, double* graddot, void* stream);
+int drc_qpid_stages_host(drc_model* model, const drc_qpik_params* params, int64_t B,
+                         const double* q, const double* qdot, const double* x_target,
+                         const double* xdot_target, const double* x_init, const double* xdot_init,
+                         double* pose, double* jac, double* man, double* dist, int32_t* pair,
+                         double* xddot_des, double* jdot, double* qpid_terms, double* graddot);
 /* Host-buffer form of drc_qpid_batch (synchronous, PCIe-inclusive). */
 int drc_qpid_host(drc_model* model, const drc_qpik_params* params, int64_t B,
                   const double* q, const double* qdot, const double* x_target,

@@ -123,6 +123,26 @@ class ModelBase {
     s.pair = pair;
     return s;
   }
+  // QPID stage outputs at (q, qdot): frame Jacobian time variation (6 x dof,
+  // row-major) and the grad_dot vectors of getManipulability / getMinDistance
+  struct QpidStages {
+    Vec jdot, man_graddot, dist_graddot;
+  };
+  QpidStages qpidStages(const Vec& q, const Vec& qdot, const std::string& link) const {
+    drc_qpik_params p;
+    check(drc_default_qpid_params(model_, 1, &p));
+    p.mode = DRC_MODE_QPID;
+    p.frame_id = link.empty() ? -1 : frameId(link);
+    QpidStages s;
+    s.jdot.resize(6 * dof_);
+    Vec gdv(mani_ + dof_), zero6(6, 0.0);
+    check(drc_qpid_stages_host(model_, &p, 1, q.data(), qdot.data(), nullptr, zero6.data(), nullptr, nullptr,
+                               nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, s.jdot.data(), nullptr,
+                               gdv.data()));
+    s.man_graddot.assign(gdv.begin(), gdv.begin() + mani_);
+    s.dist_graddot.assign(gdv.begin() + mani_, gdv.end());
+    return s;
+  }
 
  protected:
   ModelBase() = default;
@@ -172,23 +192,26 @@ class RobotData : public ModelBase {
     return v;
   }
   ManipulabilityResult getManipulability(bool with_grad, bool with_graddot, const std::string& link) const {
-    if (with_graddot) throw std::runtime_error("grad_dot is outside the QPIK path");
     Stages s = stages(q_, qdot_, link);
     ManipulabilityResult r;
     r.manipulability = s.man[0];
-    r.grad = with_grad ? Vec(s.man.begin() + 1, s.man.end()) : Vec(mani_, 0.0);
-    r.grad_dot.assign(mani_, 0.0);
+    r.grad = (with_grad || with_graddot) ? Vec(s.man.begin() + 1, s.man.end()) : Vec(mani_, 0.0);
+    r.grad_dot = with_graddot ? qpidStages(q_, qdot_, link).man_graddot : Vec(mani_, 0.0);
     return r;
   }
   MinDistResult getMinDistance(bool with_grad, bool with_graddot, bool verbose = false) const {
-    if (with_graddot) throw std::runtime_error("grad_dot is outside the QPIK path");
     Stages s = stages(q_, qdot_, "");
     MinDistResult r;
     r.distance = s.dist[0];
-    r.grad = with_grad ? Vec(s.dist.begin() + 1, s.dist.end()) : Vec(dof_, 0.0);
-    r.grad_dot.assign(dof_, 0.0);
+    r.grad = (with_grad || with_graddot) ? Vec(s.dist.begin() + 1, s.dist.end()) : Vec(dof_, 0.0);
+    r.grad_dot = with_graddot ? qpidStages(q_, qdot_, "").dist_graddot : Vec(dof_, 0.0);
     if (verbose) std::cout << "min distance " << r.distance << " (pair " << s.pair << ")\n";
     return r;
+  }
+  // getJacobianTimeVariation / computeJacobianTimeVariation (robot_data.cpp:404-417), 6 x dof row-major
+  Vec getJacobianTimeVariation(const std::string& link) const { return qpidStages(q_, qdot_, link).jdot; }
+  Vec computeJacobianTimeVariation(const Vec& q, const Vec& qdot, const std::string& link) const {
+    return qpidStages(q, qdot, link).jdot;
   }
 };
 
@@ -197,25 +220,30 @@ class RobotData : public ModelBase {
 // Shared by both controllers: gains, solver mode, batched entries.
 class ControllerBase {
  public:
+  // task gains are shared by QPIK and QPID, as the reference's Kp_task_ / Kv_task_
+  // (a MoMa QPIKStep has no Kv term: its parameters keep kv = 0)
   void setTaskGain(const Vec& Kp, const Vec& Kv) {
     if (Kp.size() != 6 || Kv.size() != 6) throw std::runtime_error("Kp and Kv must be of size 6.");
-    for (int i = 0; i < 6; ++i) {
-      params_.kp[i] = Kp[i];
-      params_.kv[i] = Kv[i];
-    }
+    setTaskKpGain(Kp);
+    setTaskKvGain(Kv);
   }
   void setTaskKpGain(const Vec& Kp) {
     if (Kp.size() != 6) throw std::runtime_error("Kp must be of size 6.");
-    for (int i = 0; i < 6; ++i) params_.kp[i] = Kp[i];
+    for (int i = 0; i < 6; ++i) params_.kp[i] = id_params_.kp[i] = Kp[i];
   }
   void setTaskKvGain(const Vec& Kv) {
     if (Kv.size() != 6) throw std::runtime_error("Kv must be of size 6.");
-    for (int i = 0; i < 6; ++i) params_.kv[i] = Kv[i];
+    for (int i = 0; i < 6; ++i) {
+      id_params_.kv[i] = Kv[i];
+      if (params_.feedforward == 0) params_.kv[i] = Kv[i];
+    }
   }
   // "exact" (certified optimum, default) or reference OSQP settings
   void setExact(bool exact) {
     drc_qpik_params d = model_->defaultParams(exact);
     params_.solver = d.solver;
+    check(drc_default_qpid_params(model_->handle(), exact ? 1 : 0, &d));
+    id_params_.solver = d.solver;
   }
   const drc_qpik_params& params() const { return params_; }
   int actuatedDof() const { return model_->getActuatorDof(); }
@@ -239,10 +267,45 @@ class ControllerBase {
       check(drc_qpik_host(model_->handle(), &p, B, q, qdot, x_target, xdot_target, x_init, xdot_init, eta_out,
                           status, iters));
   }
+  // Batched QPID* (drc_qpid_batch): qddot / eta_dot and torques [A][B].
+  void QPIDBatch(int mode, int64_t B, const double* q, const double* qdot, const double* x_target,
+                 const double* xdot_target, const double* x_init, const double* xdot_init, double t, double t0,
+                 double duration, const std::string& link, double* qddot_out, double* tau_out, int32_t* status,
+                 bool device, void* stream = nullptr, int32_t* iters = nullptr) const {
+    drc_qpik_params p = id_params_;
+    p.mode = mode;
+    p.frame_id = model_->frameId(link);
+    p.t = t;
+    p.t0 = t0;
+    p.duration = duration;
+    if (device)
+      check(drc_qpid_batch(model_->handle(), &p, B, q, qdot, x_target, xdot_target, x_init, xdot_init, qddot_out,
+                           tau_out, status, iters, stream));
+    else
+      check(drc_qpid_host(model_->handle(), &p, B, q, qdot, x_target, xdot_target, x_init, xdot_init, qddot_out,
+                          tau_out, status, iters));
+  }
 
  protected:
   ControllerBase(double dt, const ModelBase* model) : dt_(dt), model_(model) {
     params_ = model_->defaultParams(true);
+    check(drc_default_qpid_params(model_->handle(), 1, &id_params_));
+  }
+  // one QPID instance at the model's stored state; tau = gravity on failure
+  // (the kernel writes it), stderr message as the reference
+  void solveOneID(int mode, const Pose* xt, const Vec* xdt, const Pose* xi, const Vec* xdi, double t, double t0,
+                  double T, const std::string& link, Vec& qdd, Vec& tau) const {
+    const int A = model_->getActuatorDof();
+    std::array<double, 12> xt12{}, xi12{};
+    if (xt) xt12 = pose12(*xt);
+    if (xi) xi12 = pose12(*xi);
+    qdd.assign(A, 0.0);
+    tau.assign(A, 0.0);
+    int32_t status = 0;
+    QPIDBatch(mode, 1, model_->getJointPosition().data(), model_->getJointVelocity().data(),
+              xt ? xt12.data() : nullptr, xdt->data(), xi ? xi12.data() : nullptr, xdi ? xdi->data() : nullptr, t, t0,
+              T, link, qdd.data(), tau.data(), &status, false);
+    if (status != DRC_STATUS_SOLVED) std::cerr << "QP ID failed to compute optimal joint torque." << std::endl;
   }
   // one instance at the model's stored state; zeros + stderr on failure
   Vec solveOne(int mode, const Pose* xt, const Vec* xdt, const Pose* xi, const Vec* xdi, double t, double t0,
@@ -267,7 +330,7 @@ class ControllerBase {
   }
   double dt_;
   const ModelBase* model_;
-  drc_qpik_params params_;
+  drc_qpik_params params_, id_params_;
 };
 
 namespace Manipulator {
@@ -290,6 +353,28 @@ class RobotController : public ControllerBase {
     check6(xdot_init);
     return solveOne(DRC_MODE_QPIK_CUBIC, &x_target, &xdot_target, &x_init, &xdot_init, current_time, init_time,
                     duration, link);
+  }
+  // QPID / QPIDStep / QPIDCubic (robot_controller.cpp:319-361): joint torques
+  Vec QPID(const Vec& xddot_target, const std::string& link) const {
+    check6(xddot_target);
+    Vec qdd, tau;
+    solveOneID(DRC_MODE_QPID, nullptr, &xddot_target, nullptr, nullptr, 0, 0, 1, link, qdd, tau);
+    return tau;
+  }
+  Vec QPIDStep(const Pose& x_target, const Vec& xdot_target, const std::string& link) const {
+    check6(xdot_target);
+    Vec qdd, tau;
+    solveOneID(DRC_MODE_QPID_STEP, &x_target, &xdot_target, nullptr, nullptr, 0, 0, 1, link, qdd, tau);
+    return tau;
+  }
+  Vec QPIDCubic(const Pose& x_target, const Vec& xdot_target, const Pose& x_init, const Vec& xdot_init,
+                double current_time, double init_time, double duration, const std::string& link) const {
+    check6(xdot_target);
+    check6(xdot_init);
+    Vec qdd, tau;
+    solveOneID(DRC_MODE_QPID_CUBIC, &x_target, &xdot_target, &x_init, &xdot_init, current_time, init_time, duration,
+               link, qdd, tau);
+    return tau;
   }
 
  private:
@@ -343,15 +428,24 @@ class RobotData : public ModelBase {
   Pose getPose(const std::string& link) const { return pose44(stages(q_, qdot_, link).pose.data()); }
   Vec getJacobian(const std::string& link) const { return stages(q_, qdot_, link).jac; }
   MinDistResult getMinDistance(bool with_grad, bool with_graddot, bool verbose = false) const {
-    if (with_graddot) throw std::runtime_error("grad_dot is outside the QPIK path");
     Stages s = stages(q_, qdot_, "");
     MinDistResult r;
     r.distance = s.dist[0];
-    r.grad = with_grad ? Vec(s.dist.begin() + 1, s.dist.end()) : Vec(dof_, 0.0);
-    r.grad_dot.assign(dof_, 0.0);
+    r.grad = (with_grad || with_graddot) ? Vec(s.dist.begin() + 1, s.dist.end()) : Vec(dof_, 0.0);
+    r.grad_dot = with_graddot ? qpidStages(q_, qdot_, "").dist_graddot : Vec(dof_, 0.0);
     if (verbose) std::cout << "min distance " << r.distance << " (pair " << s.pair << ")\n";
     return r;
   }
+  // arm-block manipulability (robot_data.cpp:439-496)
+  ManipulabilityResult getManipulability(bool with_grad, bool with_graddot, const std::string& link) const {
+    Stages s = stages(q_, qdot_, link);
+    ManipulabilityResult r;
+    r.manipulability = s.man[0];
+    r.grad = (with_grad || with_graddot) ? Vec(s.man.begin() + 1, s.man.end()) : Vec(mani_, 0.0);
+    r.grad_dot = with_graddot ? qpidStages(q_, qdot_, link).man_graddot : Vec(mani_, 0.0);
+    return r;
+  }
+  Vec getJacobianTimeVariation(const std::string& link) const { return qpidStages(q_, qdot_, link).jdot; }
 
  private:
   JointIndex jidx_;
@@ -382,8 +476,38 @@ class RobotController : public ControllerBase {
                    duration, link),
           qdot_mobile, qdot_mani);
   }
+  // QPID / QPIDStep / QPIDCubic (robot_controller.cpp:199-250): (qddot_mobile, torque_arm)
+  void QPID(const Vec& xddot_target, const std::string& link, Vec& qddot_mobile, Vec& torque_mani) const {
+    check6(xddot_target);
+    Vec qdd, tau;
+    solveOneID(DRC_MODE_QPID, nullptr, &xddot_target, nullptr, nullptr, 0, 0, 1, link, qdd, tau);
+    splitID(qdd, tau, qddot_mobile, torque_mani);
+  }
+  void QPIDStep(const Pose& x_target, const Vec& xdot_target, const std::string& link, Vec& qddot_mobile,
+                Vec& torque_mani) const {
+    check6(xdot_target);
+    Vec qdd, tau;
+    solveOneID(DRC_MODE_QPID_STEP, &x_target, &xdot_target, nullptr, nullptr, 0, 0, 1, link, qdd, tau);
+    splitID(qdd, tau, qddot_mobile, torque_mani);
+  }
+  void QPIDCubic(const Pose& x_target, const Vec& xdot_target, const Pose& x_init, const Vec& xdot_init,
+                 double current_time, double init_time, double duration, const std::string& link, Vec& qddot_mobile,
+                 Vec& torque_mani) const {
+    check6(xdot_target);
+    check6(xdot_init);
+    Vec qdd, tau;
+    solveOneID(DRC_MODE_QPID_CUBIC, &x_target, &xdot_target, &x_init, &xdot_init, current_time, init_time, duration,
+               link, qdd, tau);
+    splitID(qdd, tau, qddot_mobile, torque_mani);
+  }
 
  private:
+  void splitID(const Vec& qdd, const Vec& tau, Vec& qddot_mobile, Vec& torque_mani) const {
+    const ActuatorIndex& a = robot_data_->getActuatorIndex();
+    const int W = robot_data_->getMobileDof(), n = robot_data_->getManipulatorDof();
+    qddot_mobile.assign(qdd.begin() + a.mobi_start, qdd.begin() + a.mobi_start + W);
+    torque_mani.assign(tau.begin() + a.mani_start, tau.begin() + a.mani_start + n);
+  }
   void split(const Vec& eta, Vec& qdot_mobile, Vec& qdot_mani) const {
     const ActuatorIndex& a = robot_data_->getActuatorIndex();
     const int W = robot_data_->getMobileDof(), n = robot_data_->getManipulatorDof();

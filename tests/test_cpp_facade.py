@@ -25,11 +25,13 @@ METHODS = {
                              "getJacobian", "getVelocity", "getManipulability", "getMinDistance",
                              "getJointPositionLimit", "getJointVelocityLimit"],
     "ManipulatorRobotController": ["setTaskGain", "setTaskKpGain", "setTaskKvGain", "QPIK", "QPIKStep", "QPIKCubic",
-                                   "QPIKBatch", "QPIKStepBatch", "QPIKCubicBatch"],
+                                   "QPIKBatch", "QPIKStepBatch", "QPIKCubicBatch", "QPID", "QPIDStep", "QPIDCubic",
+                                   "QPIDBatch", "QPIDStepBatch", "QPIDCubicBatch"],
     "MobileManipulatorRobotData": ["getVerbose", "updateState", "getDof", "getActuatorDof", "getManipulatorDof",
                                    "getMobileDof", "getJointIndex", "getActuatorIndex", "getMobileFKJacobian",
                                    "getMinDistance"],
-    "MobileManipulatorRobotController": ["setTaskGain", "QPIK", "QPIKStep", "QPIKCubic", "QPIKStepBatch"],
+    "MobileManipulatorRobotController": ["setTaskGain", "QPIK", "QPIKStep", "QPIKCubic", "QPIKStepBatch",
+                                         "QPID", "QPIDStep", "QPIDCubic", "QPIDStepBatch"],
 }
 
 
@@ -132,3 +134,34 @@ def test_reference_style_subclassing(cuda):
     assert rd.get_dof() == 7
     rd.updateState(np.zeros(7) + 0.1, np.zeros(7))
     assert rc.QPIK(np.zeros(6), "fr3_link8").shape == (7,)
+
+
+@pytest.mark.gpu
+def test_module_qpid_step_and_graddot(cuda):
+    """QPIDStep (single instance and batch) through the pybind11 module, and
+    getManipulability / getMinDistance with grad_dot and
+    getJacobianTimeVariation, against the oracle."""
+    import oracle as O
+    from _common import step_inputs, make_manipulator
+    from dyros_robot_controller_amd import robot_path
+    from dyros_robot_controller_amd.manipulator import pose_from12
+    drc = _module()
+    rd = drc.ManipulatorRobotData(robot_path("fr3"), robot_path("fr3", "srdf"))
+    rc = drc.ManipulatorRobotController(0.001, rd)
+    q, qd, xt, xdt = step_inputs(make_manipulator("fr3", cuda), "fr3", 41, 8, cuda)
+    qdd, tau, status = rc.QPIDStepBatch(q, qd, xt, xdt, "fr3_link8")
+    pm, om, spec = O.load("fr3")
+    par = O.default_qpid_params(0, exact=True)
+    for b in range(8):
+        M, g, gf = O.qpid_dynamics(pm, om, spec, q[:, b], qd[:, b])
+        st, rq, rt, dg = O.qpid_one(om, par, q[:, b], qd[:, b], M, g, gf, xt[:, b], xdt[:, b])
+        assert status[b] == st
+        np.testing.assert_allclose(tau[:, b], rt, rtol=1e-5, atol=1e-6)
+        assert rd.updateState(q[:, b], qd[:, b])
+        np.testing.assert_allclose(rc.QPIDStep(pose_from12(xt[:, b]), xdt[:, b], "fr3_link8"), rt, rtol=1e-5, atol=1e-6)
+        Jd, mgd, dgd = O.qpid_stages(om, q[:, b], qd[:, b])
+        np.testing.assert_allclose(rd.getJacobianTimeVariation("fr3_link8"), Jd, atol=1e-10)
+        mr = rd.getManipulability(True, True, "fr3_link8")
+        np.testing.assert_allclose(mr.grad_dot, mgd, rtol=1e-7, atol=1e-8)
+        dr = rd.getMinDistance(True, True, False)
+        np.testing.assert_allclose(dr.grad_dot, dgd, atol=1e-5)

@@ -226,3 +226,28 @@ def test_qpid_reference_settings_match_oracle(cuda):
     both = (status == rs) & (rs == O.SOLVED)
     err = np.abs(tau - rt).max(axis=0)[both]
     assert np.median(err) <= 1e-6, np.median(err)
+
+
+@pytest.mark.parametrize("robot", ["fr3", "husky_fr3"])
+def test_graddot_vectors_and_jdot_getters(cuda, robot):
+    """getManipulability(true, true).grad_dot, getMinDistance(true, true).grad_dot
+    and getJacobianTimeVariation through the Python mirrors (QPID stage
+    outputs) vs the oracle's literal restatement of robot_data.cpp:496-512,
+    555-569 (MoMa :477-492)."""
+    rd, ctrl, q, qd, xt, xdt = _inputs(robot, cuda, 36, 6)
+    pm, om, spec = O.load(robot)
+    for b in range(q.shape[1]):
+        Jd, mgd, dgd = O.qpid_stages(om, q[:, b], qd[:, b])
+        if om.kind == 0:
+            rd.updateState(q[:, b], qd[:, b])
+            man = rd.getManipulability(True, True, LINK[robot])
+            dist = rd.getMinDistance(True, True, False)
+            np.testing.assert_allclose(rd.getJacobianTimeVariation(LINK[robot]), Jd, atol=1e-10)
+        else:
+            rd.q_, rd.qdot_ = q[:, b].copy(), qd[:, b].copy()
+            man = rd.get_manipulability(True, True, LINK[robot])
+            dist = rd.get_min_distance(True, True)
+            np.testing.assert_allclose(rd.get_jacobian_time_variation(LINK[robot]), Jd, atol=1e-10)
+        np.testing.assert_allclose(man.grad_dot, mgd, rtol=1e-7, atol=1e-8)
+        d = O.min_distance(om, q[:, b])[0]
+        np.testing.assert_allclose(dist.grad_dot, dgd, atol=1e-5 if d > 0 else 1e-3)
