@@ -188,3 +188,24 @@ def joint_torque_step_batch(model, q, qdot=None, q_target=None, qdot_target=None
         model.handle, C.c_int64(B), _ptr(q), _ptr(qdot), _ptr(q_target), _ptr(qdot_target), _ptr(qddot_target),
         C.c_double(dt), dp(kp), dp(kv), _ptr(tau), C.c_void_p(stream)))
     return tau
+
+
+def closed_form_batch(model, params, kind, q, qdot, x_target=None, xdot_target=None, x_init=None, xdot_init=None,
+                      null=None, out=None, stream=None):
+    """``drc_clik_batch`` (kind "clik") / ``drc_osf_batch`` (kind "osf") on
+    device tensors [field][B]; returns qdot / tau [dof][B]."""
+    torch = _torch()
+    dev = q.device
+    B = q.shape[1]
+    check_shapes(model.dof, B, q=q, qdot=qdot, x_target=x_target, xdot_target=xdot_target,
+                 x_init=x_init, xdot_init=xdot_init)
+    if null is not None and tuple(null.shape) != (model.dof, B):
+        raise ValueError("null vector must be [%d][B=%d]" % (model.dof, B))
+    if out is None:
+        out = torch.empty((model.dof, B), dtype=torch.float64, device=dev)
+    if stream is None:
+        stream = torch.cuda.current_stream(dev).cuda_stream
+    fn = _capi.lib().drc_clik_batch if kind == "clik" else _capi.lib().drc_osf_batch
+    _capi.check(fn(model.handle, C.byref(params), C.c_int64(B), _ptr(q), _ptr(qdot), _ptr(x_target),
+                   _ptr(xdot_target), _ptr(x_init), _ptr(xdot_init), _ptr(null), _ptr(out), C.c_void_p(stream)))
+    return out

@@ -40,7 +40,7 @@ EXPORTED_SYMBOLS = (
     "drc_debug_kernel_times", "drc_set_concurrency", "drc_qpik_host", "drc_qpik_stages_host",
     "drc_dynamics_batch", "drc_dynamics_host", "drc_joint_torque_step_batch", "drc_joint_torque_step_host",
     "drc_default_qpid_params", "drc_qpid_batch", "drc_qpid_stages_batch", "drc_qpid_host",
-    "drc_qpid_stages_host",
+    "drc_qpid_stages_host", "drc_clik_batch", "drc_osf_batch", "drc_closed_form_host",
     "drc_error_string", "drc_last_error",
 )
 
@@ -142,6 +142,9 @@ def _load():
     lib.drc_qpid_stages_host.argtypes = [vp, C.POINTER(QPIKParams), C.c_int64, dp, dp, dp, dp, dp, dp,
                                          dp, dp, dp, dp, ip, dp, dp, dp, dp]
     lib.drc_qpid_host.argtypes = [vp, C.POINTER(QPIKParams), C.c_int64, dp, dp, dp, dp, dp, dp, dp, dp, ip, ip]
+    lib.drc_clik_batch.argtypes = [vp, C.POINTER(QPIKParams), C.c_int64, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    lib.drc_osf_batch.argtypes = [vp, C.POINTER(QPIKParams), C.c_int64, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    lib.drc_closed_form_host.argtypes = [vp, C.POINTER(QPIKParams), C.c_int, C.c_int64, dp, dp, dp, dp, dp, dp, dp, dp]
     for name in EXPORTED_SYMBOLS:
         if name not in ("drc_model_destroy", "drc_error_string", "drc_last_error"):
             getattr(lib, name).restype = C.c_int

@@ -51,6 +51,8 @@ struct KParams {
   int kT, kZ, kTe, kJ, kTg, kq, kqd, kA6, kAi, kW, kPart, kPd, kPf, kxdd, kmg, kdg, kJt, kSv, kScr, kEpa;
   int kJd, kDa, kVf, kX6, kBias, kMq, kGq;  // QPID: Jdot, arm-only Jdot, S eta, 6x6 scratch, bias | M, g
   int kGdv;                                 // QPID stage: grad_dot vectors
+  int cf;                                   // closed-form controller: 1 CLIK, 2 OSF (task_kernel<2>)
+  int kCf;                                  // its LDS work area
   int lds_doubles;
 };
 
@@ -959,6 +961,7 @@ struct IO {
   double* out2;
   double *st_jdot, *st_qpid;  // [6*nv][B] Jdot; [8][B] bias(6), man_gd, dist_gd
   double* st_gdv;             // [narm + nv][B] grad_dot vectors (manipulability | min distance)
+  const double* cf_null;      // closed-form: null_qdot / null_torque [nv][B] (may be NULL)
 };
 
 // ------------------------------------------------------------------------
@@ -1193,6 +1196,142 @@ __device__ __noinline__ void qpid_task_extras(const DevModel* M, const KParams& 
   wsync();
 }
 
+// ------------------------------------------------------------------------
+// Closed-form controllers, Manipulator::RobotController
+// (robot_controller.cpp:156-275), on the task stage's J and task vector
+// (xdd: CLIK Kp e + xdot_target; OSF Kp e + Kv edot, or xddot_target):
+//   CLIK: qdot = J^+ xdd + (I - J^+ J) nu,              J^+ = PinvCOD(J)
+//   OSF:  Lambda = PinvCOD(J M^-1 J^T), tau = J^T Lambda xdd + (I - J^T Lambda J M^-1) nu + g
+// Small dense products are lane-parallel; a 6x6 SPD inverse goes through six
+// lane-parallel Jordan exchanges when the Frobenius condition estimate
+// certifies that PinvCOD keeps every mode (< 1e5), otherwise one lane runs the
+// serial COD (PinvCOD's rank cut).
+// ------------------------------------------------------------------------
+__device__ __forceinline__ bool inv6_certified(const double* A, double* Ai) {
+  const int l = lane_id(), ii = l / 6, jj = l % 6;
+  if (l < 36) Ai[l] = A[l];
+  wsync();
+  double piv_min = 1e300;
+  for (int k = 0; k < 6; ++k) {
+    const double akk = Ai[k * 6 + k];
+    double nv_ = 0;
+    if (l < 36) {
+      const double aij = Ai[l], aik = Ai[ii * 6 + k], akj = Ai[k * 6 + jj];
+      if (ii == k && jj == k) nv_ = 1.0 / akk;
+      else if (ii == k) nv_ = akj / akk;
+      else if (jj == k) nv_ = -aik / akk;
+      else nv_ = aij - aik * akj / akk;
+    }
+    piv_min = fmin(piv_min, akk);
+    wsync();
+    if (l < 36) Ai[l] = nv_;
+    wsync();
+  }
+  const double fa = wave_sum(l < 36 ? A[l] * A[l] : 0.0), fi = wave_sum(l < 36 ? Ai[l] * Ai[l] : 0.0);
+  return piv_min > 0 && fa * fi < 1e10;
+}
+
+__device__ __noinline__ void closed_form_stage(const DevModel* M, const KParams& kp, double* S, const IO& io,
+                                               int64_t gb, int64_t LD) {
+  const int l = lane_id(), nv = kp.nv;
+  const double *J = S + kp.kJ, *xdd = S + kp.kxdd;
+  double* A6 = S + kp.kA6;
+  double* Ai = S + kp.kAi;
+  double* W = S + kp.kCf;           // 6 x nv: J^+ ^T (CLIK) / J M^-1 (OSF)
+  double* W2 = W + 6 * nv;          // 6 x nv: Lambda J M^-1 (OSF)
+  double* Mi = W2 + 6 * nv;         // nv x nv
+  double* nu = Mi + nv * nv;        // nv
+  double* gv = nu + nv;             // nv
+  double* vec = gv + 2 * nv;        // 48: task vectors
+  double* ws = vec + 48;            // serial COD work
+  if (l < nv) {
+    nu[l] = io.cf_null ? io.cf_null[(int64_t)l * LD + gb] : 0.0;
+    if (kp.cf == 2) gv[l] = io.dG[(int64_t)l * LD + gb];
+  }
+  if (kp.cf == 2)
+    for (int e = l; e < nv * nv; e += 64) Mi[e] = io.dM[(int64_t)e * LD + gb];
+  wsync();
+  double out = 0;
+  if (kp.cf == 1) {  // CLIK (robot_controller.cpp:156-172)
+    if (l < 36) {
+      const int a = l / 6, b = l % 6;
+      double s = 0;
+      for (int c = 0; c < nv; ++c) s += J[a * nv + c] * J[b * nv + c];
+      A6[l] = s;
+    }
+    wsync();
+    if (inv6_certified(A6, Ai)) {  // J^+ = J^T (J J^T)^-1, stored transposed: W[i][c] = J^+[c][i]
+      for (int e = l; e < 6 * nv; e += 64) {
+        const int i = e / nv, c = e % nv;
+        double s = 0;
+        for (int r = 0; r < 6; ++r) s += J[r * nv + c] * Ai[r * 6 + i];
+        W[e] = s;
+      }
+    } else if (l == 0) {
+      double* X = ws + 6 * nv + 36 + 6 * nv + 18 + 2 * nv;  // nv x 6 after the COD work
+      pinv_cod_rect(J, 6, nv, X, ws);
+      for (int c = 0; c < nv; ++c)
+        for (int i = 0; i < 6; ++i) W[i * nv + c] = X[c * 6 + i];
+    }
+    wsync();
+    if (l < 6) {
+      double s = 0;
+      for (int c = 0; c < nv; ++c) s += J[l * nv + c] * nu[c];
+      vec[l] = xdd[l] - s;  // xdd - J nu
+    }
+    wsync();
+    if (l < nv) {
+      double s = nu[l];
+      for (int i = 0; i < 6; ++i) s += W[i * nv + l] * vec[i];
+      out = s;
+    }
+  } else {  // OSF (robot_controller.cpp:216-230)
+    for (int e = l; e < 6 * nv; e += 64) {
+      const int i = e / nv, c = e % nv;
+      double s = 0;
+      for (int a = 0; a < nv; ++a) s += J[i * nv + a] * Mi[a * nv + c];
+      W[e] = s;
+    }
+    wsync();
+    if (l < 36) {
+      const int a = l / 6, b = l % 6;
+      double s = 0;
+      for (int c = 0; c < nv; ++c) s += W[a * nv + c] * J[b * nv + c];
+      A6[l] = s;
+    }
+    wsync();
+    if (!inv6_certified(A6, Ai)) {
+      if (l == 0) pinv_cod6(A6, Ai, ws);
+      wsync();
+    }
+    for (int e = l; e < 6 * nv; e += 64) {
+      const int i = e / nv, c = e % nv;
+      double s = 0;
+      for (int j = 0; j < 6; ++j) s += Ai[i * 6 + j] * W[j * nv + c];
+      W2[e] = s;
+    }
+    if (l < 6) {
+      double s = 0;
+      for (int j = 0; j < 6; ++j) s += Ai[l * 6 + j] * xdd[j];
+      vec[l] = s;  // F = Lambda xdd
+    }
+    wsync();
+    if (l < 6) {
+      double s = 0;
+      for (int c = 0; c < nv; ++c) s += W2[l * nv + c] * nu[c];
+      vec[6 + l] = vec[l] - s;  // F - J_T_pinv nu
+    }
+    wsync();
+    if (l < nv) {
+      double s = gv[l] + nu[l];
+      for (int i = 0; i < 6; ++i) s += J[i * nv + l] * vec[6 + i];
+      out = s;
+    }
+  }
+  if (l < nv) io.out[(int64_t)l * LD + gb] = out;
+  wsync();
+}
+
 // Occupancy target of the task kernel (waves per SIMD): the lane-serial
 // narrow phase and task-velocity code would otherwise take all 512 registers.
 #ifndef DRC_TASK_WAVES
@@ -1375,6 +1514,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRC_TAS
       }
     }
     PH(1);
+    if constexpr (PROBLEM == 2) {  // closed-form controllers: no CBF stages
+      closed_form_stage(M, kp, S, io, gb, LD);
+      continue;
+    }
     // ---------------- manipulability (arm columns c0..c0+narm) -------------
     const int narm = kp.narm, c0 = kp.c0;
     double* A6 = S + kp.kA6;
@@ -2684,7 +2827,7 @@ static int plan_layout(const DevModel& M, KParams* k, bool task_only) {
   k->kdg = takeu(nv);
   k->kJt = takeu(6 * np);
   k->kSv = takeu(3 * kMaxWheels);
-  k->kScr = takeu(96);
+  k->kScr = takeu(160);  // serial 6x6 COD work (pinv_cod_serial: 3n^2 + 3n)
   if (k->problem == 1) {  // QPID stage data (task kernel) and dynamics (QP kernel)
     k->kJd = takeu(6 * nv);
     k->kDa = takeu(6 * k->narm);
@@ -2695,7 +2838,11 @@ static int plan_layout(const DevModel& M, KParams* k, bool task_only) {
     k->kMq = takeu(k->na * k->na);
     k->kGq = takeu(k->na);
   }
-  k->kEpa = task_only ? takeu(static_cast<int>((sizeof(EpaPoly) + 7) / 8)) : 0;
+  if (k->cf) {  // W, W2 (6 x nv), M^-1, nu, g, task vectors, then the serial COD work (+ its nv x 6 result)
+    const int ws = 6 * nv + 36 + 6 * nv + 18 + 2 * nv + 6 * nv;
+    k->kCf = takeu(2 * 6 * nv + nv * nv + 3 * nv + 48 + (ws > 160 ? ws : 160));
+  }
+  k->kEpa = (task_only && !k->cf) ? takeu(static_cast<int>((sizeof(EpaPoly) + 7) / 8)) : 0;
   int kin_end = u;
   int kinv_end = k->oU0 + nx * nx + nx * ng;  // K^-1 and G K^-1
   const int N = nx + ng;
@@ -2712,10 +2859,11 @@ static int plan_layout(const DevModel& M, KParams* k, bool task_only) {
 }
 
 static int make_kparams(const drc_model_impl* mm, const drc_qpik_params* p, int stages, KParams* k,
-                        int problem = 0) {
+                        int problem = 0, int cf = 0) {
   const DevModel& M = mm->hm.dev;
   std::memset(k, 0, sizeof(*k));
   k->problem = problem;
+  k->cf = cf;
   for (int i = 0; i < 6; ++i) {
     k->kp[i] = p->kp[i];
     k->kv[i] = p->kv[i];
@@ -2980,6 +3128,65 @@ static int launch_qpid(const drc_model_impl* cm, const drc_qpik_params* params, 
                        static_cast<size_t>(kq_c.lds_doubles) * sizeof(double), st, m->d_model, kq_c, io);
     HIP_TRY(hipGetLastError());
   }
+  return DRC_OK;
+}
+
+// Closed-form controllers: [dynamics (OSF: M^-1, g)] -> task_kernel<2>.
+static int launch_closed_form(const drc_model_impl* cm, const drc_qpik_params* params, int cf, int64_t B,
+                              const double* q, const double* qdot, const double* xt, const double* xdt,
+                              const double* xi, const double* xdi, const double* nullv, double* out, void* stream) {
+  drc_model_impl* m = const_cast<drc_model_impl*>(cm);
+  if (!m || !params) return set_err(DRC_ERR_INVALID_ARGUMENT, "null model/params");
+  if (m->hm.dev.kind != 0) return set_err(DRC_ERR_INVALID_ARGUMENT, "CLIK / OSF are Manipulator::RobotController entries");
+  if (B < 0) return set_err(DRC_ERR_INVALID_ARGUMENT, "negative batch");
+  if (B == 0) return DRC_OK;
+  if (B > 0x7ffffff0) return set_err(DRC_ERR_INVALID_ARGUMENT, "batch too large");
+  if (!q || !qdot || !xdt || !out) return set_err(DRC_ERR_INVALID_ARGUMENT, "q, qdot, xdot_target and out are required");
+  if (cf == 1 && params->mode == DRC_MODE_QPIK) return set_err(DRC_ERR_INVALID_ARGUMENT, "CLIK has Step and Cubic forms only");
+  if (params->mode != DRC_MODE_QPIK && !xt) return set_err(DRC_ERR_INVALID_ARGUMENT, "x_target required");
+  if (params->mode == DRC_MODE_QPIK_CUBIC && (!xi || !xdi)) return set_err(DRC_ERR_INVALID_ARGUMENT, "x_init/xdot_init required");
+  drc_qpik_params pp = *params;
+  for (int i = 0; i < 6; ++i) pp.kv[i] = cf == 1 ? 0.0 : params->kv[i];  // CLIK: Kp e + xdot_target (:168)
+  pp.feedforward = cf == 1 ? 1.0 : 0.0;                                 // OSF: Kp e + Kv edot (:243)
+  KParams kt;
+  int rc = make_kparams(m, &pp, 1, &kt, 2, cf);
+  if (rc) return rc;
+  const DevModel& d = m->hm.dev;
+  HIP_TRY(hipSetDevice(m->device));
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  double *dMi = nullptr, *dG = nullptr;
+  if (cf == 2) {  // getMassMatrixInv (PinvCOD(M)) and getGravity (robot_data.cpp:111-118)
+    std::lock_guard<std::mutex> g(m->mu);
+    const int64_t bytes = (int64_t(d.nv) * d.nv + d.nv) * B * 8;
+    if (m->pool_bytes < bytes) {
+      if (m->pool) HIP_TRY(hipFree(m->pool));
+      m->pool = nullptr;
+      m->pool_bytes = 0;
+      HIP_TRY(hipMalloc(&m->pool, bytes));
+      m->pool_bytes = bytes;
+    }
+    if (m->dyn_list_cap < B + 1) {
+      if (m->dyn_list) HIP_TRY(hipFree(m->dyn_list));
+      m->dyn_list = nullptr;
+      m->dyn_list_cap = 0;
+      HIP_TRY(hipMalloc(&m->dyn_list, (B + 1) * sizeof(int)));
+      m->dyn_list_cap = B + 1;
+    }
+    dMi = reinterpret_cast<double*>(m->pool);
+    dG = dMi + int64_t(d.nv) * d.nv * B;
+    rc = launch_dynamics(m->d_model, d, false, B, q, qdot, nullptr, dMi, dG, nullptr, nullptr, m->dyn_list, st);
+    if (rc) return set_err(DRC_ERR_HIP, std::string("dynamics launch: ") + hipGetErrorString(hipGetLastError()));
+  }
+  const int64_t grid = B < 8192 ? B : 8192;
+  kt.xcd_map = B >= 16384 ? 1 : 0;
+  IO io{B, 0, B, q, qdot, xt, xdt, xi, xdi, out, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+        nullptr, nullptr, 0};
+  io.dM = dMi;
+  io.dG = dG;
+  io.cf_null = nullv;
+  hipLaunchKernelGGL(task_kernel<2>, dim3(static_cast<unsigned>(grid)), dim3(64),
+                     static_cast<size_t>(kt.lds_doubles) * sizeof(double), st, m->d_model, kt, io);
+  HIP_TRY(hipGetLastError());
   return DRC_OK;
 }
 
@@ -3420,6 +3627,58 @@ int drc_qpik_stages_host(drc_model* m, const drc_qpik_params* p, int64_t B, cons
   return host_call(m, p, 1, B, in, outs, rows, 5, iouts, 1);
 }
 
+
+// ---- closed-form controllers ------------------------------
+int drc_clik_batch(const drc_model* m, const drc_qpik_params* p, int64_t B, const double* q, const double* qdot,
+                   const double* xt, const double* xdt, const double* xi, const double* xdi, const double* null_qdot,
+                   double* qdot_out, void* stream) {
+  return drc_amd::launch_closed_form(m, p, 1, B, q, qdot, xt, xdt, xi, xdi, null_qdot, qdot_out, stream);
+}
+
+int drc_osf_batch(const drc_model* m, const drc_qpik_params* p, int64_t B, const double* q, const double* qdot,
+                  const double* xt, const double* xdt, const double* xi, const double* xdi, const double* null_torque,
+                  double* tau_out, void* stream) {
+  return drc_amd::launch_closed_form(m, p, 2, B, q, qdot, xt, xdt, xi, xdi, null_torque, tau_out, stream);
+}
+
+int drc_closed_form_host(drc_model* m, const drc_qpik_params* p, int kind, int64_t B, const double* q,
+                         const double* qdot, const double* xt, const double* xdt, const double* xi, const double* xdi,
+                         const double* nullv, double* out) {
+  using drc_amd::set_err;
+  if (!m || !p) return set_err(DRC_ERR_INVALID_ARGUMENT, "null model/params");
+  if (kind != 1 && kind != 2) return set_err(DRC_ERR_INVALID_ARGUMENT, "kind must be 1 (CLIK) or 2 (OSF)");
+  if (B <= 0) return B == 0 ? DRC_OK : set_err(DRC_ERR_INVALID_ARGUMENT, "negative batch");
+  if (!out) return set_err(DRC_ERR_INVALID_ARGUMENT, "out is required");
+  const int64_t n = m->hm.dev.nv;
+  std::lock_guard<std::mutex> lk(m->host_mu);
+  HIP_TRY(hipSetDevice(m->device));
+  const double* src[7] = {q, qdot, xt, xdt, xi, xdi, nullv};
+  const int64_t rows[7] = {n, n, 12, 6, 12, 6, n};
+  int64_t words = n * B;
+  for (int i = 0; i < 7; ++i) words += src[i] ? rows[i] * B : 0;
+  if (m->stage_bytes < words * 8) {
+    if (m->stage) (void)hipFree(m->stage);
+    m->stage = nullptr;
+    m->stage_bytes = 0;
+    HIP_TRY(hipMalloc(&m->stage, words * 8));
+    m->stage_bytes = words * 8;
+  }
+  if (!m->hstream) HIP_TRY(hipStreamCreateWithFlags(&m->hstream, hipStreamNonBlocking));
+  double* dp = reinterpret_cast<double*>(m->stage);
+  const double* din[7] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  for (int i = 0; i < 7; ++i)
+    if (src[i]) {
+      HIP_TRY(hipMemcpyAsync(dp, src[i], rows[i] * B * 8, hipMemcpyHostToDevice, m->hstream));
+      din[i] = dp;
+      dp += rows[i] * B;
+    }
+  int rc = drc_amd::launch_closed_form(m, p, kind, B, din[0], din[1], din[2], din[3], din[4], din[5], din[6], dp,
+                                       m->hstream);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(out, dp, n * B * 8, hipMemcpyDeviceToHost, m->hstream));
+  HIP_TRY(hipStreamSynchronize(m->hstream));
+  return DRC_OK;
+}
 
 int drc_qpid_host(drc_model* m, const drc_qpik_params* p, int64_t B, const double* q, const double* qdot,
                   const double* xt, const double* xdt, const double* xi, const double* xdi, double* qdd, double* tau,

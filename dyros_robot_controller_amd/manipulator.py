@@ -484,3 +484,75 @@ class RobotController:
             current_time, init_time, duration, link_name))
 
     QPID_step, QPID_cubic = QPIDStep, QPIDCubic
+
+    # -- closed-form controllers (robot_controller.cpp:156-275) --
+    def _run_cf(self, kind, mode, link_name, q, qdot, x_target, xdot_target, x_init=None, xdot_init=None,
+                t=0.0, t0=0.0, duration=1.0, null=None):
+        p = self._pb.params(link_name, mode, self.Kp_task_, self.Kv_task_, t, t0, duration)
+        a = lambda v: _batch.as_device(v, self.robot_data_.device)
+        return _batch.closed_form_batch(self.robot_data_.model, p, kind, a(q), a(qdot), a(x_target), a(xdot_target),
+                                        a(x_init), a(xdot_init), a(null))
+
+    def CLIK_step_batch(self, q, qdot, x_target, xdot_target, link_name, null_qdot=None):
+        return self._run_cf("clik", _capi.MODE_QPIK_STEP, link_name, q, qdot, x_target, xdot_target, null=null_qdot)
+
+    def CLIK_cubic_batch(self, q, qdot, x_target, xdot_target, x_init, xdot_init, current_time, init_time, duration,
+                         link_name, null_qdot=None):
+        return self._run_cf("clik", _capi.MODE_QPIK_CUBIC, link_name, q, qdot, x_target, xdot_target, x_init,
+                            xdot_init, current_time, init_time, duration, null=null_qdot)
+
+    def OSF_batch(self, q, qdot, xddot_target, link_name, null_torque=None):
+        return self._run_cf("osf", _capi.MODE_QPIK, link_name, q, qdot, None, xddot_target, null=null_torque)
+
+    def OSF_step_batch(self, q, qdot, x_target, xdot_target, link_name, null_torque=None):
+        return self._run_cf("osf", _capi.MODE_QPIK_STEP, link_name, q, qdot, x_target, xdot_target, null=null_torque)
+
+    def OSF_cubic_batch(self, q, qdot, x_target, xdot_target, x_init, xdot_init, current_time, init_time, duration,
+                        link_name, null_torque=None):
+        return self._run_cf("osf", _capi.MODE_QPIK_CUBIC, link_name, q, qdot, x_target, xdot_target, x_init,
+                            xdot_init, current_time, init_time, duration, null=null_torque)
+
+    @staticmethod
+    def _split_null(args, n_fixed):
+        """Reference overloads: (..., null_vec, link_name) or (..., link_name)."""
+        if len(args) == n_fixed + 2:
+            return args[:n_fixed], np.asarray(args[n_fixed], float).reshape(-1, 1), args[n_fixed + 1]
+        return args[:n_fixed], None, args[n_fixed]
+
+    def CLIKStep(self, *args):
+        """CLIKStep(x_target, xdot_target[, null_qdot], link_name) -> qdot."""
+        (x_t, xd_t), nu, link = self._split_null(args, 2)
+        q, qd = self._state()
+        return self.CLIK_step_batch(q, qd, pose_to12(x_t).reshape(12, 1), np.asarray(xd_t, float).reshape(6, 1), link,
+                                    nu).cpu().numpy()[:, 0]
+
+    def CLIKCubic(self, *args):
+        """CLIKCubic(x_target, xdot_target, x_init, xdot_init, t, t0, T[, null_qdot], link_name)."""
+        (x_t, xd_t, x_i, xd_i, t, t0, T), nu, link = self._split_null(args, 7)
+        q, qd = self._state()
+        return self.CLIK_cubic_batch(q, qd, pose_to12(x_t).reshape(12, 1), np.asarray(xd_t, float).reshape(6, 1),
+                                     pose_to12(x_i).reshape(12, 1), np.asarray(xd_i, float).reshape(6, 1), t, t0, T,
+                                     link, nu).cpu().numpy()[:, 0]
+
+    def OSF(self, *args):
+        """OSF(xddot_target[, null_torque], link_name) -> tau."""
+        (xdd,), nu, link = self._split_null(args, 1)
+        q, qd = self._state()
+        return self.OSF_batch(q, qd, np.asarray(xdd, float).reshape(6, 1), link, nu).cpu().numpy()[:, 0]
+
+    def OSFStep(self, *args):
+        """OSFStep(x_target, xdot_target[, null_torque], link_name) -> tau."""
+        (x_t, xd_t), nu, link = self._split_null(args, 2)
+        q, qd = self._state()
+        return self.OSF_step_batch(q, qd, pose_to12(x_t).reshape(12, 1), np.asarray(xd_t, float).reshape(6, 1), link,
+                                   nu).cpu().numpy()[:, 0]
+
+    def OSFCubic(self, *args):
+        """OSFCubic(x_target, xdot_target, x_init, xdot_init, t, t0, T[, null_torque], link_name)."""
+        (x_t, xd_t, x_i, xd_i, t, t0, T), nu, link = self._split_null(args, 7)
+        q, qd = self._state()
+        return self.OSF_cubic_batch(q, qd, pose_to12(x_t).reshape(12, 1), np.asarray(xd_t, float).reshape(6, 1),
+                                    pose_to12(x_i).reshape(12, 1), np.asarray(xd_i, float).reshape(6, 1), t, t0, T,
+                                    link, nu).cpu().numpy()[:, 0]
+
+    CLIK_step, CLIK_cubic, OSF_step, OSF_cubic = CLIKStep, CLIKCubic, OSFStep, OSFCubic

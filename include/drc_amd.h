@@ -303,6 +303,28 @@ int drc_qpid_host(drc_model* model, const drc_qpik_params* params, int64_t B,
                   const double* xdot_target, const double* x_init, const double* xdot_init,
                   double* qddot_out, double* tau_out, int32_t* status, int32_t* iters);
 
+/* ---- closed-form controllers -------------------------
+ * Manipulator::RobotController::CLIKStep / CLIKCubic (src/manipulator/robot_controller.cpp:156-214):
+ *   qdot = J^+ (Kp e + xdot_target) + (I - J^+ J) null_qdot,  J^+ = DyrosMath::PinvCOD(J);
+ *   params->mode DRC_MODE_QPIK_STEP (1) or DRC_MODE_QPIK_CUBIC (2); kp = Kp_task_ (kv is not used).
+ * Manipulator::RobotController::OSF / OSFStep / OSFCubic (:216-275):
+ *   Lambda = PinvCOD(J M^-1 J^T), tau = J^T Lambda xddot + (I - J^T Lambda J M^-1) null_torque + g,
+ *   xddot = xdot_target (mode 0, OSF(xddot_target)) or Kp e + Kv (xdot_target - J qdot) (modes 1, 2);
+ *   M^-1 = getMassMatrixInv, g = getGravity computed on the device in the same call.
+ * Manipulator models only.  q, qdot [dof][B]; x_target [12][B]; xdot_target [6][B]; x_init/xdot_init for the
+ * cubic forms; null_qdot / null_torque [dof][B] or NULL (the overloads without them); out [dof][B].
+ * Parameters: drc_default_qpik_params (Kp_task_ = 100, Kv_task_ = 20). */
+int drc_clik_batch(const drc_model* model, const drc_qpik_params* params, int64_t B, const double* q,
+                   const double* qdot, const double* x_target, const double* xdot_target, const double* x_init,
+                   const double* xdot_init, const double* null_qdot, double* qdot_out, void* stream);
+int drc_osf_batch(const drc_model* model, const drc_qpik_params* params, int64_t B, const double* q,
+                  const double* qdot, const double* x_target, const double* xdot_target, const double* x_init,
+                  const double* xdot_init, const double* null_torque, double* tau_out, void* stream);
+/* Host-buffer form of both (kind 1 = CLIK, 2 = OSF); synchronous. */
+int drc_closed_form_host(drc_model* model, const drc_qpik_params* params, int kind, int64_t B, const double* q,
+                         const double* qdot, const double* x_target, const double* xdot_target,
+                         const double* x_init, const double* xdot_init, const double* null_vec, double* out);
+
 #ifdef __cplusplus
 }
 #endif

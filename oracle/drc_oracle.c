@@ -201,23 +201,25 @@ static int rank_cpqr(const double* A, int n, double thr) {
 /* Moore-Penrose inverse of the QR-truncated matrix Q_r [R11 R12] P^T: what
    Eigen's CompleteOrthogonalDecomposition::pseudoInverse() returns with the
    rank cut |R_ii| > thr * max|R_ii| (math_type_define.h:563-570).
-   X = P W^T (W W^T)^-1 Q_r^T with W = R[:r, :].  n <= 16. */
-static void pinv_qr_trunc(const double* A, int n, double thr, double* X) {
+   A is m x n (row-major), X = P W^T (W W^T)^-1 Q_r^T (n x m) with W = R[:r, :].
+   m, n <= 16. */
+static void pinv_qr_trunc_mn(const double* A, int m, int n, double thr, double* X) {
     double R[256], G[256], Y[256], beta[16], v0[16], cn[16];
     int perm[16];
-    memcpy(R, A, (size_t)n * n * sizeof(double));
+    const int kmax = m < n ? m : n;
+    memcpy(R, A, (size_t)m * n * sizeof(double));
     for (int j = 0; j < n; ++j) perm[j] = j;
     double maxpiv = 0;
-    for (int k = 0; k < n; ++k) {
+    for (int k = 0; k < kmax; ++k) {
         int p = k;
         for (int j = k; j < n; ++j) {
             double s = 0;
-            for (int i = k; i < n; ++i) s += R[i * n + j] * R[i * n + j];
+            for (int i = k; i < m; ++i) s += R[i * n + j] * R[i * n + j];
             cn[j] = s;
             if (s > cn[p]) p = j;
         }
         if (p != k) {
-            for (int i = 0; i < n; ++i) { double t = R[i * n + k]; R[i * n + k] = R[i * n + p]; R[i * n + p] = t; }
+            for (int i = 0; i < m; ++i) { double t = R[i * n + k]; R[i * n + k] = R[i * n + p]; R[i * n + p] = t; }
             int t = perm[k]; perm[k] = perm[p]; perm[p] = t;
             double c = cn[k]; cn[k] = cn[p]; cn[p] = c;
         }
@@ -225,14 +227,14 @@ static void pinv_qr_trunc(const double* A, int n, double thr, double* X) {
         beta[k] = 0; v0[k] = 0;
         if (nrm > 0) {
             double x0 = R[k * n + k], alpha = x0 > 0 ? -nrm : nrm, w0 = x0 - alpha, vn = w0 * w0;
-            for (int i = k + 1; i < n; ++i) vn += R[i * n + k] * R[i * n + k];
+            for (int i = k + 1; i < m; ++i) vn += R[i * n + k] * R[i * n + k];
             double bt = vn > 0 ? 2.0 / vn : 0.0;
             for (int j = k + 1; j < n; ++j) {
                 double s = w0 * R[k * n + j];
-                for (int i = k + 1; i < n; ++i) s += R[i * n + k] * R[i * n + j];
+                for (int i = k + 1; i < m; ++i) s += R[i * n + k] * R[i * n + j];
                 s *= bt;
                 R[k * n + j] -= s * w0;
-                for (int i = k + 1; i < n; ++i) R[i * n + j] -= s * R[i * n + k];
+                for (int i = k + 1; i < m; ++i) R[i * n + j] -= s * R[i * n + k];
             }
             R[k * n + k] = alpha;
             beta[k] = bt; v0[k] = w0;
@@ -240,8 +242,8 @@ static void pinv_qr_trunc(const double* A, int n, double thr, double* X) {
         if (fabs(R[k * n + k]) > maxpiv) maxpiv = fabs(R[k * n + k]);
     }
     int r = 0;
-    for (int k = 0; k < n; ++k) if (fabs(R[k * n + k]) > thr * maxpiv) ++r;
-    memset(X, 0, (size_t)n * n * sizeof(double));
+    for (int k = 0; k < kmax; ++k) if (fabs(R[k * n + k]) > thr * maxpiv) ++r;
+    memset(X, 0, (size_t)n * m * sizeof(double));
     if (r == 0) return;
     for (int i = 0; i < r; ++i)
         for (int j = 0; j <= i; ++j) {
@@ -260,30 +262,33 @@ static void pinv_qr_trunc(const double* A, int n, double thr, double* X) {
             G[i * r + j] = t / d;
         }
     }
+    /* Y = W^T (W W^T)^-1, row c of Y: solve (G G^T) y = W[:, c] */
     for (int c = 0; c < n; ++c) {
         double* y = Y + c * r;
         for (int i = 0; i < r; ++i) y[i] = c >= i ? R[i * n + c] : 0.0;
         for (int i = 0; i < r; ++i) { double t = y[i]; for (int k = 0; k < i; ++k) t -= G[i * r + k] * y[k]; y[i] = t / G[i * r + i]; }
         for (int i = r - 1; i >= 0; --i) { double t = y[i]; for (int k = i + 1; k < r; ++k) t -= G[k * r + i] * y[k]; y[i] = t / G[i * r + i]; }
     }
-    for (int col = 0; col < n; ++col) {
+    /* X[perm[c]][col] = Y[c] . (Q^T e_col)[:r] */
+    for (int col = 0; col < m; ++col) {
         double u[16];
-        for (int i = 0; i < n; ++i) u[i] = i == col ? 1.0 : 0.0;
-        for (int k = 0; k < n; ++k) {
+        for (int i = 0; i < m; ++i) u[i] = i == col ? 1.0 : 0.0;
+        for (int k = 0; k < kmax; ++k) {
             if (beta[k] == 0) continue;
             double s = v0[k] * u[k];
-            for (int i = k + 1; i < n; ++i) s += R[i * n + k] * u[i];
+            for (int i = k + 1; i < m; ++i) s += R[i * n + k] * u[i];
             s *= beta[k];
             u[k] -= s * v0[k];
-            for (int i = k + 1; i < n; ++i) u[i] -= s * R[i * n + k];
+            for (int i = k + 1; i < m; ++i) u[i] -= s * R[i * n + k];
         }
         for (int c = 0; c < n; ++c) {
             double s = 0;
             for (int i = 0; i < r; ++i) s += Y[c * r + i] * u[i];
-            X[perm[c] * n + col] = s;
+            X[perm[c] * m + col] = s;
         }
     }
 }
+static void pinv_qr_trunc(const double* A, int n, double thr, double* X) { pinv_qr_trunc_mn(A, n, n, thr, X); }
 
 /* Cholesky LL^T in place (lower), returns 0 on failure */
 static int chol(double* A, int n) {
@@ -1693,6 +1698,99 @@ int oracle_qpid_one(const OracleModel* m, const OracleParams* p, const double* q
     return st;
 }
 
+/* ------------------------------------------------------------------------ */
+/* closed-form controllers: CLIK and OSF                 */
+/* robot_controller.cpp:156-275                                             */
+/* ------------------------------------------------------------------------ */
+/* getTaskSpaceError(x_t, xd_t, getPose, getVelocity) after the optional
+ * getTaskSpaceCubic (mode 2): e (6) and edot = xdot_target - J qdot (6) */
+static void task_error(const OracleModel* m, const Kin* k, const double* J, const OracleParams* p,
+                       const double* qdot, const double* x_target, const double* xdot_target,
+                       const double* x_init, const double* xdot_init, double* e, double* edot, double* xdt_out) {
+    int nv = m->nv;
+    double xt[12], xdt[6];
+    if (p->mode == 2) task_space_cubic(x_target, xdot_target, x_init, xdot_init, p->t, p->t0, p->duration, xt, xdt);
+    else { memcpy(xt, x_target, sizeof(xt)); memcpy(xdt, xdot_target, sizeof(xdt)); }
+    double Rt[9], pt[3], phi[3] = {0, 0, 0};
+    pose_unpack(xt, Rt, pt);
+    for (int i = 0; i < 3; ++i) e[i] = pt[i] - k->pe[i];
+    for (int i = 0; i < 3; ++i) {
+        double a[3] = {Rt[i], Rt[3 + i], Rt[6 + i]}, b[3] = {k->Te[i], k->Te[3 + i], k->Te[6 + i]}, c[3];
+        cross3(a, b, c);
+        phi[0] += c[0]; phi[1] += c[1]; phi[2] += c[2];
+    }
+    for (int i = 0; i < 3; ++i) e[3 + i] = -0.5 * phi[i];
+    for (int i = 0; i < 6; ++i) {
+        double t = 0;
+        for (int c = 0; c < nv; ++c) t += J[i * nv + c] * qdot[c];
+        edot[i] = xdt[i] - t;
+        xdt_out[i] = xdt[i];
+    }
+}
+
+/* CLIKStep / CLIKCubic (robot_controller.cpp:156-214), mode 1 / 2:
+ * qdot = J^+ (Kp e + xdot_target) + (I - J^+ J) null_qdot, J^+ = PinvCOD(J). */
+void oracle_clik_one(const OracleModel* m, const OracleParams* p, const double* q, const double* qdot,
+                     const double* x_target, const double* xdot_target, const double* x_init,
+                     const double* xdot_init, const double* null_qdot, double* out) {
+    int nv = m->nv;
+    Kin k;
+    kin_fk(m, q, &k);
+    double J[6 * ORC_MAXJ], Jp[6 * ORC_MAXJ], e[6], ed[6], xdt[6], v[6], Jn[6];
+    point_jacobian(m, &k, m->ee_joint, k.pe, J);
+    task_error(m, &k, J, p, qdot, x_target, xdot_target, x_init, xdot_init, e, ed, xdt);
+    pinv_qr_trunc_mn(J, 6, nv, 1e-6, Jp);                     /* nv x 6 */
+    for (int i = 0; i < 6; ++i) {
+        v[i] = p->kp[i] * e[i] + xdt[i];
+        double t = 0;
+        for (int c = 0; c < nv; ++c) t += J[i * nv + c] * (null_qdot ? null_qdot[c] : 0.0);
+        Jn[i] = t;
+    }
+    for (int c = 0; c < nv; ++c) {
+        double t = 0, nt = 0;
+        for (int i = 0; i < 6; ++i) { t += Jp[c * 6 + i] * v[i]; nt += Jp[c * 6 + i] * Jn[i]; }
+        out[c] = t + (null_qdot ? null_qdot[c] : 0.0) - nt;
+    }
+}
+
+/* OSF / OSFStep / OSFCubic (robot_controller.cpp:216-275), mode 0 / 1 / 2:
+ * Lambda = PinvCOD(J M^-1 J^T), tau = J^T Lambda xdd + (I - J^T Lambda J M^-1) null_torque + g
+ * with xdd = xddot_target (mode 0, passed in xdot_target) or Kp e + Kv edot.
+ * Minv (n x n, = getMassMatrixInv) and g from the caller. */
+void oracle_osf_one(const OracleModel* m, const OracleParams* p, const double* q, const double* qdot,
+                    const double* x_target, const double* xdot_target, const double* x_init,
+                    const double* xdot_init, const double* Minv, const double* g, const double* null_torque,
+                    double* out) {
+    int nv = m->nv;
+    Kin k;
+    kin_fk(m, q, &k);
+    double J[6 * ORC_MAXJ], JMi[6 * ORC_MAXJ], L[36], Lam[36], JTp[6 * ORC_MAXJ], xdd[6], F[6], w[6];
+    point_jacobian(m, &k, m->ee_joint, k.pe, J);
+    if (p->mode == 0) memcpy(xdd, xdot_target, sizeof(xdd));
+    else {
+        double e[6], ed[6], xdt[6];
+        task_error(m, &k, J, p, qdot, x_target, xdot_target, x_init, xdot_init, e, ed, xdt);
+        for (int i = 0; i < 6; ++i) xdd[i] = p->kp[i] * e[i] + p->kv[i] * ed[i];
+    }
+    for (int i = 0; i < 6; ++i)
+        for (int c = 0; c < nv; ++c) { double t = 0; for (int a = 0; a < nv; ++a) t += J[i * nv + a] * Minv[a * nv + c]; JMi[i * nv + c] = t; }
+    for (int i = 0; i < 6; ++i)
+        for (int j = 0; j < 6; ++j) { double t = 0; for (int c = 0; c < nv; ++c) t += JMi[i * nv + c] * J[j * nv + c]; L[i * 6 + j] = t; }
+    pinv_cod_sym(L, 6, Lam);
+    for (int i = 0; i < 6; ++i) {
+        double t = 0;
+        for (int j = 0; j < 6; ++j) t += Lam[i * 6 + j] * xdd[j];
+        F[i] = t;
+        for (int c = 0; c < nv; ++c) { double s2 = 0; for (int j = 0; j < 6; ++j) s2 += Lam[i * 6 + j] * JMi[j * nv + c]; JTp[i * nv + c] = s2; }
+    }
+    for (int i = 0; i < 6; ++i) { double t = 0; for (int c = 0; c < nv; ++c) t += JTp[i * nv + c] * (null_torque ? null_torque[c] : 0.0); w[i] = t; }
+    for (int c = 0; c < nv; ++c) {
+        double t = g[c] + (null_torque ? null_torque[c] : 0.0);
+        for (int i = 0; i < 6; ++i) t += J[i * nv + c] * (F[i] - w[i]);
+        out[c] = t;
+    }
+}
+
 /* stage helper: frame Jacobian time variation (getJacobianTimeVariation,
  * robot_data.cpp:404-417) and the QPID grad_dot vectors at (q, qdot) */
 void oracle_qpid_stages(const OracleModel* m, const double* q, const double* qdot, double* Jdot,
@@ -1818,3 +1916,6 @@ void oracle_manipulability(const OracleModel* m, const double* q, double* man, d
     int c0 = m->kind == 1 ? m->mani_start : 0, nc = m->kind == 1 ? m->n_arm : m->nv;
     manip(m, &k, J, c0, nc, man, grad);
 }
+
+/* DyrosMath::PinvCOD of an m x n matrix (tests) */
+void oracle_pinv_cod(const double* A, int m, int n, double* X) { pinv_qr_trunc_mn(A, m, n, 1e-6, X); }

@@ -135,6 +135,19 @@ void oracle_point_jacobian_dot(const OracleModel* m, const double* q, const doub
                                const double* p, double* J, double* Jdot);
 void oracle_joint_placement(const OracleModel* m, const double* q, int jid, double* T12);
 
+/* CLIKStep / CLIKCubic (mode 1 / 2) and OSF / OSFStep / OSFCubic (mode 0 / 1
+ * / 2) of Manipulator::RobotController (robot_controller.cpp:156-275).
+ * null_qdot / null_torque may be NULL (the overloads without them). */
+void oracle_clik_one(const OracleModel* m, const OracleParams* p, const double* q, const double* qdot,
+                     const double* x_target, const double* xdot_target, const double* x_init,
+                     const double* xdot_init, const double* null_qdot, double* out);
+void oracle_osf_one(const OracleModel* m, const OracleParams* p, const double* q, const double* qdot,
+                    const double* x_target, const double* xdot_target, const double* x_init,
+                    const double* xdot_init, const double* Minv, const double* g, const double* null_torque,
+                    double* out);
+
+void oracle_pinv_cod(const double* A, int m, int n, double* X);
+
 /* stage helpers exposed for tests */
 void oracle_fk_pose(const OracleModel* m, const double* q, double* pose12, double* J6xn);
 void oracle_min_distance(const OracleModel* m, const double* q, double* dist, double* grad, int* pair);

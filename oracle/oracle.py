@@ -341,3 +341,35 @@ def joint_placement(om, q, jid):
     out[:3, :3] = T[:9].reshape(3, 3)
     out[:3, 3] = T[9:]
     return out
+
+
+# ---------------------------------------------------------------------------
+# closed-form controllers: CLIK / OSF (robot_controller.cpp:156-275)
+# ---------------------------------------------------------------------------
+def clik_one(om, params, q, qdot, x_target, xdot_target, x_init=None, xdot_init=None, null_qdot=None):
+    f = lambda a, n: np.ascontiguousarray(a if a is not None else np.zeros(n), float)
+    out = np.zeros(om.nv)
+    nq = None if null_qdot is None else np.ascontiguousarray(null_qdot, float)
+    lib().oracle_clik_one(C.byref(om), C.byref(params), _ptr(f(q, om.nv)), _ptr(f(qdot, om.nv)), _ptr(f(x_target, 12)),
+                          _ptr(f(xdot_target, 6)), _ptr(f(x_init, 12)), _ptr(f(xdot_init, 6)), _ptr(nq), _ptr(out))
+    return out
+
+
+def osf_one(om, params, q, qdot, Minv, g, x_target=None, xdot_target=None, x_init=None, xdot_init=None,
+            null_torque=None):
+    f = lambda a, n: np.ascontiguousarray(a if a is not None else np.zeros(n), float)
+    out = np.zeros(om.nv)
+    nt = None if null_torque is None else np.ascontiguousarray(null_torque, float)
+    lib().oracle_osf_one(C.byref(om), C.byref(params), _ptr(f(q, om.nv)), _ptr(f(qdot, om.nv)), _ptr(f(x_target, 12)),
+                         _ptr(f(xdot_target, 6)), _ptr(f(x_init, 12)), _ptr(f(xdot_init, 6)),
+                         _ptr(np.ascontiguousarray(Minv, float)), _ptr(np.ascontiguousarray(g, float)), _ptr(nt),
+                         _ptr(out))
+    return out
+
+
+def pinv_cod(A):
+    A = np.ascontiguousarray(A, float)
+    m, n = A.shape
+    X = np.zeros((n, m))
+    lib().oracle_pinv_cod(_ptr(A), C.c_int(m), C.c_int(n), _ptr(X))
+    return X
