@@ -257,6 +257,39 @@ PYBIND11_MODULE(dyros_robot_controller_cpp_wrapper, m) {
       .def("QPIDCubic", [](const MN_RC& s, const Arr& xt, const Arr& xdt, const Arr& xi, const Arr& xdi, double t,
                            double t0, double T, const std::string& l) {
         return to_arr(s.QPIDCubic(to_pose(xt), to_vec(xdt), to_pose(xi), to_vec(xdi), t, t0, T, l));
+      })
+      // CLIK / OSF with the reference's overloads (bindings.cpp:398-426)
+      .def("CLIKStep", [](const MN_RC& s, const Arr& x, const Arr& xd, const std::string& l) {
+        return to_arr(s.CLIKStep(to_pose(x), to_vec(xd), l));
+      })
+      .def("CLIKStep", [](const MN_RC& s, const Arr& x, const Arr& xd, const Arr& nu, const std::string& l) {
+        return to_arr(s.CLIKStep(to_pose(x), to_vec(xd), to_vec(nu), l));
+      })
+      .def("CLIKCubic", [](const MN_RC& s, const Arr& xt, const Arr& xdt, const Arr& xi, const Arr& xdi, double t,
+                           double t0, double T, const std::string& l) {
+        return to_arr(s.CLIKCubic(to_pose(xt), to_vec(xdt), to_pose(xi), to_vec(xdi), t, t0, T, l));
+      })
+      .def("CLIKCubic", [](const MN_RC& s, const Arr& xt, const Arr& xdt, const Arr& xi, const Arr& xdi, double t,
+                           double t0, double T, const Arr& nu, const std::string& l) {
+        return to_arr(s.CLIKCubic(to_pose(xt), to_vec(xdt), to_pose(xi), to_vec(xdi), t, t0, T, to_vec(nu), l));
+      })
+      .def("OSF", [](const MN_RC& s, const Arr& xdd, const std::string& l) { return to_arr(s.OSF(to_vec(xdd), l)); })
+      .def("OSF", [](const MN_RC& s, const Arr& xdd, const Arr& nu, const std::string& l) {
+        return to_arr(s.OSF(to_vec(xdd), to_vec(nu), l));
+      })
+      .def("OSFStep", [](const MN_RC& s, const Arr& x, const Arr& xd, const std::string& l) {
+        return to_arr(s.OSFStep(to_pose(x), to_vec(xd), l));
+      })
+      .def("OSFStep", [](const MN_RC& s, const Arr& x, const Arr& xd, const Arr& nu, const std::string& l) {
+        return to_arr(s.OSFStep(to_pose(x), to_vec(xd), to_vec(nu), l));
+      })
+      .def("OSFCubic", [](const MN_RC& s, const Arr& xt, const Arr& xdt, const Arr& xi, const Arr& xdi, double t,
+                          double t0, double T, const std::string& l) {
+        return to_arr(s.OSFCubic(to_pose(xt), to_vec(xdt), to_pose(xi), to_vec(xdi), t, t0, T, l));
+      })
+      .def("OSFCubic", [](const MN_RC& s, const Arr& xt, const Arr& xdt, const Arr& xi, const Arr& xdi, double t,
+                          double t0, double T, const Arr& nu, const std::string& l) {
+        return to_arr(s.OSFCubic(to_pose(xt), to_vec(xdt), to_pose(xi), to_vec(xdi), t, t0, T, to_vec(nu), l));
       });
   add_controller_common<MN_RC, MN_RD>(mnrc);
 

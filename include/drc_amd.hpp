@@ -376,8 +376,72 @@ class RobotController : public ControllerBase {
                link, qdd, tau);
     return tau;
   }
+  // CLIKStep / CLIKCubic (robot_controller.cpp:156-214): joint velocities
+  Vec CLIKStep(const Pose& x_target, const Vec& xdot_target, const Vec& null_qdot, const std::string& link) const {
+    return closedForm(1, DRC_MODE_QPIK_STEP, &x_target, xdot_target, nullptr, nullptr, 0, 0, 1, &null_qdot, link);
+  }
+  Vec CLIKStep(const Pose& x_target, const Vec& xdot_target, const std::string& link) const {
+    return closedForm(1, DRC_MODE_QPIK_STEP, &x_target, xdot_target, nullptr, nullptr, 0, 0, 1, nullptr, link);
+  }
+  Vec CLIKCubic(const Pose& x_target, const Vec& xdot_target, const Pose& x_init, const Vec& xdot_init,
+                double current_time, double init_time, double duration, const Vec& null_qdot,
+                const std::string& link) const {
+    return closedForm(1, DRC_MODE_QPIK_CUBIC, &x_target, xdot_target, &x_init, &xdot_init, current_time, init_time,
+                      duration, &null_qdot, link);
+  }
+  Vec CLIKCubic(const Pose& x_target, const Vec& xdot_target, const Pose& x_init, const Vec& xdot_init,
+                double current_time, double init_time, double duration, const std::string& link) const {
+    return closedForm(1, DRC_MODE_QPIK_CUBIC, &x_target, xdot_target, &x_init, &xdot_init, current_time, init_time,
+                      duration, nullptr, link);
+  }
+  // OSF / OSFStep / OSFCubic (robot_controller.cpp:216-275): joint torques
+  Vec OSF(const Vec& xddot_target, const Vec& null_torque, const std::string& link) const {
+    return closedForm(2, DRC_MODE_QPIK, nullptr, xddot_target, nullptr, nullptr, 0, 0, 1, &null_torque, link);
+  }
+  Vec OSF(const Vec& xddot_target, const std::string& link) const {
+    return closedForm(2, DRC_MODE_QPIK, nullptr, xddot_target, nullptr, nullptr, 0, 0, 1, nullptr, link);
+  }
+  Vec OSFStep(const Pose& x_target, const Vec& xdot_target, const Vec& null_torque, const std::string& link) const {
+    return closedForm(2, DRC_MODE_QPIK_STEP, &x_target, xdot_target, nullptr, nullptr, 0, 0, 1, &null_torque, link);
+  }
+  Vec OSFStep(const Pose& x_target, const Vec& xdot_target, const std::string& link) const {
+    return closedForm(2, DRC_MODE_QPIK_STEP, &x_target, xdot_target, nullptr, nullptr, 0, 0, 1, nullptr, link);
+  }
+  Vec OSFCubic(const Pose& x_target, const Vec& xdot_target, const Pose& x_init, const Vec& xdot_init,
+               double current_time, double init_time, double duration, const Vec& null_torque,
+               const std::string& link) const {
+    return closedForm(2, DRC_MODE_QPIK_CUBIC, &x_target, xdot_target, &x_init, &xdot_init, current_time, init_time,
+                      duration, &null_torque, link);
+  }
+  Vec OSFCubic(const Pose& x_target, const Vec& xdot_target, const Pose& x_init, const Vec& xdot_init,
+               double current_time, double init_time, double duration, const std::string& link) const {
+    return closedForm(2, DRC_MODE_QPIK_CUBIC, &x_target, xdot_target, &x_init, &xdot_init, current_time, init_time,
+                      duration, nullptr, link);
+  }
 
  private:
+  Vec closedForm(int kind, int mode, const Pose* xt, const Vec& xdt, const Pose* xi, const Vec* xdi, double t,
+                 double t0, double T, const Vec* nullv, const std::string& link) const {
+    check6(xdt);
+    if (xdi) check6(*xdi);
+    const int n = robot_data_->getDof();
+    if (nullv && static_cast<int>(nullv->size()) != n) throw std::runtime_error("null vector must be of size dof_.");
+    drc_qpik_params p = id_params_;  // Kp_task_ / Kv_task_
+    p.mode = mode;
+    p.frame_id = robot_data_->frameId(link);
+    p.t = t;
+    p.t0 = t0;
+    p.duration = T;
+    std::array<double, 12> xt12{}, xi12{};
+    if (xt) xt12 = pose12(*xt);
+    if (xi) xi12 = pose12(*xi);
+    Vec out(n, 0.0);
+    check(drc_closed_form_host(robot_data_->handle(), &p, kind, 1, robot_data_->getJointPosition().data(),
+                               robot_data_->getJointVelocity().data(), xt ? xt12.data() : nullptr, xdt.data(),
+                               xi ? xi12.data() : nullptr, xdi ? xdi->data() : nullptr,
+                               nullv ? nullv->data() : nullptr, out.data()));
+    return out;
+  }
   std::shared_ptr<RobotData> robot_data_;
 };
 

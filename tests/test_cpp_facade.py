@@ -26,7 +26,8 @@ METHODS = {
                              "getJointPositionLimit", "getJointVelocityLimit"],
     "ManipulatorRobotController": ["setTaskGain", "setTaskKpGain", "setTaskKvGain", "QPIK", "QPIKStep", "QPIKCubic",
                                    "QPIKBatch", "QPIKStepBatch", "QPIKCubicBatch", "QPID", "QPIDStep", "QPIDCubic",
-                                   "QPIDBatch", "QPIDStepBatch", "QPIDCubicBatch"],
+                                   "QPIDBatch", "QPIDStepBatch", "QPIDCubicBatch", "CLIKStep", "CLIKCubic",
+                                   "OSF", "OSFStep", "OSFCubic"],
     "MobileManipulatorRobotData": ["getVerbose", "updateState", "getDof", "getActuatorDof", "getManipulatorDof",
                                    "getMobileDof", "getJointIndex", "getActuatorIndex", "getMobileFKJacobian",
                                    "getMinDistance"],
@@ -165,3 +166,32 @@ def test_module_qpid_step_and_graddot(cuda):
         np.testing.assert_allclose(mr.grad_dot, mgd, rtol=1e-7, atol=1e-8)
         dr = rd.getMinDistance(True, True, False)
         np.testing.assert_allclose(dr.grad_dot, dgd, atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_module_clik_osf(cuda):
+    import oracle as O
+    import pyref as R
+    from _common import step_inputs, make_manipulator
+    from dyros_robot_controller_amd import robot_path
+    from dyros_robot_controller_amd.manipulator import pose_from12
+    drc = _module()
+    rd = drc.ManipulatorRobotData(robot_path("fr3"), robot_path("fr3", "srdf"))
+    rc = drc.ManipulatorRobotController(0.001, rd)
+    q, qd, xt, xdt = step_inputs(make_manipulator("fr3", cuda), "fr3", 42, 4, cuda)
+    pm, om, spec = O.load("fr3")
+    par = O.default_params(0)
+    for b in range(4):
+        assert rd.updateState(q[:, b], qd[:, b])
+        T = pose_from12(xt[:, b])
+        par.mode = 1
+        np.testing.assert_allclose(rc.CLIKStep(T, xdt[:, b], "fr3_link8"),
+                                   O.clik_one(om, par, q[:, b], qd[:, b], xt[:, b], xdt[:, b]), rtol=1e-8, atol=1e-8)
+        nu = np.linspace(-1, 1, 7)
+        np.testing.assert_allclose(rc.CLIKStep(T, xdt[:, b], nu, "fr3_link8"),
+                                   O.clik_one(om, par, q[:, b], qd[:, b], xt[:, b], xdt[:, b], null_qdot=nu),
+                                   rtol=1e-8, atol=1e-8)
+        d = R.dynamics(pm, q[:, b], qd[:, b])
+        np.testing.assert_allclose(rc.OSFStep(T, xdt[:, b], nu, "fr3_link8"),
+                                   O.osf_one(om, par, q[:, b], qd[:, b], d["Minv"], d["g"], xt[:, b], xdt[:, b],
+                                             null_torque=nu), rtol=1e-6, atol=1e-6)
