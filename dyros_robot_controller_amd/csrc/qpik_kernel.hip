@@ -42,7 +42,8 @@ struct KParams {
   int rJac, rMan, rDist, rXdd, rQ, rLen;  // per-instance task record (doubles)
   int problem;                         // 0 QPIK, 1 QPID (torque-level QP)
   int rQd, rBias, rMgd, rDgd;          // QPID extras of the task record
-  int nbuf;                            // polish work-vector stride (64, or 128 when nx + ng > 64)
+  int nbuf;                            // polish work-vector stride (>= ncap)
+  int ncap;                            // largest polish KKT the LDS plan holds (nx + ng, or 48 for QPID)
   drc_solver_settings s;
   // persistent QP region
   int oP, oG, oQ, oAB, oL, oU, oD, oE, oRho, oX, oZ, oY, oDY, oXT, oZT, oT1, oT2, oRed, oSc;
@@ -92,7 +93,15 @@ __device__ unsigned long long g_phase_cycles[64];
 
 // scalar slots in the oSc region
 enum { SC_C = 0, SC_RHO, SC_MAN, SC_DIST, SC_PAIR, SC_PRI, SC_DUA, SC_EPSP, SC_EPSD, SC_PRIS, SC_DUAS,
-       SC_NAX, SC_NZ, SC_NPX, SC_NATY, SC_NQ, SC_NF, SC_NR, SC_WIN, SC_COUNT };
+       SC_NAX, SC_NZ, SC_NPX, SC_NATY, SC_NQ, SC_NF, SC_NR, SC_WIN, SC_PFAIL, SC_COUNT };
+// Parity mode tries the certified polish at every termination check, but only
+// until this many attempts failed on a not-yet-converged iterate; after that
+// only at convergence (bounds the cost of slow or non-converging instances —
+// the oracle makes the same decisions, oracle/drc_oracle.c:POLISH_MAX_EARLY)
+constexpr int kPolishMaxEarly = 4;
+// ... and at convergence (eps_abs / eps_rel met) until this many attempts in
+// total failed; after that only the tight ADMM fallback (eps_fallback) ends it
+constexpr int kPolishMaxTotal = 12;
 
 // ------------------------------------------------------------------------
 // small serial helpers (lane 0)
@@ -260,9 +269,13 @@ __device__ void so3_exp(V3 w, double* R) {
 // Compile-time QP dimensions (nx variables, ng general rows, np = leading
 // block of P).  Dims<0,0,0> is the runtime-sized fallback; the named robots
 // get fully unrolled inner products (LDS loads issued ahead of the FMAs).
-template <int NX, int NG, int NP>
+// QP shape: compile-time sizes (0 = runtime, from KParams).  reg: the
+// register-resident Ruiz / K^-1 / ADMM path (QPIK shapes); otherwise the LDS
+// path, whose loops still unroll when the sizes are compile-time.
+template <int NX, int NG, int NP, bool REG = (NX > 0)>
 struct Dims {
   static constexpr int nx = NX, ng = NG, np = NP;
+  static constexpr bool reg = REG;
 };
 #define DNX (QD::nx ? QD::nx : kp.nx)
 #define DNG (QD::ng ? QD::ng : kp.ng)
@@ -425,7 +438,7 @@ __device__ __noinline__ void factor_kinv_regs(const KParams& kp, double* S) {
 
 template <class QD>
 __device__ __forceinline__ void factor_any(const KParams& kp, double* S) {
-  if constexpr (QD::nx > 0) factor_kinv_regs<QD>(kp, S);
+  if constexpr (QD::reg) factor_kinv_regs<QD>(kp, S);
   else factor_kinv<QD>(kp, S);
 }
 
@@ -558,7 +571,7 @@ __device__ __noinline__ int admm_check(const KParams& kp, double* S, int it, int
     // parity mode: a certified polish is exact whatever the ADMM residual,
     // so try it at every check (the active set settles long before OSQP's
     // eps_rel termination)
-    if (kp.s.exact && !conv) {
+    if (kp.s.exact && !conv && sc[SC_PFAIL] < kPolishMaxEarly) {
       CK_T(34);
       const bool ok_ = polish<QD>(kp, S, true);
       CK_T(35);
@@ -568,6 +581,7 @@ __device__ __noinline__ int admm_check(const KParams& kp, double* S, int it, int
         *status = DRC_STATUS_SOLVED;
         return 2;
       }
+      if (lane_id() == 0) sc[SC_PFAIL] += 1.0;
       factor_any<QD>(kp, S);
       CK_T(38);  // polish used the union region
       residuals<QD>(kp, S, x, z, y, kp.s.eps_abs, kp.s.eps_rel);
@@ -578,17 +592,20 @@ __device__ __noinline__ int admm_check(const KParams& kp, double* S, int it, int
         *status = DRC_STATUS_SOLVED;
         return 2;
       }
-      CK_T(34);
-      const bool ok_ = polish<QD>(kp, S, true);
-      CK_T(35);
-      CK_N(36);
-      if (ok_) {
-        CK_N(37);
-        *status = DRC_STATUS_SOLVED;
-        return 2;
+      if (sc[SC_PFAIL] < kPolishMaxTotal) {
+        CK_T(34);
+        const bool ok_ = polish<QD>(kp, S, true);
+        CK_T(35);
+        CK_N(36);
+        if (ok_) {
+          CK_N(37);
+          *status = DRC_STATUS_SOLVED;
+          return 2;
+        }
+        if (lane_id() == 0) sc[SC_PFAIL] += 1.0;
+        factor_any<QD>(kp, S);
+        CK_T(38);
       }
-      factor_any<QD>(kp, S);
-      CK_T(38);
       residuals<QD>(kp, S, x, z, y, kp.s.eps_fallback, kp.s.eps_fallback);
       if (sc[SC_PRI] < sc[SC_EPSP] && sc[SC_DUA] < sc[SC_EPSD]) {
         *status = DRC_STATUS_SOLVED;
@@ -658,6 +675,7 @@ __device__ __forceinline__ bool eqp(const KParams& kp, double* S, int actb, int 
   unsigned long long freeMask = __ballot(l < nx && actb == 0);
   unsigned long long rowMask = __ballot(l < ng && actg != 0);
   const int nF = __popcll(freeMask), nR = __popcll(rowMask), N = nF + nR;
+  if (N > kp.ncap) return false;  // uniform: this polish attempt fails, ADMM continues
   double* U = S + kp.oU0;
   int* Fidx = reinterpret_cast<int*>(U);  // 64 ints
   int* Ridx = Fidx + 64;                   // 64 ints
@@ -2174,6 +2192,7 @@ __device__ __forceinline__ int qp_admm(const KParams& kp, const KParams& kpl, do
   int status = DRC_STATUS_MAX_ITER;
   (void)G;
   PHG_DECL
+  if (l == 0) sc[SC_PFAIL] = 0.0;
   set_rho<QD>(kp, S, kp.s.rho);
   factor_any<QD>(kpl, S);
   PHG(24);
@@ -2187,7 +2206,7 @@ __device__ __forceinline__ int qp_admm(const KParams& kp, const KParams& kpl, do
   double* xt = S + kp.oXT;
   const double sig = kp.s.sigma, al = kp.s.alpha;
   int it;
-  if constexpr (QD::nx > 0) {
+  if constexpr (QD::reg) {
     constexpr int NX = QD::nx, NG = QD::ng;
     double Gc[NG], Kr[NX], GKr[NX];
     prep_admm_mats<QD>(kpl, S);
@@ -2348,11 +2367,12 @@ __device__ __forceinline__ int qp_admm(const KParams& kp, const KParams& kpl, do
         const bool conv = sc[SC_PRI] < sc[SC_EPSP] && sc[SC_DUA] < sc[SC_EPSD];
         // parity mode: a certified polish is exact whatever the ADMM
         // residual, so also try it every 4th check (slow-ADMM vertices)
-        if (kp.s.exact && !conv) {
+        if (kp.s.exact && !conv && sc[SC_PFAIL] < kPolishMaxEarly) {
           if (polish<QD>(kp, S, true)) {
             status = DRC_STATUS_SOLVED;
             break;
           }
+          if (l == 0) sc[SC_PFAIL] += 1.0;
           factor_kinv<QD>(kp, S);  // polish used the union region
           residuals<QD>(kp, S, x, z, y, kp.s.eps_abs, kp.s.eps_rel);
         }
@@ -2361,11 +2381,14 @@ __device__ __forceinline__ int qp_admm(const KParams& kp, const KParams& kpl, do
             status = DRC_STATUS_SOLVED;
             break;
           }
-          if (polish<QD>(kp, S, true)) {
-            status = DRC_STATUS_SOLVED;
-            break;
+          if (sc[SC_PFAIL] < kPolishMaxTotal) {
+            if (polish<QD>(kp, S, true)) {
+              status = DRC_STATUS_SOLVED;
+              break;
+            }
+            if (l == 0) sc[SC_PFAIL] += 1.0;
+            factor_kinv<QD>(kp, S);  // polish used the union region
           }
-          factor_kinv<QD>(kp, S);  // polish used the union region
           residuals<QD>(kp, S, x, z, y, kp.s.eps_fallback, kp.s.eps_fallback);
           if (sc[SC_PRI] < sc[SC_EPSP] && sc[SC_DUA] < sc[SC_EPSD]) {
             status = DRC_STATUS_SOLVED;
@@ -2426,7 +2449,7 @@ qp_kernel(const DevModel* __restrict__ M0, const KParams kp, const IO io) {
     qp_assemble<QD>(M, kp, S, io, b);
     PH(0);
     int status, iters = 0;
-    if constexpr (QD::nx > 0) status = qp_scale_regs<QD>(kpl, S);
+    if constexpr (QD::reg) status = qp_scale_regs<QD>(kpl, S);
     else status = qp_scale<QD>(kp, S);
     PH(1);
     if (status != DRC_STATUS_NONFINITE) status = qp_admm<QD>(kp, kpl, S, &iters);
@@ -2576,9 +2599,11 @@ __device__ __forceinline__ void qpid_assemble(const DevModel* M, const KParams& 
   wsync();
 }
 
+// QD: Dims<nx, ng, np, false> for the bundled robots' QPID shapes (loops
+// unroll, loads pipeline), Dims<0, 0, 0> otherwise.
+template <class QD>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 8)))
 qpid_kernel(const DevModel* __restrict__ M0, const KParams kp, const IO io) {
-  using QD = Dims<0, 0, 0>;
   extern __shared__ __attribute__((aligned(16))) double S[];
   __shared__ KParams kpl;
   const int l = lane_id();
@@ -2844,8 +2869,13 @@ static int plan_layout(const DevModel& M, KParams* k, bool task_only) {
   }
   k->kEpa = (task_only && !k->cf) ? takeu(static_cast<int>((sizeof(EpaPoly) + 7) / 8)) : 0;
   int kin_end = u;
-  int kinv_end = k->oU0 + nx * nx + nx * ng;  // K^-1 and G K^-1
-  const int N = nx + ng;
+  // K^-1, and G K^-1 for the register ADMM (QPIK shapes); QPID runs the LDS path (K^-1 only)
+  int kinv_end = k->oU0 + nx * nx + (k->problem == 1 ? 0 : nx * ng);
+  // polish KKT: free variables + active G rows.  QPID's (<= 81) is capped at 48 —
+  // typically 7 qdd + 7 tau + 7 equality rows + the few active CBF rows and free
+  // slacks — which halves the per-wave LDS; a larger guess fails that polish try
+  const int N = k->problem == 1 ? 48 : nx + ng;
+  k->ncap = N;
   k->nbuf = N > 64 ? 128 : 64;
   int pol_end = k->oU0 + 64 + 64 + 128 + k->nbuf * 5 + N * (N + 1) / 2;
   int end = kin_end;
@@ -3124,8 +3154,18 @@ static int launch_qpid(const drc_model_impl* cm, const drc_qpik_params* params, 
                      static_cast<size_t>(kt_c.lds_doubles) * sizeof(double), st, m->d_model, kt_c, io);
   HIP_TRY(hipGetLastError());
   if (!stages) {
-    hipLaunchKernelGGL(qpid_kernel, dim3(static_cast<unsigned>(grid)), dim3(64),
-                       static_cast<size_t>(kq_c.lds_doubles) * sizeof(double), st, m->d_model, kq_c, io);
+    const dim3 g(static_cast<unsigned>(grid)), blk(64);
+    const size_t lds = static_cast<size_t>(kq_c.lds_doubles) * sizeof(double);
+    if (kq_c.nx == 44 && kq_c.ng == 37 && kq_c.np == 7)  // FR3
+      hipLaunchKernelGGL((qpid_kernel<Dims<44, 37, 7, false>>), g, blk, lds, st, m->d_model, kq_c, io);
+    else if (kq_c.nx == 38 && kq_c.ng == 32 && kq_c.np == 6)  // UR5e
+      hipLaunchKernelGGL((qpid_kernel<Dims<38, 32, 6, false>>), g, blk, lds, st, m->d_model, kq_c, io);
+    else if (kq_c.nx == 18 && kq_c.ng == 39 && kq_c.np == 9)  // Husky-FR3
+      hipLaunchKernelGGL((qpid_kernel<Dims<18, 39, 9, false>>), g, blk, lds, st, m->d_model, kq_c, io);
+    else if (kq_c.nx == 22 && kq_c.ng == 41 && kq_c.np == 11)  // XLS-FR3
+      hipLaunchKernelGGL((qpid_kernel<Dims<22, 41, 11, false>>), g, blk, lds, st, m->d_model, kq_c, io);
+    else
+      hipLaunchKernelGGL((qpid_kernel<Dims<0, 0, 0>>), g, blk, lds, st, m->d_model, kq_c, io);
     HIP_TRY(hipGetLastError());
   }
   return DRC_OK;

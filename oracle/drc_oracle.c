@@ -1165,6 +1165,11 @@ static int qp_eqp(const QPW* w, const OracleSettings* s, const int* flag, double
  * (Nocedal & Wright Alg. 16.3) from the first feasible polished point:
  * drop the worst wrong-sign multiplier, step to the equality-QP minimiser
  * with a ratio test, add the blocking row.  Exact on termination. */
+/* parity mode polishes at every check, but a not-yet-converged iterate gets at
+ * most POLISH_MAX_EARLY failed attempts; later only at convergence (same
+ * decisions as the kernel's kPolishMaxEarly) */
+#define POLISH_MAX_EARLY 4
+#define POLISH_MAX_TOTAL 12   /* then at convergence only the tight ADMM fallback */
 #define POLISH_FEAS_ATTEMPTS 4
 #define POLISH_AS_ITERS 24
 static int qp_polish(QPW* w, const OracleSettings* s, int strict) {
@@ -1286,7 +1291,7 @@ int oracle_solve_qp(int n, int m, const double* P, const double* qv, const doubl
     memset(w.x, 0, sizeof(w.x));
     memset(w.z, 0, sizeof(w.z));
     memset(w.y, 0, sizeof(w.y));
-    int status = ORC_MAX_ITER, it, pol = 0;
+    int status = ORC_MAX_ITER, it, pol = 0, pfail = 0;
     double alpha = s->alpha;
     for (it = 1; it <= s->max_iter; ++it) {
         double xt[ORC_MAXX], zt[ORC_MAXC], rhs[ORC_MAXX];
@@ -1315,12 +1320,16 @@ int oracle_solve_qp(int n, int m, const double* P, const double* qv, const doubl
             /* parity mode: a certified polish is exact whatever the ADMM
              * residual, so try it at every check (the active set settles
              * long before OSQP's eps_rel termination) */
-            if (s->exact && !conv && qp_polish(&w, s, 1)) {
-                status = ORC_SOLVED; pol = 1; break;
+            if (s->exact && !conv && pfail < POLISH_MAX_EARLY) {
+                if (qp_polish(&w, s, 1)) { status = ORC_SOLVED; pol = 1; break; }
+                ++pfail;
             }
             if (conv) {
                 if (!s->exact) { status = ORC_SOLVED; break; }
-                if (qp_polish(&w, s, 1)) { status = ORC_SOLVED; pol = 1; break; }
+                if (pfail < POLISH_MAX_TOTAL) {
+                    if (qp_polish(&w, s, 1)) { status = ORC_SOLVED; pol = 1; break; }
+                    ++pfail;
+                }
                 /* tight ADMM-only fallback */
                 Res t2;
                 qp_residuals(&w, &t2, w.x, w.z, w.y, s->eps_fallback, s->eps_fallback);

@@ -27,7 +27,7 @@ from dyros_robot_controller_amd import _batch, _capi  # noqa: E402
 HBM_PEAK_GBS = 8000.0
 
 
-def run(robot, B, steps, warmup, dev, cpu_n, exact):
+def run(robot, B, steps, warmup, dev, cpu_n, exact, max_iter=None):
     import oracle as O
     from _common import LINK, make_manipulator, make_moma, moma_step_inputs, step_inputs
     from dyros_robot_controller_amd import manipulator, mobile_manipulator as MM
@@ -41,6 +41,8 @@ def run(robot, B, steps, warmup, dev, cpu_n, exact):
         q, qd, xt, xdt = step_inputs(rd, robot, 12345, B, dev)
         ctrl = manipulator.RobotController(0.001, rd, solver_mode="exact" if exact else "osqp_default")
     p = ctrl._pbd.params(LINK[robot], _capi.MODE_QPID_STEP, ctrl.Kp_task_, ctrl.Kv_task_)
+    if max_iter:
+        p.solver.max_iter = max_iter
     a = lambda v: _batch.as_device(v, dev)
     dq, dqd, dxt, dxdt = a(q), a(qd), a(xt), a(xdt)
     na, D = rd.model.actuated_dof, rd.model.dof
@@ -68,7 +70,8 @@ def run(robot, B, steps, warmup, dev, cpu_n, exact):
     out = dict(robot=robot, B=B, mode="exact" if exact else "osqp_default", ms_per_call=ms,
                solves_per_s=B / (ms * 1e-3), bytes_per_solve=bytes_per,
                achieved_GBs=B * bytes_per / (ms * 1e-3) / 1e9, hbm_frac=B * bytes_per / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-               solved_frac=float(np.mean(stv == _capi.STATUS_SOLVED)), admm_iters_mean=float(iters.float().mean()))
+               solved_frac=float(np.mean(stv == _capi.STATUS_SOLVED)), admm_iters_mean=float(iters.float().mean()),
+               admm_iters_p99=float(np.percentile(iters.cpu().numpy(), 99)), admm_iters_max=int(iters.max()))
     if cpu_n:
         par = O.default_qpid_params(om.kind, exact=exact)
         par.mode = 1
@@ -90,10 +93,11 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--cpu", type=int, default=300)
     ap.add_argument("--osqp-default", action="store_true")
+    ap.add_argument("--max-iter", type=int, default=0, help="diagnostic: override OSQP max_iter")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     for r in args.robots.split(","):
-        print(json.dumps(run(r, args.B, args.steps, args.warmup, dev, args.cpu, not args.osqp_default)), flush=True)
+        print(json.dumps(run(r, args.B, args.steps, args.warmup, dev, args.cpu, not args.osqp_default, args.max_iter)), flush=True)
 
 
 if __name__ == "__main__":
