@@ -190,6 +190,7 @@ def main():
                                                 "frac": fl / FP64_VECTOR_PEAK_TFS,
                                                 "flops_per_solve": flops_per_solve(nv, it_mean)}},
             "non_solved": int(n_bad), "admm_iters_mean": it_mean,
+            "admm_iters_p99_max": [float(np.percentile(iters.cpu().numpy(), 99)), int(iters.max().item())],
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(robot, q, qd, xt, xdt)

@@ -1,6 +1,6 @@
 """Summarise a tools/profile_round.sh run into committed profiles.
 
-    python tools/pmc_summary.py <tag> [robot batch]
+    python tools/pmc_summary.py <tag> [robot batch chunks]
 
 Reads gpurun_out/prof_<tag>/ and writes
   profiles/<tag>_bench.json          the bench line of that run
@@ -48,6 +48,7 @@ def main():
     tag = sys.argv[1]
     robot = sys.argv[2] if len(sys.argv) > 2 else "fr3"
     batch = int(sys.argv[3]) if len(sys.argv) > 3 else 65536
+    chunks = int(sys.argv[4]) if len(sys.argv) > 4 else 2   # sub-batches per drc_qpik_batch call (bench default)
     src = os.path.join(ROOT, "gpurun_out", "prof_" + tag)
     dst = os.path.join(ROOT, "profiles")
     os.makedirs(dst, exist_ok=True)
@@ -67,8 +68,11 @@ def main():
         kern[k] = {"FETCH_SIZE_KiB_raw": fetch.get(k), "WRITE_SIZE_KiB_raw": write.get(k),
                    "fetch_bytes": 2 * 1024 * fetch.get(k, 0.0), "write_bytes": 1024 * write.get(k, 0.0),
                    "dispatches": [nf.get(k, 0), nw.get(k, 0)], "avg_duration_ns": avg.get(k)}
-    out = {"robot": robot, "batch": batch, "tag": tag, "kernels": kern,
-           "hbm_bytes_per_step": sum(v["fetch_bytes"] + v["write_bytes"] for v in kern.values()),
+    per_dispatch = sum(v["fetch_bytes"] + v["write_bytes"] for v in kern.values())
+    # each dispatch pair covers one sub-batch (batch / chunks instances); a step is one call
+    out = {"robot": robot, "batch": batch, "chunks": chunks, "tag": tag, "kernels": kern,
+           "hbm_bytes_per_step": chunks * per_dispatch,
+           "hbm_bytes_per_instance": chunks * per_dispatch / batch,
            "corrections": "FETCH_SIZE KiB x1024 x2 (gfx950 half-count), WRITE_SIZE KiB x1024",
            "kernel_stats_avg_ns": avg}
     for name in (tag + "_pmc.json", "pmc_traffic.json"):
