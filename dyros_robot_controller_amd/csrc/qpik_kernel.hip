@@ -272,10 +272,14 @@ __device__ void so3_exp(V3 w, double* R) {
 // QP shape: compile-time sizes (0 = runtime, from KParams).  reg: the
 // register-resident Ruiz / K^-1 / ADMM path (QPIK shapes); otherwise the LDS
 // path, whose loops still unroll when the sizes are compile-time.
-template <int NX, int NG, int NP, bool REG = (NX > 0)>
+// schur: the register ADMM solves K x~ = rhs through the Schur complement of
+// K's auxiliary block (every variable past np — slacks — sits in exactly one G
+// row, so that block is diagonal): S = K_cc - K_ca D^-1 K_ac is np x np.
+template <int NX, int NG, int NP, bool REG = (NX > 0), bool SCHUR = false>
 struct Dims {
   static constexpr int nx = NX, ng = NG, np = NP;
   static constexpr bool reg = REG;
+  static constexpr bool schur = SCHUR;
 };
 #define DNX (QD::nx ? QD::nx : kp.nx)
 #define DNG (QD::ng ? QD::ng : kp.ng)
@@ -436,9 +440,98 @@ __device__ __noinline__ void factor_kinv_regs(const KParams& kp, double* S) {
   wsync();
 }
 
+// ------------------------------------------------------------------------
+// Schur-complement factorisation (QD::schur).  Variables j >= np ("aux":
+// slacks) appear in the cost only linearly and each sits in exactly one G row
+// a(r) (QP_IK.cpp:99-131), so with rows r = 0..ng-1, bound rows b:
+//   K_cc = P + sigma I + diag(rho_b ab^2) + sum_r rho_r G_rc G_rc^T
+//   K_aa = diag(d_a),  d_a = sigma + rho_b(a) ab_a^2 + rho_r g_r^2   (g_r = G[r][a(r)])
+//   S    = K_cc - K_ca K_aa^-1 K_ac = P + sigma I + diag(rho_b ab^2) + sum_r w_r G_rc G_rc^T,
+//   w_r  = rho_r - (rho_r g_r)^2 / d_a.
+// LDS union layout: S^-1 (np x np) | G_c S^-1 (ng x np) | d | coef = rho_r g_r / d | aux (int).
+// Same linear solve as K^-1 (different rounding).
+// ------------------------------------------------------------------------
+template <class QD>
+__device__ __noinline__ void schur_setup(const KParams& kp, double* S) {
+  constexpr int NX = QD::nx, NG = QD::ng, NP = QD::np;
+  const int l = lane_id();
+  const double *P = S + kp.oP, *G = S + kp.oG, *ab = S + kp.oAB, *rho = S + kp.oRho;
+  double* Si = S + kp.oU0;             // NP x NP
+  double* GS = Si + NP * NP;           // NG x NP
+  double* dv = GS + NG * NP;           // NG
+  double* cf = dv + NG;                // NG
+  double* wt = cf + NG;                // NG (row weights w_r)
+  int* aux = reinterpret_cast<int*>(wt + NG);  // NG
+  const double sig = kp.s.sigma;
+  if (l < NG) {
+    int a = -1;
+    for (int j = NP; j < NX; ++j)
+      if (G[l * NX + j] != 0.0) a = j;
+    const double rr = rho[NX + l];
+    double d = 1.0, w = rr, c = 0.0;
+    if (a >= 0) {
+      const double g = G[l * NX + a];
+      d = sig + rho[a] * ab[a] * ab[a] + rr * g * g;
+      c = rr * g / d;
+      w = rr - rr * g * c;
+    }
+    aux[l] = a;
+    dv[l] = d;
+    cf[l] = c;
+    wt[l] = w;
+  }
+  wsync();
+  if (l < NP) {  // row l of S
+#pragma unroll
+    for (int c = 0; c < NP; ++c) {
+      double sv = P[l * NP + c];
+      if (c == l) sv += sig + rho[l] * ab[l] * ab[l];
+#pragma unroll
+      for (int r = 0; r < NG; ++r) sv += wt[r] * G[r * NX + l] * G[r * NX + c];
+      Si[l * NP + c] = sv;
+    }
+  }
+  wsync();
+  // Gauss-Jordan in registers, lane l holding row l (S is SPD)
+  const int lr = l < NP ? l : 0;
+  double Sr[NP];
+#pragma unroll
+  for (int c = 0; c < NP; ++c) Sr[c] = Si[lr * NP + c];
+#pragma unroll
+  for (int k = 0; k < NP; ++k) {
+    if (l == k) {
+      const double pv = 1.0 / Sr[k];
+      Sr[k] = 1.0;
+#pragma unroll
+      for (int j = 0; j < NP; ++j) Sr[j] *= pv;
+    }
+    const double f = Sr[k];
+    if (l != k) Sr[k] = 0.0;
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+      const double rkj = bcast(Sr[j], k);
+      if (l != k) Sr[j] -= f * rkj;
+    }
+  }
+  if (l < NP) {
+#pragma unroll
+    for (int c = 0; c < NP; ++c) Si[l * NP + c] = Sr[c];
+  }
+  wsync();
+  for (int e = l; e < NG * NP; e += 64) {  // G_c S^-1
+    const int r = e / NP, c = e % NP;
+    double sv = 0;
+#pragma unroll
+    for (int k = 0; k < NP; ++k) sv += G[r * NX + k] * Si[k * NP + c];
+    GS[e] = sv;
+  }
+  wsync();
+}
+
 template <class QD>
 __device__ __forceinline__ void factor_any(const KParams& kp, double* S) {
-  if constexpr (QD::reg) factor_kinv_regs<QD>(kp, S);
+  if constexpr (QD::schur) schur_setup<QD>(kp, S);
+  else if constexpr (QD::reg) factor_kinv_regs<QD>(kp, S);
   else factor_kinv<QD>(kp, S);
 }
 
@@ -508,6 +601,7 @@ __device__ __forceinline__ double bcast(double v, int lane) {
 // so the ADMM loop's register file stays free)
 template <class QD>
 __device__ __noinline__ void prep_admm_mats(const KParams& kp, double* S) {
+  if constexpr (QD::schur) return;  // schur_setup already formed G_c S^-1
   constexpr int NX = QD::nx, NG = QD::ng;
   const int l = lane_id();
   const double* K = S + kp.oU0;
@@ -2206,7 +2300,166 @@ __device__ __forceinline__ int qp_admm(const KParams& kp, const KParams& kpl, do
   double* xt = S + kp.oXT;
   const double sig = kp.s.sigma, al = kp.s.alpha;
   int it;
-  if constexpr (QD::reg) {
+  if constexpr (QD::schur) {
+    // Lane roles: l < NP core variable l (and its bound row); NP + r < NP + NG:
+    // G row r together with its auxiliary variable a(r) and that variable's
+    // bound row.  R[] holds, on core lanes, row l of S^-1 then column l of
+    // G_c; on row lanes, row r of G_c S^-1.  Per iteration:
+    //   rows: t_a = r_a / d_a, u_r = w_r - rho_r g_r t_a       (w = rho z - y)
+    //   core: r'_c = sigma x_c - q_c + ab_c w_b + sum_r G_rc u_r   (NG broadcasts)
+    //   core: x~_c = S^-1 r';  rows: v_r = G_r,c x~_c = (G_c S^-1)_r r'   (NP broadcasts)
+    //   rows: x~_a = t_a - coef_r v_r,  (G x~)_r = v_r + g_r x~_a
+    constexpr int NX = QD::nx, NG = QD::ng, NP = QD::np;
+    static_assert(NP + NG <= 64, "one lane per core variable and per G row");
+    const double* Si = S + kp.oU0;
+    const double* GS = Si + NP * NP;
+    const double* dv = GS + NG * NP;
+    const double* cf = dv + NG;
+    const int* aux = reinterpret_cast<const int*>(cf + 2 * NG);
+    const double* G = S + kp.oG;
+    double R[NP + NG];
+    const bool hc = l < NP, hr = l >= NP && l < NP + NG;
+    const int rr_ = hr ? l - NP : 0, lc_ = hc ? l : 0;
+    auto load_regs = [&]() {
+      if (hc) {
+#pragma unroll
+        for (int c = 0; c < NP; ++c) R[c] = Si[lc_ * NP + c];
+#pragma unroll
+        for (int i = 0; i < NG; ++i) R[NP + i] = G[i * NX + lc_];
+      } else {
+#pragma unroll
+        for (int c = 0; c < NP; ++c) R[c] = GS[rr_ * NP + c];
+#pragma unroll
+        for (int i = 0; i < NG; ++i) R[NP + i] = 0.0;
+      }
+    };
+    load_regs();
+    PHG(25);
+#ifdef DRC_PHASE_TIMING
+    unsigned long long tchk = 0;
+#endif
+    const int a_ = hr ? aux[rr_] : -1;           // auxiliary variable of row r (or -1)
+    const bool ha = a_ >= 0;
+    const int ia = ha ? a_ : 0, ig = NX + rr_;   // its bound row, the G row
+    // core lane: its bound row; row lane: the G row and the aux bound row
+    const double ab_c = ab[lc_], q_c = qq[lc_], lo_c = lo[lc_], up_c = up[lc_];
+    const double g_r = ha ? G[rr_ * NX + ia] : 0.0, ab_a = ab[ia], q_a = qq[ia];
+    const double lo_a = lo[ia], up_a = up[ia], lo_g = lo[ig], up_g = up[ig];
+    double d_r = dv[rr_], c_r = cf[rr_];
+    double rc = rv[lc_], ra = rv[ia], rg = rv[ig];
+    double xc = 0, zc = 0, yc = 0, dyc = 0, xa = 0, za = 0, ya = 0, dya = 0, zg = 0, yg = 0, dyg = 0;
+    for (it = 1; it <= kp.s.max_iter; ++it) {
+      double u = 0, ta = 0, loc = 0;
+      if (hr) {
+        const double wg = rg * zg - yg;
+        if (ha) {
+          const double r_a = sig * xa - q_a + ab_a * (ra * za - ya) + g_r * wg;
+          ta = r_a / d_r;
+          u = wg - rg * g_r * ta;
+        } else {
+          u = wg;
+        }
+      }
+      if (hc) loc = sig * xc - q_c + ab_c * (rc * zc - yc);
+      double r0 = 0, r1 = 0;
+#pragma unroll
+      for (int i = 0; i < NG; ++i) {
+        const double ui = bcast(u, NP + i);
+        if (i & 1) r1 += R[NP + i] * ui;
+        else r0 += R[NP + i] * ui;
+      }
+      const double rp = loc + (r0 + r1);
+      double s0 = 0, s1 = 0;
+#pragma unroll
+      for (int c = 0; c < NP; ++c) {
+        const double rpc = bcast(rp, c);
+        if (c & 1) s1 += R[c] * rpc;
+        else s0 += R[c] * rpc;
+      }
+      const double sv = s0 + s1;  // core: x~_c; row: v_r = G_r,c x~_c
+      if (hc) {
+        const double zr = al * ab_c * sv + (1 - al) * zc;
+        double zn = zr + yc / rc;
+        zn = fmin(fmax(zn, lo_c), up_c);
+        dyc = rc * (zr - zn);
+        yc += dyc;
+        zc = zn;
+        xc = al * sv + (1 - al) * xc;
+      }
+      if (hr) {
+        const double xta = ha ? ta - c_r * sv : 0.0;
+        {  // G row
+          const double zr = al * (sv + g_r * xta) + (1 - al) * zg;
+          double zn = zr + yg / rg;
+          zn = fmin(fmax(zn, lo_g), up_g);
+          dyg = rg * (zr - zn);
+          yg += dyg;
+          zg = zn;
+        }
+        if (ha) {  // bound row of the aux variable
+          const double zr = al * ab_a * xta + (1 - al) * za;
+          double zn = zr + ya / ra;
+          zn = fmin(fmax(zn, lo_a), up_a);
+          dya = ra * (zr - zn);
+          ya += dya;
+          za = zn;
+          xa = al * xta + (1 - al) * xa;
+        }
+      }
+      const bool check = kp.s.check_termination > 0 && it % kp.s.check_termination == 0;
+      const bool adapt = kp.s.adaptive_rho && kp.s.adaptive_rho_interval > 0 && it % kp.s.adaptive_rho_interval == 0;
+      if (!(check || adapt) && it < kp.s.max_iter) continue;
+      // publish the iterate for the (LDS) residual / polish / rho code
+      if (hc) {
+        x[l] = xc;
+        z[l] = zc;
+        y[l] = yc;
+        dy[l] = dyc;
+      }
+      if (hr) {
+        z[ig] = zg;
+        y[ig] = yg;
+        dy[ig] = dyg;
+        if (ha) {
+          x[ia] = xa;
+          z[ia] = za;
+          y[ia] = ya;
+          dy[ia] = dya;
+        }
+      }
+      wsync();
+      if (!(check || adapt)) continue;  // last iteration: published for the output
+#ifdef DRC_PHASE_TIMING
+      const unsigned long long tc0 = __builtin_amdgcn_s_memtime();
+#endif
+      const int act = admm_check<QD>(kpl, S, it, check, adapt, &status);
+#ifdef DRC_PHASE_TIMING
+      tchk += __builtin_amdgcn_s_memtime() - tc0;
+#endif
+      if (act == 2) break;
+      load_regs();  // S^-1 / rho may have changed, the iterate may be polished
+      d_r = dv[rr_];
+      c_r = cf[rr_];
+      rc = rv[lc_];
+      ra = rv[ia];
+      rg = rv[ig];
+      xc = x[lc_];
+      zc = z[lc_];
+      yc = y[lc_];
+      xa = x[ia];
+      za = z[ia];
+      ya = y[ia];
+      zg = z[ig];
+      yg = y[ig];
+    }
+#ifdef DRC_PHASE_TIMING
+    PHG(26);
+    if (l == 0) {
+      atomicAdd(&g_phase_cycles[27], tchk);
+      atomicAdd(&g_phase_cycles[26], 0ull - tchk);
+    }
+#endif
+  } else if constexpr (QD::reg) {
     constexpr int NX = QD::nx, NG = QD::ng;
     double Gc[NG], Kr[NX], GKr[NX];
     prep_admm_mats<QD>(kpl, S);
@@ -3063,13 +3316,13 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
       // compile-time QP shapes of the bundled robots; anything else runs the
       // runtime-sized instantiation
       if (kq_c.nx == 23 && kq_c.ng == 16 && kq_c.np == 7)
-        hipLaunchKernelGGL((qp_kernel<Dims<23, 16, 7>>), g, blk, lds, cs, m->d_model, kq_c, io);  // FR3
+        hipLaunchKernelGGL((qp_kernel<Dims<23, 16, 7, true, true>>), g, blk, lds, cs, m->d_model, kq_c, io);  // FR3
       else if (kq_c.nx == 20 && kq_c.ng == 14 && kq_c.np == 6)
-        hipLaunchKernelGGL((qp_kernel<Dims<20, 14, 6>>), g, blk, lds, cs, m->d_model, kq_c, io);  // UR5e
+        hipLaunchKernelGGL((qp_kernel<Dims<20, 14, 6, true, true>>), g, blk, lds, cs, m->d_model, kq_c, io);  // UR5e
       else if (kq_c.nx == 9 && kq_c.ng == 16 && kq_c.np == 9)
-        hipLaunchKernelGGL((qp_kernel<Dims<9, 16, 9>>), g, blk, lds, cs, m->d_model, kq_c, io);  // Husky-FR3
+        hipLaunchKernelGGL((qp_kernel<Dims<9, 16, 9, true, true>>), g, blk, lds, cs, m->d_model, kq_c, io);  // Husky-FR3
       else if (kq_c.nx == 11 && kq_c.ng == 16 && kq_c.np == 11)
-        hipLaunchKernelGGL((qp_kernel<Dims<11, 16, 11>>), g, blk, lds, cs, m->d_model, kq_c, io);  // XLS-FR3
+        hipLaunchKernelGGL((qp_kernel<Dims<11, 16, 11, true, true>>), g, blk, lds, cs, m->d_model, kq_c, io);  // XLS-FR3
       else
         hipLaunchKernelGGL((qp_kernel<Dims<0, 0, 0>>), g, blk, lds, cs, m->d_model, kq_c, io);
       HIP_TRY(hipGetLastError());
