@@ -3410,13 +3410,13 @@ static int launch_qpid(const drc_model_impl* cm, const drc_qpik_params* params, 
     const dim3 g(static_cast<unsigned>(grid)), blk(64);
     const size_t lds = static_cast<size_t>(kq_c.lds_doubles) * sizeof(double);
     if (kq_c.nx == 44 && kq_c.ng == 37 && kq_c.np == 7)  // FR3
-      hipLaunchKernelGGL((qpid_kernel<Dims<44, 37, 7, false>>), g, blk, lds, st, m->d_model, kq_c, io);
+      hipLaunchKernelGGL((qpid_kernel<Dims<44, 37, 7, false, true>>), g, blk, lds, st, m->d_model, kq_c, io);
     else if (kq_c.nx == 38 && kq_c.ng == 32 && kq_c.np == 6)  // UR5e
-      hipLaunchKernelGGL((qpid_kernel<Dims<38, 32, 6, false>>), g, blk, lds, st, m->d_model, kq_c, io);
+      hipLaunchKernelGGL((qpid_kernel<Dims<38, 32, 6, false, true>>), g, blk, lds, st, m->d_model, kq_c, io);
     else if (kq_c.nx == 18 && kq_c.ng == 39 && kq_c.np == 9)  // Husky-FR3
-      hipLaunchKernelGGL((qpid_kernel<Dims<18, 39, 9, false>>), g, blk, lds, st, m->d_model, kq_c, io);
+      hipLaunchKernelGGL((qpid_kernel<Dims<18, 39, 9, false, true>>), g, blk, lds, st, m->d_model, kq_c, io);
     else if (kq_c.nx == 22 && kq_c.ng == 41 && kq_c.np == 11)  // XLS-FR3
-      hipLaunchKernelGGL((qpid_kernel<Dims<22, 41, 11, false>>), g, blk, lds, st, m->d_model, kq_c, io);
+      hipLaunchKernelGGL((qpid_kernel<Dims<22, 41, 11, false, true>>), g, blk, lds, st, m->d_model, kq_c, io);
     else
       hipLaunchKernelGGL((qpid_kernel<Dims<0, 0, 0>>), g, blk, lds, st, m->d_model, kq_c, io);
     HIP_TRY(hipGetLastError());
