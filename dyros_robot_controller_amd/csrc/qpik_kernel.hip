@@ -448,7 +448,7 @@ __device__ __noinline__ void factor_kinv_regs(const KParams& kp, double* S) {
 //   K_aa = diag(d_a),  d_a = sigma + rho_b(a) ab_a^2 + rho_r g_r^2   (g_r = G[r][a(r)])
 //   S    = K_cc - K_ca K_aa^-1 K_ac = P + sigma I + diag(rho_b ab^2) + sum_r w_r G_rc G_rc^T,
 //   w_r  = rho_r - (rho_r g_r)^2 / d_a.
-// LDS union layout: S^-1 (np x np) | G_c S^-1 (ng x np) | d | coef = rho_r g_r / d | aux (int).
+// LDS union layout: S^-1 (np x np) | G_c S^-1 (ng x np) | 1/d | coef = rho_r g_r / d | w | aux (int).
 // Same linear solve as K^-1 (different rounding).
 // ------------------------------------------------------------------------
 template <class QD>
@@ -476,7 +476,7 @@ __device__ __noinline__ void schur_setup(const KParams& kp, double* S) {
       w = rr - rr * g * c;
     }
     aux[l] = a;
-    dv[l] = d;
+    dv[l] = 1.0 / d;  // the ADMM loop multiplies by 1 / d_a
     cf[l] = c;
     wt[l] = w;
   }
@@ -2354,7 +2354,7 @@ __device__ __forceinline__ int qp_admm(const KParams& kp, const KParams& kpl, do
         const double wg = rg * zg - yg;
         if (ha) {
           const double r_a = sig * xa - q_a + ab_a * (ra * za - ya) + g_r * wg;
-          ta = r_a / d_r;
+          ta = r_a * d_r;  // d_r holds 1 / d_a
           u = wg - rg * g_r * ta;
         } else {
           u = wg;
