@@ -770,6 +770,13 @@ __device__ __forceinline__ bool eqp(const KParams& kp, double* S, int actb, int 
   unsigned long long rowMask = __ballot(l < ng && actg != 0);
   const int nF = __popcll(freeMask), nR = __popcll(rowMask), N = nF + nR;
   if (N > kp.ncap) return false;  // uniform: this polish attempt fails, ADMM continues
+#ifdef DRC_PHASE_TIMING
+  const unsigned long long eq_t0 = __builtin_amdgcn_s_memtime();
+  if (l == 0) {
+    atomicAdd(&g_phase_cycles[41], 1ull);
+    atomicAdd(&g_phase_cycles[42], (unsigned long long)N);
+  }
+#endif
   double* U = S + kp.oU0;
   int* Fidx = reinterpret_cast<int*>(U);  // 64 ints
   int* Ridx = Fidx + 64;                   // 64 ints
@@ -871,6 +878,9 @@ __device__ __forceinline__ bool eqp(const KParams& kp, double* S, int actb, int 
     yy[l] = -g / ab[l];
   }
   wsync();
+#ifdef DRC_PHASE_TIMING
+  if (l == 0) atomicAdd(&g_phase_cycles[40], __builtin_amdgcn_s_memtime() - eq_t0);
+#endif
   return true;
 }
 
@@ -960,7 +970,13 @@ __device__ __forceinline__ bool polish(const KParams& kp, double* S, bool strict
       zz[nx + l] = fmin(fmax(axg, lo[nx + l]), up[nx + l]);
     }
     wsync();
+#ifdef DRC_PHASE_TIMING
+    const unsigned long long rs_t0 = __builtin_amdgcn_s_memtime();
+#endif
     residuals<QD>(kp, S, xx, zz, yy, kp.s.eps_exact, kp.s.eps_exact);
+#ifdef DRC_PHASE_TIMING
+    if (l == 0) atomicAdd(&g_phase_cycles[43], __builtin_amdgcn_s_memtime() - rs_t0);
+#endif
     const double pr1 = sc[SC_PRI], dr1 = sc[SC_DUA], epsp = sc[SC_EPSP], epsd = sc[SC_EPSD], c = sc[SC_C];
     bool ok = (pr1 < pr0 && dr1 < dr0) || (pr1 < pr0 && dr0 < 1e-10) || (dr1 < dr0 && pr0 < 1e-10);
     double wv = 0;
@@ -2347,6 +2363,7 @@ __device__ __forceinline__ int qp_admm(const KParams& kp, const KParams& kpl, do
     const double lo_a = lo[ia], up_a = up[ia], lo_g = lo[ig], up_g = up[ig];
     double d_r = dv[rr_], c_r = cf[rr_];
     double rc = rv[lc_], ra = rv[ia], rg = rv[ig];
+    double irc = 1.0 / rc, ira = 1.0 / ra, irg = 1.0 / rg;  // y / rho as a product in the loop
     double xc = 0, zc = 0, yc = 0, dyc = 0, xa = 0, za = 0, ya = 0, dya = 0, zg = 0, yg = 0, dyg = 0;
     for (it = 1; it <= kp.s.max_iter; ++it) {
       double u = 0, ta = 0, loc = 0;
@@ -2379,7 +2396,7 @@ __device__ __forceinline__ int qp_admm(const KParams& kp, const KParams& kpl, do
       const double sv = s0 + s1;  // core: x~_c; row: v_r = G_r,c x~_c
       if (hc) {
         const double zr = al * ab_c * sv + (1 - al) * zc;
-        double zn = zr + yc / rc;
+        double zn = zr + yc * irc;
         zn = fmin(fmax(zn, lo_c), up_c);
         dyc = rc * (zr - zn);
         yc += dyc;
@@ -2390,7 +2407,7 @@ __device__ __forceinline__ int qp_admm(const KParams& kp, const KParams& kpl, do
         const double xta = ha ? ta - c_r * sv : 0.0;
         {  // G row
           const double zr = al * (sv + g_r * xta) + (1 - al) * zg;
-          double zn = zr + yg / rg;
+          double zn = zr + yg * irg;
           zn = fmin(fmax(zn, lo_g), up_g);
           dyg = rg * (zr - zn);
           yg += dyg;
@@ -2398,7 +2415,7 @@ __device__ __forceinline__ int qp_admm(const KParams& kp, const KParams& kpl, do
         }
         if (ha) {  // bound row of the aux variable
           const double zr = al * ab_a * xta + (1 - al) * za;
-          double zn = zr + ya / ra;
+          double zn = zr + ya * ira;
           zn = fmin(fmax(zn, lo_a), up_a);
           dya = ra * (zr - zn);
           ya += dya;
@@ -2443,6 +2460,9 @@ __device__ __forceinline__ int qp_admm(const KParams& kp, const KParams& kpl, do
       rc = rv[lc_];
       ra = rv[ia];
       rg = rv[ig];
+      irc = 1.0 / rc;
+      ira = 1.0 / ra;
+      irg = 1.0 / rg;
       xc = x[lc_];
       zc = z[lc_];
       yc = y[lc_];
