@@ -755,6 +755,123 @@ __device__ __forceinline__ void ldl_solve(const double* L, const double* dg, int
   }
 }
 
+// Register form of eqp for compile-time shapes and small reduced KKTs
+// (N <= kEqpRegCap, the common case: most q-dot are at their bounds or the
+// active set is small).  Lane i holds row i of the unregularised KKT (K0) and
+// of the inverse of the regularised one, formed by a Gauss-Jordan sweep with
+// the pivot row moving by v_readlane (no pivoting: the regularised KKT is
+// quasi-definite, so the natural order has nonzero pivots, as the LDL^T).
+// Solve and iterative refinement against K0 are N broadcasts each.  Same
+// system, assembly, refinement count and outputs as eqp's LDS LDL^T; only
+// the rounding of the factorisation differs.
+constexpr int kEqpRegCap = 16;
+template <class QD>
+__device__ __forceinline__ bool eqp_regs(const KParams& kp, double* S, int actb, int actg, double* xx, double* yy,
+                                         unsigned long long freeMask, unsigned long long rowMask, int nF, int nR) {
+  constexpr int NX = QD::nx, NG = QD::ng, NP = QD::np, M = NX + NG, NK = kEqpRegCap;
+  const int l = lane_id(), N = nF + nR;
+  const double *P = S + kp.oP, *G = S + kp.oG, *q = S + kp.oQ, *ab = S + kp.oAB, *lo = S + kp.oL,
+               *up = S + kp.oU;
+  int* Fidx = reinterpret_cast<int*>(S + kp.oU0);  // 64 ints
+  int* Ridx = Fidx + 64;                           // 64 ints
+  const unsigned long long below = (1ull << l) - 1;
+  if (l < NX && actb == 0) Fidx[__popcll(freeMask & below)] = l;
+  if (l < NG && actg != 0) Ridx[__popcll(rowMask & below)] = l;
+  if (l < NX) xx[l] = actb == 0 ? 0.0 : (actb < 0 ? lo[l] : up[l]) / ab[l];
+  wsync();
+  // right-hand sides by their owners: variable l (free) and G row l (active)
+  double rF = 0.0, rG = 0.0;
+  if (l < NX && actb == 0) {
+    double r = -q[l];
+    if (l < NP)
+      for (int c = 0; c < NP; ++c)
+        if (xx[c] != 0.0) r -= P[l * NP + c] * xx[c];
+    rF = r;
+  }
+  if (l < NG && actg != 0) {
+    double r = actg < 0 ? lo[NX + l] : up[NX + l];
+    for (int c = 0; c < NX; ++c)
+      if (xx[c] != 0.0) r -= G[l * NX + c] * xx[c];
+    rG = r;
+  }
+  const bool hf = l < nF, hr = l >= nF && l < N;
+  const int fi = hf ? Fidx[l] : 0, gi = hr ? Ridx[l - nF] : 0;
+  const double rF_ = __shfl(rF, fi, 64), rG_ = __shfl(rG, gi, 64);
+  const double rhs = hf ? rF_ : (hr ? rG_ : 0.0);
+  // row l of K0: columns j < nF are the free variables, j >= nF the active rows
+  double K0[NK], Ki[NK];
+  {
+    unsigned long long fm = freeMask, rm = rowMask;
+#pragma unroll
+    for (int j = 0; j < NK; ++j) {
+      double v = 0.0;
+      if (j < nF) {
+        const int fj = __builtin_ctzll(fm);
+        fm &= fm - 1;
+        if (hf) v = (fi < NP && fj < NP) ? P[fi * NP + fj] : 0.0;
+        else if (hr) v = G[gi * NX + fj];
+      } else if (j < N) {
+        const int gj = __builtin_ctzll(rm);
+        rm &= rm - 1;
+        if (hf) v = G[gj * NX + fi];
+      }
+      K0[j] = v;
+      Ki[j] = v + (j == l ? (hf ? kp.s.delta : (hr ? -kp.s.delta : 0.0)) : 0.0);
+    }
+  }
+  // Gauss-Jordan inverse of the regularised KKT
+#pragma unroll
+  for (int k = 0; k < NK; ++k) {
+    if (k >= N) break;
+    const double piv = bcast(Ki[k], k);
+    if (piv == 0.0) return false;  // uniform
+    if (l == k) {
+      const double p = 1.0 / Ki[k];
+      Ki[k] = 1.0;
+#pragma unroll
+      for (int j = 0; j < NK; ++j) Ki[j] *= p;
+    }
+    const double f = Ki[k];
+    if (l != k) Ki[k] = 0.0;
+#pragma unroll
+    for (int j = 0; j < NK; ++j) {
+      if (j >= N) break;
+      const double rkj = bcast(Ki[j], k);
+      if (l != k) Ki[j] -= f * rkj;
+    }
+  }
+  auto apply = [&](const double (&A)[NK], double v) {  // row l of A times the vector held by lanes 0..N-1
+    double s0 = 0, s1 = 0;
+#pragma unroll
+    for (int j = 0; j < NK; ++j) {
+      if (j >= N) break;
+      const double vj = bcast(v, j);
+      if (j & 1) s1 += A[j] * vj;
+      else s0 += A[j] * vj;
+    }
+    return s0 + s1;
+  };
+  double sol = apply(Ki, rhs);
+  for (int it = 0; it < kp.s.polish_refine_iter; ++it) {
+    const double res = rhs - apply(K0, sol);
+    sol += apply(Ki, res);
+  }
+  if (hf) xx[fi] = sol;
+  for (int row = l; row < M; row += 64) yy[row] = 0.0;
+  wsync();
+  if (hr) yy[NX + gi] = sol;
+  wsync();
+  if (l < NX && actb != 0) {  // bound multipliers from stationarity
+    double g = q[l];
+    if (l < NP)
+      for (int c = 0; c < NP; ++c) g += P[l * NP + c] * xx[c];
+    for (int i = 0; i < NG; ++i) g += G[i * NX + l] * yy[NX + i];
+    yy[l] = -g / ab[l];
+  }
+  wsync();
+  return true;
+}
+
 // Equality-constrained QP on the flagged rows (OSQP polish's reduced KKT):
 // bound-active variables are fixed at their bound (eliminated exactly), the
 // active G rows enter [P_FF + dI, G_RF^T; G_RF, -dI] solved by a packed
@@ -777,6 +894,15 @@ __device__ __forceinline__ bool eqp(const KParams& kp, double* S, int actb, int 
     atomicAdd(&g_phase_cycles[42], (unsigned long long)N);
   }
 #endif
+  if constexpr (QD::nx > 0) {
+    if (N <= kEqpRegCap) {
+      const bool ok_ = eqp_regs<QD>(kp, S, actb, actg, xx, yy, freeMask, rowMask, nF, nR);
+#ifdef DRC_PHASE_TIMING
+      if (l == 0) atomicAdd(&g_phase_cycles[40], __builtin_amdgcn_s_memtime() - eq_t0);
+#endif
+      return ok_;
+    }
+  }
   double* U = S + kp.oU0;
   int* Fidx = reinterpret_cast<int*>(U);  // 64 ints
   int* Ridx = Fidx + 64;                   // 64 ints
