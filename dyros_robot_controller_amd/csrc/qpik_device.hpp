@@ -26,28 +26,71 @@ constexpr double kDivTol = 1e-30;
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 __device__ __forceinline__ void wsync() { __syncthreads(); }
 
+// Wave reductions: DPP within each row of 16 lanes (quad swaps, half-row
+// and row mirrors: every lane of a row ends with the row's value), then the
+// four row values through v_readlane.  No LDS crossbar (ds_bpermute) round
+// trips; called with the whole wave active.
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int v) {
+  return __builtin_amdgcn_update_dpp(v, v, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = dpp_i<CTRL>(static_cast<int>(b)), hi = dpp_i<CTRL>(static_cast<int>(b >> 32));
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double rd_lane(double v, int lane) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane(static_cast<int>(b), lane);
+  const int hi = __builtin_amdgcn_readlane(static_cast<int>(b >> 32), lane);
+  return __hiloint2double(hi, lo);
+}
+constexpr int kDppQuad1032 = 0xB1, kDppQuad2301 = 0x4E, kDppHalfMirror = 0x141, kDppMirror = 0x140;
 __device__ __forceinline__ double wave_max(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
-  return v;
+  v = fmax(v, dpp_d<kDppQuad1032>(v));
+  v = fmax(v, dpp_d<kDppQuad2301>(v));
+  v = fmax(v, dpp_d<kDppHalfMirror>(v));
+  v = fmax(v, dpp_d<kDppMirror>(v));
+  return fmax(fmax(rd_lane(v, 0), rd_lane(v, 16)), fmax(rd_lane(v, 32), rd_lane(v, 48)));
 }
 __device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  v += dpp_d<kDppQuad1032>(v);
+  v += dpp_d<kDppQuad2301>(v);
+  v += dpp_d<kDppHalfMirror>(v);
+  v += dpp_d<kDppMirror>(v);
+  return (rd_lane(v, 0) + rd_lane(v, 16)) + (rd_lane(v, 32) + rd_lane(v, 48));
 }
 // argmin with ties broken toward the smaller index (reference: first strict
-// minimum in pair order, robot_data.cpp:434-442)
-__device__ __forceinline__ void wave_argmin(double& v, int& idx) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    double ov = __shfl_xor(v, o, 64);
-    int oi = __shfl_xor(idx, o, 64);
-    if (ov < v || (ov == v && oi < idx)) {
-      v = ov;
-      idx = oi;
-    }
+// minimum in pair order, robot_data.cpp:434-442); the (value, index) order
+// is total, so the result does not depend on the reduction tree
+__device__ __forceinline__ void argmin_step(double& v, int& idx, double ov, int oi) {
+  if (ov < v || (ov == v && oi < idx)) {
+    v = ov;
+    idx = oi;
   }
+}
+template <int CTRL>
+__device__ __forceinline__ void argmin_dpp(double& v, int& idx) {
+  const double ov = dpp_d<CTRL>(v);
+  const int oi = dpp_i<CTRL>(idx);
+  argmin_step(v, idx, ov, oi);
+}
+__device__ __forceinline__ void wave_argmin(double& v, int& idx) {
+  argmin_dpp<kDppQuad1032>(v, idx);
+  argmin_dpp<kDppQuad2301>(v, idx);
+  argmin_dpp<kDppHalfMirror>(v, idx);
+  argmin_dpp<kDppMirror>(v, idx);
+  double bv = rd_lane(v, 0);
+  int bi = __builtin_amdgcn_readlane(idx, 0);
+#pragma unroll
+  for (int r = 16; r < 64; r += 16) {
+    const double ov = rd_lane(v, r);
+    const int oi = __builtin_amdgcn_readlane(idx, r);
+    argmin_step(bv, bi, ov, oi);
+  }
+  v = bv;
+  idx = bi;
 }
 
 // ------------------------------------------------------------ 3-vectors
