@@ -49,7 +49,7 @@ struct KParams {
   int oP, oG, oQ, oAB, oL, oU, oD, oE, oRho, oX, oZ, oY, oDY, oXT, oZT, oT1, oT2, oRed, oSc;
   // union region (kinematics | K^-1 | polish)
   int oU0;
-  int kT, kZ, kTe, kJ, kTg, kq, kqd, kA6, kAi, kW, kPart, kPd, kPf, kxdd, kmg, kdg, kJt, kSv, kScr, kEpa;
+  int kT, kZ, kTe, kJ, kTg, kq, kqd, kA6, kAi, kW, kPart, kPd, kPf, kCand, kxdd, kmg, kdg, kJt, kSv, kScr, kEpa;
   int kJd, kDa, kVf, kX6, kBias, kMq, kGq;  // QPID: Jdot, arm-only Jdot, S eta, 6x6 scratch, bias | M, g
   int kGdv;                                 // QPID stage: grad_dot vectors
   int cf;                                   // closed-form controller: 1 CLIK, 2 OSF (task_kernel<2>)
@@ -1902,9 +1902,22 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRC_TAS
     }
     ub = -wave_max(-ub);
     PH(3);
-    // exact GJK only where the swept-core bound can still win
-    for (int p = l; p < M->npairs; p += 64) {
-      if (pf[p] == 0.0 && pd[p] - 1e-9 <= ub) {
+    // exact GJK only where the swept-core bound can still win.  The candidates
+    // are compacted into a list first, so a wave runs them in ceil(n / 64)
+    // rounds instead of one round per 64 pair slots.
+    {
+      int* cand = reinterpret_cast<int*>(S + kp.kCand);
+      int ncand = 0;
+      for (int p0 = 0; p0 < M->npairs; p0 += 64) {
+        const int p = p0 + l;
+        const bool c = p < M->npairs && pf[p] == 0.0 && pd[p] - 1e-9 <= ub;
+        const unsigned long long m = __ballot(c);
+        if (c) cand[ncand + __popcll(m & ((1ull << l) - 1))] = p;
+        ncand += __popcll(m);
+      }
+      wsync();
+      for (int c = l; c < ncand; c += 64) {
+        const int p = cand[c];
         const int ga = M->pair_a[p], gb = M->pair_b[p];
         Shape A{M->gtype[ga], Tg + 12 * ga, M->gparam[ga][0], M->gparam[ga][1], M->gparam[ga][2]};
         Shape Bs{M->gtype[gb], Tg + 12 * gb, M->gparam[gb][0], M->gparam[gb][1], M->gparam[gb][2]};
@@ -3240,18 +3253,18 @@ static int plan_layout(const DevModel& M, KParams* k, bool task_only) {
   k->kTg = takeu(ng_ * 12);
   k->kq = takeu(nv);
   k->kqd = takeu(nv);
-  k->kA6 = takeu(36);
-  k->kAi = takeu(36);
-  k->kW = takeu(k->narm * 6);
-  k->kPart = takeu(k->narm * k->narm);
   k->kPd = takeu(M.npairs);
   k->kPf = takeu(M.npairs);
   k->kxdd = takeu(6);
   k->kmg = takeu(k->narm);
   k->kdg = takeu(nv);
-  k->kJt = takeu(6 * np);
   k->kSv = takeu(3 * kMaxWheels);
-  k->kScr = takeu(160);  // serial 6x6 COD work (pinv_cod_serial: 3n^2 + 3n)
+  const bool epa = task_only && !k->cf;
+  // QPID's task extras read Ai and W after the collision stage
+  if (!epa || k->problem == 1) {
+    k->kAi = takeu(36);
+    k->kW = takeu(k->narm * 6);
+  }
   if (k->problem == 1) {  // QPID stage data (task kernel) and dynamics (QP kernel)
     k->kJd = takeu(6 * nv);
     k->kDa = takeu(6 * k->narm);
@@ -3266,7 +3279,31 @@ static int plan_layout(const DevModel& M, KParams* k, bool task_only) {
     const int ws = 6 * nv + 36 + 6 * nv + 18 + 2 * nv + 6 * nv;
     k->kCf = takeu(2 * 6 * nv + nv * nv + 3 * nv + 48 + (ws > 160 ? ws : 160));
   }
-  k->kEpa = (task_only && !k->cf) ? takeu(static_cast<int>((sizeof(EpaPoly) + 7) / 8)) : 0;
+  // Regions dead once the collision stage starts (manipulability work, the
+  // QP kernel's task Jacobian), then the EPA polytope laid over them: they
+  // share LDS, which keeps the QPIK task kernel within 20 KB per wave
+  // (8 waves per CU).  The GJK candidate list lives in the polytope's space
+  // too (it is consumed before EPA starts).
+  const int scr0 = u;
+  if (epa && k->problem != 1) {
+    k->kAi = takeu(36);
+    k->kW = takeu(k->narm * 6);
+  }
+  k->kA6 = takeu(36);
+  k->kPart = takeu(k->narm * k->narm);
+  k->kJt = takeu(6 * np);
+  k->kScr = takeu(160);  // serial 6x6 COD work (pinv_cod_serial: 3n^2 + 3n)
+  if (epa) {
+    k->kEpa = scr0;
+    const int ep = scr0 + ((static_cast<int>((sizeof(EpaPoly) + 7) / 8) + 1) & ~1);
+    u = u > ep ? u : ep;
+    k->kCand = scr0;  // int list of the GJK candidates
+    const int ce = scr0 + (M.npairs + 1) / 2;
+    u = u > ce ? u : ce;
+  } else {
+    k->kEpa = 0;
+    k->kCand = takeu((M.npairs + 1) / 2);
+  }
   int kin_end = u;
   // K^-1, and G K^-1 for the register ADMM (QPIK shapes); QPID runs the LDS path (K^-1 only)
   int kinv_end = k->oU0 + nx * nx + (k->problem == 1 ? 0 : nx * ng);
