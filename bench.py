@@ -98,7 +98,7 @@ def main():
     ap.add_argument("--batch", type=int, default=65536, help="instances per GPU")
     ap.add_argument("--robot", default="fr3", choices=sorted(LINKS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--chunks", type=int, default=2, help="concurrent sub-batches per call")
+    ap.add_argument("--chunks", type=int, default=3, help="concurrent sub-batches per call")
     args = ap.parse_args()
 
     import torch

@@ -210,7 +210,7 @@ int drc_debug_kernel_times(drc_model* model, double* wall_ms, double* task_ms, d
 
 /* Concurrency of drc_qpik_batch: the batch is split into up to `chunks`
  * contiguous sub-batches (each >= 16384 instances) that run on internal
- * streams forked from and joined back to the caller's stream (default 2).
+ * streams forked from and joined back to the caller's stream (default 3).
  * Results do not depend on it. */
 int drc_set_concurrency(drc_model* model, int chunks);
 
