@@ -243,15 +243,16 @@ DRC_HD __forceinline__ void cs_try(const SV2 (&S)[4], CsBest& B) {
     B.l[3] = l3;
   }
 }
-template <int MASK>
+// masks MASK, MASK-1, ..., LO
+template <int MASK, int LO, bool DONE = (MASK < LO)>
 struct CsLoop {
   DRC_HD static __forceinline__ void run(const SV2 (&S)[4], CsBest& B) {
     cs_try<MASK>(S, B);
-    CsLoop<MASK - 1>::run(S, B);
+    CsLoop<MASK - 1, LO>::run(S, B);
   }
 };
-template <>
-struct CsLoop<0> {
+template <int MASK, int LO>
+struct CsLoop<MASK, LO, true> {
   DRC_HD static __forceinline__ void run(const SV2 (&)[4], CsBest&) {}
 };
 template <int N>
@@ -261,7 +262,13 @@ DRC_HD __forceinline__ int closest_n(SV2 (&S)[4], V3* v, double (&lam)[4]) {
   B.mask = 0;
   B.v = v3(0, 0, 0);
   B.l[0] = B.l[1] = B.l[2] = B.l[3] = 0;
-  CsLoop<(1 << N) - 1>::run(S, B);
+  // The newest vertex is S[N-1] and the masks holding it come first in the
+  // descending order.  GJK appends a support point only when it improves on
+  // |v| by the gap tolerance, so the closest point then involves it and the
+  // masks without it (sub-simplices of the previous simplex, no closer than
+  // |v|) are searched only when none with it is valid (oracle: same rule).
+  CsLoop<(1 << N) - 1, 1 << (N - 1)>::run(S, B);
+  if (N > 1 && B.mask == 0) CsLoop<(1 << (N - 1)) - 1, 1>::run(S, B);
   const int bmask = B.mask;
   *v = B.v;
   const double b0 = B.l[0], b1 = B.l[1], b2 = B.l[2], b3 = B.l[3];

@@ -388,7 +388,12 @@ static void sup_md(const Shape* A, const Shape* B, const double* d, SV* o) {
 static int closest_simplex(SV* S, int n, double* v, double* lam_out) {
     double best = INFINITY, bl[4] = {0};
     int bmask = 0;
+    /* masks holding the newest vertex S[n-1] come first; the others (the
+     * previous simplex's faces, no closer than |v|: GJK appends a support
+     * point only when it improves by the gap tolerance) are searched only
+     * when none of the first group is valid */
     for (int mask = (1 << n) - 1; mask > 0; --mask) {
+        if (mask == (1 << (n - 1)) - 1 && bmask != 0) break;
         int idx[4], k = 0;
         for (int i = 0; i < n; ++i) if (mask & (1 << i)) idx[k++] = i;
         double lam[4];

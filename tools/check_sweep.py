@@ -1,0 +1,40 @@
+"""Diagnostic: exact-mode QPIK call time vs the termination-check interval
+(check_termination; the adaptive-rho interval follows it or stays at 25).
+The certified optimum does not depend on it; the ADMM iterations before the
+first polish attempt and the failed attempts do."""
+import sys
+import json
+import torch
+sys.path[:0] = [".", "tests", "oracle"]
+from _common import make_manipulator, step_inputs  # noqa: E402
+from dyros_robot_controller_amd import _batch, _capi, manipulator  # noqa: E402
+
+dev = torch.device("cuda", 0)
+robot = sys.argv[1] if len(sys.argv) > 1 else "fr3"
+link = {"fr3": "fr3_link8", "ur5e": "tool0"}[robot]
+B = 65536
+rd = make_manipulator(robot, dev)
+q, qd, xt, xdt = step_inputs(rd, robot, 12345, B, dev)
+args = [_batch.as_device(a, dev) for a in (q, qd, xt, xdt)]
+st = torch.cuda.current_stream(dev)
+ref = None
+for ct, ar in [(25, 25), (20, 20), (15, 15), (10, 10), (15, 25), (10, 25), (5, 25)]:
+    p = manipulator.QPIKParamsBuilder(rd.model, exact=True).params(link, _capi.MODE_QPIK_STEP)
+    p.solver.check_termination = ct
+    p.solver.adaptive_rho_interval = ar
+    it = torch.zeros(B, dtype=torch.int32, device=dev)
+    call = lambda: _batch.qpik_batch(rd.model, p, *args, iters=it)
+    out, status = call()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(10):
+        call()
+    e1.record(st)
+    torch.cuda.synchronize()
+    o = out.cpu()
+    if ref is None:
+        ref = o
+    print(json.dumps(dict(check=ct, adapt=ar, ms=e0.elapsed_time(e1) / 10, iters_mean=float(it.float().mean()),
+                          iters_max=int(it.max()), solved=float((status == 0).float().mean()),
+                          maxdiff_vs_25=float((o - ref).abs().max()))), flush=True)
