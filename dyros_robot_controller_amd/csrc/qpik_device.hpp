@@ -145,9 +145,9 @@ DRC_HD __forceinline__ V3 support(const Shape& s, V3 d) {
   if (s.type == kSphere) return v3(s.T[9], s.T[10], s.T[11]);
   V3 dl = rotT(s.T, d), loc;
   if (s.type == kCylinder) {
-    double rho = sqrt(dl.x * dl.x + dl.y * dl.y);
-    loc.x = rho > 0 ? s.p0 * dl.x / rho : 0.0;
-    loc.y = rho > 0 ? s.p0 * dl.y / rho : 0.0;
+    const double rho = sqrt(dl.x * dl.x + dl.y * dl.y), f = rho > 0 ? s.p0 / rho : 0.0;
+    loc.x = f * dl.x;
+    loc.y = f * dl.y;
     loc.z = dl.z > 0 ? s.p1 : -s.p1;
   } else {
     loc.x = dl.x > 0 ? s.p0 : -s.p0;
@@ -208,8 +208,9 @@ DRC_HD __forceinline__ void cs_try(const SV2 (&S)[4], CsBest& B) {
     const double r0 = -dot(D0, w0), r1 = -dot(D1, w0);
     const double det = G0 * G4 - G1 * G3;
     if (fabs(det) < 1e-300) return;
-    l1 = (r0 * G4 - G1 * r1) / det;
-    l2 = (G0 * r1 - r0 * G3) / det;
+    const double id = 1.0 / det;
+    l1 = (r0 * G4 - G1 * r1) * id;
+    l2 = (G0 * r1 - r0 * G3) * id;
     l0 = 1 - (l1 + l2);
     if (l0 < -1e-14 || l1 < -1e-14 || l2 < -1e-14) return;
   } else if (k == 4) {
@@ -219,9 +220,10 @@ DRC_HD __forceinline__ void cs_try(const SV2 (&S)[4], CsBest& B) {
     const double r0 = -dot(D0, w0), r1 = -dot(D1, w0), r2 = -dot(D2, w0);
     const double det = a * (e * ii - f * h) - b * (dd * ii - f * g) + c * (dd * h - e * g);
     if (fabs(det) < 1e-300) return;
-    l1 = (r0 * (e * ii - f * h) - b * (r1 * ii - f * r2) + c * (r1 * h - e * r2)) / det;
-    l2 = (a * (r1 * ii - f * r2) - r0 * (dd * ii - f * g) + c * (dd * r2 - r1 * g)) / det;
-    l3 = (a * (e * r2 - r1 * h) - b * (dd * r2 - r1 * g) + r0 * (dd * h - e * g)) / det;
+    const double id = 1.0 / det;
+    l1 = (r0 * (e * ii - f * h) - b * (r1 * ii - f * r2) + c * (r1 * h - e * r2)) * id;
+    l2 = (a * (r1 * ii - f * r2) - r0 * (dd * ii - f * g) + c * (dd * r2 - r1 * g)) * id;
+    l3 = (a * (e * r2 - r1 * h) - b * (dd * r2 - r1 * g) + r0 * (dd * h - e * g)) * id;
     l0 = 1 - ((l1 + l2) + l3);
     if (l0 < -1e-14 || l1 < -1e-14 || l2 < -1e-14 || l3 < -1e-14) return;
   }

@@ -1184,16 +1184,32 @@ __device__ __forceinline__ bool polish(const KParams& kp, double* S, bool strict
 // are dealt to the 8 XCDs round-robin), so a line is fetched once per L2 and
 // stores to it merge there before write-back; otherwise plain grid-stride.
 // Placement only affects speed, never which instances run.
+//
+// Work queue (queue != nullptr): the waves of residue class x = blockIdx & 7
+// take the positions of sequence x from an atomic counter (queue[x], zeroed
+// before the launch) instead of a fixed stride, so a straggler instance
+// (thousands of ADMM iterations, a deep EPA) holds up only its own wave and
+// never the instances that would have followed it.  Every wave leaves once
+// its counter passes the sequence end; all 8 classes have waves (grid >= 8).
 struct InstSeq {
   int64_t j0, step, n;
   int xcd, map;
-  __device__ __forceinline__ InstSeq(int64_t B, int map_) {
+  int* queue;
+  __device__ __forceinline__ InstSeq(int64_t B, int map_, int* queue_ = nullptr) {
     map = map_;
+    queue = queue_;
     xcd = blockIdx.x & 7;
     j0 = map ? (blockIdx.x >> 3) : blockIdx.x;
     step = map ? (gridDim.x >> 3) : gridDim.x;
     n = map ? ((B + 127) >> 7) << 4 : B;
   }
+  __device__ __forceinline__ int64_t fetch() const {
+    int v = 0;
+    if (lane_id() == 0) v = atomicAdd(queue + (map ? xcd : 0), 1);
+    return __builtin_amdgcn_readfirstlane(v);
+  }
+  __device__ __forceinline__ int64_t first() const { return queue ? fetch() : j0; }
+  __device__ __forceinline__ int64_t next(int64_t j) const { return queue ? fetch() : j + step; }
   __device__ __forceinline__ int64_t at(int64_t j) const {
     return map ? ((((j >> 4) << 3) + xcd) << 4) + (j & 15) : j;
   }
@@ -1216,6 +1232,7 @@ struct IO {
   double *st_jdot, *st_qpid;  // [6*nv][B] Jdot; [8][B] bias(6), man_gd, dist_gd
   double* st_gdv;             // [narm + nv][B] grad_dot vectors (manipulability | min distance)
   const double* cf_null;      // closed-form: null_qdot / null_torque [nv][B] (may be NULL)
+  int* queue;                 // per-launch work-queue counters (8, zeroed), or NULL: fixed stride
 };
 
 // ------------------------------------------------------------------------
@@ -1601,8 +1618,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRC_TAS
   const int64_t B = io.B;
   EpaPoly* ews = reinterpret_cast<EpaPoly*>(S + kp.kEpa);  // LDS-resident polytope
   PH_DECL
-  const InstSeq seq(B, kp.xcd_map);
-  for (int64_t j = seq.j0; j < seq.n; j += seq.step) {
+  const InstSeq seq(B, kp.xcd_map, io.queue);
+  for (int64_t j = seq.first(); j < seq.n; j = seq.next(j)) {
     const int64_t b = seq.at(j);
     if (b >= B) continue;
     const int64_t gb = io.b0 + b, LD = io.ld;  // position in the caller's [field][B] arrays
@@ -2851,8 +2868,8 @@ qp_kernel(const DevModel* __restrict__ M0, const KParams kp, const IO io) {
   }
   const int64_t B = io.B;
   PH_DECL
-  const InstSeq seq(B, kp.xcd_map);
-  for (int64_t j = seq.j0; j < seq.n; j += seq.step) {
+  const InstSeq seq(B, kp.xcd_map, io.queue);
+  for (int64_t j = seq.first(); j < seq.n; j = seq.next(j)) {
     const int64_t b = seq.at(j);
     if (b >= B) continue;
     const int64_t gb = io.b0 + b, LD = io.ld;  // position in the caller's [field][B] arrays
@@ -3026,8 +3043,8 @@ qpid_kernel(const DevModel* __restrict__ M0, const KParams kp, const IO io) {
     wsync();
   }
   const int64_t B = io.B;
-  const InstSeq seq(B, kp.xcd_map);
-  for (int64_t j = seq.j0; j < seq.n; j += seq.step) {
+  const InstSeq seq(B, kp.xcd_map, io.queue);
+  for (int64_t j = seq.first(); j < seq.n; j = seq.next(j)) {
     const int64_t b = seq.at(j);
     if (b >= B) continue;
     const int64_t gb = io.b0 + b, LD = io.ld;
@@ -3071,6 +3088,10 @@ struct drc_model_impl {
   drc_joint_index jidx{};
   drc_actuator_index aidx{};
   void* pool = nullptr;  // task data when the caller does not keep it
+  // work-queue counters: [slot][kernel (task, QP)][8 XCD classes]; slots
+  // 0..15 the QPIK sub-batches, 16 QPID, 17 the closed-form controllers
+  static constexpr int kQueueSlotQpid = 16, kQueueSlotCf = 17, kQueueInts = 18 * 2 * 8;
+  int* d_queue = nullptr;
   int64_t pool_bytes = 0;
   int timing = 0;  // drc_debug_kernel_timing: HIP events around each launch
   // timed calls: {caller-stream start, caller-stream end, per chunk: task start, task end, qp end}
@@ -3202,6 +3223,7 @@ static int mobile_fk_jacobian(const drc_kinematic_param& p, int* W, double out[3
 static int upload(drc_model_impl* m) {
   HIP_TRY(hipSetDevice(m->device));
   HIP_TRY(hipMalloc(&m->d_model, sizeof(DevModel)));
+  HIP_TRY(hipMalloc(&m->d_queue, drc_model_impl::kQueueInts * sizeof(int)));
   HIP_TRY(hipMemcpy(m->d_model, &m->hm.dev, sizeof(DevModel), hipMemcpyHostToDevice));
   return DRC_OK;
 }
@@ -3484,6 +3506,9 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
     const int64_t gq = Bc < 8192 ? Bc : 8192, gt = Bc < 8192 ? Bc : 8192;
     IO io{Bc, b0, B, q, qdot, xt, xdt, xi, xdi, out, status, iters, pose, jac, man, dist, xdd, pair,
           rec ? rec + b0 * stride : nullptr, stride};
+    int* qc = m->d_queue + c * 16;  // c < 16 (drc_set_concurrency)
+    HIP_TRY(hipMemsetAsync(qc, 0, 16 * sizeof(int), cs));
+    io.queue = qc;
     hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr;
     if (timed) {
       if (int r = mkev(&e0)) return r;
@@ -3496,6 +3521,7 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
     HIP_TRY(hipGetLastError());
     if (timed) HIP_TRY(hipEventRecord(e1, cs));
     if (!stages) {
+      io.queue = qc + 8;
       const size_t lds = static_cast<size_t>(kq_c.lds_doubles) * sizeof(double);
       const dim3 g(static_cast<unsigned>(gq)), blk(64);
       // compile-time QP shapes of the bundled robots; anything else runs the
@@ -3588,10 +3614,14 @@ static int launch_qpid(const drc_model_impl* cm, const drc_qpik_params* params, 
   io.st_jdot = jdot;
   io.st_qpid = qpid_st;
   io.st_gdv = gdv;
+  int* qc = m->d_queue + drc_model_impl::kQueueSlotQpid * 16;
+  HIP_TRY(hipMemsetAsync(qc, 0, 16 * sizeof(int), st));
+  io.queue = qc;
   hipLaunchKernelGGL(task_kernel<1>, dim3(static_cast<unsigned>(grid)), dim3(64),
                      static_cast<size_t>(kt_c.lds_doubles) * sizeof(double), st, m->d_model, kt_c, io);
   HIP_TRY(hipGetLastError());
   if (!stages) {
+    io.queue = qc + 8;
     const dim3 g(static_cast<unsigned>(grid)), blk(64);
     const size_t lds = static_cast<size_t>(kq_c.lds_doubles) * sizeof(double);
     if (kq_c.nx == 44 && kq_c.ng == 37 && kq_c.np == 7)  // FR3
@@ -3662,6 +3692,8 @@ static int launch_closed_form(const drc_model_impl* cm, const drc_qpik_params* p
   io.dM = dMi;
   io.dG = dG;
   io.cf_null = nullv;
+  io.queue = m->d_queue + drc_model_impl::kQueueSlotCf * 16;
+  HIP_TRY(hipMemsetAsync(io.queue, 0, 8 * sizeof(int), st));
   hipLaunchKernelGGL(task_kernel<2>, dim3(static_cast<unsigned>(grid)), dim3(64),
                      static_cast<size_t>(kt.lds_doubles) * sizeof(double), st, m->d_model, kt, io);
   HIP_TRY(hipGetLastError());
@@ -3819,6 +3851,7 @@ void drc_model_destroy(drc_model* m) {
   (void)hipSetDevice(m->device);
   for (hipStream_t ls : m->lanes) (void)hipStreamSynchronize(ls);
   if (m->d_model) (void)hipFree(m->d_model);
+  if (m->d_queue) (void)hipFree(m->d_queue);
   if (m->pool) (void)hipFree(m->pool);
   if (m->dyn_list) (void)hipFree(m->dyn_list);
   for (hipStream_t ls : m->lanes) (void)hipStreamDestroy(ls);

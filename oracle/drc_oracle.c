@@ -365,8 +365,9 @@ static void support(const Shape* s, const double* d, double* out) {
     matTvec3(s->T, d, dl);
     if (s->type == 1) {
         double r = s->prm[0], h = s->prm[1], rho = sqrt(dl[0] * dl[0] + dl[1] * dl[1]);
-        loc[0] = rho > 0 ? r * dl[0] / rho : 0;
-        loc[1] = rho > 0 ? r * dl[1] / rho : 0;
+        double f = rho > 0 ? r / rho : 0;  /* one division (kernel: same) */
+        loc[0] = f * dl[0];
+        loc[1] = f * dl[1];
         loc[2] = dl[2] > 0 ? h : -h;
     } else {
         for (int i = 0; i < 3; ++i) loc[i] = dl[i] > 0 ? s->prm[i] : -s->prm[i];
@@ -408,15 +409,17 @@ static int closest_simplex(SV* S, int n, double* v, double* lam_out) {
             else if (d == 2) {
                 double det = G[0] * G[4] - G[1] * G[3];
                 if (fabs(det) < 1e-300) continue;
-                mu[0] = (r[0] * G[4] - G[1] * r[1]) / det;
-                mu[1] = (G[0] * r[1] - r[0] * G[3]) / det;
+                double id = 1.0 / det;
+                mu[0] = (r[0] * G[4] - G[1] * r[1]) * id;
+                mu[1] = (G[0] * r[1] - r[0] * G[3]) * id;
             } else {
                 double a = G[0], b = G[1], c = G[2], dd = G[3], e = G[4], f = G[5], g = G[6], h = G[7], ii = G[8];
                 double det = a * (e * ii - f * h) - b * (dd * ii - f * g) + c * (dd * h - e * g);
                 if (fabs(det) < 1e-300) continue;
-                mu[0] = (r[0] * (e * ii - f * h) - b * (r[1] * ii - f * r[2]) + c * (r[1] * h - e * r[2])) / det;
-                mu[1] = (a * (r[1] * ii - f * r[2]) - r[0] * (dd * ii - f * g) + c * (dd * r[2] - r[1] * g)) / det;
-                mu[2] = (a * (e * r[2] - r[1] * h) - b * (dd * r[2] - r[1] * g) + r[0] * (dd * h - e * g)) / det;
+                double id = 1.0 / det;
+                mu[0] = (r[0] * (e * ii - f * h) - b * (r[1] * ii - f * r[2]) + c * (r[1] * h - e * r[2])) * id;
+                mu[1] = (a * (r[1] * ii - f * r[2]) - r[0] * (dd * ii - f * g) + c * (dd * r[2] - r[1] * g)) * id;
+                mu[2] = (a * (e * r[2] - r[1] * h) - b * (dd * r[2] - r[1] * g) + r[0] * (dd * h - e * g)) * id;
             }
             double s = 0;
             for (int i = 0; i < d; ++i) s += mu[i];
