@@ -2162,6 +2162,9 @@ __device__ __forceinline__ void qp_assemble(const DevModel* M, const KParams& kp
   double* xdd = S + kp.kxdd;
   double* mg = S + kp.kmg;
   double* dgv = S + kp.kdg;
+#ifdef DRC_PHASE_TIMING
+  const unsigned long long as_t0 = __builtin_amdgcn_s_memtime();
+#endif
   {  // task record written by task_kernel (one coalesced read)
     const double* rec = io.rec + b * io.rec_stride;
     for (int e = l; e < kp.rLen; e += 64) {
@@ -2176,6 +2179,9 @@ __device__ __forceinline__ void qp_assemble(const DevModel* M, const KParams& kp
     }
   }
   wsync();
+#ifdef DRC_PHASE_TIMING
+  if (lane_id() == 0) atomicAdd(&g_phase_cycles[44], __builtin_amdgcn_s_memtime() - as_t0);
+#endif
   const double bestd = S[kp.oSc + SC_DIST];
   // ---------------- QP assembly (QP_IK.cpp:69-131 / MoMa :59-128) --------
   const int nx = DNX, ng = DNG, np = DNP, m = DM;
