@@ -2339,7 +2339,10 @@ __device__ __forceinline__ int qp_scale(const KParams& kp, double* S) {
         for (int c = 0; c < np; ++c) P[l * np + c] *= ct;
       if (l < nx) qq[l] *= ct;
       if (l == 0) sc[SC_C] *= ct;
+      // fixed point (as qp_scale_regs and the oracle)
+      const bool ones = (l >= nx || (Dt[l] == 1.0 && Et[l] == 1.0)) && (l >= ng || Et[nx + l] == 1.0);
       wsync();
+      if (ct == 1.0 && __all(ones)) break;
     }
     for (int row = l; row < m; row += 64) {
       lo[row] = fmax(lo[row], -kInf) * E[row];
@@ -2429,6 +2432,9 @@ __device__ __noinline__ int qp_scale_regs(const KParams& kp, double* S) {
       for (int c = 0; c < NP; ++c) Prow[c] *= ct;
     if (hx) ql *= ct;
     cs *= ct;
+    // fixed point: every factor of this pass was exactly 1, so the remaining
+    // passes would repeat it bit for bit (oracle: same exit)
+    if (ct == 1.0 && __all((!hx || (Dt == 1.0 && Et == 1.0)) && (!hg || EtG == 1.0))) break;
   }
   if (hp)
 #pragma unroll

@@ -1039,6 +1039,12 @@ static void qp_scale(QPW* w, int iters) {
         for (int i = 0; i < n * n; ++i) w->P[i] *= ct;
         for (int j = 0; j < n; ++j) w->q[j] *= ct;
         w->c *= ct;
+        /* fixed point: every factor of this pass was exactly 1, so the
+         * remaining passes would repeat it bit for bit (kernel: same exit) */
+        int ones = ct == 1.0;
+        for (int j = 0; j < n && ones; ++j) ones = Dt[j] == 1.0;
+        for (int i = 0; i < m && ones; ++i) ones = Et[i] == 1.0;
+        if (ones) break;
     }
     for (int i = 0; i < m; ++i) {
         w->l[i] *= w->E[i];

@@ -1,5 +1,6 @@
 """Diagnostic: exact-mode QPIK call time vs the termination-check interval
-(check_termination; the adaptive-rho interval follows it or stays at 25).
+(check_termination; the adaptive-rho interval follows it or stays at 25) or
+the Ruiz iteration count (argv[2] == "scaling").
 The certified optimum does not depend on it; the ADMM iterations before the
 first polish attempt and the failed attempts do."""
 import sys
@@ -18,10 +19,14 @@ q, qd, xt, xdt = step_inputs(rd, robot, 12345, B, dev)
 args = [_batch.as_device(a, dev) for a in (q, qd, xt, xdt)]
 st = torch.cuda.current_stream(dev)
 ref = None
-for ct, ar in [(25, 25), (20, 20), (15, 15), (10, 10), (15, 25), (10, 25), (5, 25)]:
+knobs = sys.argv[2] if len(sys.argv) > 2 else "check"
+grid = ([(25, 25, 10), (20, 20, 10), (15, 15, 10), (10, 10, 10), (15, 25, 10), (10, 25, 10), (5, 25, 10)]
+        if knobs == "check" else [(25, 25, 10), (25, 25, 5), (25, 25, 3), (25, 25, 1), (25, 25, 0)])
+for ct, ar, sc in grid:
     p = manipulator.QPIKParamsBuilder(rd.model, exact=True).params(link, _capi.MODE_QPIK_STEP)
     p.solver.check_termination = ct
     p.solver.adaptive_rho_interval = ar
+    p.solver.scaling = sc
     it = torch.zeros(B, dtype=torch.int32, device=dev)
     call = lambda: _batch.qpik_batch(rd.model, p, *args, iters=it)
     out, status = call()
@@ -35,6 +40,6 @@ for ct, ar in [(25, 25), (20, 20), (15, 15), (10, 10), (15, 25), (10, 25), (5, 2
     o = out.cpu()
     if ref is None:
         ref = o
-    print(json.dumps(dict(check=ct, adapt=ar, ms=e0.elapsed_time(e1) / 10, iters_mean=float(it.float().mean()),
+    print(json.dumps(dict(check=ct, adapt=ar, scaling=sc, ms=e0.elapsed_time(e1) / 10, iters_mean=float(it.float().mean()),
                           iters_max=int(it.max()), solved=float((status == 0).float().mean()),
                           maxdiff_vs_25=float((o - ref).abs().max()))), flush=True)
