@@ -1078,6 +1078,7 @@ __device__ __forceinline__ bool polish(const KParams& kp, double* S, bool strict
         if (l < nx) xc[l] += alpha * (xx[l] - xc[l]);
         wsync();
         if (enc != 0x7fffffff && amin < 1.0) {
+          CK_N(47);
           const int row = enc >> 2, sd = (enc & 3) - 1;
           if (row < nx) { if (l == row) actb = sd; }
           else if (l == row - nx) actg = sd;
@@ -1136,32 +1137,46 @@ __device__ __forceinline__ bool polish(const KParams& kp, double* S, bool strict
     }
     if (!strict) break;
     if (have_feas) {
-      if (worst == 0x7fffffff) break;  // KKT residual failure, not an active-set issue
+      if (worst == 0x7fffffff) {
+        CK_N(48);
+        break;  // KKT residual failure, not an active-set issue
+      }
+      CK_N(46);
       if (worst < nx) { if (l == worst) actb = 0; }
       else if (l == worst - nx) actg = 0;
       if (l < nx) xc[l] = xx[l];
       wsync();
     } else {
       if (it >= kPolishFeasAttempts - 1) break;
+      // not yet feasible: add every violated inactive row at its violated
+      // side (QPIK: the ADMM guess typically misses a couple), or only the
+      // most violated one (QPID); the oracle makes the same choice
+      // (polish_add_all)
+      int sb = 0, sg = 0, add = 0x7fffffff;
       double av = 0;
-      int add = 0x7fffffff;
       if (l < nx && actb == 0) {
-        double vlo = (lo[l] - axb) / E[l] - epsp, vhi = (axb - up[l]) / E[l] - epsp;
+        const double vlo = (lo[l] - axb) / E[l] - epsp, vhi = (axb - up[l]) / E[l] - epsp;
+        if (vlo > 0 || vhi > 0) sb = vhi > vlo ? 1 : -1;
         if (vlo > av) { av = vlo; add = l * 4 + 0; }
         if (vhi > av) { av = vhi; add = l * 4 + 2; }
       }
       if (l < ng && actg == 0) {
         const int row = nx + l;
-        double vlo = (lo[row] - axg) / E[row] - epsp, vhi = (axg - up[row]) / E[row] - epsp;
+        const double vlo = (lo[row] - axg) / E[row] - epsp, vhi = (axg - up[row]) / E[row] - epsp;
+        if (vlo > 0 || vhi > 0) sg = vhi > vlo ? 1 : -1;
         if (vlo > av) { av = vlo; add = row * 4 + 0; }
         if (vhi > av) { av = vhi; add = row * 4 + 2; }
       }
-      wave_argmax(av, add);
-      if (add == 0x7fffffff) {
+      CK_N(45);
+      if (!__any(sb != 0 || sg != 0)) {
         if (worst == 0x7fffffff) break;
         if (worst < nx) { if (l == worst) actb = 0; }
         else if (l == worst - nx) actg = 0;
+      } else if (kp.problem == 0) {
+        if (sb) actb = sb;
+        if (sg) actg = sg;
       } else {
+        wave_argmax(av, add);
         const int row = add >> 2, sd = (add & 3) - 1;
         if (row < nx) { if (l == row) actb = sd; }
         else if (l == row - nx) actg = sd;

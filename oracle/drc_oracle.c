@@ -1146,6 +1146,11 @@ static int qp_eqp(const QPW* w, const OracleSettings* s, const int* flag, double
     double b[ORC_MAXC];
     for (int i = 0; i < m; ++i)
         if (flag[i]) { act[nact] = i; b[nact++] = flag[i] < 0 ? w->l[i] : w->u[i]; }
+    if (s->polish_cap > 0) {  /* the kernel's size: free variables + active G rows (rows n.. of A = [I; G]) */
+        int nfix = 0;
+        for (int i = 0; i < n; ++i) nfix += flag[i] != 0;
+        if (n - nfix + (nact - nfix) > s->polish_cap) return 0;
+    }
     int N = n + nact;
     double Dg[ORC_MAXX + ORC_MAXC], rhs[ORC_MAXX + ORC_MAXC], sol[ORC_MAXX + ORC_MAXC], r[ORC_MAXX + ORC_MAXC];
     for (int i = 0; i < N * N; ++i) K0[i] = 0;
@@ -1260,20 +1265,26 @@ static int qp_polish(QPW* w, const OracleSettings* s, int strict) {
             memcpy(xc, xp, n * sizeof(double));
         } else {
             if (it >= POLISH_FEAS_ATTEMPTS - 1) return 0;
-            /* not yet feasible: add the most violated inactive row */
-            int add = -1, af = 0;
+            /* not yet feasible: add every violated inactive row at its
+             * violated side (QPIK: the ADMM guess typically misses a
+             * couple), or only the most violated one (QPID) */
+            int add[ORC_MAXC], nadd = 0, best = -1, bf = 0;
             double av = 0;
             for (int i = 0; i < m; ++i) {
+                add[i] = 0;
                 if (flag[i]) continue;
                 double lo = (w->l[i] - ax[i]) / w->E[i] - tmp.eps_pri, hi = (ax[i] - w->u[i]) / w->E[i] - tmp.eps_pri;
-                if (lo > av) { av = lo; add = i; af = -1; }
-                if (hi > av) { av = hi; add = i; af = 1; }
+                if (lo > 0 || hi > 0) { add[i] = hi > lo ? 1 : -1; ++nadd; }
+                if (lo > av) { av = lo; best = i; bf = -1; }
+                if (hi > av) { av = hi; best = i; bf = 1; }
             }
-            if (add < 0) {
+            if (nadd == 0) {
                 if (worst < 0) return 0;
                 flag[worst] = 0;
+            } else if (s->polish_add_all) {
+                for (int i = 0; i < m; ++i) if (add[i]) flag[i] = add[i];
             } else {
-                flag[add] = af;
+                flag[best] = bf;
             }
         }
     }
@@ -1395,6 +1406,8 @@ void oracle_default_params(int kind, OracleParams* p, int exact) {
     s->adaptive_rho = 1; s->adaptive_rho_interval = 25; s->adaptive_rho_tolerance = 5;
     s->polish = exact ? 1 : 0; s->polish_refine_iter = 3; s->delta = 1e-6;
     s->exact = exact; s->eps_exact = 1e-9; s->eps_fallback = 1e-7;
+    s->polish_cap = 0;
+    s->polish_add_all = 1;
 }
 
 int oracle_qpik_one(const OracleModel* m, const OracleParams* p, const double* q, const double* qdot,
@@ -1551,6 +1564,8 @@ void oracle_default_qpid_params(int kind, OracleParams* p, int exact) {
      * near OSQP's delta = 1e-6, where 3 refinement steps cannot certify at
      * eps_exact: parity mode regularises the polish with delta = 1e-10 */
     if (exact) p->solver.delta = 1e-10;
+    p->solver.polish_cap = 48;              /* the kernel's QPID polish KKT (ncap)     */
+    p->solver.polish_add_all = 0;           /* one row per step (kernel: problem 1)    */
 }
 
 /* Manipulator::QPID (src/manipulator/QP_ID.cpp:7-193) and MobileManipulator::

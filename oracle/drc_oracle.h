@@ -69,6 +69,12 @@ typedef struct OracleSettings {
     int exact;                       /* certified polish + tight fallback   */
     double eps_exact;                /* strict KKT acceptance               */
     double eps_fallback;             /* ADMM-only tight termination         */
+    int polish_cap;                  /* max reduced-KKT size (free variables
+                                      * + active G rows), 0 = none; the
+                                      * kernel's QPID buffers hold 48       */
+    int polish_add_all;              /* infeasible polish point: add every
+                                      * violated row (QPIK) or only the most
+                                      * violated one (QPID)                 */
 } OracleSettings;
 
 typedef struct OracleParams {

@@ -66,6 +66,8 @@ class OracleSettings(C.Structure):
         ("exact", C.c_int),
         ("eps_exact", C.c_double),
         ("eps_fallback", C.c_double),
+        ("polish_cap", C.c_int),
+        ("polish_add_all", C.c_int),
     ]
 
 

@@ -101,7 +101,7 @@ def test_qpid_stages_match_oracle(cuda, robot):
 
 
 def _check_parity(om, spec, q, qdd, tau, status, rq, rt, rs, diags, dyn):
-    assert np.array_equal(status, rs), (status, rs)
+    assert np.array_equal(status, rs), [(int(i), int(status[i]), int(rs[i])) for i in np.flatnonzero(status != rs)]
     ok = rs == O.SOLVED
     scale = np.maximum(1.0, np.maximum(np.abs(rq).max(axis=0), np.abs(rt).max(axis=0)))
     rel = np.maximum(np.abs(qdd - rq).max(axis=0), np.abs(tau - rt).max(axis=0)) / scale

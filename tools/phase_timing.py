@@ -38,3 +38,4 @@ print("straggler EPA step split: scan+support+tests %.0f, grow %.0f cycles/step"
 print("admm_check: residuals %.0f cyc/inst (%d calls), polish %.0f cyc/inst (%d attempts, %d accepted), refactor after polish %.0f cyc/inst" % (v[32] / B, v[33], v[35] / B, v[36], v[37], v[38] / B))
 print("eqp: %d calls, %.0f cycles/call, mean KKT size %.1f; polish residuals %.0f cycles/call" % (v[41], v[40] / max(v[41], 1), v[42] / max(v[41], 1), v[43] / max(v[41], 1)))
 print("qp record load (inside load+assemble): %.0f cyc/inst" % (v[44] / B))
+print("polish steps: infeasible->add/drop %d, wrong dual sign->drop %d, ratio-test blocks %d, KKT residual failures %d" % (v[45], v[46], v[47], v[48]))
