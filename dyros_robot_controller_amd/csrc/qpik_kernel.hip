@@ -780,18 +780,23 @@ __device__ __forceinline__ bool eqp_regs(const KParams& kp, double* S, int actb,
   if (l < NX) xx[l] = actb == 0 ? 0.0 : (actb < 0 ? lo[l] : up[l]) / ab[l];
   wsync();
   // right-hand sides by their owners: variable l (free) and G row l (active)
+  // (free variables hold xx = 0 here, so the sums run over the fixed part;
+  // unconditional and unrolled, the LDS loads issue back to back)
   double rF = 0.0, rG = 0.0;
   if (l < NX && actb == 0) {
     double r = -q[l];
-    if (l < NP)
-      for (int c = 0; c < NP; ++c)
-        if (xx[c] != 0.0) r -= P[l * NP + c] * xx[c];
+    if (l < NP) {
+      const int lp = l < NP ? l : 0;
+#pragma unroll
+      for (int c = 0; c < NP; ++c) r -= P[lp * NP + c] * xx[c];
+    }
     rF = r;
   }
   if (l < NG && actg != 0) {
-    double r = actg < 0 ? lo[NX + l] : up[NX + l];
-    for (int c = 0; c < NX; ++c)
-      if (xx[c] != 0.0) r -= G[l * NX + c] * xx[c];
+    const int lg = l < NG ? l : 0;
+    double r = actg < 0 ? lo[NX + lg] : up[NX + lg];
+#pragma unroll
+    for (int c = 0; c < NX; ++c) r -= G[lg * NX + c] * xx[c];
     rG = r;
   }
   const bool hf = l < nF, hr = l >= nF && l < N;
@@ -862,11 +867,16 @@ __device__ __forceinline__ bool eqp_regs(const KParams& kp, double* S, int actb,
   if (hr) yy[NX + gi] = sol;
   wsync();
   if (l < NX && actb != 0) {  // bound multipliers from stationarity
-    double g = q[l];
-    if (l < NP)
-      for (int c = 0; c < NP; ++c) g += P[l * NP + c] * xx[c];
-    for (int i = 0; i < NG; ++i) g += G[i * NX + l] * yy[NX + i];
-    yy[l] = -g / ab[l];
+    const int lx = l < NX ? l : 0;
+    double g = q[lx];
+    if (l < NP) {
+      const int lp = l < NP ? l : 0;
+#pragma unroll
+      for (int c = 0; c < NP; ++c) g += P[lp * NP + c] * xx[c];
+    }
+#pragma unroll
+    for (int i = 0; i < NG; ++i) g += G[i * NX + lx] * yy[NX + i];
+    yy[lx] = -g / ab[lx];
   }
   wsync();
   return true;
