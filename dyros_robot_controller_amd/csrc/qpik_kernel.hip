@@ -289,40 +289,49 @@ struct Dims {
 // ------------------------------------------------------------------------
 // OSQP residuals (lane-parallel): fills SC_* slots.  x, z, y in LDS (scaled)
 // ------------------------------------------------------------------------
-template <class QD>
+template <class QD, bool UNSCALED = true>
 __device__ __forceinline__ void residuals(const KParams& kp, double* S, const double* x, const double* z, const double* y,
                           double eps_abs, double eps_rel) {
+  // UNSCALED = false (the polish's certification) skips the unscaled norms
+  // that only adaptive rho reads (SC_PRIS .. SC_NQ keep the ADMM values)
   const int l = lane_id(), nx = DNX, ng = DNG, np = DNP;
   const double *P = S + kp.oP, *G = S + kp.oG, *q = S + kp.oQ, *ab = S + kp.oAB, *D = S + kp.oD, *E = S + kp.oE;
   double pr = 0, prs = 0, nAx = 0, nz = 0, nAxs = 0, nzs = 0;
   double dr = 0, drs = 0, nPx = 0, nAty = 0, nq = 0, nPxs = 0, nAtys = 0, nqs = 0;
   if (l < nx) {  // bound row l and variable l
-    double ax = ab[l] * x[l], r = ax - z[l];
+    const int lx = l < nx ? l : 0;
+    double ax = ab[lx] * x[lx], r = ax - z[lx];
     prs = fabs(r);
-    pr = fabs(r / E[l]);
-    nAx = fabs(ax / E[l]);
-    nz = fabs(z[l] / E[l]);
+    pr = fabs(r / E[lx]);
+    nAx = fabs(ax / E[lx]);
+    nz = fabs(z[lx] / E[lx]);
     nAxs = fabs(ax);
-    nzs = fabs(z[l]);
+    nzs = fabs(z[lx]);
     double px = 0;
-    if (l < np)
-      for (int c = 0; c < np; ++c) px += P[l * np + c] * x[c];
-    double aty = ab[l] * y[l];
-    for (int i = 0; i < ng; ++i) aty += G[i * nx + l] * y[nx + i];
-    double rr = px + q[l] + aty;
+    if (l < np) {
+      const int lp = l < np ? l : 0;
+#pragma unroll
+      for (int c = 0; c < np; ++c) px += P[lp * np + c] * x[c];
+    }
+    double aty = ab[lx] * y[lx];
+#pragma unroll
+    for (int i = 0; i < ng; ++i) aty += G[i * nx + lx] * y[nx + i];
+    double rr = px + q[lx] + aty;
     drs = fabs(rr);
-    dr = fabs(rr / D[l]);
-    nPx = fabs(px / D[l]);
-    nAty = fabs(aty / D[l]);
-    nq = fabs(q[l] / D[l]);
+    dr = fabs(rr / D[lx]);
+    nPx = fabs(px / D[lx]);
+    nAty = fabs(aty / D[lx]);
+    nq = fabs(q[lx] / D[lx]);
     nPxs = fabs(px);
     nAtys = fabs(aty);
-    nqs = fabs(q[l]);
+    nqs = fabs(q[lx]);
   }
   if (l < ng) {
+    const int lg = l < ng ? l : 0;
     double ax = 0;
-    for (int j = 0; j < nx; ++j) ax += G[l * nx + j] * x[j];
-    int row = nx + l;
+#pragma unroll
+    for (int j = 0; j < nx; ++j) ax += G[lg * nx + j] * x[j];
+    int row = nx + lg;
     double r = ax - z[row];
     prs = fmax(prs, fabs(r));
     pr = fmax(pr, fabs(r / E[row]));
@@ -332,31 +341,35 @@ __device__ __forceinline__ void residuals(const KParams& kp, double* S, const do
     nzs = fmax(nzs, fabs(z[row]));
   }
   pr = wave_max(pr);
-  prs = wave_max(prs);
   nAx = wave_max(nAx);
   nz = wave_max(nz);
-  nAxs = wave_max(nAxs);
-  nzs = wave_max(nzs);
   dr = wave_max(dr);
-  drs = wave_max(drs);
   nPx = wave_max(nPx);
   nAty = wave_max(nAty);
   nq = wave_max(nq);
-  nPxs = wave_max(nPxs);
-  nAtys = wave_max(nAtys);
-  nqs = wave_max(nqs);
+  if constexpr (UNSCALED) {
+    prs = wave_max(prs);
+    nAxs = wave_max(nAxs);
+    nzs = wave_max(nzs);
+    drs = wave_max(drs);
+    nPxs = wave_max(nPxs);
+    nAtys = wave_max(nAtys);
+    nqs = wave_max(nqs);
+  }
   double c = S[kp.oSc + SC_C];
   if (l == 0) {
     double* sc = S + kp.oSc;
     sc[SC_PRI] = pr;
     sc[SC_DUA] = dr / c;
-    sc[SC_PRIS] = prs;
-    sc[SC_DUAS] = drs;
-    sc[SC_NAX] = nAxs;
-    sc[SC_NZ] = nzs;
-    sc[SC_NPX] = nPxs;
-    sc[SC_NATY] = nAtys;
-    sc[SC_NQ] = nqs;
+    if constexpr (UNSCALED) {
+      sc[SC_PRIS] = prs;
+      sc[SC_DUAS] = drs;
+      sc[SC_NAX] = nAxs;
+      sc[SC_NZ] = nzs;
+      sc[SC_NPX] = nPxs;
+      sc[SC_NATY] = nAtys;
+      sc[SC_NQ] = nqs;
+    }
     sc[SC_EPSP] = eps_abs + eps_rel * fmax(nAx, nz);
     sc[SC_EPSD] = eps_abs + eps_rel * fmax(fmax(nPx, nAty), nq) / c;
   }
@@ -1110,7 +1123,7 @@ __device__ __forceinline__ bool polish(const KParams& kp, double* S, bool strict
 #ifdef DRC_PHASE_TIMING
     const unsigned long long rs_t0 = __builtin_amdgcn_s_memtime();
 #endif
-    residuals<QD>(kp, S, xx, zz, yy, kp.s.eps_exact, kp.s.eps_exact);
+    residuals<QD, false>(kp, S, xx, zz, yy, kp.s.eps_exact, kp.s.eps_exact);
 #ifdef DRC_PHASE_TIMING
     if (l == 0) atomicAdd(&g_phase_cycles[43], __builtin_amdgcn_s_memtime() - rs_t0);
 #endif
