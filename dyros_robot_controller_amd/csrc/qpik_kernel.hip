@@ -1083,11 +1083,12 @@ __device__ __forceinline__ bool polish(const KParams& kp, double* S, bool strict
           if (a < amin) { amin = a; blk = l; side = sd; }
         }
         if (l < ng && actg == 0) {
-          const int row = nx + l;
+          const int lg = l < ng ? l : 0, row = nx + lg;
           double axc = 0, ap = 0, a = 2.0;
+#pragma unroll
           for (int j = 0; j < nx; ++j) {
-            axc += G[l * nx + j] * xc[j];
-            ap += G[l * nx + j] * (xx[j] - xc[j]);
+            axc += G[lg * nx + j] * xc[j];
+            ap += G[lg * nx + j] * (xx[j] - xc[j]);
           }
           int sd = 0;
           if (ap < 0 && lo[row] > -kInf * kMinScaling) { a = (lo[row] - axc) / ap; sd = -1; }
@@ -1116,8 +1117,10 @@ __device__ __forceinline__ bool polish(const KParams& kp, double* S, bool strict
       zz[l] = fmin(fmax(axb, lo[l]), up[l]);
     }
     if (l < ng) {
-      for (int j = 0; j < nx; ++j) axg += G[l * nx + j] * xx[j];
-      zz[nx + l] = fmin(fmax(axg, lo[nx + l]), up[nx + l]);
+      const int lg = l < ng ? l : 0;
+#pragma unroll
+      for (int j = 0; j < nx; ++j) axg += G[lg * nx + j] * xx[j];
+      zz[nx + lg] = fmin(fmax(axg, lo[nx + lg]), up[nx + lg]);
     }
     wsync();
 #ifdef DRC_PHASE_TIMING
