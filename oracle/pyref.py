@@ -710,7 +710,8 @@ def feasible(A, l, u):
 def solve_qp_exact(P, qv, A, l, u, iters=80):
     """Returns (x, y, status) with OSQP sign convention for y (y>0 on an
     active upper bound, y<0 on an active lower bound). status 1 = solved,
-    3 = primal infeasible."""
+    3 = primal infeasible, 0 = no finite iterate (never happens on the test
+    instances; callers treat it as a failure of the certificate)."""
     if not feasible(A, l, u):
         return None, None, 3
     C, d, sgn = _ineq_form(A, l, u)
@@ -724,12 +725,23 @@ def solve_qp_exact(P, qv, A, l, u, iters=80):
     x = np.zeros(n)
     s = np.maximum(C @ x - d, 1.0)
     lam = np.ones(mc)
+    # the iterate with the smallest merit max(|rd|, |rp|, mu) is kept: once mu
+    # reaches ~1e-14 the Newton matrix is numerically singular (P has a null
+    # space on QPID's qdd block) and further steps can diverge to inf/NaN
+    best, best_merit = (x.copy(), s.copy(), lam.copy()), np.inf
     for it in range(iters):
         rd = P @ x + qv - C.T @ lam
         rp = C @ x - d - s
         mu = s @ lam / mc
+        merit = max(np.max(np.abs(rd)), np.max(np.abs(rp)), mu)
+        if not np.isfinite(merit):
+            break
+        if merit < best_merit:
+            best, best_merit = (x.copy(), s.copy(), lam.copy()), merit
         if np.max(np.abs(rd)) < 1e-11 and np.max(np.abs(rp)) < 1e-11 and mu < 1e-14:
             break
+        if mu < 1e-16 and merit > 1e3 * best_merit:
+            break                      # diverging after convergence: keep the best iterate
 
         def newton(rs):
             # P dx - C^T dlam = -rd ; C dx - ds = -rp ; lam ds + s dlam = -rs
@@ -752,8 +764,13 @@ def solve_qp_exact(P, qv, A, l, u, iters=80):
         sigma = (mu_aff / mu) ** 3
         rs = s * lam + ds * dl - sigma * mu
         dx, ds, dl = newton(rs)
+        if not (np.all(np.isfinite(dx)) and np.all(np.isfinite(ds)) and np.all(np.isfinite(dl))):
+            break
         a = 0.995 * min(step(s, ds), step(lam, dl))
         x += a * dx; s += a * ds; lam += a * dl
+    x, s, lam = best
+    if not np.isfinite(best_merit):
+        return None, None, 0           # the interior point never produced a finite iterate
     # active-set refinement: equality-constrained solve on the active rows
     act = [k for k in range(mc) if lam[k] > s[k]]
     Ca, da = C[act], d[act]
@@ -770,6 +787,8 @@ def solve_qp_exact(P, qv, A, l, u, iters=80):
     lam = lam / rn * cs
     for k, (i, sg) in enumerate(sgn):
         y[i] += sg * lam[k]
+    if not (np.all(np.isfinite(x)) and np.all(np.isfinite(y))):
+        return None, None, 0           # never report a non-finite point as solved
     return x, y, 1
 
 
