@@ -44,6 +44,10 @@ def make_inputs(rd, robot, B, seed, offset, dev):
     lo, hi = rd.getJointPositionLimit()
     _, vmax = rd.getJointVelocityLimit()
     q, qd = workload.joint_states(lo, hi, vmax, seed, B, offset)
+    # SURVEY §8d stress tiers (10 % each: joint limit, near-singular, CBF-active
+    # self-collision), judged by the product's own stage kernel
+    workload.apply_stress(q, lo, hi, list(range(len(lo))), seed, offset,
+                          workload.device_evaluator(rd.model, LINKS[robot], dev))
     pb = manipulator.QPIKParamsBuilder(rd.model, exact=True)
     p = pb.params(LINKS[robot], _capi.MODE_QPIK)
     dq, dqd = _batch.as_device(q, dev), _batch.as_device(qd, dev)

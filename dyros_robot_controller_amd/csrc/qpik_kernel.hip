@@ -18,6 +18,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -675,6 +676,11 @@ __device__ __noinline__ int admm_check(const KParams& kp, double* S, int it, int
   CK_N(33);
   if (check) {
     const bool conv = sc[SC_PRI] < sc[SC_EPSP] && sc[SC_DUA] < sc[SC_EPSD];
+#ifdef DRC_QP_DEBUG
+    if (lane_id() == 0 && it <= 200)
+      printf("it %d rho %.4g pri %.3e/%.3e dua %.3e/%.3e x3 %.6f\n", it, sc[SC_RHO], sc[SC_PRI], sc[SC_EPSP],
+             sc[SC_DUA], sc[SC_EPSD], x[3] * S[kp.oD + 3]);
+#endif
     // parity mode: a certified polish is exact whatever the ADMM residual,
     // so try it at every check (the active set settles long before OSQP's
     // eps_rel termination)
@@ -1062,6 +1068,28 @@ __device__ __forceinline__ bool polish(const KParams& kp, double* S, bool strict
   bool have_feas = false;
   const int iters = strict ? kPolishFeasAttempts + kPolishAsIters : 1;
   for (int it = 0; it < iters; ++it) {
+    {
+      // a working-set G row with no weight on the free variables depends on
+      // the fixed bounds alone and makes the reduced KKT singular (its
+      // solution then hangs on rounding noise, e.g. the structurally-zero
+      // manipulability gradient of the first/last joint).  When the fixed
+      // values already satisfy it strictly it is not active: drop it (the
+      // oracle's qp_polish applies the same rule)
+      const unsigned long long fixed = __ballot(l < nx && actb != 0), atup = __ballot(l < nx && actb > 0);
+      if (l < ng && actg != 0) {
+        const int lg = l < ng ? l : 0, row = nx + lg;
+        double sf = 0, sa = 0, act = 0;
+#pragma unroll
+        for (int j = 0; j < nx; ++j) {
+          const double g = G[lg * nx + j];
+          sa = fmax(sa, fabs(g));
+          if (!((fixed >> j) & 1ull)) sf = fmax(sf, fabs(g));
+          else act += g * (((atup >> j) & 1ull) ? up[j] : lo[j]) / ab[j];
+        }
+        const double b = actg < 0 ? lo[row] : up[row], slack = actg < 0 ? act - b : b - act;
+        if (sf <= 1e-12 * sa && slack > 1e-12 * (fabs(act) + fabs(b))) actg = 0;
+      }
+    }
     if (!eqp<QD>(kp, S, actb, actg, xx, yy)) break;
     if (have_feas) {
       double stepmax = 0, xnorm = 0;
@@ -1147,6 +1175,14 @@ __device__ __forceinline__ bool polish(const KParams& kp, double* S, bool strict
       }
       wave_argmax(wv, worst);
       if (worst != 0x7fffffff) ok = false;
+#ifdef DRC_QP_DEBUG
+      {
+        const unsigned long long fb = __ballot(l < nx && actb != 0), fg = __ballot(l < ng && actg != 0);
+        if (l == 0)
+          printf("polish it %d feas %d pri %.2e dua %.2e worst %d (%.2e) havefeas %d bmask %llx gmask %llx\n", it,
+                 (int)feasible, pr1, dr1, worst, wv, (int)have_feas, fb, fg);
+      }
+#endif
       if (!ok && feasible && !have_feas) {
         if (l < nx) xc[l] = xx[l];
         have_feas = true;
@@ -3133,6 +3169,25 @@ qpid_kernel(const DevModel* __restrict__ M0, const KParams kp, const IO io) {
 // ==========================================================================
 namespace drc_amd {
 
+// Per-stream scratch of a model: the task-record pool, the work-queue
+// counters and the fork/join lanes.  Calls on one stream are ordered by that
+// stream, so they may share it; calls on two streams get disjoint contexts
+// (the C-ABI's "reentrant per stream", include/drc_amd.h).
+struct StreamCtx {
+  hipStream_t stream = nullptr;
+  void* pool = nullptr;  // task records / QPID dynamics / OSF M^-1, g
+  int64_t pool_bytes = 0;
+  // work-queue counters: [slot][kernel (task, QP)][8 XCD classes]; slots
+  // 0..15 the QPIK sub-batches, 16 QPID, 17 the closed-form controllers
+  static constexpr int kQueueSlotQpid = 16, kQueueSlotCf = 17, kQueueInts = 18 * 2 * 8;
+  int* d_queue = nullptr;
+  std::vector<hipStream_t> lanes;  // concurrent sub-batches (drc_set_concurrency)
+  std::vector<hipEvent_t> joins;
+  hipEvent_t fork = nullptr;
+  int* dyn_list = nullptr;  // instances whose M_inv needs the serial COD
+  int64_t dyn_list_cap = 0;
+};
+
 struct drc_model_impl {
   HostModel hm;
   DevModel* d_model = nullptr;
@@ -3140,12 +3195,7 @@ struct drc_model_impl {
   drc_kinematic_param kparam{};
   drc_joint_index jidx{};
   drc_actuator_index aidx{};
-  void* pool = nullptr;  // task data when the caller does not keep it
-  // work-queue counters: [slot][kernel (task, QP)][8 XCD classes]; slots
-  // 0..15 the QPIK sub-batches, 16 QPID, 17 the closed-form controllers
-  static constexpr int kQueueSlotQpid = 16, kQueueSlotCf = 17, kQueueInts = 18 * 2 * 8;
-  int* d_queue = nullptr;
-  int64_t pool_bytes = 0;
+  std::vector<std::unique_ptr<StreamCtx>> ctxs;  // one per caller stream seen
   int timing = 0;  // drc_debug_kernel_timing: HIP events around each launch
   // timed calls: {caller-stream start, caller-stream end, per chunk: task start, task end, qp end}
   std::vector<std::vector<hipEvent_t>> events;
@@ -3156,18 +3206,15 @@ struct drc_model_impl {
   // 1 / 2 / 3 / 4 chunks = 7.3 / 8.5 / 8.9 / 7.3 M solves/s; 3 lanes plus the
   // caller's stream fit the 4 hardware queues a process gets by default)
   int chunks = 3;
-  std::vector<hipStream_t> lanes;
-  std::vector<hipEvent_t> joins;
-  hipEvent_t fork = nullptr;
   // host-buffer entry points: device staging + an internal stream
   std::mutex host_mu;
   void* stage = nullptr;
   int64_t stage_bytes = 0;
   hipStream_t hstream = nullptr;
-  // drc_dynamics_batch: queue of instances whose M_inv needs the serial COD
-  int* dyn_list = nullptr;
-  int64_t dyn_list_cap = 0;
-  std::mutex mu;
+  std::mutex mu;         // the context list, timing events, concurrency
+  std::mutex launch_mu;  // one call's launch sequence is enqueued as a unit, so
+                         // two host threads sharing a stream cannot interleave
+                         // their kernels on its scratch
 };
 
 static thread_local std::string g_last_error;
@@ -3180,6 +3227,39 @@ static int set_err(int code, const std::string& msg) {
     hipError_t e_ = (expr);                                                             \
     if (e_ != hipSuccess) return set_err(DRC_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
   } while (0)
+
+// The scratch context of `st` (created on first use; caller holds m->mu).
+static int stream_ctx(drc_model_impl* m, hipStream_t st, StreamCtx** out) {
+  for (auto& c : m->ctxs)
+    if (c->stream == st) {
+      *out = c.get();
+      return DRC_OK;
+    }
+  std::unique_ptr<StreamCtx> c(new StreamCtx());
+  c->stream = st;
+  HIP_TRY(hipMalloc(&c->d_queue, StreamCtx::kQueueInts * sizeof(int)));
+  *out = c.get();
+  m->ctxs.push_back(std::move(c));
+  return DRC_OK;
+}
+static int ensure_pool(StreamCtx* c, int64_t bytes) {
+  if (c->pool_bytes >= bytes) return DRC_OK;
+  if (c->pool) HIP_TRY(hipFree(c->pool));  // synchronises: no launch still reads it
+  c->pool = nullptr;
+  c->pool_bytes = 0;
+  HIP_TRY(hipMalloc(&c->pool, bytes));
+  c->pool_bytes = bytes;
+  return DRC_OK;
+}
+static void free_ctx(StreamCtx* c) {
+  for (hipStream_t ls : c->lanes) (void)hipStreamSynchronize(ls);
+  if (c->d_queue) (void)hipFree(c->d_queue);
+  if (c->pool) (void)hipFree(c->pool);
+  if (c->dyn_list) (void)hipFree(c->dyn_list);
+  for (hipStream_t ls : c->lanes) (void)hipStreamDestroy(ls);
+  for (hipEvent_t e : c->joins) (void)hipEventDestroy(e);
+  if (c->fork) (void)hipEventDestroy(c->fork);
+}
 
 // DyrosMath::PinvCOD on a small dense matrix (host, model build only):
 // Moore-Penrose inverse via the normal equations' symmetric eigen-system,
@@ -3276,7 +3356,6 @@ static int mobile_fk_jacobian(const drc_kinematic_param& p, int* W, double out[3
 static int upload(drc_model_impl* m) {
   HIP_TRY(hipSetDevice(m->device));
   HIP_TRY(hipMalloc(&m->d_model, sizeof(DevModel)));
-  HIP_TRY(hipMalloc(&m->d_queue, drc_model_impl::kQueueInts * sizeof(int)));
   HIP_TRY(hipMemcpy(m->d_model, &m->hm.dev, sizeof(DevModel), hipMemcpyHostToDevice));
   return DRC_OK;
 }
@@ -3479,8 +3558,10 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
                   double* dist, int32_t* pair, double* xdd, void* stream) {
   drc_model_impl* m = const_cast<drc_model_impl*>(cm);
   if (!m || !params) return set_err(DRC_ERR_INVALID_ARGUMENT, "null model/params");
+  std::lock_guard<std::mutex> launch_lock(m->launch_mu);
   if (B < 0) return set_err(DRC_ERR_INVALID_ARGUMENT, "negative batch");
   if (B == 0) return DRC_OK;
+  if (B > 0x7ffffff0) return set_err(DRC_ERR_INVALID_ARGUMENT, "batch too large");  // 32-bit work-queue counters
   if (!q || !qdot || !xdt) return set_err(DRC_ERR_INVALID_ARGUMENT, "q, qdot and xdot_target are required");
   if (params->mode != DRC_MODE_QPIK && !xt) return set_err(DRC_ERR_INVALID_ARGUMENT, "x_target required for QPIKStep/QPIKCubic");
   if (params->mode == DRC_MODE_QPIK_CUBIC && (!xi || !xdi))
@@ -3503,16 +3584,13 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
   const int64_t stride = (kt.rLen + 15) & ~int64_t(15);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   double* rec = nullptr;
+  StreamCtx* cx = nullptr;
   {
     std::lock_guard<std::mutex> g(m->mu);
+    if (int r = stream_ctx(m, st, &cx)) return r;
     if (!stages) {
-      if (m->pool_bytes < stride * B * 8) {
-        if (m->pool) HIP_TRY(hipFree(m->pool));
-        m->pool = nullptr;
-        HIP_TRY(hipMalloc(&m->pool, stride * B * 8));
-        m->pool_bytes = stride * B * 8;
-      }
-      rec = reinterpret_cast<double*>(m->pool);
+      if (int r = ensure_pool(cx, stride * B * 8)) return r;
+      rec = reinterpret_cast<double*>(cx->pool);
     }
   }
   // sub-batches: whole multiples of 16 Ki instances per chunk (each keeps the
@@ -3533,15 +3611,15 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
   };
   {
     std::lock_guard<std::mutex> g(m->mu);
-    while (static_cast<int>(m->lanes.size()) < S) {
+    while (static_cast<int>(cx->lanes.size()) < S) {
       hipStream_t ls;
       hipEvent_t je;
       HIP_TRY(hipStreamCreateWithFlags(&ls, hipStreamNonBlocking));
       HIP_TRY(hipEventCreateWithFlags(&je, hipEventDisableTiming));
-      m->lanes.push_back(ls);
-      m->joins.push_back(je);
+      cx->lanes.push_back(ls);
+      cx->joins.push_back(je);
     }
-    if (!m->fork) HIP_TRY(hipEventCreateWithFlags(&m->fork, hipEventDisableTiming));
+    if (!cx->fork) HIP_TRY(hipEventCreateWithFlags(&cx->fork, hipEventDisableTiming));
   }
   hipEvent_t e_start = nullptr, e_end = nullptr;
   if (timed) {
@@ -3549,17 +3627,17 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
     if (int r = mkev(&e_end)) return r;
     HIP_TRY(hipEventRecord(e_start, st));
   }
-  if (S > 1) HIP_TRY(hipEventRecord(m->fork, st));
+  if (S > 1) HIP_TRY(hipEventRecord(cx->fork, st));
   for (int c = 0; c < S; ++c) {
     const int64_t b0 = B * c / S, b1 = B * (c + 1) / S, Bc = b1 - b0;
-    hipStream_t cs = S > 1 ? m->lanes[c] : st;
-    if (S > 1) HIP_TRY(hipStreamWaitEvent(cs, m->fork, 0));
+    hipStream_t cs = S > 1 ? cx->lanes[c] : st;
+    if (S > 1) HIP_TRY(hipStreamWaitEvent(cs, cx->fork, 0));
     KParams kt_c = kt, kq_c = kq;
     kt_c.xcd_map = kq_c.xcd_map = Bc >= 16384 ? 1 : 0;
     const int64_t gq = Bc < 8192 ? Bc : 8192, gt = Bc < 8192 ? Bc : 8192;
     IO io{Bc, b0, B, q, qdot, xt, xdt, xi, xdi, out, status, iters, pose, jac, man, dist, xdd, pair,
           rec ? rec + b0 * stride : nullptr, stride};
-    int* qc = m->d_queue + c * 16;  // c < 16 (drc_set_concurrency)
+    int* qc = cx->d_queue + c * 16;  // c < 16 (drc_set_concurrency)
     HIP_TRY(hipMemsetAsync(qc, 0, 16 * sizeof(int), cs));
     io.queue = qc;
     hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr;
@@ -3592,10 +3670,10 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
       HIP_TRY(hipGetLastError());
     }
     if (timed) HIP_TRY(hipEventRecord(e2, cs));
-    if (S > 1) HIP_TRY(hipEventRecord(m->joins[c], cs));
+    if (S > 1) HIP_TRY(hipEventRecord(cx->joins[c], cs));
   }
   if (S > 1)
-    for (int c = 0; c < S; ++c) HIP_TRY(hipStreamWaitEvent(st, m->joins[c], 0));
+    for (int c = 0; c < S; ++c) HIP_TRY(hipStreamWaitEvent(st, cx->joins[c], 0));
   if (timed) {
     HIP_TRY(hipEventRecord(e_end, st));
     std::lock_guard<std::mutex> g(m->mu);
@@ -3615,6 +3693,7 @@ static int launch_qpid(const drc_model_impl* cm, const drc_qpik_params* params, 
                        double* qpid_st, double* gdv, void* stream) {
   drc_model_impl* m = const_cast<drc_model_impl*>(cm);
   if (!m || !params) return set_err(DRC_ERR_INVALID_ARGUMENT, "null model/params");
+  std::lock_guard<std::mutex> launch_lock(m->launch_mu);
   if (B < 0) return set_err(DRC_ERR_INVALID_ARGUMENT, "negative batch");
   if (B == 0) return DRC_OK;
   if (B > 0x7ffffff0) return set_err(DRC_ERR_INVALID_ARGUMENT, "batch too large");
@@ -3637,17 +3716,15 @@ static int launch_qpid(const drc_model_impl* cm, const drc_qpik_params* params, 
   const int na = kt.na, nv = d.nv;
   const int64_t dyn_words = stages ? 0 : (int64_t(na) * na + na + (d.kind == 1 ? nv : 0)) * B;
   double *rec = nullptr, *dM = nullptr, *dG = nullptr, *dGf = nullptr;
-  if (!stages) {
+  StreamCtx* cx = nullptr;
+  {
     std::lock_guard<std::mutex> g(m->mu);
-    const int64_t bytes = (stride * B + dyn_words) * 8;
-    if (m->pool_bytes < bytes) {
-      if (m->pool) HIP_TRY(hipFree(m->pool));
-      m->pool = nullptr;
-      m->pool_bytes = 0;
-      HIP_TRY(hipMalloc(&m->pool, bytes));
-      m->pool_bytes = bytes;
-    }
-    rec = reinterpret_cast<double*>(m->pool);
+    if (int r = stream_ctx(m, st, &cx)) return r;
+    if (!stages)
+      if (int r = ensure_pool(cx, (stride * B + dyn_words) * 8)) return r;
+  }
+  if (!stages) {
+    rec = reinterpret_cast<double*>(cx->pool);
     dM = rec + stride * B;
     dG = dM + int64_t(na) * na * B;
     dGf = d.kind == 1 ? dG + int64_t(na) * B : nullptr;
@@ -3667,7 +3744,7 @@ static int launch_qpid(const drc_model_impl* cm, const drc_qpik_params* params, 
   io.st_jdot = jdot;
   io.st_qpid = qpid_st;
   io.st_gdv = gdv;
-  int* qc = m->d_queue + drc_model_impl::kQueueSlotQpid * 16;
+  int* qc = cx->d_queue + StreamCtx::kQueueSlotQpid * 16;
   HIP_TRY(hipMemsetAsync(qc, 0, 16 * sizeof(int), st));
   io.queue = qc;
   hipLaunchKernelGGL(task_kernel<1>, dim3(static_cast<unsigned>(grid)), dim3(64),
@@ -3698,6 +3775,7 @@ static int launch_closed_form(const drc_model_impl* cm, const drc_qpik_params* p
                               const double* xi, const double* xdi, const double* nullv, double* out, void* stream) {
   drc_model_impl* m = const_cast<drc_model_impl*>(cm);
   if (!m || !params) return set_err(DRC_ERR_INVALID_ARGUMENT, "null model/params");
+  std::lock_guard<std::mutex> launch_lock(m->launch_mu);
   if (m->hm.dev.kind != 0) return set_err(DRC_ERR_INVALID_ARGUMENT, "CLIK / OSF are Manipulator::RobotController entries");
   if (B < 0) return set_err(DRC_ERR_INVALID_ARGUMENT, "negative batch");
   if (B == 0) return DRC_OK;
@@ -3716,26 +3794,25 @@ static int launch_closed_form(const drc_model_impl* cm, const drc_qpik_params* p
   HIP_TRY(hipSetDevice(m->device));
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   double *dMi = nullptr, *dG = nullptr;
-  if (cf == 2) {  // getMassMatrixInv (PinvCOD(M)) and getGravity (robot_data.cpp:111-118)
+  StreamCtx* cx = nullptr;
+  {
     std::lock_guard<std::mutex> g(m->mu);
-    const int64_t bytes = (int64_t(d.nv) * d.nv + d.nv) * B * 8;
-    if (m->pool_bytes < bytes) {
-      if (m->pool) HIP_TRY(hipFree(m->pool));
-      m->pool = nullptr;
-      m->pool_bytes = 0;
-      HIP_TRY(hipMalloc(&m->pool, bytes));
-      m->pool_bytes = bytes;
+    if (int r = stream_ctx(m, st, &cx)) return r;
+    if (cf == 2) {
+      if (int r = ensure_pool(cx, (int64_t(d.nv) * d.nv + d.nv) * B * 8)) return r;
+      if (cx->dyn_list_cap < B + 1) {
+        if (cx->dyn_list) HIP_TRY(hipFree(cx->dyn_list));
+        cx->dyn_list = nullptr;
+        cx->dyn_list_cap = 0;
+        HIP_TRY(hipMalloc(&cx->dyn_list, (B + 1) * sizeof(int)));
+        cx->dyn_list_cap = B + 1;
+      }
     }
-    if (m->dyn_list_cap < B + 1) {
-      if (m->dyn_list) HIP_TRY(hipFree(m->dyn_list));
-      m->dyn_list = nullptr;
-      m->dyn_list_cap = 0;
-      HIP_TRY(hipMalloc(&m->dyn_list, (B + 1) * sizeof(int)));
-      m->dyn_list_cap = B + 1;
-    }
-    dMi = reinterpret_cast<double*>(m->pool);
+  }
+  if (cf == 2) {  // getMassMatrixInv (PinvCOD(M)) and getGravity (robot_data.cpp:111-118)
+    dMi = reinterpret_cast<double*>(cx->pool);
     dG = dMi + int64_t(d.nv) * d.nv * B;
-    rc = launch_dynamics(m->d_model, d, false, B, q, qdot, nullptr, dMi, dG, nullptr, nullptr, m->dyn_list, st);
+    rc = launch_dynamics(m->d_model, d, false, B, q, qdot, nullptr, dMi, dG, nullptr, nullptr, cx->dyn_list, st);
     if (rc) return set_err(DRC_ERR_HIP, std::string("dynamics launch: ") + hipGetErrorString(hipGetLastError()));
   }
   const int64_t grid = B < 8192 ? B : 8192;
@@ -3745,7 +3822,7 @@ static int launch_closed_form(const drc_model_impl* cm, const drc_qpik_params* p
   io.dM = dMi;
   io.dG = dG;
   io.cf_null = nullv;
-  io.queue = m->d_queue + drc_model_impl::kQueueSlotCf * 16;
+  io.queue = cx->d_queue + StreamCtx::kQueueSlotCf * 16;
   HIP_TRY(hipMemsetAsync(io.queue, 0, 8 * sizeof(int), st));
   hipLaunchKernelGGL(task_kernel<2>, dim3(static_cast<unsigned>(grid)), dim3(64),
                      static_cast<size_t>(kt.lds_doubles) * sizeof(double), st, m->d_model, kt, io);
@@ -3902,16 +3979,10 @@ int drc_model_create_mobile_manipulator(const drc_kinematic_param* param, const 
 void drc_model_destroy(drc_model* m) {
   if (!m) return;
   (void)hipSetDevice(m->device);
-  for (hipStream_t ls : m->lanes) (void)hipStreamSynchronize(ls);
+  for (auto& c : m->ctxs) drc_amd::free_ctx(c.get());
   if (m->d_model) (void)hipFree(m->d_model);
-  if (m->d_queue) (void)hipFree(m->d_queue);
-  if (m->pool) (void)hipFree(m->pool);
-  if (m->dyn_list) (void)hipFree(m->dyn_list);
-  for (hipStream_t ls : m->lanes) (void)hipStreamDestroy(ls);
   if (m->hstream) (void)hipStreamSynchronize(m->hstream), (void)hipStreamDestroy(m->hstream);
   if (m->stage) (void)hipFree(m->stage);
-  for (hipEvent_t e : m->joins) (void)hipEventDestroy(e);
-  if (m->fork) (void)hipEventDestroy(m->fork);
   for (auto& ev : m->events)
     for (hipEvent_t e : ev) (void)hipEventDestroy(e);
   delete m;
@@ -4302,17 +4373,20 @@ int drc_dynamics_batch(drc_model* m, int actuated, int64_t B, const double* q, c
     return drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "actuated dynamics need a mobile-manipulator model");
   if (B > 0x7ffffff0) return drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "batch too large");
   HIP_TRY(hipSetDevice(m->device));
+  std::lock_guard<std::mutex> launch_lock(m->launch_mu);
   int* list = nullptr;
   if (M_inv) {
     std::lock_guard<std::mutex> lk(m->mu);
-    if (m->dyn_list_cap < B + 1) {
-      if (m->dyn_list) HIP_TRY(hipFree(m->dyn_list));
-      m->dyn_list = nullptr;
-      m->dyn_list_cap = 0;
-      HIP_TRY(hipMalloc(&m->dyn_list, (B + 1) * sizeof(int)));
-      m->dyn_list_cap = B + 1;
+    drc_amd::StreamCtx* cx = nullptr;
+    if (int r = drc_amd::stream_ctx(m, reinterpret_cast<hipStream_t>(stream), &cx)) return r;
+    if (cx->dyn_list_cap < B + 1) {
+      if (cx->dyn_list) HIP_TRY(hipFree(cx->dyn_list));
+      cx->dyn_list = nullptr;
+      cx->dyn_list_cap = 0;
+      HIP_TRY(hipMalloc(&cx->dyn_list, (B + 1) * sizeof(int)));
+      cx->dyn_list_cap = B + 1;
     }
-    list = m->dyn_list;
+    list = cx->dyn_list;
   }
   const int rc = drc_amd::launch_dynamics(m->d_model, m->hm.dev, actuated != 0, B, q, qdot, M, M_inv, g, nle, c,
                                           list, reinterpret_cast<hipStream_t>(stream));

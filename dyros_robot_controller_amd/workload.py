@@ -63,6 +63,88 @@ def mobile_states(lower, upper, vel, joint_index, n_arm, n_wheel, seed, B, offse
     return q, qd
 
 
+# -- stress tiers (SURVEY.md §8d "Stress tiers, 10% each") ---------------------
+# Instance b belongs to one tier, drawn from its own counter stream, so the tier
+# of an instance does not depend on the batch size or on the shard it lands in.
+TIER_NOMINAL, TIER_JOINT_LIMIT, TIER_SINGULAR, TIER_COLLISION = 0, 1, 2, 3
+STRESS_MARGIN = 0.05      # tier 1: within 0.05 rad of a joint limit
+STRESS_MAN = 0.03         # tier 2: manipulability below 0.03 (near-singular)
+STRESS_DIST = 0.06        # tier 3: min self-distance below 0.06 m (CBF row live)
+
+
+def tiers(seed, B, offset=0, frac=0.1):
+    u = uniform(seed, 900, B, offset)
+    t = np.zeros(B, np.int32)
+    t[u < frac] = TIER_JOINT_LIMIT
+    t[(u >= frac) & (u < 2 * frac)] = TIER_SINGULAR
+    t[(u >= 2 * frac) & (u < 3 * frac)] = TIER_COLLISION
+    return t
+
+
+def _candidate_block(lower, upper, rows, seed, rnd, B, offset):
+    """Round `rnd` of the rejection sampler: fresh in-limit joint values for
+    the given rows (joint indices), from streams keyed by (seed, round, row)."""
+    out = {}
+    for k, j in enumerate(rows):
+        u = uniform(seed, 4000 + 64 * rnd + k, B, offset)
+        out[j] = lower[j] + STRESS_MARGIN + (upper[j] - lower[j] - 2 * STRESS_MARGIN) * u
+    return out
+
+
+def apply_stress(q, lower, upper, rows, seed, offset, evaluate, max_rounds=48):
+    """Turns 30 % of a batch of states into the three stress tiers, in place.
+
+    q: [nv][B] joint positions (full vectors); rows: the arm joint indices the
+    tiers act on (manipulator: all joints; mobile manipulator: the arm block).
+    evaluate(q_subset [nv][k]) -> (manipulability [k], min distance [k]) is the
+    caller's stage evaluator (the device's stage kernel in bench.py; the oracle
+    in CPU tests).  Tier 1 moves one arm joint to within STRESS_MARGIN of a limit
+    (inside it).  Tiers 2/3 redraw the arm joints round by round until m <
+    STRESS_MAN / d < STRESS_DIST; an instance that no round satisfies keeps its
+    last draw (counted in the returned stats).  Returns (tier [B], stats)."""
+    nv, B = q.shape
+    tier = tiers(seed, B, offset)
+    # tier 1: joint j = floor(u n), lower or upper side, depth U(0, margin)
+    ua, ub, uc = (uniform(seed, 950 + i, B, offset) for i in range(3))
+    jsel = np.minimum((ua * len(rows)).astype(int), len(rows) - 1)
+    for b in np.nonzero(tier == TIER_JOINT_LIMIT)[0]:
+        j = rows[jsel[b]]
+        q[j, b] = lower[j] + STRESS_MARGIN * uc[b] if ub[b] < 0.5 else upper[j] - STRESS_MARGIN * uc[b]
+    stats = {"joint_limit": int(np.sum(tier == TIER_JOINT_LIMIT))}
+    for t, key in ((TIER_SINGULAR, "singular"), (TIER_COLLISION, "collision")):
+        todo = np.nonzero(tier == t)[0]
+        hit = 0
+        for rnd in range(max_rounds):
+            if todo.size == 0:
+                break
+            cand = _candidate_block(lower, upper, rows, seed + 7919 * t, rnd, B, offset)
+            for j in rows:
+                q[j, todo] = cand[j][todo]
+            m, d = evaluate(np.ascontiguousarray(q[:, todo]))
+            ok = (np.asarray(m) < STRESS_MAN) if t == TIER_SINGULAR else (np.asarray(d) < STRESS_DIST)
+            hit += int(ok.sum())
+            todo = todo[~ok]
+        stats[key] = hit
+        stats[key + "_unmet"] = int(todo.size)
+    return tier, stats
+
+
+def device_evaluator(model, link_name, device):
+    """apply_stress evaluator backed by the product's stage kernel
+    (drc_qpik_stages_batch): manipulability of ``link_name`` and min self-distance."""
+    from . import _batch, _capi
+    from .manipulator import QPIKParamsBuilder
+    p = QPIKParamsBuilder(model, exact=True).params(link_name, _capi.MODE_QPIK)
+
+    def evaluate(qs):
+        k = qs.shape[1]
+        z = _batch.as_device(np.zeros_like(qs), device)
+        st = _batch.stages_batch(model, p, _batch.as_device(qs, device), z, None,
+                                 _batch.as_device(np.zeros((6, k)), device))
+        return st["man"][0].cpu().numpy(), st["dist"][0].cpu().numpy()
+    return evaluate
+
+
 def so3_exp_batch(w):
     """w [3][B] -> R [B][3][3]"""
     th = np.sqrt(np.sum(w * w, axis=0))

@@ -11,8 +11,11 @@
  *  - Batched arrays are structure-of-arrays, field-major: element (f, b) of
  *    a [F][B] array is at ptr[f * B + b].  All batched pointers are DEVICE
  *    pointers owned by the caller (HBM resident); `stream` is a hipStream_t
- *    (NULL = default stream).  Calls are asynchronous on that stream and
- *    reentrant per stream.
+ *    (NULL = default stream).  Calls are asynchronous on that stream.  A
+ *    model keeps its per-call scratch (task records, work-queue counters,
+ *    fork/join lanes) per caller stream, so calls on one model from several
+ *    streams run concurrently without sharing scratch, and calls from several
+ *    host threads are safe (each call's launches are enqueued as a unit).
  *  - Poses are 12 doubles: R column-major (9) then p (3) — Eigen::Affine3d
  *    `linear()` memory order followed by `translation()`.
  *  - Velocities / twists are [v(3); w(3)] in the world frame

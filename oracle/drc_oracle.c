@@ -1201,6 +1201,22 @@ static int qp_polish(QPW* w, const OracleSettings* s, int strict) {
     double xp[ORC_MAXX], yp[ORC_MAXC], zp[ORC_MAXC], ax[ORC_MAXC], xc[ORC_MAXX];
     int have_feasible = 0;
     for (int it = 0; it < (strict ? POLISH_FEAS_ATTEMPTS + POLISH_AS_ITERS : 1); ++it) {
+        /* a working-set row with no weight on the free variables depends on
+         * the fixed bounds alone and makes the reduced KKT singular; when the
+         * fixed values already satisfy it strictly it is not active: drop it
+         * (the kernel's polish applies the same rule) */
+        for (int i = n; i < m; ++i) {
+            if (!flag[i]) continue;
+            double sf = 0, sa = 0, act = 0;
+            for (int j = 0; j < n; ++j) {
+                double g = w->A[i * n + j];
+                sa = fmax(sa, fabs(g));
+                if (!flag[j]) sf = fmax(sf, fabs(g));
+                else act += g * (flag[j] > 0 ? w->u[j] : w->l[j]) / w->A[j * n + j];
+            }
+            double b = flag[i] < 0 ? w->l[i] : w->u[i], slack = flag[i] < 0 ? act - b : b - act;
+            if (sf <= 1e-12 * sa && slack > 1e-12 * (fabs(act) + fabs(b))) flag[i] = 0;
+        }
         if (!qp_eqp(w, s, flag, xp, yp)) return 0;
         double stepmax = 0, xnorm = 0;
         if (have_feasible) {
@@ -1245,9 +1261,12 @@ static int qp_polish(QPW* w, const OracleSettings* s, int strict) {
                 if (viol > wv) { wv = viol; worst = i; }
             }
             if (worst >= 0) ok = 0;
-            if (getenv("ORC_DEBUG"))
-                fprintf(stderr, "polish it %d feas %d pri %.2e dua %.2e worst %d (%.2e) havefeas %d\n", it, feasible,
+            if (getenv("ORC_DEBUG")) {
+                fprintf(stderr, "polish it %d feas %d pri %.2e dua %.2e worst %d (%.2e) havefeas %d flags", it, feasible,
                         tmp.pri_res, tmp.dua_res, worst, wv, have_feasible);
+                for (int i = 0; i < m; ++i) if (flag[i]) fprintf(stderr, " %d%c", i, flag[i] < 0 ? 'l' : 'u');
+                fprintf(stderr, "\n");
+            }
             if (!ok && feasible && !have_feasible) { memcpy(xc, xp, n * sizeof(double)); have_feasible = 1; }
         }
         if (ok) {
@@ -1342,6 +1361,9 @@ int oracle_solve_qp(int n, int m, const double* P, const double* qv, const doubl
         if (check || adapt) qp_residuals(&w, &w.r, w.x, w.z, w.y, s->eps_abs, s->eps_rel);
         if (check) {
             int conv = w.r.pri_res < w.r.eps_pri && w.r.dua_res < w.r.eps_dua;
+            if (getenv("ORC_DEBUG") && it <= 200)
+                fprintf(stderr, "it %d rho %.4g pri %.3e/%.3e dua %.3e/%.3e x3 %.6f\n", it, w.rho, w.r.pri_res, w.r.eps_pri,
+                        w.r.dua_res, w.r.eps_dua, w.x[3] * w.D[3]);
             /* parity mode: a certified polish is exact whatever the ADMM
              * residual, so try it at every check (the active set settles
              * long before OSQP's eps_rel termination) */
@@ -1410,9 +1432,13 @@ void oracle_default_params(int kind, OracleParams* p, int exact) {
     s->polish_add_all = 1;
 }
 
-int oracle_qpik_one(const OracleModel* m, const OracleParams* p, const double* q, const double* qdot,
-                    const double* x_target, const double* xdot_target, const double* x_init,
-                    const double* xdot_init, double* out, OracleDiag* diag) {
+/* dist_in (optional): the distance stage (d, grad[nv]) supplied by the caller
+ * instead of computed — parity tests feed the device's narrow-phase result so
+ * the QP assembly and solve are compared on identical distance data */
+static int qpik_one_impl(const OracleModel* m, const OracleParams* p, const double* q, const double* qdot,
+                         const double* x_target, const double* xdot_target, const double* x_init,
+                         const double* xdot_init, const double* dist_in, const double* man_in, double* out,
+                         OracleDiag* diag) {
     int nv = m->nv;
     Kin k;
     kin_fk(m, q, &k);
@@ -1463,8 +1489,10 @@ int oracle_qpik_one(const OracleModel* m, const OracleParams* p, const double* q
     double man, mgrad[ORC_MAXJ], dist, dgrad[ORC_MAXJ];
     int pair;
     int c0 = moma ? m->mani_start : 0, narm = moma ? m->n_arm : nv;
-    manip(m, &k, J, c0, narm, &man, mgrad);
-    min_distance(m, &k, &dist, dgrad, &pair);
+    if (man_in) { man = man_in[0]; memcpy(mgrad, man_in + 1, narm * sizeof(double)); }
+    else manip(m, &k, J, c0, narm, &man, mgrad);
+    if (dist_in) { dist = dist_in[0]; memcpy(dgrad, dist_in + 1, nv * sizeof(double)); pair = -1; }
+    else min_distance(m, &k, &dist, dgrad, &pair);
     /* QP assembly */
     static __thread double P[ORC_MAXX * ORC_MAXX], A[ORC_MAXC * ORC_MAXX];
     double qv[ORC_MAXX], l[ORC_MAXC], u[ORC_MAXC];
@@ -1547,6 +1575,12 @@ int oracle_qpik_one(const OracleModel* m, const OracleParams* p, const double* q
         diag->polished = pol;
     }
     return st;
+}
+
+int oracle_qpik_one(const OracleModel* m, const OracleParams* p, const double* q, const double* qdot,
+                    const double* x_target, const double* xdot_target, const double* x_init,
+                    const double* xdot_init, double* out, OracleDiag* diag) {
+    return qpik_one_impl(m, p, q, qdot, x_target, xdot_target, x_init, xdot_init, NULL, NULL, out, diag);
 }
 
 /* ------------------------------------------------------------------------ */
@@ -1867,7 +1901,7 @@ void oracle_joint_placement(const OracleModel* m, const double* q, int jid, doub
 /* ------------------------------------------------------------------------ */
 typedef struct Job {
     const OracleModel* m; const OracleParams* p; int64_t B, lo, hi;
-    const double *q, *qdot, *xt, *xdt, *xi, *xdi;
+    const double *q, *qdot, *xt, *xdt, *xi, *xdi, *dist_in, *man_in;
     double* out; int32_t* status; int32_t* iters; int64_t fails;
 } Job;
 
@@ -1882,8 +1916,13 @@ static void* worker(void* arg) {
         for (int i = 0; i < 6; ++i) xdt[i] = j->xdt[i * j->B + b];
         for (int i = 0; i < 12; ++i) xi[i] = j->xi ? j->xi[i * j->B + b] : 0;
         for (int i = 0; i < 6; ++i) xdi[i] = j->xdi ? j->xdi[i * j->B + b] : 0;
+        double din[1 + ORC_MAXJ], mi[1 + ORC_MAXJ];
+        int narm = m->kind == 1 ? m->n_arm : nv;
+        if (j->dist_in) for (int i = 0; i <= nv; ++i) din[i] = j->dist_in[i * j->B + b];
+        if (j->man_in) for (int i = 0; i <= narm; ++i) mi[i] = j->man_in[i * j->B + b];
         OracleDiag dg;
-        int st = oracle_qpik_one(m, j->p, q, qd, xt, xdt, xi, xdi, out, &dg);
+        int st = qpik_one_impl(m, j->p, q, qd, xt, xdt, xi, xdi, j->dist_in ? din : NULL, j->man_in ? mi : NULL, out,
+                               &dg);
         for (int i = 0; i < na; ++i) j->out[i * j->B + b] = out[i];
         if (j->status) j->status[b] = st;
         if (j->iters) j->iters[b] = dg.iters;
@@ -1892,10 +1931,11 @@ static void* worker(void* arg) {
     return NULL;
 }
 
-int64_t oracle_qpik_batch(const OracleModel* m, const OracleParams* p, int64_t B, const double* q,
+static int64_t qpik_batch_impl(const OracleModel* m, const OracleParams* p, int64_t B, const double* q,
                           const double* qdot, const double* x_target, const double* xdot_target,
                           const double* x_init, const double* xdot_init, double* out, int32_t* status,
-                          int32_t* iters, int nthreads) {
+                          int32_t* iters, int nthreads, const double* dist_in,
+                               const double* man_in) {
     if (nthreads < 1) nthreads = 1;
     if (nthreads > 256) nthreads = 256;
     Job jobs[256];
@@ -1905,13 +1945,31 @@ int64_t oracle_qpik_batch(const OracleModel* m, const OracleParams* p, int64_t B
         Job* j = &jobs[t];
         j->m = m; j->p = p; j->B = B; j->lo = t * per; j->hi = (t + 1) * per < B ? (t + 1) * per : B;
         if (j->lo > B) j->lo = B;
-        j->q = q; j->qdot = qdot; j->xt = x_target; j->xdt = xdot_target; j->xi = x_init; j->xdi = xdot_init;
+        j->q = q; j->qdot = qdot; j->xt = x_target; j->xdt = xdot_target; j->xi = x_init; j->xdi = xdot_init; j->dist_in = dist_in; j->man_in = man_in;
         j->out = out; j->status = status; j->iters = iters; j->fails = 0;
         pthread_create(&th[t], NULL, worker, j);
     }
     int64_t fails = 0;
     for (int t = 0; t < nthreads; ++t) { pthread_join(th[t], NULL); fails += jobs[t].fails; }
     return fails;
+}
+
+int64_t oracle_qpik_batch(const OracleModel* m, const OracleParams* p, int64_t B, const double* q,
+                          const double* qdot, const double* x_target, const double* xdot_target,
+                          const double* x_init, const double* xdot_init, double* out, int32_t* status,
+                          int32_t* iters, int nthreads) {
+    return qpik_batch_impl(m, p, B, q, qdot, x_target, xdot_target, x_init, xdot_init, out, status, iters,
+                           nthreads, NULL, NULL);
+}
+
+/* as oracle_qpik_batch with stage data given: dist_in [1+nv][B] = (d, grad),
+ * man_in [1+narm][B] = (m, grad) (either may be NULL: computed) */
+int64_t oracle_qpik_batch_dist(const OracleModel* m, const OracleParams* p, int64_t B, const double* q,
+                               const double* qdot, const double* x_target, const double* xdot_target,
+                               const double* x_init, const double* xdot_init, const double* dist_in,
+                               const double* man_in, double* out, int32_t* status, int32_t* iters, int nthreads) {
+    return qpik_batch_impl(m, p, B, q, qdot, x_target, xdot_target, x_init, xdot_init, out, status, iters,
+                           nthreads, dist_in, man_in);
 }
 
 /* ------------------------------------------------------------------------ */

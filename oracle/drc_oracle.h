@@ -125,6 +125,14 @@ int64_t oracle_qpik_batch(const OracleModel* m, const OracleParams* p, int64_t B
                           const double* x_target, const double* xdot_target,
                           const double* x_init, const double* xdot_init,
                           double* out, int32_t* status, int32_t* iters, int nthreads);
+/* Same with stage data supplied (parity of the QP on identical data):
+ * dist_in [1+nv][B] = (d, grad d) replaces getMinDistance's result, man_in
+ * [1+narm][B] = (m, grad m) getManipulability's; NULL = computed. */
+int64_t oracle_qpik_batch_dist(const OracleModel* m, const OracleParams* p, int64_t B,
+                               const double* q, const double* qdot,
+                               const double* x_target, const double* xdot_target,
+                               const double* x_init, const double* xdot_init, const double* dist_in,
+                               const double* man_in, double* out, int32_t* status, int32_t* iters, int nthreads);
 
 /* QPID / QPIDStep / QPIDCubic for one instance (mode 0 takes the task
  * acceleration in xdot_target).  M, g: na x na (row-major) and na, the

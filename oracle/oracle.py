@@ -112,6 +112,10 @@ def lib():
         _lib.oracle_qpik_batch.restype = C.c_int64
         _lib.oracle_qpik_batch.argtypes = [C.POINTER(OracleModel), C.POINTER(OracleParams), C.c_int64,
                                            d, d, d, d, d, d, d, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.c_int]
+        _lib.oracle_qpik_batch_dist.restype = C.c_int64
+        _lib.oracle_qpik_batch_dist.argtypes = [C.POINTER(OracleModel), C.POINTER(OracleParams), C.c_int64,
+                                                d, d, d, d, d, d, d, d, d, C.POINTER(C.c_int32),
+                                                C.POINTER(C.c_int32), C.c_int]
         _lib.oracle_solve_qp.restype = C.c_int
     return _lib
 
@@ -240,6 +244,24 @@ def qpik_batch(om, params, q, qdot, x_target, xdot_target, x_init=None, xdot_ini
     lib().oracle_qpik_batch(C.byref(om), C.byref(params), C.c_int64(B), *[_ptr(a) for a in arrs], _ptr(out),
                             status.ctypes.data_as(C.POINTER(C.c_int32)), iters.ctypes.data_as(C.POINTER(C.c_int32)),
                             C.c_int(nthreads))
+    return out, status, iters
+
+
+def qpik_batch_dist(om, params, q, qdot, x_target, xdot_target, dist, x_init=None, xdot_init=None, nthreads=1,
+                    man=None):
+    """qpik_batch with the distance stage supplied (dist [1+nv][B] = d, grad;
+    optionally man [1+narm][B] = m, grad): the QP of QP_IK.cpp:59-131 on the
+    caller's stage data."""
+    B = q.shape[1]
+    na = om.n_wheel + om.n_arm if om.kind == 1 else om.nv
+    out = np.zeros((na, B))
+    status = np.zeros(B, np.int32)
+    iters = np.zeros(B, np.int32)
+    arrs = [np.ascontiguousarray(a, float) if a is not None else None
+            for a in (q, qdot, x_target, xdot_target, x_init, xdot_init, dist, man)]
+    lib().oracle_qpik_batch_dist(C.byref(om), C.byref(params), C.c_int64(B), *[_ptr(a) for a in arrs], _ptr(out),
+                                 status.ctypes.data_as(C.POINTER(C.c_int32)),
+                                 iters.ctypes.data_as(C.POINTER(C.c_int32)), C.c_int(nthreads))
     return out, status, iters
 
 

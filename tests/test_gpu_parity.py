@@ -11,20 +11,23 @@ Tolerances (FP64 throughout):
                          1e-3 when penetrating (EPA face-barycentre witnesses on
                          curved surfaces); larger only where the
                          min distance is non-smooth (gradient ill-defined)
-  QP-IK qdot* (exact)    1e-9 median; 1e-4 abs and task-space residual
-                         |J dq|_inf <= 1e-4 (BASELINE.json north_star bound)
-                         except on <= 5% of instances where the distance
-                         constraint is active and the optimum amplifies the
-                         narrow-phase witness tolerance: there the kernel's
-                         qdot must be the exact optimum (1e-7) of the QP built
-                         from its own stage data; status identical
+  QP-IK qdot* (exact)    (tests/_common.py:assert_qpik_parity)
+                         on the device's distance stage: EVERY instance within
+                         1e-6 abs and task residual |J dq|_inf <= 1e-6
+                         (north_star bound 1e-4), status identical;
+                         end to end: status identical, median 1e-9, and the
+                         instances beyond 1e-4 at most the measured count in
+                         EXPECTED_OFF, each explained by a distance stage
+                         within the narrow-phase tolerance above (penetrating
+                         witness gradients up to 2e-2: EPA at hpp-fcl's
+                         64-vertex cap on cylinder pairs).  Inputs include the
+                         SURVEY §8d stress tiers (ids "stress").
 """
 import numpy as np
 import pytest
 
 import oracle as O
-from _common import (LINK, make_manipulator, nonsmooth_min_distance, oracle_batch, qp_from_stages, stage_pose,
-                     stage_step, step_inputs)
+from _common import LINK, assert_qpik_parity, make_manipulator, narrow_phase_close, oracle_batch, stage_pose, step_inputs
 from dyros_robot_controller_amd import manipulator
 
 pytestmark = pytest.mark.gpu
@@ -34,7 +37,7 @@ pytestmark = pytest.mark.gpu
 def test_stages_match_oracle(cuda, robot):
     rd = make_manipulator(robot, cuda)
     B = 256
-    q, qd, xt, xdt = step_inputs(rd, robot, 1, B, cuda)
+    q, qd, xt, xdt = step_inputs(rd, robot, 1, B, cuda, stress=True)
     st = stage_pose(rd.model, cuda, q, qd, LINK[robot])
     pm, om, spec = O.load(robot)
     n = om.nv
@@ -48,47 +51,26 @@ def test_stages_match_oracle(cuda, robot):
         assert abs(st["man"][0, b] - m) <= 1e-10 * max(1.0, m)
         np.testing.assert_allclose(st["man"][1:, b], mg, atol=1e-8)
         d, dg, pair = O.min_distance(om, q[:, b])
-        assert abs(st["dist"][0, b] - d) <= (1e-9 if d > 0 else 1e-6), (b, st["dist"][0, b], d)
         if st["pair"][b] != pair:  # exact tie in distance only
             dk, _, _ = O.pair_distance(om, q[:, b], int(st["pair"][b]))
             assert abs(dk - d) <= (1e-9 if d > 0 else 1e-6)
-        elif np.max(np.abs(st["dist"][1:, b] - dg)) > (1e-5 if d > 0 else 1e-3):
-            assert nonsmooth_min_distance(om, q[:, b]), b
+        assert narrow_phase_close(om, q[:, b], st["dist"][0, b], st["dist"][1:, b]), (b, st["dist"][0, b], d)
 
 
+# end-to-end instances beyond 1e-4 at these seeds (measured; see assert_qpik_parity)
+EXPECTED_OFF = {("fr3", False): 0, ("ur5e", False): 4, ("fr3", True): 0, ("ur5e", True): 2}
+
+
+@pytest.mark.parametrize("stress", [False, True], ids=["nominal", "stress"])
 @pytest.mark.parametrize("robot", ["fr3", "ur5e"])
-def test_qpik_step_exact_matches_oracle(cuda, robot):
+def test_qpik_step_exact_matches_oracle(cuda, robot, stress):
     rd = make_manipulator(robot, cuda)
     ctrl = manipulator.RobotController(0.001, rd, solver_mode="exact")
     B = 512
-    q, qd, xt, xdt = step_inputs(rd, robot, 2, B, cuda)
+    q, qd, xt, xdt = step_inputs(rd, robot, 2, B, cuda, stress=stress)
     out, status = ctrl.QPIK_step_batch(q, qd, xt, xdt, LINK[robot])
     out, status = out.cpu().numpy(), status.cpu().numpy()
-    ref, rstat, _, om = oracle_batch(robot, q, qd, xt, xdt, exact=True)
-    assert np.array_equal(status, rstat)
-    err = np.abs(out - ref).max(axis=0)
-    assert np.median(err) <= 1e-9
-    st = stage_step(rd.model, cuda, q, qd, xt, xdt, LINK[robot])
-    pm = O.load(robot)[0]
-    off = []
-    for b in range(B):
-        _, J = O.fk_pose(om, q[:, b])
-        if err[b] <= 1e-4 and np.max(np.abs(J @ (out[:, b] - ref[:, b]))) <= 1e-4:
-            continue
-        off.append(b)
-        if nonsmooth_min_distance(om, q[:, b]):
-            continue  # reference gradient ill-defined
-        # Otherwise the distance constraint is active and the optimum is
-        # sensitive to its gradient: the kernel must still return the exact
-        # optimum of the QP built from its own stage data, and that data must
-        # agree with the oracle within the narrow-phase tolerances.
-        x = qp_from_stages(pm, q, st, b, LINK[robot])
-        assert x is not None and np.max(np.abs(out[:, b] - x)) <= 1e-7, (b, err[b])
-        d, dg, _ = O.min_distance(om, q[:, b])
-        assert abs(st["dist"][0, b] - d) <= (1e-9 if d > 0 else 1e-6)
-        assert np.max(np.abs(st["dist"][1:, b] - dg)) <= (1e-5 if d > 0 else 1e-3), b
-    print("%s: %d/%d instances outside 1e-4 (active, gradient-sensitive distance row)" % (robot, len(off), B))
-    assert len(off) <= 0.05 * B, off
+    assert_qpik_parity(robot, rd.model, q, qd, xt, xdt, out, status, EXPECTED_OFF[robot, stress])
 
 
 def test_qpik_step_osqp_default_matches_oracle(cuda):
