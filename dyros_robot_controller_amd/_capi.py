@@ -36,6 +36,7 @@ MAX_WHEELS = 8
 EXPORTED_SYMBOLS = (
     "drc_model_create_manipulator", "drc_model_create_mobile_manipulator", "drc_model_destroy",
     "drc_model_info", "drc_model_limits", "drc_model_find_frame", "drc_model_mobile_fk_jacobian",
+    "drc_mobile_fk_jacobian", "drc_mobile_ik_jacobian",
     "drc_default_qpik_params", "drc_qpik_batch", "drc_qpik_stages_batch", "drc_debug_kernel_timing",
     "drc_debug_kernel_times", "drc_set_concurrency", "drc_qpik_host", "drc_qpik_stages_host",
     "drc_dynamics_batch", "drc_dynamics_host", "drc_joint_torque_step_batch", "drc_joint_torque_step_host",
@@ -121,6 +122,8 @@ def _load():
     lib.drc_model_limits.argtypes = [vp, dp, dp, dp, dp]
     lib.drc_model_find_frame.argtypes = [vp, C.c_char_p, ip]
     lib.drc_model_mobile_fk_jacobian.argtypes = [vp, dp]
+    lib.drc_mobile_fk_jacobian.argtypes = [C.POINTER(KinematicParam), dp, dp, ip]
+    lib.drc_mobile_ik_jacobian.argtypes = [C.POINTER(KinematicParam), dp, dp, ip]
     lib.drc_default_qpik_params.argtypes = [vp, C.c_int, C.POINTER(QPIKParams)]
     lib.drc_qpik_batch.argtypes = [vp, C.POINTER(QPIKParams), C.c_int64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     lib.drc_qpik_stages_batch.argtypes = [vp, C.POINTER(QPIKParams), C.c_int64, vp, vp, vp, vp, vp, vp,

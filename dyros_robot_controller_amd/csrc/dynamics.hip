@@ -26,6 +26,7 @@
 #include <hip/hip_runtime.h>
 
 #include "dynamics.hpp"
+#include "mobile_fk.hpp"
 #include "model.hpp"
 #include "pinv_cod.hpp"
 #include "qpik_device.hpp"
@@ -398,6 +399,14 @@ __global__ void __launch_bounds__(kDT) __attribute__((amdgpu_waves_per_eu(4, 8))
     const int vs = M0->virtual_start, ms = M0->mani_start, ws = M0->mobi_start;
     const int am = M0->act_mani_start, aw = M0->act_mobi_start, W = M0->n_wheel, nar = M0->n_arm;
     const double yaw = sq[(vs + 2) * kDI + g], cy = cos(yaw), sy = sin(yaw);
+    // J_mobile at this robot's wheel positions (caster: steer dependent)
+    double jm[3][kMaxWheels];
+    {
+      double wp[kMaxWheels];
+#pragma unroll
+      for (int w = 0; w < kMaxWheels; ++w) wp[w] = w < W ? sq[(ws + w) * kDI + g] : 0.0;
+      mobile_fk(M0, wp, jm);
+    }
     // lane's actuated column: rows/weights of S e_j (<= 4 nonzeros)
     int rr[4] = {0, 0, 0, 0};
     double rw[4] = {0, 0, 0, 0};
@@ -407,7 +416,10 @@ __global__ void __launch_bounds__(kDT) __attribute__((amdgpu_waves_per_eu(4, 8))
         rw[0] = 1;
       } else if (j >= aw && j < aw + W) {
         const int w = j - aw;
-        const double j0 = M0->J_mobile[0][w], j1 = M0->J_mobile[1][w], j2 = M0->J_mobile[2][w];
+        double j0 = 0, j1 = 0, j2 = 0;
+#pragma unroll
+        for (int k = 0; k < kMaxWheels; ++k)
+          if (k == w) j0 = jm[0][k], j1 = jm[1][k], j2 = jm[2][k];
         rr[0] = ws + w; rw[0] = 1;
         rr[1] = vs;     rw[1] = cy * j0 - sy * j1;
         rr[2] = vs + 1; rw[2] = sy * j0 + cy * j1;
@@ -442,7 +454,10 @@ __global__ void __launch_bounds__(kDT) __attribute__((amdgpu_waves_per_eu(4, 8))
         for (int i = 0; i < kMaxJoints; ++i) s += i == r0 ? t[i] : 0.0;
       } else {
         const int w = bb - aw;
-        const double j0 = M0->J_mobile[0][w], j1 = M0->J_mobile[1][w], j2 = M0->J_mobile[2][w];
+        double j0 = 0, j1 = 0, j2 = 0;
+#pragma unroll
+        for (int k = 0; k < kMaxWheels; ++k)
+          if (k == w) j0 = jm[0][k], j1 = jm[1][k], j2 = jm[2][k];
         const double w0 = cy * j0 - sy * j1, w1 = sy * j0 + cy * j1;
 #pragma unroll
         for (int i = 0; i < kMaxJoints; ++i)

@@ -17,6 +17,7 @@ constexpr int kMaxWheels = 8;
 
 enum JointType : int { kRevolute = 0, kPrismatic = 1 };
 enum GeomType : int { kSphere = 0, kCylinder = 1, kBox = 2 };
+enum DriveKind : int { kDriveDifferential = 0, kDriveMecanum = 1, kDriveCaster = 2 };  // DRC_DRIVE_*
 
 // Flat, POD model image in HBM.  Transforms are 12 doubles: R row-major, p.
 struct DevModel {
@@ -39,7 +40,10 @@ struct DevModel {
   double gparam[kMaxGeoms][3];     // sphere r | cylinder r, h/2 | box half extents
   double gbound[kMaxGeoms];        // conservative core/bounding radius for the broad phase
   int16_t pair_a[kMaxPairs], pair_b[kMaxPairs];
-  double J_mobile[3][kMaxWheels];  // base twist = J_mobile * wheel velocity
+  double J_mobile[3][kMaxWheels];  // base twist = J_mobile * wheel velocity (differential, mecanum)
+  int drive;                       // DriveKind; caster: J_mobile depends on the steer angles (mobile_fk.hpp)
+  double wheel_radius, wheel_offset;
+  double caster_pos[kMaxWheels / 2][2];  // base2wheel_positions of the casters
   // rigid-body inertia carried by each joint (links behind fixed joints merged,
   // Pinocchio appendBodyToJoint), in the joint frame:
   // {mass, com x, y, z, Ixx, Iyy, Izz, Ixy, Ixz, Iyz} with I about the com

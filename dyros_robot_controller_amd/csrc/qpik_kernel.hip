@@ -25,6 +25,7 @@
 
 #include "../../include/drc_amd.h"
 #include "dynamics.hpp"
+#include "mobile_fk.hpp"
 #include "model.hpp"
 #include "pinv_cod.hpp"
 #include "qpik_device.hpp"
@@ -1377,6 +1378,23 @@ __device__ __forceinline__ void body_velocity(const DevModel* M, const double* T
 //       = sum_{c in arm} qdot_c n.(JB_dot - JA_dot)[:, c]   (robot_data.cpp:496-512).
 // full: also the reference's grad_dot VECTORS (stage outputs) into kGdv =
 //   [getManipulability grad_dot (narm) | getMinDistance grad_dot (nv)].
+// J_mobile of this instance (row stride kMaxWheels) staged in LDS (kSv): the
+// model table for the configuration-independent drives; a caster base's
+// depends on the steer angles q[mobi_start + 2i] and is evaluated by lane 0.
+// Wave-uniform call (contains a wave barrier).
+__device__ __forceinline__ const double (*mobile_jac(const DevModel* M, const KParams& kp, double* S,
+                                                     const double* q))[kMaxWheels] {
+  double(*Jm)[kMaxWheels] = reinterpret_cast<double(*)[kMaxWheels]>(S + kp.kSv);
+  const int l = lane_id();
+  if (M->drive == kDriveCaster) {
+    if (l == 0) mobile_fk(M, q + M->mobi_start, Jm);
+  } else if (l < 3 * kMaxWheels) {
+    Jm[l / kMaxWheels][l % kMaxWheels] = M->J_mobile[l / kMaxWheels][l % kMaxWheels];
+  }
+  wsync();
+  return Jm;
+}
+
 __device__ __noinline__ void qpid_task_extras(const DevModel* M, const KParams& kp, double* S, double bestd,
                                               int besti, bool full) {
   const int l = lane_id(), nv = kp.nv, narm = kp.narm, c0 = kp.c0;
@@ -1393,6 +1411,7 @@ __device__ __noinline__ void qpid_task_extras(const DevModel* M, const KParams& 
     if (arm & (1u << c)) va = va + qd[c] * jc;
   }
   double dsum = 0;
+  const double(*Jm)[kMaxWheels] = mobile_jac(M, kp, S, qv);  // read for mobile manipulators only
   if (l < nv) {
     const int j = l + 1;
     V3 lin = v3(0, 0, 0), ang = v3(0, 0, 0), lina = v3(0, 0, 0), anga = v3(0, 0, 0);
@@ -1414,7 +1433,7 @@ __device__ __noinline__ void qpid_task_extras(const DevModel* M, const KParams& 
       const double yaw = qv[M->virtual_start + 2], cy = cos(yaw), sy = sin(yaw);
       v = 0;
       for (int w = 0; w < M->n_wheel; ++w) {
-        const double j0 = M->J_mobile[0][w], j1 = M->J_mobile[1][w], j2 = M->J_mobile[2][w];
+        const double j0 = Jm[0][w], j1 = Jm[1][w], j2 = Jm[2][w];
         const double sw = r == 0 ? cy * j0 - sy * j1 : (r == 1 ? sy * j0 + cy * j1 : j2);
         v += sw * qd[M->mobi_start + w];
       }
@@ -2270,6 +2289,7 @@ __device__ __forceinline__ void qp_assemble(const DevModel* M, const KParams& kp
   } else {
     // J~ = J S  (mobile_manipulator/robot_data.cpp:407-410); S virtual block = Rz(yaw) J_mobile
     const double yaw = qv[M->virtual_start + 2], cy = cos(yaw), sy = sin(yaw);
+    const double(*Jm)[kMaxWheels] = mobile_jac(M, kp, S, qv);
     for (int e = l; e < 6 * np; e += 64) {
       const int r = e / np, a = e % np;
       double v = 0;
@@ -2277,9 +2297,9 @@ __device__ __forceinline__ void qp_assemble(const DevModel* M, const KParams& kp
       if (am >= 0 && am < M->n_arm) {
         v = J[r * nv + M->mani_start + am];
       } else if (aw >= 0 && aw < M->n_wheel) {
-        const double s0 = cy * M->J_mobile[0][aw] - sy * M->J_mobile[1][aw];
-        const double s1 = sy * M->J_mobile[0][aw] + cy * M->J_mobile[1][aw];
-        const double s2 = M->J_mobile[2][aw];
+        const double s0 = cy * Jm[0][aw] - sy * Jm[1][aw];
+        const double s1 = sy * Jm[0][aw] + cy * Jm[1][aw];
+        const double s2 = Jm[2][aw];
         const int vs = M->virtual_start;
         v = J[r * nv + M->mobi_start + aw] + J[r * nv + vs] * s0 + J[r * nv + vs + 1] * s1 + J[r * nv + vs + 2] * s2;
       }
@@ -3034,6 +3054,7 @@ __device__ __forceinline__ void qpid_assemble(const DevModel* M, const KParams& 
     for (int e = l; e < 6 * np; e += 64) Jt[e] = J[(e / np) * nv + e % np];
   } else {  // J~ = J S (robot_data.cpp:407-410)
     const double yaw = qv[M->virtual_start + 2], cy = cos(yaw), sy = sin(yaw);
+    const double(*Jm)[kMaxWheels] = mobile_jac(M, kp, S, qv);
     for (int e = l; e < 6 * np; e += 64) {
       const int r = e / np, c = e % np;
       double v = 0;
@@ -3041,9 +3062,9 @@ __device__ __forceinline__ void qpid_assemble(const DevModel* M, const KParams& 
       if (am >= 0 && am < M->n_arm) {
         v = J[r * nv + M->mani_start + am];
       } else if (aw >= 0 && aw < M->n_wheel) {
-        const double s0 = cy * M->J_mobile[0][aw] - sy * M->J_mobile[1][aw];
-        const double s1 = sy * M->J_mobile[0][aw] + cy * M->J_mobile[1][aw];
-        const double s2 = M->J_mobile[2][aw];
+        const double s0 = cy * Jm[0][aw] - sy * Jm[1][aw];
+        const double s1 = sy * Jm[0][aw] + cy * Jm[1][aw];
+        const double s2 = Jm[2][aw];
         const int vs = M->virtual_start;
         v = J[r * nv + M->mobi_start + aw] + J[r * nv + vs] * s0 + J[r * nv + vs + 1] * s1 + J[r * nv + vs + 2] * s2;
       }
@@ -3318,9 +3339,11 @@ static void pinv_small(const double* A, int r, int c, double* X /* c x r */) {
     }
 }
 
-// Mobile::RobotData::computeFKJacobian for the config-independent drives
-// (src/mobile/robot_data.cpp:138-176).
-static int mobile_fk_jacobian(const drc_kinematic_param& p, int* W, double out[3][kMaxWheels]) {
+// Mobile::RobotData::computeFKJacobian (src/mobile/robot_data.cpp:123-204) at
+// the wheel positions `wheel_pos` (used by the caster drive only; may be NULL
+// for the configuration-independent drives, then zero steer angles).
+static int mobile_fk_jacobian(const drc_kinematic_param& p, int* W, double out[3][kMaxWheels],
+                              const double* wheel_pos = nullptr) {
   for (int r = 0; r < 3; ++r)
     for (int c = 0; c < kMaxWheels; ++c) out[r][c] = 0;
   if (p.type == DRC_DRIVE_DIFFERENTIAL) {
@@ -3350,7 +3373,61 @@ static int mobile_fk_jacobian(const drc_kinematic_param& p, int* W, double out[3
     *W = n;
     return DRC_OK;
   }
-  return set_err(DRC_ERR_UNSUPPORTED, "caster drive: the FK Jacobian depends on steer angles (not supported by the batched whole-body kernel)");
+  if (p.type == DRC_DRIVE_CASTER) {  // CasterFKJacobian (:179-204): W = 2 x casters
+    const int C = p.n_wheels;
+    if (C < 1 || 2 * C > kMaxWheels) return set_err(DRC_ERR_INVALID_ARGUMENT, "caster count out of range");
+    double zero[kMaxWheels] = {0};
+    caster_fk_jacobian(C, p.wheel_radius, p.wheel_offset, p.base2wheel_positions, wheel_pos ? wheel_pos : zero, out);
+    *W = 2 * C;
+    return DRC_OK;
+  }
+  return set_err(DRC_ERR_INVALID_ARGUMENT, "unknown drive type");
+}
+
+// Mobile::RobotController::computeIKJacobian (src/mobile/robot_controller.cpp:55-125):
+// wheel velocities = J_ik (W x 3, row-major) * base twist.
+static int mobile_ik_jacobian(const drc_kinematic_param& p, const double* wheel_pos, double* J, int* W) {
+  const double r = p.wheel_radius;
+  if (p.type == DRC_DRIVE_DIFFERENTIAL) {  // DifferentialIKJacobian (:76-84)
+    *W = 2;
+    const double e[6] = {1 / r, 0, -p.base_width / (2 * r), 1 / r, 0, p.base_width / (2 * r)};
+    for (int i = 0; i < 6; ++i) J[i] = e[i];
+    return DRC_OK;
+  }
+  if (p.type == DRC_DRIVE_MECANUM) {  // MecanumIKJacobian (:86-107)
+    const int n = p.n_wheels;
+    if (n < 1 || n > kMaxWheels) return set_err(DRC_ERR_INVALID_ARGUMENT, "mecanum wheel count out of range");
+    for (int i = 0; i < n; ++i) {
+      const double g = p.roller_angles[i], px = p.base2wheel_positions[i][0], py = p.base2wheel_positions[i][1],
+                   pt = p.base2wheel_angles[i];
+      const double a0 = std::cos(pt) - std::tan(g) * std::sin(pt), a1 = std::sin(pt) + std::tan(g) * std::cos(pt);
+      J[i * 3 + 0] = a0 / r;
+      J[i * 3 + 1] = a1 / r;
+      J[i * 3 + 2] = (-a0 * py + a1 * px) / r;
+    }
+    *W = n;
+    return DRC_OK;
+  }
+  if (p.type == DRC_DRIVE_CASTER) {  // CasterIKJacobian (:109-125), steer angle = wheel_pos(2i)
+    const int C = p.n_wheels;
+    if (C < 1 || 2 * C > kMaxWheels) return set_err(DRC_ERR_INVALID_ARGUMENT, "caster count out of range");
+    const double b = p.wheel_offset;
+    for (int i = 0; i < C; ++i) {
+      const double phi = wheel_pos ? wheel_pos[2 * i] : 0.0, sp = std::sin(phi), cp = std::cos(phi);
+      const double px = p.base2wheel_positions[i][0], py = p.base2wheel_positions[i][1];
+      double* r0 = J + (2 * i) * 3;
+      double* r1 = J + (2 * i + 1) * 3;
+      r0[0] = -sp / b;
+      r0[1] = cp / b;
+      r0[2] = (px * cp + py * sp) / b - 1;
+      r1[0] = cp / r;
+      r1[1] = sp / r;
+      r1[2] = (px * sp - py * cp) / r;
+    }
+    *W = 2 * C;
+    return DRC_OK;
+  }
+  return set_err(DRC_ERR_INVALID_ARGUMENT, "unknown drive type");
 }
 
 static int upload(drc_model_impl* m) {
@@ -3947,6 +4024,15 @@ int drc_model_create_mobile_manipulator(const drc_kinematic_param* param, const 
     delete m;
     return rc;
   }
+  d.drive = param->type;
+  d.wheel_radius = param->wheel_radius;
+  d.wheel_offset = param->wheel_offset;
+  for (int i = 0; i < drc_amd::kMaxWheels / 2; ++i)
+    for (int k = 0; k < 2; ++k) d.caster_pos[i][k] = param->base2wheel_positions[i][k];
+  if (param->type == DRC_DRIVE_CASTER && !(param->wheel_offset != 0)) {
+    delete m;
+    return drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "caster drive needs a nonzero wheel_offset");
+  }
   // MobileManipulator::RobotData ctor (mobile_manipulator/robot_data.cpp:18-25)
   const int virtual_dof = 3;
   d.kind = 1;
@@ -4028,9 +4114,32 @@ int drc_model_mobile_fk_jacobian(const drc_model* m, double* J) {
   if (!m || !J) return drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "null argument");
   const drc_amd::DevModel& d = m->hm.dev;
   if (d.kind != 1) return drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "not a mobile manipulator");
+  if (d.drive == drc_amd::kDriveCaster)
+    return drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT,
+                            "caster drive: J_mobile depends on the steer angles (drc_mobile_fk_jacobian)");
   for (int r = 0; r < 3; ++r)
     for (int c = 0; c < d.n_wheel; ++c) J[r * d.n_wheel + c] = d.J_mobile[r][c];
   return DRC_OK;
+}
+
+int drc_mobile_fk_jacobian(const drc_kinematic_param* p, const double* wheel_pos, double* J, int* n_wheels) {
+  if (!p || !J || !n_wheels) return drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "null argument");
+  if (p->type == DRC_DRIVE_CASTER && !wheel_pos)
+    return drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "caster drive: wheel positions required");
+  double Jm[3][drc_amd::kMaxWheels];
+  int W = 0;
+  if (int rc = drc_amd::mobile_fk_jacobian(*p, &W, Jm, wheel_pos)) return rc;
+  for (int r = 0; r < 3; ++r)
+    for (int c = 0; c < W; ++c) J[r * W + c] = Jm[r][c];
+  *n_wheels = W;
+  return DRC_OK;
+}
+
+int drc_mobile_ik_jacobian(const drc_kinematic_param* p, const double* wheel_pos, double* J, int* n_wheels) {
+  if (!p || !J || !n_wheels) return drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "null argument");
+  if (p->type == DRC_DRIVE_CASTER && !wheel_pos)
+    return drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "caster drive: wheel positions required");
+  return drc_amd::mobile_ik_jacobian(*p, wheel_pos, J, n_wheels);
 }
 
 int drc_default_qpik_params(const drc_model* m, int exact, drc_qpik_params* p) {

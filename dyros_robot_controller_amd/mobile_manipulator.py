@@ -37,7 +37,7 @@ from .manipulator import QPIKParamsBuilder, _ModelHandle, _default_device, pose_
 
 
 class DriveType(IntEnum):
-    """drc/type_define.py:6-9 (Caster bases are not supported by the kernel)."""
+    """drc/type_define.py:6-9."""
     Differential = _capi.DRIVE_DIFFERENTIAL
     Mecanum = _capi.DRIVE_MECANUM
     Caster = _capi.DRIVE_CASTER
@@ -63,6 +63,8 @@ class KinematicParam:
         if self.type == DriveType.Mecanum and (roller_angles is None or base2wheel_positions is None
                                                or base2wheel_angles is None):
             raise ValueError("Mecanum drive requires roller_angles, base2wheel_positions, base2wheel_angles")
+        if self.type == DriveType.Caster and (base2wheel_positions is None or not wheel_offset):
+            raise ValueError("Caster drive requires base2wheel_positions and a nonzero wheel_offset")
 
     def c_struct(self):
         p = _capi.KinematicParam()
@@ -81,6 +83,13 @@ class KinematicParam:
                 p.base2wheel_positions[i][0] = float(self.base2wheel_positions[i][0])
                 p.base2wheel_positions[i][1] = float(self.base2wheel_positions[i][1])
                 p.base2wheel_angles[i] = float(self.base2wheel_angles[i])
+        if self.type == DriveType.Caster:   # n_wheels counts casters (2 joints each, robot_data.cpp:27-30)
+            n = len(self.base2wheel_positions)
+            if 2 * n > _capi.MAX_WHEELS:
+                raise ValueError("at most %d casters" % (_capi.MAX_WHEELS // 2))
+            for i in range(n):
+                p.base2wheel_positions[i][0] = float(self.base2wheel_positions[i][0])
+                p.base2wheel_positions[i][1] = float(self.base2wheel_positions[i][1])
         p.n_wheels = n
         p.wheel_offset = float(self.wheel_offset) if self.wheel_offset is not None else 0.0
         return p
@@ -127,10 +136,7 @@ class RobotData:
         n = self.model.dof
         self._lims = [np.zeros(n) for _ in range(4)]
         _capi.check(_capi.lib().drc_model_limits(h, *(a.ctypes.data_as(C.POINTER(C.c_double)) for a in self._lims)))
-        self._Jm = np.zeros((3, self.model.mobi_dof))
-        Jm = np.zeros(3 * _capi.MAX_WHEELS)
-        _capi.check(_capi.lib().drc_model_mobile_fk_jacobian(h, Jm.ctypes.data_as(C.POINTER(C.c_double))))
-        self._Jm = Jm[:3 * self.model.mobi_dof].reshape(3, self.model.mobi_dof)
+        self._kp_c = kp
         self.q_ = np.zeros(n)
         self.qdot_ = np.zeros(n)
         self._dyn_cache = {}
@@ -154,10 +160,22 @@ class RobotData:
     def get_actuator_index(self):
         return self._aidx
 
-    def get_mobile_FK_jacobian(self):
-        return self._Jm.copy()
+    def compute_mobile_FK_jacobian(self, q_mobile):
+        """Mobile::RobotData::computeFKJacobian(q_mobile) (mobile/robot_data.cpp:123-204):
+        constant for differential / mecanum bases, steer-angle dependent for casters."""
+        W = self.model.mobi_dof
+        J = np.zeros(3 * W)
+        qm = np.ascontiguousarray(np.asarray(q_mobile, float).reshape(-1))
+        if qm.size != W:
+            raise ValueError("q_mobile must have %d entries" % W)
+        nw = C.c_int()
+        dp = lambda a: a.ctypes.data_as(C.POINTER(C.c_double))
+        _capi.check(_capi.lib().drc_mobile_fk_jacobian(C.byref(self._kp_c), dp(qm), dp(J), C.byref(nw)))
+        return J.reshape(3, W)
 
-    compute_mobile_FK_jacobian = lambda self, q_mobile=None: self.get_mobile_FK_jacobian()  # noqa: E731
+    def get_mobile_FK_jacobian(self):
+        ji = self.get_joint_index()
+        return self.compute_mobile_FK_jacobian(self.q_[ji.mobi_start:ji.mobi_start + self.model.mobi_dof])
 
     def get_joint_position_limit(self):
         return self._lims[0].copy(), self._lims[1].copy()

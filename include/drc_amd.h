@@ -65,7 +65,7 @@ typedef struct drc_kinematic_param {
     double wheel_radius;
     double max_lin_speed, max_ang_speed, max_lin_acc, max_ang_acc;
     double base_width;                              /* differential */
-    int n_wheels;                                   /* mecanum / caster entries used */
+    int n_wheels;                                   /* mecanum wheels / casters (W = 2 per caster) */
     double roller_angles[DRC_MAX_WHEELS];
     double base2wheel_positions[DRC_MAX_WHEELS][2];
     double base2wheel_angles[DRC_MAX_WHEELS];
@@ -144,8 +144,19 @@ int drc_model_limits(const drc_model* model, double* q_lb, double* q_ub, double*
 int drc_model_find_frame(const drc_model* model, const char* link_name, int* frame_id);
 
 /* Mobile FK Jacobian J_mobile (3 x W, row-major) of the base
- * (mobile/robot_data.cpp:123-176); host array. */
+ * (mobile/robot_data.cpp:123-176); host array.  Differential / mecanum only:
+ * a caster base's J_mobile depends on the steer angles (drc_mobile_fk_jacobian). */
 int drc_model_mobile_fk_jacobian(const drc_model* model, double* J3xW);
+
+/* Mobile::RobotData::computeFKJacobian(wheel_pos) (mobile/robot_data.cpp:123-204)
+ * for any drive, host arrays: J3xW [3][W] row-major; wheel_pos [W] (caster:
+ * steer angle at 2i, drive angle at 2i+1; ignored otherwise, may be NULL);
+ * *n_wheels receives W.  KinematicParam.n_wheels counts mecanum wheels or
+ * casters (W = 2 x casters, :27-30). */
+int drc_mobile_fk_jacobian(const drc_kinematic_param* param, const double* wheel_pos, double* J3xW, int* n_wheels);
+/* Mobile::RobotController::computeIKJacobian (mobile/robot_controller.cpp:55-125):
+ * wheel velocities = J [W][3] row-major * base twist; same arguments. */
+int drc_mobile_ik_jacobian(const drc_kinematic_param* param, const double* wheel_pos, double* JWx3, int* n_wheels);
 
 /* Reference defaults for the model kind (robot_controller ctor gains, QP
  * constants, OSQP defaults).  exact=0: the reference's OSQP settings

@@ -330,6 +330,42 @@ static void pinv_cod_sym(const double* A, int n, double* X) {
     pinv_qr_trunc(A, n, 1e-6, X);
 }
 
+/* Mobile::RobotData::computeFKJacobian (src/mobile/robot_data.cpp:123-204):
+ * the constant table for differential / mecanum; CasterFKJacobian (:179-204)
+ * at the steer angles q[mobi_start + 2i]:
+ *   J = PinvCOD(Jp~^T Jp~) Jp~^T Jq^-1                                       */
+static void mobile_fk_jac(const OracleModel* m, const double* q, double J[3][8]) {
+    if (m->drive != 2) { memcpy(J, m->J_mobile, sizeof(double) * 24); return; }
+    int W = m->n_wheel, C = W / 2;
+    double Jp[16 * 3], Jq[16 * 16], N[9], Ni[9];
+    memset(Jp, 0, sizeof(Jp));
+    memset(Jq, 0, sizeof(Jq));
+    double r = m->wheel_radius, b = m->wheel_offset;
+    for (int i = 0; i < C; ++i) {
+        double phi = q[m->mobi_start + 2 * i], px = m->caster_pos[i][0], py = m->caster_pos[i][1];
+        double* r0 = Jp + (2 * i) * 3;
+        double* r1 = Jp + (2 * i + 1) * 3;
+        r0[0] = 1; r0[1] = 0; r0[2] = -(py + b * sin(phi));
+        r1[0] = 0; r1[1] = 1; r1[2] = px + b * cos(phi);
+        Jq[(2 * i) * W + 2 * i] = b * sin(phi);     Jq[(2 * i) * W + 2 * i + 1] = r * cos(phi);
+        Jq[(2 * i + 1) * W + 2 * i] = -b * cos(phi); Jq[(2 * i + 1) * W + 2 * i + 1] = r * sin(phi);
+    }
+    for (int a = 0; a < 3; ++a)
+        for (int c = 0; c < 3; ++c) { double t = 0; for (int k = 0; k < W; ++k) t += Jp[k * 3 + a] * Jp[k * 3 + c]; N[a * 3 + c] = t; }
+    pinv_cod_sym(N, 3, Ni);
+    for (int a = 0; a < 3; ++a)
+        for (int w = 0; w < 8; ++w) {
+            double t = 0;
+            if (w < W)
+                for (int k = 0; k < W; ++k) {
+                    double pk = 0;   /* (Ni Jp~^T)[a][k] */
+                    for (int c = 0; c < 3; ++c) pk += Ni[a * 3 + c] * Jp[k * 3 + c];
+                    t += pk * Jq[k * W + w];
+                }
+            J[a][w] = t;
+        }
+}
+
 /* ------------------------------------------------------------------------ */
 /* manipulability  (robot_data.cpp:519-553; MoMa :439-475)                  */
 /* ------------------------------------------------------------------------ */
@@ -1453,11 +1489,12 @@ static int qpik_one_impl(const OracleModel* m, const OracleParams* p, const doub
         for (int i = 0; i < m->n_arm; ++i) S[(m->mani_start + i) * na + m->act_mani_start + i] = 1;
         for (int i = 0; i < m->n_wheel; ++i) S[(m->mobi_start + i) * na + m->act_mobi_start + i] = 1;
         double yaw = q[m->virtual_start + 2], cy = cos(yaw), sy = sin(yaw);
-        double Rz[9] = {cy, -sy, 0, sy, cy, 0, 0, 0, 1};
+        double Rz[9] = {cy, -sy, 0, sy, cy, 0, 0, 0, 1}, Jmob[3][8];
+        mobile_fk_jac(m, q, Jmob);
         for (int r = 0; r < 3; ++r)
             for (int wcol = 0; wcol < m->n_wheel; ++wcol) {
                 double s = 0;
-                for (int c = 0; c < 3; ++c) s += Rz[3 * r + c] * m->J_mobile[c][wcol];
+                for (int c = 0; c < 3; ++c) s += Rz[3 * r + c] * Jmob[c][wcol];
                 S[(m->virtual_start + r) * na + m->act_mobi_start + wcol] = s;
             }
     }
@@ -1629,11 +1666,12 @@ int oracle_qpid_one(const OracleModel* m, const OracleParams* p, const double* q
         for (int i = 0; i < m->n_arm; ++i) S[(m->mani_start + i) * na + m->act_mani_start + i] = 1;
         for (int i = 0; i < m->n_wheel; ++i) S[(m->mobi_start + i) * na + m->act_mobi_start + i] = 1;
         double yaw = q[m->virtual_start + 2], cy = cos(yaw), sy = sin(yaw);
-        double Rz[9] = {cy, -sy, 0, sy, cy, 0, 0, 0, 1};
+        double Rz[9] = {cy, -sy, 0, sy, cy, 0, 0, 0, 1}, Jmob[3][8];
+        mobile_fk_jac(m, q, Jmob);
         for (int r = 0; r < 3; ++r)
             for (int wc = 0; wc < m->n_wheel; ++wc) {
                 double t = 0;
-                for (int c = 0; c < 3; ++c) t += Rz[3 * r + c] * m->J_mobile[c][wc];
+                for (int c = 0; c < 3; ++c) t += Rz[3 * r + c] * Jmob[c][wc];
                 S[(m->virtual_start + r) * na + m->act_mobi_start + wc] = t;
             }
         for (int i = 0; i < m->n_arm; ++i) eta[m->act_mani_start + i] = qdot[m->mani_start + i];
@@ -1980,6 +2018,11 @@ void oracle_fk_pose(const OracleModel* m, const double* q, double* pose12, doubl
     kin_fk(m, q, &k);
     memcpy(pose12, k.Te, 12 * sizeof(double));
     if (J) point_jacobian(m, &k, m->ee_joint, k.pe, J);
+}
+void oracle_mobile_fk_jacobian(const OracleModel* m, const double* q, double* J) {
+    double Jm[3][8];
+    mobile_fk_jac(m, q, Jm);
+    for (int r = 0; r < 3; ++r) for (int c = 0; c < m->n_wheel; ++c) J[r * m->n_wheel + c] = Jm[r][c];
 }
 void oracle_min_distance(const OracleModel* m, const double* q, double* dist, double* grad, int* pair) {
     Kin k;

@@ -56,6 +56,10 @@ typedef struct OracleModel {
     int virtual_start, mani_start, mobi_start;   /* JointIndex            */
     int act_mani_start, act_mobi_start;          /* ActuatorIndex         */
     double J_mobile[3][8];           /* base twist / wheel velocity (3xW)   */
+    int drive;                       /* 0 differential, 1 mecanum, 2 caster  */
+    double wheel_radius, wheel_offset;
+    double caster_pos[4][2];         /* caster: base2wheel_positions; J_mobile
+                                      * then follows the steer angles       */
 } OracleModel;
 
 typedef struct OracleSettings {

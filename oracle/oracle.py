@@ -51,6 +51,9 @@ class OracleModel(C.Structure):
         ("act_mani_start", C.c_int),
         ("act_mobi_start", C.c_int),
         ("J_mobile", (C.c_double * 8) * 3),
+        ("drive", C.c_int),
+        ("wheel_radius", C.c_double), ("wheel_offset", C.c_double),
+        ("caster_pos", (C.c_double * 2) * 4),
     ]
 
 
@@ -143,6 +146,25 @@ def mecanum_fk_jacobian(radius, positions, angles, rollers):
     return pinv_cod(Jinv)
 
 
+def caster_fk_jacobian(radius, offset, positions, wheel_pos):
+    """Mobile::RobotData::CasterFKJacobian (src/mobile/robot_data.cpp:179-204)
+    at the wheel positions (steer angle of caster i at 2i)."""
+    from pyref import pinv_cod
+    C_ = len(positions)
+    Jp = np.zeros((2 * C_, 3))
+    Jq = np.zeros((2 * C_, 2 * C_))
+    for i, (px, py) in enumerate(positions):
+        phi = wheel_pos[2 * i]
+        Jp[2 * i] = [1, 0, -(py + offset * np.sin(phi))]
+        Jp[2 * i + 1] = [0, 1, px + offset * np.cos(phi)]
+        Jq[2 * i:2 * i + 2, 2 * i:2 * i + 2] = [[offset * np.sin(phi), radius * np.cos(phi)],
+                                                [-offset * np.cos(phi), radius * np.sin(phi)]]
+    return pinv_cod(Jp.T @ Jp) @ Jp.T @ Jq
+
+
+CASTER_FR3 = dict(radius=0.08, offset=0.05, positions=[(0.25, 0.2), (-0.25, -0.2)])
+
+
 def differential_fk_jacobian(radius, width):
     """Mobile::RobotData::DifferentialFKJacobian (src/mobile/robot_data.cpp:138-147)."""
     return np.array([[radius / 2, radius / 2], [0, 0], [-radius / width, radius / width]])
@@ -159,6 +181,11 @@ ROBOTS = {
                     J_mobile=lambda: mecanum_fk_jacobian(
                         0.120, [(0.2225, 0.2045), (0.2225, -0.2045), (-0.2225, 0.2045), (-0.2225, -0.2045)],
                         [0, 0, 0, 0], [-np.pi / 4, np.pi / 4, np.pi / 4, -np.pi / 4])),
+    # J_mobile(wheel_pos): the caster base's FK Jacobian follows the steer angles
+    "caster_fr3": dict(urdf="caster_fr3/caster_fr3.urdf", srdf="caster_fr3/caster_fr3.srdf", ee="fr3_link8", kind=1,
+                       n_arm=7, n_wheel=4, joint_index=(0, 3, 10), actuator_index=(0, 7), drive=2,
+                       J_mobile=lambda wheel_pos: caster_fk_jacobian(CASTER_FR3["radius"], CASTER_FR3["offset"],
+                                                                     CASTER_FR3["positions"], wheel_pos)),
 }
 
 
@@ -200,10 +227,16 @@ def load(robot):
         om.n_arm, om.n_wheel = spec["n_arm"], spec["n_wheel"]
         om.virtual_start, om.mani_start, om.mobi_start = spec["joint_index"]
         om.act_mani_start, om.act_mobi_start = spec["actuator_index"]
-        Jm = spec["J_mobile"]()
-        for r in range(3):
-            for c in range(spec["n_wheel"]):
-                om.J_mobile[r][c] = Jm[r, c]
+        om.drive = spec.get("drive", 0)
+        if om.drive == 2:
+            om.wheel_radius, om.wheel_offset = CASTER_FR3["radius"], CASTER_FR3["offset"]
+            for i, (px, py) in enumerate(CASTER_FR3["positions"]):
+                om.caster_pos[i][0], om.caster_pos[i][1] = px, py
+        else:
+            Jm = spec["J_mobile"]()
+            for r in range(3):
+                for c in range(spec["n_wheel"]):
+                    om.J_mobile[r][c] = Jm[r, c]
     return pm, om, spec
 
 
@@ -270,6 +303,13 @@ def fk_pose(om, q):
     J = np.zeros(6 * om.nv)
     lib().oracle_fk_pose(C.byref(om), _ptr(np.ascontiguousarray(q, float)), _ptr(pose), _ptr(J))
     return pose, J.reshape(6, om.nv)
+
+
+def mobile_fk_jacobian(om, q):
+    """The C oracle's J_mobile (3 x W) at the full joint vector q."""
+    J = np.zeros(3 * om.n_wheel)
+    lib().oracle_mobile_fk_jacobian(C.byref(om), _ptr(np.ascontiguousarray(q, float)), _ptr(J))
+    return J.reshape(3, om.n_wheel)
 
 
 def min_distance(om, q):

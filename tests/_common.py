@@ -8,7 +8,8 @@ import oracle as O
 import pyref as R
 from dyros_robot_controller_amd import manipulator, mobile_manipulator, robot_path, workload, _batch, _capi
 
-LINK = {"fr3": "fr3_link8", "ur5e": "tool0", "husky_fr3": "fr3_link8", "xls_fr3": "fr3_link8"}
+LINK = {"fr3": "fr3_link8", "ur5e": "tool0", "husky_fr3": "fr3_link8", "xls_fr3": "fr3_link8",
+        "caster_fr3": "fr3_link8"}
 
 
 def make_manipulator(robot, device):
@@ -88,8 +89,10 @@ def task_jacobian(robot, om, q):
     spec = O.ROBOTS[robot]
     if spec["kind"] == 0:
         return J
-    S = R.selection_matrix(om.nv, spec["n_arm"], spec["n_wheel"], spec["joint_index"], spec["actuator_index"],
-                           spec["J_mobile"](), q[spec["joint_index"][0] + 2])
+    vs, ms, ws = spec["joint_index"]
+    Jm = spec["J_mobile"](q[ws:ws + spec["n_wheel"]]) if spec.get("drive") == 2 else spec["J_mobile"]()
+    S = R.selection_matrix(om.nv, spec["n_arm"], spec["n_wheel"], spec["joint_index"], spec["actuator_index"], Jm,
+                           q[vs + 2])
     return J @ S
 
 
@@ -178,6 +181,10 @@ def moma_kinematic_param(robot):
     MM = mobile_manipulator
     if robot == "husky_fr3":
         return MM.KinematicParam(MM.DriveType.Differential, 0.165, base_width=0.555)
+    if robot == "caster_fr3":
+        c = O.CASTER_FR3
+        return MM.KinematicParam(MM.DriveType.Caster, c["radius"], base2wheel_positions=c["positions"],
+                                 wheel_offset=c["offset"])
     return MM.KinematicParam(MM.DriveType.Mecanum, 0.120, roller_angles=[-np.pi / 4, np.pi / 4, np.pi / 4, -np.pi / 4],
                              base2wheel_positions=[(0.2225, 0.2045), (0.2225, -0.2045), (-0.2225, 0.2045),
                                                    (-0.2225, -0.2045)],

@@ -34,7 +34,7 @@ EXPECTED_OFF_CUBIC = {("fr3", "before"): 0, ("fr3", "inside"): 0, ("fr3", "at_en
 
 
 def _setup(cuda, robot, seed, B):
-    moma = robot in ("husky_fr3", "xls_fr3")
+    moma = robot in ("husky_fr3", "xls_fr3", "caster_fr3")
     rd = make_moma(robot, cuda) if moma else make_manipulator(robot, cuda)
     ctrl = (MM if moma else manipulator).RobotController(0.001, rd, solver_mode="exact")
     q, qd, xt, xdt = (moma_step_inputs if moma else step_inputs)(rd, robot, seed, B, cuda, stress=True)

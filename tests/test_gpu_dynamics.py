@@ -56,7 +56,7 @@ def test_manipulator_dynamics_match_oracle(cuda, robot):
         _check(dev, R.dynamics(pm, q[:, b], qd[:, b]), b)
 
 
-@pytest.mark.parametrize("robot", ["husky_fr3", "xls_fr3"])
+@pytest.mark.parametrize("robot", ["husky_fr3", "xls_fr3", "caster_fr3"])
 def test_moma_dynamics_match_oracle(cuda, robot):
     pm, _, spec = O.load(robot)
     rd = make_moma(robot, cuda)
@@ -67,8 +67,10 @@ def test_moma_dynamics_match_oracle(cuda, robot):
     full, act = _run(rd, q, qd), _run(rd, q, qd, actuated=True)
     for b in range(B):
         _check(full, R.dynamics(pm, q[:, b], qd[:, b]), b)
+        ws = spec["joint_index"][2]
+        Jm = spec["J_mobile"](q[ws:ws + spec["n_wheel"], b]) if spec.get("drive") == 2 else spec["J_mobile"]()
         S = R.selection_matrix(pm.nv, spec["n_arm"], spec["n_wheel"], spec["joint_index"], spec["actuator_index"],
-                               spec["J_mobile"](), q[spec["joint_index"][0] + 2, b])
+                               Jm, q[spec["joint_index"][0] + 2, b])
         _check(act, R.dynamics_actuated(pm, q[:, b], qd[:, b], S), b)
 
 

@@ -13,6 +13,8 @@ tags dropped) and three authored models the reference does not ship
                   with 3 virtual joints (x, y, yaw), SURVEY.md §7 step 0.
 * ``xls_fr3``   — 4-wheel mecanum base (Summit-XLS wheel geometry from
                   ``examples/C++/src/xls_controller.cpp:16-30``) + FR3.
+* ``caster_fr3`` — base on two powered casters (steer + drive joint each,
+                  DriveType::Caster, src/mobile/robot_data.cpp:179-204) + FR3.
 
 Joint naming of the mobile models is chosen so that the Pinocchio/urdfdom
 depth-first, name-sorted traversal yields [virtual(3) | arm(7) | wheels(W)],
@@ -228,7 +230,7 @@ def gen_ur5e():
 
 def gen_mobile(kind, links, joints, disabled):
     """Whole-body fixtures: world -x-> -y-> -yaw-> base_link; FR3 on top."""
-    name = "husky_fr3" if kind == "husky" else "xls_fr3"
+    name = {"husky": "husky_fr3", "xls": "xls_fr3", "caster": "caster_fr3"}[kind]
     d = os.path.join(OUT, name)
     os.makedirs(d, exist_ok=True)
     w = UrdfWriter(name)
@@ -245,6 +247,20 @@ def gen_mobile(kind, links, joints, disabled):
                   ("wheel_right_joint", "wheel_right_link", [0, -0.2775, 0.165])]
         wheel_r, wheel_w = 0.165, 0.11
         mount = [0.25, 0, 0.34]
+    elif kind == "caster":
+        # two powered casters at (0.25, 0.2) and (-0.25, -0.2): steer axis z at the
+        # position, wheel (r 0.08) trailing by the offset b = 0.05 along the steer
+        # direction (the contact point of CasterFKJacobian, robot_data.cpp:193-196)
+        base_cols = [([0, 0, 0.24], [0, 0, 0], ("box", [0.70, 0.52, 0.20]))]
+        w.link("base_link", (40.0, [0, 0, 0.24], [0.9, 0, 0, 1.7, 0, 2.4]), base_cols)
+        wheels = []
+        for i, (px, py) in enumerate([(0.25, 0.2), (-0.25, -0.2)]):
+            sl = "caster_%d_steer_link" % i
+            w.link(sl, (0.8, [0, 0, 0], [1e-3, 0, 0, 1e-3, 0, 1e-3]))
+            wheels.append(("wheel_c%d_0steer_joint" % i, sl, [px, py, 0.16], "steer"))
+            wheels.append(("wheel_c%d_1drive_joint" % i, "caster_%d_wheel_link" % i, [0.05, 0, -0.08], sl))
+        wheel_r, wheel_w = 0.08, 0.05
+        mount = [0.15, 0, 0.34]
     else:
         # Summit-XLS-like chassis, mecanum wheels at (+-0.2225, +-0.2045), r 0.12
         base_cols = [([0, 0, 0.25], [0, 0, 0], ("box", [0.62, 0.30, 0.22]))]
@@ -255,7 +271,13 @@ def gen_mobile(kind, links, joints, disabled):
                   ("wheel_rr_joint", "wheel_rr_link", [-0.2225, -0.2045, 0.12])]
         wheel_r, wheel_w = 0.12, 0.09
         mount = [0.18, 0, 0.36]
+    if kind == "caster":   # (joint, child, xyz, parent | "steer")
+        wheels, casters = [(jn, wl, xyz) for (jn, wl, xyz, _) in wheels], wheels
+    else:
+        casters = None
     for (_, wl, _) in wheels:
+        if casters and wl.endswith("steer_link"):
+            continue
         w.link(wl, (2.6, [0, 0, 0], cyl_inertia(2.6, wheel_r, wheel_w)),
                [([0, 0, 0], [0, 0, 0], ("cylinder", [wheel_r, wheel_w]))])
     emit_fr3_arm(w, links, joints, mount_parent="base_link", mount_xyz=mount, skip_base=True)
@@ -263,8 +285,16 @@ def gen_mobile(kind, links, joints, disabled):
     w.joint("virtual_1_y_joint", "prismatic", "virtual_x_link", "virtual_y_link", [0, 0, 0], [0, 0, 0], [0, 1, 0], (-big, big, 10.0, 1e4))
     w.joint("virtual_2_yaw_joint", "revolute", "virtual_y_link", "base_link", [0, 0, 0], [0, 0, 0], [0, 0, 1], (-big, big, 10.0, 1e4))
     # wheel joints: declared revolute, wheel axis = link z, rotated so z is lateral
-    for (jn, wl, xyz) in wheels:
-        w.joint(jn, "revolute", "base_link", wl, xyz, [-math.pi / 2, 0, 0], [0, 0, 1], (-big, big, 30.0, 100))
+    if casters:   # steer: base_link -> steer link about z; drive: steer link -> wheel about the lateral axis
+        for (jn, wl, xyz, par) in casters:
+            if par == "steer":
+                w.joint(jn, "revolute", "base_link", wl, xyz, [0, 0, 0], [0, 0, 1], (-big, big, 10.0, 100))
+            else:
+                w.joint(jn, "revolute", par, wl, xyz, [-math.pi / 2, 0, 0], [0, 0, 1], (-big, big, 30.0, 100))
+        wheels = [(jn, wl, xyz) for (jn, wl, xyz, par) in casters if par != "steer"]
+    else:
+        for (jn, wl, xyz) in wheels:
+            w.joint(jn, "revolute", "base_link", wl, xyz, [-math.pi / 2, 0, 0], [0, 0, 1], (-big, big, 30.0, 100))
     with open(os.path.join(d, name + ".urdf"), "w") as fh:
         fh.write(w.text())
     extra = [("base_link", "fr3_link0", "Adjacent"), ("base_link", "fr3_link1", "Never")]
@@ -284,6 +314,7 @@ def main():
     gen_ur5e()
     gen_mobile("husky", links, joints, disabled)
     gen_mobile("xls", links, joints, disabled)
+    gen_mobile("caster", links, joints, disabled)
     print("wrote", OUT)
 
 
