@@ -24,7 +24,9 @@
 #ifndef DRC_AMD_HPP
 #define DRC_AMD_HPP
 
+#include <algorithm>
 #include <array>
+#include <cmath>
 #include <cstdint>
 #include <iostream>
 #include <memory>
@@ -123,6 +125,34 @@ class ModelBase {
     s.pair = pair;
     return s;
   }
+  // joint-space dynamics at (q, qdot) (drc_dynamics_host): M, M^-1 row-major
+  // n x n, g, nle, c [n]; actuated: the S^T (.) S projections of a mobile
+  // manipulator (n = actuated dof)
+  struct Dyn {
+    Vec M, Minv, g, nle, c;
+  };
+  Dyn dynamics(const Vec& q, const Vec& qdot, bool actuated = false) const {
+    const int n = actuated ? act_ : dof_;
+    Dyn d;
+    d.M.assign(n * n, 0.0);
+    d.Minv.assign(n * n, 0.0);
+    d.g.assign(n, 0.0);
+    d.nle.assign(n, 0.0);
+    d.c.assign(n, 0.0);
+    check(drc_dynamics_host(model_, actuated ? 1 : 0, 1, q.data(), qdot.data(), d.M.data(), d.Minv.data(),
+                            d.g.data(), d.nle.data(), d.c.data()));
+    return d;
+  }
+  // updateDynamics' cached quantities at the stored state (robot_data.cpp:109-124)
+  const Dyn& stateDynamics(bool actuated = false) const {
+    Dyn& d = actuated ? dyn_act_ : dyn_;
+    bool& ok = actuated ? dyn_act_ok_ : dyn_ok_;
+    if (!ok) {
+      d = dynamics(q_, qdot_, actuated);
+      ok = true;
+    }
+    return d;
+  }
   // QPID stage outputs at (q, qdot): frame Jacobian time variation (6 x dof,
   // row-major) and the grad_dot vectors of getManipulability / getMinDistance
   struct QpidStages {
@@ -155,11 +185,61 @@ class ModelBase {
     q_.assign(dof_, 0.0);
     qdot_.assign(dof_, 0.0);
   }
+  void setState(const Vec& q, const Vec& qdot) {
+    q_ = q;
+    qdot_ = qdot;
+    dyn_ok_ = dyn_act_ok_ = false;
+  }
   drc_model* model_ = nullptr;
   int dof_ = 0, act_ = 0, mani_ = 0, mobi_ = 0;
   std::array<Vec, 4> lims_;
   Vec q_, qdot_;
+  mutable Dyn dyn_, dyn_act_;
+  mutable bool dyn_ok_ = false, dyn_act_ok_ = false;
 };
+
+inline MinDistResult minDist(const Vec& dist, const Vec& graddot, bool with_grad, bool with_graddot) {
+  MinDistResult r;
+  const size_t n = dist.size() - 1;
+  r.distance = dist[0];
+  r.grad = (with_grad || with_graddot) ? Vec(dist.begin() + 1, dist.end()) : Vec(n, 0.0);
+  r.grad_dot = with_graddot ? graddot : Vec(n, 0.0);
+  return r;
+}
+inline ManipulabilityResult manip(const Vec& man, const Vec& graddot, bool with_grad, bool with_graddot) {
+  ManipulabilityResult r;
+  const size_t n = man.size() - 1;
+  r.manipulability = man[0];
+  r.grad = (with_grad || with_graddot) ? Vec(man.begin() + 1, man.end()) : Vec(n, 0.0);
+  r.grad_dot = with_graddot ? graddot : Vec(n, 0.0);
+  return r;
+}
+inline Vec matvec(const Vec& A, const Vec& x, int rows) {  // A rows x x.size(), row-major
+  const int cols = static_cast<int>(x.size());
+  Vec y(rows, 0.0);
+  for (int r = 0; r < rows; ++r)
+    for (int c = 0; c < cols; ++c) y[r] += A[r * cols + c] * x[c];
+  return y;
+}
+// DyrosMath::cubicVector / cubicDotVector (math_type_define.h:62-143,179-229)
+inline Vec cubicVector(double t, double t0, double tf, const Vec& x0, const Vec& xf, const Vec& xd0, const Vec& xdf,
+                       bool dot) {
+  Vec out(x0.size());
+  for (size_t i = 0; i < x0.size(); ++i) {
+    if (t < t0) {
+      out[i] = dot ? xd0[i] : x0[i];
+      continue;
+    }
+    if (t > tf) {
+      out[i] = dot ? xdf[i] : xf[i];
+      continue;
+    }
+    const double e = t - t0, T = tf - t0, T2 = T * T, T3 = T2 * T, dx = xf[i] - x0[i];
+    const double a2 = 3 * dx / T2 - 2 * xd0[i] / T - xdf[i] / T, a3 = -2 * dx / T3 + (xd0[i] + xdf[i]) / T2;
+    out[i] = dot ? xd0[i] + 2 * a2 * e + 3 * a3 * e * e : x0[i] + xd0[i] * e + a2 * e * e + a3 * e * e * e;
+  }
+  return out;
+}
 
 namespace Manipulator {
 
@@ -173,9 +253,35 @@ class RobotData : public ModelBase {
   }
   bool updateState(const Vec& q, const Vec& qdot) {
     if (static_cast<int>(q.size()) != dof_ || static_cast<int>(qdot.size()) != dof_) return false;
-    q_ = q;
-    qdot_ = qdot;
+    setState(q, qdot);
     return true;
+  }
+  // getters of updateDynamics' quantities (robot_data.h:176-198), n x n row-major
+  Vec getMassMatrix() const { return stateDynamics().M; }
+  Vec getMassMatrixInv() const { return stateDynamics().Minv; }
+  Vec getGravity() const { return stateDynamics().g; }
+  Vec getCoriolis() const { return stateDynamics().c; }
+  Vec getNonlinearEffects() const { return stateDynamics().nle; }
+  // stateless variants (robot_data.h:70-144)
+  Vec computeMassMatrix(const Vec& q) const { return dynamics(q, Vec(dof_, 0.0)).M; }
+  Vec computeGravity(const Vec& q) const { return dynamics(q, Vec(dof_, 0.0)).g; }
+  Vec computeCoriolis(const Vec& q, const Vec& qdot) const { return dynamics(q, qdot).c; }
+  Vec computeNonlinearEffects(const Vec& q, const Vec& qdot) const { return dynamics(q, qdot).nle; }
+  Vec computeVelocity(const Vec& q, const Vec& qdot, const std::string& link) const {
+    return matvec(computeJacobian(q, link), qdot, 6);
+  }
+  MinDistResult computeMinDistance(const Vec& q, const Vec& qdot, bool with_grad, bool with_graddot,
+                                   bool verbose = false) const {
+    Stages s = stages(q, qdot, "");
+    MinDistResult r = minDist(s.dist, with_graddot ? qpidStages(q, qdot, "").dist_graddot : Vec(), with_grad,
+                              with_graddot);
+    if (verbose) std::cout << "min distance " << r.distance << " (pair " << s.pair << ")\n";
+    return r;
+  }
+  ManipulabilityResult computeManipulability(const Vec& q, const Vec& qdot, bool with_grad, bool with_graddot,
+                                             const std::string& link) const {
+    Stages s = stages(q, qdot, link);
+    return manip(s.man, with_graddot ? qpidStages(q, qdot, link).man_graddot : Vec(), with_grad, with_graddot);
   }
   Pose computePose(const Vec& q, const std::string& link) const {
     return pose44(stages(q, Vec(dof_, 0.0), link).pose.data());
@@ -213,9 +319,105 @@ class RobotData : public ModelBase {
   Vec computeJacobianTimeVariation(const Vec& q, const Vec& qdot, const std::string& link) const {
     return qpidStages(q, qdot, link).jdot;
   }
+
+ protected:
+  RobotData() = default;  // MobileManipulator::RobotData adopts its own model
 };
 
 }  // namespace Manipulator
+
+namespace Mobile {
+
+using KinematicParam = drc_kinematic_param;
+
+// Mobile::RobotData (include/dyros_robot_controller/mobile/robot_data.h,
+// src/mobile/robot_data.cpp): wheel state, FK Jacobian, base twist.  Host
+// arithmetic (a 3 x W matrix per call) through the C-ABI.
+class RobotData {
+ public:
+  explicit RobotData(const KinematicParam& param) : param_(param) {
+    Vec J(3 * DRC_MAX_WHEELS), w0(DRC_MAX_WHEELS, 0.0);
+    check(drc_mobile_fk_jacobian(&param_, w0.data(), J.data(), &wheel_num_));
+    wheel_pos_.assign(wheel_num_, 0.0);
+    wheel_vel_.assign(wheel_num_, 0.0);
+    J_mobile_.assign(J.begin(), J.begin() + 3 * wheel_num_);
+    base_vel_.assign(3, 0.0);
+  }
+  virtual ~RobotData() = default;
+  std::string getVerbose() const {
+    static const char* names[3] = {"Differential", "Mecanum", "Caster"};
+    return std::string("type ") + (param_.type >= 0 && param_.type < 3 ? names[param_.type] : "Unknown") +
+           ", wheel_num " + std::to_string(wheel_num_) + ", wheel_radius " + std::to_string(param_.wheel_radius);
+  }
+  bool updateState(const Vec& wheel_pos, const Vec& wheel_vel) {
+    if (static_cast<int>(wheel_pos.size()) != wheel_num_ || static_cast<int>(wheel_vel.size()) != wheel_num_)
+      return false;
+    wheel_pos_ = wheel_pos;
+    wheel_vel_ = wheel_vel;
+    J_mobile_ = computeFKJacobian(wheel_pos);
+    base_vel_ = matvec(J_mobile_, wheel_vel_, 3);
+    return true;
+  }
+  Vec computeBaseVel(const Vec& wheel_pos, const Vec& wheel_vel) const {
+    return matvec(computeFKJacobian(wheel_pos), wheel_vel, 3);
+  }
+  Vec computeFKJacobian(const Vec& wheel_pos) const {  // 3 x W row-major
+    if (static_cast<int>(wheel_pos.size()) != wheel_num_) throw std::runtime_error("wheel_pos must be of size wheel_num.");
+    Vec J(3 * DRC_MAX_WHEELS);
+    int W = 0;
+    check(drc_mobile_fk_jacobian(&param_, wheel_pos.data(), J.data(), &W));
+    return Vec(J.begin(), J.begin() + 3 * W);
+  }
+  int getWheelNum() const { return wheel_num_; }
+  const KinematicParam& getKineParam() const { return param_; }
+  const Vec& getWheelPosition() const { return wheel_pos_; }
+  const Vec& getWheelVelocity() const { return wheel_vel_; }
+  const Vec& getBaseVel() const { return base_vel_; }
+  const Vec& getFKJacobian() const { return J_mobile_; }
+
+ protected:
+  KinematicParam param_;
+  int wheel_num_ = 0;
+  Vec wheel_pos_, wheel_vel_, J_mobile_, base_vel_;
+};
+
+// Mobile::RobotController (src/mobile/robot_controller.cpp): wheel IK and
+// base-velocity saturation.
+class RobotController {
+ public:
+  RobotController(double dt, std::shared_ptr<RobotData> robot_data) : dt_(dt), robot_data_(std::move(robot_data)) {}
+  Vec computeIKJacobian() const {  // W x 3 row-major (:55-125)
+    const Vec& wp = robot_data_->getWheelPosition();
+    Vec J(DRC_MAX_WHEELS * 3);
+    int W = 0;
+    check(drc_mobile_ik_jacobian(&robot_data_->getKineParam(), wp.data(), J.data(), &W));
+    return Vec(J.begin(), J.begin() + 3 * W);
+  }
+  Vec computeWheelVel(const Vec& base_vel) const {  // (:48-52)
+    if (base_vel.size() != 3) throw std::runtime_error("base_vel must be of size 3.");
+    return matvec(computeIKJacobian(), base_vel, robot_data_->getWheelNum());
+  }
+  // VelocityCommand (:18-46): speed and yaw-rate saturation, then wheel IK
+  Vec VelocityCommand(const Vec& desired_base_vel) const {
+    if (desired_base_vel.size() != 3) throw std::runtime_error("desired_base_vel must be of size 3.");
+    const KinematicParam& p = robot_data_->getKineParam();
+    double vx = desired_base_vel[0], vy = desired_base_vel[1];
+    double speed = std::sqrt(vx * vx + vy * vy), dx = 0, dy = 0;
+    if (std::fabs(speed) >= 1e-4) {
+      dx = vx / speed;
+      dy = vy / speed;
+    }
+    speed = std::min(std::max(speed, -p.max_lin_speed), p.max_lin_speed);
+    const double w = std::min(std::max(desired_base_vel[2], -p.max_ang_speed), p.max_ang_speed);
+    return computeWheelVel({dx * speed, dy * speed, w});
+  }
+
+ private:
+  double dt_;
+  std::shared_ptr<RobotData> robot_data_;
+};
+
+}  // namespace Mobile
 
 // Shared by both controllers: gains, solver mode, batched entries.
 class ControllerBase {
@@ -338,7 +540,51 @@ namespace Manipulator {
 class RobotController : public ControllerBase {
  public:
   RobotController(double dt, std::shared_ptr<RobotData> robot_data)
-      : ControllerBase(dt, robot_data.get()), robot_data_(std::move(robot_data)) {}
+      : ControllerBase(dt, robot_data.get()), robot_data_(std::move(robot_data)),
+        Kp_joint_(robot_data_->getDof(), 400.0), Kv_joint_(robot_data_->getDof(), 40.0) {}
+  // joint-space gains and helpers (robot_controller.cpp:21-155)
+  void setJointGain(const Vec& Kp, const Vec& Kv) {
+    if (Kp.size() != Kp_joint_.size() || Kv.size() != Kv_joint_.size())
+      throw std::runtime_error("Kp and Kv must be of size dof_.");
+    Kp_joint_ = Kp;
+    Kv_joint_ = Kv;
+  }
+  void setJointKpGain(const Vec& Kp) {
+    if (Kp.size() != Kp_joint_.size()) throw std::runtime_error("Kp must be of size dof_.");
+    Kp_joint_ = Kp;
+  }
+  void setJointKvGain(const Vec& Kv) {
+    if (Kv.size() != Kv_joint_.size()) throw std::runtime_error("Kv must be of size dof_.");
+    Kv_joint_ = Kv;
+  }
+  Vec moveJointPositionCubic(const Vec& q_target, const Vec& qdot_target, const Vec& q_init, const Vec& qdot_init,
+                             double current_time, double init_time, double duration) const {
+    return cubicVector(current_time, init_time, init_time + duration, q_init, q_target, qdot_init, qdot_target, false);
+  }
+  Vec moveJointVelocityCubic(const Vec& q_target, const Vec& qdot_target, const Vec& q_init, const Vec& qdot_init,
+                             double current_time, double init_time, double duration) const {
+    return cubicVector(current_time, init_time, init_time + duration, q_init, q_target, qdot_init, qdot_target, true);
+  }
+  // M qddot + g with the cached M, g of the stored state (robot_controller.cpp:115-118)
+  Vec moveJointTorqueStep(const Vec& qddot_target) const {
+    const int n = robot_data_->getDof();
+    Vec tau = matvec(robot_data_->getMassMatrix(), qddot_target, n), g = robot_data_->getGravity();
+    for (int i = 0; i < n; ++i) tau[i] += g[i];
+    return tau;
+  }
+  Vec moveJointTorqueStep(const Vec& q_target, const Vec& qdot_target) const {  // (:120-125)
+    const Vec &q = robot_data_->getJointPosition(), &qd = robot_data_->getJointVelocity();
+    Vec qdd(q.size());
+    for (size_t i = 0; i < q.size(); ++i)
+      qdd[i] = Kp_joint_[i] * (q_target[i] - q[i]) + Kv_joint_[i] * (qdot_target[i] - qd[i]);
+    return moveJointTorqueStep(qdd);
+  }
+  Vec moveJointTorqueCubic(const Vec& q_target, const Vec& qdot_target, const Vec& q_init, const Vec& qdot_init,
+                           double current_time, double init_time, double duration) const {
+    return moveJointTorqueStep(
+        moveJointPositionCubic(q_target, qdot_target, q_init, qdot_init, current_time, init_time, duration),
+        moveJointVelocityCubic(q_target, qdot_target, q_init, qdot_init, current_time, init_time, duration));
+  }
   Vec QPIK(const Vec& xdot_target, const std::string& link) const {
     check6(xdot_target);
     return solveOne(DRC_MODE_QPIK, nullptr, &xdot_target, nullptr, nullptr, 0, 0, 1, link);
@@ -443,6 +689,7 @@ class RobotController : public ControllerBase {
     return out;
   }
   std::shared_ptr<RobotData> robot_data_;
+  Vec Kp_joint_, Kv_joint_;
 };
 
 }  // namespace Manipulator
@@ -453,11 +700,14 @@ using KinematicParam = drc_kinematic_param;
 using JointIndex = drc_joint_index;
 using ActuatorIndex = drc_actuator_index;
 
-class RobotData : public ModelBase {
+// MobileManipulator::RobotData (mobile_manipulator/robot_data.h:42): a
+// Manipulator::RobotData over the whole-body model and a Mobile::RobotData of
+// the base, as the reference's multiple inheritance.
+class RobotData : public Manipulator::RobotData, public Mobile::RobotData {
  public:
   RobotData(const KinematicParam& param, const JointIndex& joint_idx, const ActuatorIndex& actuator_idx,
             const std::string& urdf, const std::string& srdf = "", const std::string& packages = "", int device = 0)
-      : jidx_(joint_idx), aidx_(actuator_idx) {
+      : Mobile::RobotData(param), jidx_(joint_idx), aidx_(actuator_idx) {
     drc_model* m = nullptr;
     check(drc_model_create_mobile_manipulator(&param, &joint_idx, &actuator_idx, urdf.c_str(), srdf.c_str(),
                                               packages.c_str(), device, &m));
@@ -471,45 +721,117 @@ class RobotData : public ModelBase {
     for (size_t i = 0; i < v_mani.size(); ++i) v[jidx_.mani_start + i] = v_mani[i];
     return v;
   }
+  // getActuatorVector (:429-437)
+  Vec actuatorVector(const Vec& v_mobile, const Vec& v_mani) const {
+    Vec v(act_, 0.0);
+    for (size_t i = 0; i < v_mobile.size(); ++i) v[aidx_.mobi_start + i] = v_mobile[i];
+    for (size_t i = 0; i < v_mani.size(); ++i) v[aidx_.mani_start + i] = v_mani[i];
+    return v;
+  }
   bool updateState(const Vec& q_virtual, const Vec& q_mobile, const Vec& q_mani, const Vec& qdot_virtual,
                    const Vec& qdot_mobile, const Vec& qdot_mani) {
     if (q_virtual.size() != 3 || static_cast<int>(q_mobile.size()) != mobi_ ||
         static_cast<int>(q_mani.size()) != mani_)
       return false;
-    q_ = jointVector(q_virtual, q_mobile, q_mani);
-    qdot_ = jointVector(qdot_virtual, qdot_mobile, qdot_mani);
+    setState(jointVector(q_virtual, q_mobile, q_mani), jointVector(qdot_virtual, qdot_mobile, qdot_mani));
+    Mobile::RobotData::updateState(q_mobile, qdot_mobile);
     return true;
   }
   int getManipulatorDof() const { return mani_; }
   int getMobileDof() const { return mobi_; }
+  int getActuatordDof() const { return act_; }  // (sic) mobile_manipulator/robot_data.h:359
   const JointIndex& getJointIndex() const { return jidx_; }
   const ActuatorIndex& getActuatorIndex() const { return aidx_; }
-  Vec getMobileFKJacobian() const {  // 3 x W row-major
-    Vec J(3 * mobi_);
-    check(drc_model_mobile_fk_jacobian(model_, J.data()));
-    return J;
+  Vec block(const Vec& v, int start, int n) const { return Vec(v.begin() + start, v.begin() + start + n); }
+  Vec getVirtualJointPosition() const { return block(q_, jidx_.virtual_start, 3); }
+  Vec getMobileJointPosition() const { return block(q_, jidx_.mobi_start, mobi_); }
+  Vec getManiJointPosition() const { return block(q_, jidx_.mani_start, mani_); }
+  Vec getVirtualJointVelocity() const { return block(qdot_, jidx_.virtual_start, 3); }
+  Vec getMobileJointVelocity() const { return block(qdot_, jidx_.mobi_start, mobi_); }
+  Vec getManiJointVelocity() const { return block(qdot_, jidx_.mani_start, mani_); }
+  Vec getJointPositionActuated() const { return actuatorVector(getMobileJointPosition(), getManiJointPosition()); }
+  Vec getJointVelocityActuated() const { return actuatorVector(getMobileJointVelocity(), getManiJointVelocity()); }
+  // mobile base (:344-357): J_mobile at the wheel positions and the base twist
+  Vec computeMobileFKJacobian(const Vec& q_mobile) const { return computeFKJacobian(q_mobile); }
+  Vec computeMobileBaseVel(const Vec& q_mobile, const Vec& qdot_mobile) const {
+    return computeBaseVel(q_mobile, qdot_mobile);
   }
-  Pose getPose(const std::string& link) const { return pose44(stages(q_, qdot_, link).pose.data()); }
-  Vec getJacobian(const std::string& link) const { return stages(q_, qdot_, link).jac; }
-  MinDistResult getMinDistance(bool with_grad, bool with_graddot, bool verbose = false) const {
-    Stages s = stages(q_, qdot_, "");
-    MinDistResult r;
-    r.distance = s.dist[0];
-    r.grad = (with_grad || with_graddot) ? Vec(s.dist.begin() + 1, s.dist.end()) : Vec(dof_, 0.0);
-    r.grad_dot = with_graddot ? qpidStages(q_, qdot_, "").dist_graddot : Vec(dof_, 0.0);
-    if (verbose) std::cout << "min distance " << r.distance << " (pair " << s.pair << ")\n";
-    return r;
+  Vec getMobileFKJacobian() const { return computeFKJacobian(getMobileJointPosition()); }
+  Vec getMobileBaseVel() const { return computeBaseVel(getMobileJointPosition(), getMobileJointVelocity()); }
+  // selection matrix S (dof x A, row-major; :22-25,115-120,367-387)
+  Vec computeSelectionMatrix(const Vec& q_virtual, const Vec& q_mobile) const {
+    Vec S(dof_ * act_, 0.0), Jm = computeFKJacobian(q_mobile);
+    for (int i = 0; i < mani_; ++i) S[(jidx_.mani_start + i) * act_ + aidx_.mani_start + i] = 1;
+    for (int i = 0; i < mobi_; ++i) S[(jidx_.mobi_start + i) * act_ + aidx_.mobi_start + i] = 1;
+    const double cy = std::cos(q_virtual.at(2)), sy = std::sin(q_virtual.at(2));
+    const double Rz[3][3] = {{cy, -sy, 0}, {sy, cy, 0}, {0, 0, 1}};
+    for (int r = 0; r < 3; ++r)
+      for (int w = 0; w < mobi_; ++w) {
+        double t = 0;
+        for (int k = 0; k < 3; ++k) t += Rz[r][k] * Jm[k * mobi_ + w];
+        S[(jidx_.virtual_start + r) * act_ + aidx_.mobi_start + w] = t;
+      }
+    return S;
   }
-  // arm-block manipulability (robot_data.cpp:439-496)
-  ManipulabilityResult getManipulability(bool with_grad, bool with_graddot, const std::string& link) const {
-    Stages s = stages(q_, qdot_, link);
-    ManipulabilityResult r;
-    r.manipulability = s.man[0];
-    r.grad = (with_grad || with_graddot) ? Vec(s.man.begin() + 1, s.man.end()) : Vec(mani_, 0.0);
-    r.grad_dot = with_graddot ? qpidStages(q_, qdot_, link).man_graddot : Vec(mani_, 0.0);
-    return r;
+  Vec getSelectionMatrix() const { return computeSelectionMatrix(getVirtualJointPosition(), getMobileJointPosition()); }
+  // J S (6 x A row-major; :389-415, Sdot neglected as the reference)
+  Vec times(const Vec& J, const Vec& S) const {
+    Vec out(6 * act_, 0.0);
+    for (int r = 0; r < 6; ++r)
+      for (int k = 0; k < dof_; ++k)
+        for (int a = 0; a < act_; ++a) out[r * act_ + a] += J[r * dof_ + k] * S[k * act_ + a];
+    return out;
   }
-  Vec getJacobianTimeVariation(const std::string& link) const { return qpidStages(q_, qdot_, link).jdot; }
+  Vec computeJacobianActuated(const Vec& q_virtual, const Vec& q_mobile, const Vec& q_mani,
+                              const std::string& link) const {
+    return times(computeJacobian(jointVector(q_virtual, q_mobile, q_mani), link),
+                 computeSelectionMatrix(q_virtual, q_mobile));
+  }
+  Vec computeJacobianTimeVariationActuated(const Vec& q_virtual, const Vec& q_mobile, const Vec& q_mani,
+                                           const Vec& qdot_virtual, const Vec& qdot_mobile, const Vec& qdot_mani,
+                                           const std::string& link) const {
+    return times(computeJacobianTimeVariation(jointVector(q_virtual, q_mobile, q_mani),
+                                              jointVector(qdot_virtual, qdot_mobile, qdot_mani), link),
+                 computeSelectionMatrix(q_virtual, q_mobile));
+  }
+  Vec getJacobianActuated(const std::string& link) const { return times(getJacobian(link), getSelectionMatrix()); }
+  Vec getJacobianActuatedTimeVariation(const std::string& link) const {
+    return times(getJacobianTimeVariation(link), getSelectionMatrix());
+  }
+  // actuated dynamics (:126-144 cached, :187-227 stateless); M n x n row-major
+  Vec getMassMatrixActuated() const { return stateDynamics(true).M; }
+  Vec getMassMatrixActuatedInv() const { return stateDynamics(true).Minv; }
+  Vec getGravityActuated() const { return stateDynamics(true).g; }
+  Vec getCoriolisActuated() const { return stateDynamics(true).c; }
+  Vec getNonlinearEffectsActuated() const { return stateDynamics(true).nle; }
+  // the actuated velocities (qdot_mobile, qdot_mani) map to joints by S (virtual rows = Rz J_mobile)
+  Vec actuatedJointVelocity(const Vec& q_virtual, const Vec& q_mobile, const Vec& qdot_mobile,
+                            const Vec& qdot_mani) const {
+    return matvec(computeSelectionMatrix(q_virtual, q_mobile), actuatorVector(qdot_mobile, qdot_mani), dof_);
+  }
+  Vec computeMassMatrixActuated(const Vec& q_virtual, const Vec& q_mobile, const Vec& q_mani) const {
+    return dynamics(jointVector(q_virtual, q_mobile, q_mani), Vec(dof_, 0.0), true).M;
+  }
+  Vec computeGravityActuated(const Vec& q_virtual, const Vec& q_mobile, const Vec& q_mani) const {
+    return dynamics(jointVector(q_virtual, q_mobile, q_mani), Vec(dof_, 0.0), true).g;
+  }
+  Vec computeCoriolisActuated(const Vec& q_virtual, const Vec& q_mobile, const Vec& q_mani, const Vec& qdot_mobile,
+                              const Vec& qdot_mani) const {
+    return dynamics(jointVector(q_virtual, q_mobile, q_mani),
+                    actuatedJointVelocity(q_virtual, q_mobile, qdot_mobile, qdot_mani), true).c;
+  }
+  Vec computeNonlinearEffectsActuated(const Vec& q_virtual, const Vec& q_mobile, const Vec& q_mani,
+                                      const Vec& qdot_mobile, const Vec& qdot_mani) const {
+    return dynamics(jointVector(q_virtual, q_mobile, q_mani),
+                    actuatedJointVelocity(q_virtual, q_mobile, qdot_mobile, qdot_mani), true).nle;
+  }
+  // whole-body task space with the joint blocks (:229-286)
+  ManipulabilityResult computeManipulability(const Vec& q_mani, const Vec& qdot_mani, bool with_grad,
+                                             bool with_graddot, const std::string& link) const {
+    return Manipulator::RobotData::computeManipulability(jointVector(Vec(3, 0.0), Vec(mobi_, 0.0), q_mani),
+                                                         jointVector(Vec(3, 0.0), Vec(mobi_, 0.0), qdot_mani),
+                                                         with_grad, with_graddot, link);
+  }
 
  private:
   JointIndex jidx_;
@@ -519,7 +841,56 @@ class RobotData : public ModelBase {
 class RobotController : public ControllerBase {
  public:
   RobotController(double dt, std::shared_ptr<RobotData> robot_data)
-      : ControllerBase(dt, robot_data.get()), robot_data_(std::move(robot_data)) {}
+      : ControllerBase(dt, static_cast<const Manipulator::RobotData*>(robot_data.get())),
+        robot_data_(std::move(robot_data)), Kp_mani_joint_(robot_data_->getManipulatorDof(), 400.0),
+        Kv_mani_joint_(robot_data_->getManipulatorDof(), 40.0) {}
+  // arm joint-space gains and helpers (mobile_manipulator/robot_controller.cpp:24-145)
+  void setManipulatorJointGain(const Vec& Kp, const Vec& Kv) {
+    if (Kp.size() != Kp_mani_joint_.size() || Kv.size() != Kv_mani_joint_.size())
+      throw std::runtime_error("Kp and Kv must be of size mani_dof_.");
+    Kp_mani_joint_ = Kp;
+    Kv_mani_joint_ = Kv;
+  }
+  void setManipulatorJointKpGain(const Vec& Kp) {
+    if (Kp.size() != Kp_mani_joint_.size()) throw std::runtime_error("Kp must be of size mani_dof_.");
+    Kp_mani_joint_ = Kp;
+  }
+  void setManipulatorJointKvGain(const Vec& Kv) {
+    if (Kv.size() != Kv_mani_joint_.size()) throw std::runtime_error("Kv must be of size mani_dof_.");
+    Kv_mani_joint_ = Kv;
+  }
+  Vec moveManipulatorJointPositionCubic(const Vec& q_target, const Vec& qdot_target, const Vec& q_init,
+                                        const Vec& qdot_init, double current_time, double init_time,
+                                        double duration) const {
+    return cubicVector(current_time, init_time, init_time + duration, q_init, q_target, qdot_init, qdot_target, false);
+  }
+  // arm block of M qddot + g at the stored state (:96-104)
+  Vec moveManipulatorJointTorqueStep(const Vec& qddot_mani_target) const {
+    const int n = robot_data_->getManipulatorDof(), D = robot_data_->getDof();
+    const int s0 = robot_data_->getJointIndex().mani_start;
+    const Vec &M = robot_data_->getMassMatrix(), &g = robot_data_->getGravity();
+    Vec tau(n, 0.0);
+    for (int i = 0; i < n; ++i) {
+      tau[i] = g[s0 + i];
+      for (int j = 0; j < n; ++j) tau[i] += M[(s0 + i) * D + s0 + j] * qddot_mani_target[j];
+    }
+    return tau;
+  }
+  Vec moveManipulatorJointTorqueStep(const Vec& q_mani_target, const Vec& qdot_mani_target) const {  // (:106-114)
+    const Vec q = robot_data_->getManiJointPosition(), qd = robot_data_->getManiJointVelocity();
+    Vec qdd(q.size());
+    for (size_t i = 0; i < q.size(); ++i)
+      qdd[i] = Kp_mani_joint_[i] * (q_mani_target[i] - q[i]) + Kv_mani_joint_[i] * (qdot_mani_target[i] - qd[i]);
+    return moveManipulatorJointTorqueStep(qdd);
+  }
+  Vec moveManipulatorJointTorqueCubic(const Vec& q_target, const Vec& qdot_target, const Vec& q_init,
+                                      const Vec& qdot_init, double current_time, double init_time,
+                                      double duration) const {
+    const double tf = init_time + duration;
+    return moveManipulatorJointTorqueStep(
+        cubicVector(current_time, init_time, tf, q_init, q_target, qdot_init, qdot_target, false),
+        cubicVector(current_time, init_time, tf, q_init, q_target, qdot_init, qdot_target, true));
+  }
   // (qdot_mobile, qdot_mani) split by ActuatorIndex (robot_controller.cpp:182-196)
   void QPIK(const Vec& xdot_target, const std::string& link, Vec& qdot_mobile, Vec& qdot_mani) const {
     check6(xdot_target);
@@ -579,6 +950,7 @@ class RobotController : public ControllerBase {
     qdot_mani.assign(eta.begin() + a.mani_start, eta.begin() + a.mani_start + n);
   }
   std::shared_ptr<RobotData> robot_data_;
+  Vec Kp_mani_joint_, Kv_mani_joint_;
 };
 
 }  // namespace MobileManipulator

@@ -195,3 +195,93 @@ def test_module_clik_osf(cuda):
         np.testing.assert_allclose(rc.OSFStep(T, xdt[:, b], nu, "fr3_link8"),
                                    O.osf_one(om, par, q[:, b], qd[:, b], d["Minv"], d["g"], xt[:, b], xdt[:, b],
                                              null_torque=nu), rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_module_dynamics_and_task_getters(cuda):
+    """The getters/compute* the reference's drc layer calls, through the
+    module, against the numpy restatement (robot_data.h:70-198)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    import pyref as R
+    drc = _module()
+    robot = "fr3"
+    pm, om, spec = O.load(robot)
+    rd = drc.ManipulatorRobotData(os.path.join(ROOT, "dyros_robot_controller_amd", "robots", "fr3", "fr3.urdf"),
+                                  os.path.join(ROOT, "dyros_robot_controller_amd", "robots", "fr3", "fr3.srdf"), "")
+    rng = np.random.default_rng(4)
+    lo, hi = np.array(pm.lower), np.array(pm.upper)
+    q, qd = rng.uniform(lo + 0.1, hi - 0.1), rng.uniform(-0.5, 0.5, 7)
+    assert rd.updateState(q, qd)
+    dyn = R.dynamics(pm, q, qd)
+    np.testing.assert_allclose(rd.getMassMatrix(), dyn["M"], atol=1e-10)
+    np.testing.assert_allclose(rd.computeMassMatrix(q), dyn["M"], atol=1e-10)
+    np.testing.assert_allclose(rd.getGravity(), dyn["g"], atol=1e-10)
+    np.testing.assert_allclose(rd.getNonlinearEffects(), dyn["nle"], atol=1e-10)
+    np.testing.assert_allclose(rd.getCoriolis(), dyn["nle"] - dyn["g"], atol=1e-10)
+    np.testing.assert_allclose(rd.getMassMatrixInv() @ rd.getMassMatrix(), np.eye(7), atol=1e-8)
+    J = rd.getJacobian("fr3_link8")
+    np.testing.assert_allclose(rd.computeVelocity(q, qd, "fr3_link8"), J @ qd, atol=1e-12)
+    d, dg, _ = O.min_distance(om, q)
+    r = rd.computeMinDistance(q, qd, True, False)
+    assert abs(r.distance - d) <= 1e-9
+    m, mg = O.manipulability(om, q)
+    r = rd.computeManipulability(q, qd, True, False, "fr3_link8")
+    assert abs(r.manipulability - m) <= 1e-10
+    ctrl = drc.ManipulatorRobotController(0.001, rd)
+    qdd = rng.normal(size=7)
+    np.testing.assert_allclose(ctrl.moveJointTorqueStep(qdd), dyn["M"] @ qdd + dyn["g"], atol=1e-9)
+    qt, qdt = q + 0.01, qd * 0.5
+    np.testing.assert_allclose(ctrl.moveJointTorqueStep(qt, qdt),
+                               dyn["M"] @ (400 * (qt - q) + 40 * (qdt - qd)) + dyn["g"], atol=1e-8)
+    # cubic helpers at the ends of the profile
+    np.testing.assert_allclose(ctrl.moveJointPositionCubic(qt, qdt, q, qd, 2.0, 0.0, 1.0), qt)
+    np.testing.assert_allclose(ctrl.moveJointVelocityCubic(qt, qdt, q, qd, -1.0, 0.0, 1.0), qd)
+
+
+@pytest.mark.gpu
+def test_module_moma_getters(cuda):
+    """MobileManipulatorRobotData's actuated quantities (robot_data.cpp:107-144,
+    367-415) through the module: S, J S, S^T M S, base FK, caster base."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    import pyref as R
+    drc = _module()
+    robot = "caster_fr3"
+    pm, om, spec = O.load(robot)
+    c = O.CASTER_FR3
+    kp = drc.KinematicParam()
+    kp.type = drc.DriveType.Caster
+    kp.wheel_radius, kp.wheel_offset = c["radius"], c["offset"]
+    kp.base2wheel_positions = [list(p) for p in c["positions"]]
+    ji, ai = drc.JointIndex(), drc.ActuatorIndex()
+    ji.virtual_start, ji.mani_start, ji.mobi_start = spec["joint_index"]
+    ai.mani_start, ai.mobi_start = spec["actuator_index"]
+    base = os.path.join(ROOT, "dyros_robot_controller_amd", "robots", robot)
+    rd = drc.MobileManipulatorRobotData(kp, ji, ai, os.path.join(base, robot + ".urdf"),
+                                        os.path.join(base, robot + ".srdf"), "")
+    rng = np.random.default_rng(9)
+    qv, qm = np.array([0.3, -0.2, 0.7]), rng.uniform(-np.pi, np.pi, 4)
+    lo, hi = np.array(pm.lower)[3:10], np.array(pm.upper)[3:10]
+    qa = rng.uniform(lo + 0.1, hi - 0.1)
+    dv, dm, da = rng.normal(size=3) * 0.1, rng.normal(size=4), rng.normal(size=7) * 0.2
+    assert rd.updateState(qv, qm, qa, dv, dm, da)
+    q = np.concatenate([qv, qa, qm])
+    qdot = np.concatenate([dv, da, dm])
+    Jm = spec["J_mobile"](qm)
+    np.testing.assert_allclose(rd.getMobileFKJacobian(), Jm, atol=1e-12)
+    np.testing.assert_allclose(rd.getMobileBaseVel(), Jm @ dm, atol=1e-12)
+    S = R.selection_matrix(om.nv, 7, 4, spec["joint_index"], spec["actuator_index"], Jm, qv[2])
+    np.testing.assert_allclose(rd.getSelectionMatrix(), S, atol=1e-12)
+    np.testing.assert_allclose(rd.getJacobianActuated("fr3_link8"), rd.getJacobian("fr3_link8") @ S, atol=1e-12)
+    dyn = R.dynamics(pm, q, qdot)
+    np.testing.assert_allclose(rd.getMassMatrix(), dyn["M"], atol=1e-9)
+    np.testing.assert_allclose(rd.getMassMatrixActuated(), S.T @ dyn["M"] @ S, atol=1e-9)
+    np.testing.assert_allclose(rd.getGravityActuated(), S.T @ dyn["g"], atol=1e-9)
+    np.testing.assert_allclose(rd.computeMassMatrixActuated(qv, qm, qa), S.T @ dyn["M"] @ S, atol=1e-9)
+    np.testing.assert_allclose(rd.getManiJointPosition(), qa)
+    np.testing.assert_allclose(rd.getJointPositionActuated(), np.concatenate([qa, qm]))
+    ctrl = drc.MobileManipulatorRobotController(0.001, rd)
+    qdd = rng.normal(size=7)
+    np.testing.assert_allclose(ctrl.moveManipulatorJointTorqueStep(qdd),
+                               dyn["M"][3:10, 3:10] @ qdd + dyn["g"][3:10], atol=1e-9)
