@@ -1,14 +1,22 @@
 #!/usr/bin/env python3
-"""Headline benchmark: batched QP-IK solves/s (FR3 7-DoF QPIKStep, 65 536
-instances per GPU) + achieved HBM GB/s vs peak (BASELINE.json "metric").
+"""Headline benchmark: batched QP-IK solves/s + achieved HBM GB/s vs peak
+(BASELINE.json "metric"), on the configurations BASELINE.json names:
 
-One "step" = one control cycle of the whole batch through the product path
-(drc_qpik_batch: task-space kernel + QP kernel), inputs resident in HBM.
-Multi-GPU: one process per GPU (torchrun), instances sharded across ranks
-with no data-path collective (weak scaling: 65 536 per GPU); a barrier and a
-max-reduction of the timed region are the only collectives.
+  default       FR3 7-DoF QPIKStep, 65 536 instances per GPU (the metric's config)
+  --robot ur5e                     UR5e 6-DoF, 65 536 per GPU (HBM-roofline / counter run)
+  --robot husky_fr3 --batch 16384  Husky-FR3 whole-body QPIKStep
+  --robot xls_fr3 --global-batch 524288   XLS-FR3 whole-body, fixed global batch over N GPUs
+  (also caster_fr3)
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--robot fr3]
+One "step" = one control cycle of the batch through the product path
+(drc_qpik_batch: task-space kernel + QP kernel), inputs resident in HBM,
+SURVEY §8d's workload including the three 10 % stress tiers.  Multi-GPU: one
+process per GPU (torchrun), instances sharded as contiguous ranges with no
+data-path collective; weak scaling by default (--batch per GPU), strong
+scaling with --global-batch.  A barrier and a max-reduction of the timed
+region are the only collectives.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--robot fr3] [--batch B | --global-batch G]
 """
 import argparse
 import json
@@ -23,72 +31,90 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 FP64_VECTOR_PEAK_TFS = 78.6    # AMD spec, FP64 vector
-LINKS = {"fr3": "fr3_link8", "ur5e": "tool0"}
+DEFAULT_BATCH = {"fr3": 65536, "ur5e": 65536, "husky_fr3": 16384, "xls_fr3": 65536, "caster_fr3": 65536}
+METRIC = "QP-IK solves/s (FR3 7-DoF, batch 65k) + achieved HBM GB/s vs peak"
 
 
-def algorithmic_bytes(nv):
-    """per solve, HBM in (q, qdot [nv], x_target [12], xdot_target [6])
-    + out (qdot* [nv] f64, status i32).  FR3: 256 + 60 = 316 B."""
-    return (2 * nv + 12 + 6) * 8 + nv * 8 + 4
+def algorithmic_bytes(dof, actuated):
+    """per solve, HBM in (q, qdot [dof], x_target [12],
+    xdot_target [6]) + out (qdot* [actuated] f64, status i32).
+    FR3 316 B, UR5e 292 B, Husky-FR3 412 B, XLS-FR3 460 B."""
+    return (2 * dof + 12 + 6) * 8 + actuated * 8 + 4
 
 
-def flops_per_solve(nv, iters):
-    """SURVEY §8(d) static estimate for FR3-sized problems: 52k setup +
-    1.3k per ADMM iteration (reported as an estimate, not measured)."""
+def flops_per_solve(iters):
+    """SURVEY §8(d) static estimate for FR3-sized problems (52k setup +
+    1.3k per ADMM iteration); the counter-based figure is roofline.fp64_valu."""
     return 52e3 + 1.3e3 * iters
 
 
 def make_inputs(rd, robot, B, seed, offset, dev):
-    import torch
-    from dyros_robot_controller_amd import _batch, _capi, manipulator, workload
-    lo, hi = rd.getJointPositionLimit()
-    _, vmax = rd.getJointVelocityLimit()
-    q, qd = workload.joint_states(lo, hi, vmax, seed, B, offset)
-    # SURVEY §8d stress tiers (10 % each: joint limit, near-singular, CBF-active
-    # self-collision), judged by the product's own stage kernel
-    workload.apply_stress(q, lo, hi, list(range(len(lo))), seed, offset,
-                          workload.device_evaluator(rd.model, LINKS[robot], dev))
-    pb = manipulator.QPIKParamsBuilder(rd.model, exact=True)
-    p = pb.params(LINKS[robot], _capi.MODE_QPIK)
+    """States (with the stress tiers, judged by the product's stage kernel) and
+    targets near the current pose, [field][B] numpy + device copies."""
+    from dyros_robot_controller_amd import BUNDLED, _batch, _capi, manipulator, workload
+    spec = BUNDLED[robot]
+    link = spec["link"]
+    ev = workload.device_evaluator(rd.model, link, dev)
+    if spec["kind"] == "manipulator":
+        lo, hi = rd.getJointPositionLimit()
+        _, vmax = rd.getJointVelocityLimit()
+        q, qd = workload.joint_states(lo, hi, vmax, seed, B, offset)
+        arm = list(range(len(lo)))
+    else:
+        lo, hi = rd.get_joint_position_limit()
+        _, vmax = rd.get_joint_velocity_limit()
+        ji = rd.get_joint_index()
+        q, qd = workload.mobile_states(lo, hi, vmax, (ji.virtual_start, ji.mani_start, ji.mobi_start),
+                                       rd.get_manipulator_dof(), rd.get_mobile_dof(), seed, B, offset)
+        arm = list(range(ji.mani_start, ji.mani_start + rd.get_manipulator_dof()))
+    tier, stats = workload.apply_stress(q, lo, hi, arm, seed, offset, ev)
+    p = manipulator.QPIKParamsBuilder(rd.model, exact=True).params(link, _capi.MODE_QPIK)
     dq, dqd = _batch.as_device(q, dev), _batch.as_device(qd, dev)
     st = _batch.stages_batch(rd.model, p, dq, dqd, None, _batch.as_device(np.zeros((6, B)), dev))
     xt, xdt = workload.perturb_targets(st["pose"].cpu().numpy(), seed, B, offset)
-    return q, qd, xt, xdt, dq, dqd, _batch.as_device(xt, dev), _batch.as_device(xdt, dev)
+    return (q, qd, xt, xdt), (dq, dqd, _batch.as_device(xt, dev), _batch.as_device(xdt, dev)), stats
 
 
-def cpu_baseline(robot, q, qd, xt, xdt, budget_s=1.5):
+def cpu_baseline(robot, q, qd, xt, xdt, target_s=4.0, warmups=3, runs=5):
     """Oracle restatement of the reference CPU path (OSQP-default settings,
-    fresh setup per solve) on this host's cores, bounded sample."""
+    fresh setup per solve) on this host's cores: 1 thread and all threads
+    (capped at 16, the box's CPU share), each 3 warm-up + 5 timed runs over a
+    bounded sample of the same batch, median reported (BASELINE.md plan)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     _, om, spec = O.load(robot)
     par = O.default_params(spec["kind"], exact=False)
-    threads = max(1, min(16, os.cpu_count() or 1))   # box CPU share is 16
-    n = min(q.shape[1], 2048)
-    t0 = time.time()
-    O.qpik_batch(om, par, q[:, :n], qd[:, :n], xt[:, :n], xdt[:, :n], nthreads=threads)
-    dt = time.time() - t0
-    per = dt / n
-    n2 = int(min(q.shape[1], max(n, budget_s / max(per, 1e-9))))
-    t0 = time.time()
-    O.qpik_batch(om, par, q[:, :n2], qd[:, :n2], xt[:, :n2], xdt[:, :n2], nthreads=threads)
-    dt = time.time() - t0
-    return {"value": n2 / dt, "unit": "solves/s", "cores": threads, "kind": "port",
-            "sample": "first %d instances of the same batch, oracle/drc_oracle.c QPIKStep with the "
-                      "reference OSQP settings (eps 1e-3, no polish, fresh setup per solve), "
-                      "%d pthreads, %.2f s wall" % (n2, threads, dt)}
+    cores = max(1, min(16, os.cpu_count() or 1))
+
+    def timed(n, threads):
+        t0 = time.perf_counter()
+        O.qpik_batch(om, par, q[:, :n], qd[:, :n], xt[:, :n], xdt[:, :n], nthreads=threads)
+        return time.perf_counter() - t0
+
+    out = {}
+    for threads in (1, cores):
+        n = min(q.shape[1], 256 * threads)
+        per = timed(n, threads) / n                      # calibration run
+        n = int(min(q.shape[1], max(64, target_s / (warmups + runs) / max(per, 1e-9))))
+        for _ in range(warmups):
+            timed(n, threads)
+        ts = sorted(timed(n, threads) for _ in range(runs))
+        out[threads] = (n / ts[len(ts) // 2], n)
+    (v1, n1), (vc, nc) = out[1], out[cores]
+    return {"value": vc, "unit": "solves/s", "cores": cores, "kind": "port",
+            "single_thread": {"value": v1, "cores": 1, "sample_instances": n1},
+            "sample": "first %d instances of the same batch (1 thread: %d), oracle/drc_oracle.c QPIKStep with the "
+                      "reference OSQP settings (eps 1e-3, no polish, fresh setup per solve), %d pthreads; median of "
+                      "%d timed runs after %d warm-ups" % (nc, n1, cores, runs, warmups)}
 
 
-def load_traffic(robot, B):
-    """HBM bytes per drc_qpik_batch call (both kernels) from the committed
-    rocprofv3 PMC summary (tools/pmc_summary.py), if it matches this workload
-    and this build; else None."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+def load_profile(name, robot, B):
+    """A committed profiles/ summary for this workload and batch, or None."""
     try:
-        with open(path) as fh:
+        with open(os.path.join(ROOT, "profiles", name)) as fh:
             d = json.load(fh)
         if d.get("robot") == robot and int(d.get("batch")) == B:
-            return d.get("hbm_bytes_per_step")
+            return d
     except Exception:
         pass
     return None
@@ -99,8 +125,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=65536, help="instances per GPU")
-    ap.add_argument("--robot", default="fr3", choices=sorted(LINKS))
+    ap.add_argument("--robot", default="fr3", choices=sorted(DEFAULT_BATCH))
+    ap.add_argument("--batch", type=int, default=None, help="instances per GPU (weak scaling)")
+    ap.add_argument("--global-batch", type=int, default=None, help="fixed total instances (strong scaling)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--chunks", type=int, default=3, help="concurrent sub-batches per call")
     args = ap.parse_args()
@@ -108,7 +135,8 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from dyros_robot_controller_amd import dist as ddist
+    from dyros_robot_controller_amd import BUNDLED, _capi, dist as ddist, make_robot
+    from dyros_robot_controller_amd import manipulator, mobile_manipulator
     rank, world, local = ddist.env_rank()
     backend = os.environ.get("DRC_DIST_BACKEND", "nccl")   # gloo: rehearse N ranks on one GPU
     if world > 1:
@@ -117,19 +145,25 @@ def main():
     dev = torch.device("cuda", local % max(torch.cuda.device_count(), 1))
     torch.cuda.set_device(dev)
 
-    from dyros_robot_controller_amd import manipulator, robot_path
-    robot, B = args.robot, args.batch
-    rd = manipulator.RobotData(robot_path(robot), robot_path(robot, "srdf"), device=dev)
-    ctrl = manipulator.RobotController(0.001, rd, solver_mode="exact")
-    offset, _ = ddist.shard(rank, B)   # contiguous instance range of this rank
-    q, qd, xt, xdt, dq, dqd, dxt, dxdt = make_inputs(rd, robot, B, 12345, offset, dev)
+    robot = args.robot
+    spec = BUNDLED[robot]
+    if args.global_batch:
+        offset, B = ddist.shard_global(rank, world, args.global_batch)
+        scaling, total_per_step = "strong", args.global_batch
+    else:
+        B = args.batch or DEFAULT_BATCH[robot]
+        offset, _ = ddist.shard(rank, B)   # contiguous instance range of this rank
+        scaling, total_per_step = "weak", B * world
+    rd = make_robot(robot, dev)
+    mod = manipulator if spec["kind"] == "manipulator" else mobile_manipulator
+    ctrl = mod.RobotController(0.001, rd, solver_mode="exact")
+    (q, qd, xt, xdt), (dq, dqd, dxt, dxdt), tiers = make_inputs(rd, robot, B, 12345, offset, dev)
     iters = torch.zeros(B, dtype=torch.int32, device=dev)
-    link = LINKS[robot]
+    link = spec["link"]
 
     def step():
         return ctrl.QPIK_step_batch(dq, dqd, dxt, dxdt, link, iters=iters)
 
-    from dyros_robot_controller_amd import _capi
     import ctypes as C
     handle = rd.model.handle
     _capi.check(_capi.lib().drc_set_concurrency(handle, args.chunks))
@@ -166,35 +200,45 @@ def main():
                                               dev if backend == "nccl" else "cpu")
 
     if rank == 0:
-        nv = rd.getDof()
-        total = B * world * args.steps
+        dof, act = rd.model.dof, rd.model.actuated_dof
+        total = total_per_step * args.steps
         value = total / wall
         ms_per_step = 1e3 * wall / args.steps
-        per_launch_bytes = algorithmic_bytes(nv) * B
+        bps = algorithmic_bytes(dof, act)
+        per_launch_bytes = bps * B
         achieved = per_launch_bytes / (kernel_ms * 1e-3) / 1e9
-        traffic = load_traffic(robot, B)
-        fl = flops_per_solve(nv, it_mean) * B / (kernel_ms * 1e-3) / 1e12
+        traffic = load_profile("pmc_traffic_%s.json" % robot, robot, B) or load_profile("pmc_traffic.json", robot, B)
+        fl = flops_per_solve(it_mean) * B / (kernel_ms * 1e-3) / 1e12
+        roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic.get("hbm_bytes_per_step") if traffic else None,
+                "kernel": "drc_qpik_batch call (task_kernel + qp_kernel per sub-batch, %d concurrent sub-batches)"
+                          % args.chunks,
+                "bytes_per_solve": bps, "bytes_per_launch": per_launch_bytes,
+                "kernel_ms": kernel_ms, "task_kernel_ms_sum": task_ms, "qp_kernel_ms_sum": qp_ms,
+                "step_event_ms": step_event_ms,
+                "fp64_valu_estimate": {"achieved_tflops": fl, "peak_tflops": FP64_VECTOR_PEAK_TFS,
+                                       "frac": fl / FP64_VECTOR_PEAK_TFS,
+                                       "flops_per_solve": flops_per_solve(it_mean)}}
+        valu = load_profile("valu_counters_%s.json" % robot, robot, B)
+        if valu:   # counter-based FP64 work per call (tools/valu_summary.py over rocprofv3 --pmc passes)
+            f = valu["fp64_flops_per_step"]
+            roof["fp64_valu"] = {"achieved_tflops": f / (kernel_ms * 1e-3) / 1e12, "peak_tflops": FP64_VECTOR_PEAK_TFS,
+                                 "frac": f / (kernel_ms * 1e-3) / 1e12 / FP64_VECTOR_PEAK_TFS,
+                                 "fp64_flops_per_step": f, "lane_efficiency": valu.get("lane_efficiency"),
+                                 "source": "profiles/valu_counters_%s.json" % robot}
         line = {
-            "metric": "QP-IK solves/s (FR3 7-DoF, batch 65k) + achieved HBM GB/s vs peak",
-            "value": value, "unit": "solves/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "f64", "data": "synthetic",
-            "config": {"workload": "%s QPIKStep (exact: certified OSQP polish), %d instances per GPU"
-                                   % (robot.upper(), B),
-                       "robot": robot, "batch_per_gpu": B, "global_batch": B * world,
+            "metric": METRIC, "value": value, "unit": "solves/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": scaling,
+            "vs_baseline": None, "dtype": "f64", "data": "synthetic (SURVEY 8d workload with the stress tiers)",
+            "config": {"workload": "%s QPIKStep (exact: certified OSQP polish), %d instances per GPU%s"
+                                   % (robot.upper(), B, ", global batch %d" % args.global_batch
+                                      if args.global_batch else ""),
+                       "robot": robot, "batch_per_gpu": B, "global_batch": total_per_step,
                        "parallelism": "dp%d (instances sharded, no data-path collective)" % world},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "drc_qpik_batch call (task_kernel + qp_kernel per sub-batch, %d concurrent "
-                                   "sub-batches)" % args.chunks,
-                         "bytes_per_solve": algorithmic_bytes(nv), "bytes_per_launch": per_launch_bytes,
-                         "kernel_ms": kernel_ms, "task_kernel_ms_sum": task_ms, "qp_kernel_ms_sum": qp_ms,
-                         "step_event_ms": step_event_ms,
-                         "fp64_valu_estimate": {"achieved_tflops": fl, "peak_tflops": FP64_VECTOR_PEAK_TFS,
-                                                "frac": fl / FP64_VECTOR_PEAK_TFS,
-                                                "flops_per_solve": flops_per_solve(nv, it_mean)}},
+            "roofline": roof,
             "non_solved": int(n_bad), "admm_iters_mean": it_mean,
             "admm_iters_p99_max": [float(np.percentile(iters.cpu().numpy(), 99)), int(iters.max().item())],
+            "stress_tiers": tiers,
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(robot, q, qd, xt, xdt)

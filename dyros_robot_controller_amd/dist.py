@@ -33,6 +33,30 @@ def shard(rank, per_rank):
     return rank * per_rank, per_rank
 
 
+def shard_global(rank, world, global_batch):
+    """Strong scaling: ``rank``'s contiguous range [r G / W, (r + 1) G / W) of a
+    fixed global batch G (SURVEY §8e partitioning).  Returns (offset, count)."""
+    lo = rank * global_batch // world
+    hi = (rank + 1) * global_batch // world
+    return lo, hi - lo
+
+
+def gather_outputs(local, counts, world):
+    """Optional epilogue: all-gather every rank's [F][B_r] output
+    block into one [F][sum B_r] tensor on each rank (instance order = rank
+    order).  Blocks are padded to the largest shard for the collective."""
+    import torch
+    if world == 1:
+        return local
+    import torch.distributed as dist
+    F, Bmax = local.shape[0], max(counts)
+    pad = torch.zeros((F, Bmax), dtype=local.dtype, device=local.device)
+    pad[:, :local.shape[1]] = local
+    parts = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(parts, pad)
+    return torch.cat([p[:, :c] for p, c in zip(parts, counts)], dim=1)
+
+
 def reduce_stats(wall_s, n_bad, iters_mean, world, device="cpu"):
     """Whole-job timing and counters: max wall time over ranks (the job ends
     with the slowest rank), sum of non-solved instances, mean of the per-rank

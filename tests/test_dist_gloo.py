@@ -75,3 +75,43 @@ def test_two_rank_sharding_matches_single_process(tmp_path):
         s = g[r, n * per_rank:]
         np.testing.assert_array_equal(o, out[:, r * per_rank:(r + 1) * per_rank])
         np.testing.assert_array_equal(s, status[r * per_rank:(r + 1) * per_rank])
+
+
+def _worker_strong(rank, world, port, global_batch, outdir):
+    import sys
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")]
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    from dyros_robot_controller_amd import dist as ddist
+    from _common import oracle_batch
+    r, w, _ = ddist.env_rank()
+    d = ddist.init("gloo")
+    off, cnt = ddist.shard_global(r, w, global_batch)
+    counts = [ddist.shard_global(k, w, global_batch)[1] for k in range(w)]
+    q, qd, xt, xdt = _inputs("ur5e", 777, cnt, off)
+    out, status, _, _ = oracle_batch("ur5e", q, qd, xt, xdt, exact=True, nthreads=1)
+    full = ddist.gather_outputs(torch.from_numpy(out), counts, w)
+    if r == 0:
+        np.save(os.path.join(outdir, "full.npy"), full.numpy())
+    d.barrier()
+    d.destroy_process_group()
+
+
+def test_strong_scaling_shards_and_output_gather(tmp_path):
+    """--global-batch mode: a fixed global batch (odd size) split into
+    contiguous ranges over 3 ranks; the optional all-gather epilogue returns
+    the whole batch in instance order."""
+    import sys
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "oracle")]
+    from _common import oracle_batch
+    from dyros_robot_controller_amd import dist as ddist
+    world, G = 3, 23
+    assert sum(ddist.shard_global(r, world, G)[1] for r in range(world)) == G
+    assert [ddist.shard_global(r, world, G)[0] for r in range(world)] == [0, 7, 15]
+    mp.start_processes(_worker_strong, args=(world, _free_port(), G, str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    full = np.load(tmp_path / "full.npy")
+    q, qd, xt, xdt = _inputs("ur5e", 777, G, 0)
+    out, _, _, _ = oracle_batch("ur5e", q, qd, xt, xdt, exact=True, nthreads=1)
+    np.testing.assert_array_equal(full, out)

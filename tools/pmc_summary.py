@@ -6,7 +6,7 @@ Reads gpurun_out/prof_<tag>/ and writes
   profiles/<tag>_bench.json          the bench line of that run
   profiles/<tag>_kernel_stats.csv    rocprofv3 --kernel-trace --stats summary
   profiles/<tag>_pmc.json            per-kernel FETCH_SIZE / WRITE_SIZE per launch
-  profiles/pmc_traffic.json          the same, as read by bench.py (latest run)
+  profiles/pmc_traffic_<robot>.json  the same, as read by bench.py (latest run of that robot)
 
 Corrections (MI355X_MICROARCH.md, HBM section): FETCH_SIZE and WRITE_SIZE
 are in KiB; on gfx950 FETCH_SIZE counts half the bytes of a streaming read,
@@ -31,16 +31,33 @@ def short(name):
     return None
 
 
-def counters(d, cname):
+MAIN_GRID = 8192 * 64   # work-items of the bench's task/QP dispatches (grid capped at 8192 waves)
+
+
+def counters(d, cname, grid=MAIN_GRID):
+    """Per-kernel average of a counter over the bench's own dispatches (the
+    workload generator's stage launches on instance subsets have smaller grids)."""
     per = defaultdict(list)
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
             for row in csv.DictReader(fh):
-                if row.get("Counter_Name") != cname:
+                if row.get("Counter_Name") != cname or int(row.get("Grid_Size", grid)) != grid:
                     continue
                 k = short(row.get("Kernel_Name", ""))
                 if k:
                     per[k].append(float(row["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in per.items()}, {k: len(v) for k, v in per.items()}
+
+
+def trace_durations(d, grid=MAIN_GRID):
+    """Per-kernel average duration (ns) of the bench's dispatches from the kernel trace."""
+    per = defaultdict(list)
+    for f in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                k = short(row.get("Kernel_Name", ""))
+                if k and int(row["Grid_Size_X"]) == grid:
+                    per[k].append(float(row["End_Timestamp"]) - float(row["Start_Timestamp"]))
     return {k: sum(v) / len(v) for k, v in per.items()}, {k: len(v) for k, v in per.items()}
 
 
@@ -55,12 +72,7 @@ def main():
     shutil.copy(os.path.join(src, "bench.json"), os.path.join(dst, tag + "_bench.json"))
     stats = glob.glob(os.path.join(src, "kt", "**", "*kernel_stats.csv"), recursive=True)
     shutil.copy(stats[0], os.path.join(dst, tag + "_kernel_stats.csv"))
-    avg = {}
-    with open(stats[0]) as fh:
-        for row in csv.DictReader(fh):
-            k = short(row["Name"])
-            if k:
-                avg[k] = float(row["AverageNs"])
+    avg, ndisp = trace_durations(os.path.join(src, "kt"))
     fetch, nf = counters(os.path.join(src, "fetch"), "FETCH_SIZE")
     write, nw = counters(os.path.join(src, "write"), "WRITE_SIZE")
     kern = {}
@@ -74,8 +86,10 @@ def main():
            "hbm_bytes_per_step": chunks * per_dispatch,
            "hbm_bytes_per_instance": chunks * per_dispatch / batch,
            "corrections": "FETCH_SIZE KiB x1024 x2 (gfx950 half-count), WRITE_SIZE KiB x1024",
-           "kernel_stats_avg_ns": avg}
-    for name in (tag + "_pmc.json", "pmc_traffic.json"):
+           "main_dispatch_avg_ns": avg, "main_dispatches_traced": ndisp,
+           "note": "averages over the bench's own dispatches (grid %d work-items); the kernel_stats csv "
+                   "also counts the workload generator's stage launches" % MAIN_GRID}
+    for name in (tag + "_pmc.json", "pmc_traffic_%s.json" % robot):
         with open(os.path.join(dst, name), "w") as fh:
             json.dump(out, fh, indent=1)
     print(json.dumps(out, indent=1))

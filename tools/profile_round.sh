@@ -21,3 +21,4 @@ timeout -k 10 420 rocprofv3 --pmc FETCH_SIZE -f csv -d $OUT/fetch -o fetch -- py
 echo "fetch pass done"
 timeout -k 10 420 rocprofv3 --pmc WRITE_SIZE -f csv -d $OUT/write -o write -- python3 $ROOT/bench.py --steps 3 --warmup 1 --no-cpu-baseline $ARGS > $OUT/write.log 2>&1
 echo "write pass done"
+bash $ROOT/tools/valu_pass.sh $TAG $ARGS
