@@ -9,7 +9,7 @@ dev = torch.device("cuda", 0)
 robot = sys.argv[1] if len(sys.argv) > 1 else "fr3"
 B = int(sys.argv[2]) if len(sys.argv) > 2 else 65536
 rd = make_manipulator(robot, dev)
-q, qd, xt, xdt = step_inputs(rd, robot, 7, B, dev)
+q, qd, xt, xdt = step_inputs(rd, robot, 7, B, dev, stress=True)
 ctrl = manipulator.RobotController(0.001, rd)
 _capi.lib().drc_set_concurrency(rd.model.handle, 1)  # one sub-batch: per-instance cycles without overlap
 link = "fr3_link8" if robot == "fr3" else "tool0"
