@@ -130,6 +130,9 @@ def main():
     ap.add_argument("--global-batch", type=int, default=None, help="fixed total instances (strong scaling)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--chunks", type=int, default=3, help="concurrent sub-batches per call")
+    ap.add_argument("--task-stage", type=int, default=0, choices=(0, 1, 2),
+                    help="0 wave-per-instance task kernel (default), 1 lane stage + side-stream hand-backs, "
+                         "2 lane stage + serial hand-backs (drc_debug_lane_stage)")
     args = ap.parse_args()
 
     import torch
@@ -167,6 +170,7 @@ def main():
     import ctypes as C
     handle = rd.model.handle
     _capi.check(_capi.lib().drc_set_concurrency(handle, args.chunks))
+    _capi.check(_capi.lib().drc_debug_lane_stage(handle, args.task_stage))
     for _ in range(args.warmup):
         out, status = step()
     torch.cuda.synchronize()
@@ -234,7 +238,9 @@ def main():
                                    % (robot.upper(), B, ", global batch %d" % args.global_batch
                                       if args.global_batch else ""),
                        "robot": robot, "batch_per_gpu": B, "global_batch": total_per_step,
-                       "parallelism": "dp%d (instances sharded, no data-path collective)" % world},
+                       "parallelism": "dp%d (instances sharded, no data-path collective)" % world,
+                       "task_stage": ["wave-per-instance", "lane-per-instance + side-stream hand-backs",
+                                      "lane-per-instance + serial hand-backs"][args.task_stage]},
             "roofline": roof,
             "non_solved": int(n_bad), "admm_iters_mean": it_mean,
             "admm_iters_p99_max": [float(np.percentile(iters.cpu().numpy(), 99)), int(iters.max().item())],

@@ -452,6 +452,17 @@ int build_model_from_urdf(const std::string& urdf_path, const std::string& srdf_
     m.pair_a[p] = static_cast<int16_t>(pairs[p].first);
     m.pair_b[p] = static_cast<int16_t>(pairs[p].second);
   }
+  // GJK candidate slots of the lane-per-instance task stage: the pairs with
+  // no sphere (no closed form), numbered in pair order
+  m.ncand_slots = 0;
+  for (int p = 0; p < m.npairs; ++p) {
+    m.cand_slot[p] = -1;
+    if (m.gtype[m.pair_a[p]] != kSphere && m.gtype[m.pair_b[p]] != kSphere) {
+      if (m.ncand_slots < kMaxCandSlots) m.cand_pair[m.ncand_slots] = static_cast<int16_t>(p);
+      m.cand_slot[p] = static_cast<int16_t>(m.ncand_slots < kMaxCandSlots ? m.ncand_slots : -1);
+      ++m.ncand_slots;
+    }
+  }
   return DRC_OK;
 }
 

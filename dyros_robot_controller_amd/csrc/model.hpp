@@ -14,6 +14,7 @@ constexpr int kMaxGeoms = 64;
 constexpr int kMaxPairs = 1024;
 constexpr int kMaxFrames = 64;
 constexpr int kMaxWheels = 8;
+constexpr int kMaxCandSlots = 128;  // non-sphere pairs the lane-per-instance task stage tracks
 
 enum JointType : int { kRevolute = 0, kPrismatic = 1 };
 enum GeomType : int { kSphere = 0, kCylinder = 1, kBox = 2 };
@@ -40,6 +41,9 @@ struct DevModel {
   double gparam[kMaxGeoms][3];     // sphere r | cylinder r, h/2 | box half extents
   double gbound[kMaxGeoms];        // conservative core/bounding radius for the broad phase
   int16_t pair_a[kMaxPairs], pair_b[kMaxPairs];
+  int16_t cand_slot[kMaxPairs];       // pair -> GJK candidate slot (pairs without a sphere), or -1
+  int16_t cand_pair[kMaxCandSlots];   // slot -> pair
+  int ncand_slots;                    // non-sphere pairs (> kMaxCandSlots: lane stage not used)
   double J_mobile[3][kMaxWheels];  // base twist = J_mobile * wheel velocity (differential, mecanum)
   int drive;                       // DriveKind; caster: J_mobile depends on the steer angles (mobile_fk.hpp)
   double wheel_radius, wheel_offset;

@@ -297,15 +297,70 @@ DRC_HD __forceinline__ int closest_n(SV2 (&S)[4], V3* v, double (&lam)[4]) {
   return k;
 }
 
+// closest_n for a per-lane simplex size n (lane-per-instance GJK, where
+// lanes of one wave hold simplices of different sizes): one descending pass
+// over all 15 masks, each taken only where it exists for this lane's n, with
+// the same two phases (masks holding the newest vertex, then the rest if none
+// of those was valid) -- per lane bit-identical to closest_n<n>, at the cost
+// of closest_n<4> instead of the sum over the sizes present in the wave.
+template <int MASK>
+struct CsAny {
+  DRC_HD static __forceinline__ void run(const SV2 (&S)[4], int n, CsBest& B, bool& allow2) {
+    if (MASK + 1 == (1 << (n - 1))) allow2 = B.mask == 0;  // entering phase 2
+    if (MASK < (1 << n) && (MASK >= (1 << (n - 1)) || allow2)) cs_try<MASK>(S, B);
+    CsAny<MASK - 1>::run(S, n, B, allow2);
+  }
+};
+template <>
+struct CsAny<0> {
+  DRC_HD static __forceinline__ void run(const SV2 (&)[4], int, CsBest&, bool&) {}
+};
+DRC_HD __forceinline__ int closest_any(SV2 (&S)[4], int n, V3* v, double (&lam)[4]) {
+  CsBest B;
+  B.best = 0;
+  B.mask = 0;
+  B.v = v3(0, 0, 0);
+  B.l[0] = B.l[1] = B.l[2] = B.l[3] = 0;
+  bool allow2 = false;
+  CsAny<15>::run(S, n, B, allow2);
+  const int bmask = B.mask;
+  *v = B.v;
+  SV2 T[4] = {S[0], S[0], S[0], S[0]};
+  int k = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const bool keep = (bmask >> i) & 1;
+#pragma unroll
+    for (int t = 0; t <= i; ++t) {
+      const bool here = keep && k == t;
+      T[t].w = v3(here ? S[i].w.x : T[t].w.x, here ? S[i].w.y : T[t].w.y, here ? S[i].w.z : T[t].w.z);
+      T[t].a = v3(here ? S[i].a.x : T[t].a.x, here ? S[i].a.y : T[t].a.y, here ? S[i].a.z : T[t].a.z);
+    }
+    k += keep;
+  }
+#pragma unroll
+  for (int t = 0; t < 4; ++t) S[t] = T[t];
+  lam[0] = B.l[0];
+  lam[1] = B.l[1];
+  lam[2] = B.l[2];
+  lam[3] = B.l[3];
+  return k;
+}
+
 // GJK on the cores (same iteration, tolerances and duplicate test as
-// oracle/drc_oracle.c:gjk).  The simplex stays in registers.
+// oracle/drc_oracle.c:gjk).  The simplex stays in registers.  ANY: the
+// closest-point step for per-lane simplex sizes (closest_any).
 struct GjkState {
   SV2 S[4];
   double lam[4];
   V3 v;
-  int n, intersect;
+  int n, intersect, pruned;
 };
-DRC_HD __forceinline__ void gjk_run(const Shape& A, const Shape& B, GjkState& g) {
+// cut: the caller only needs the distance if it is <= cut.  Every support
+// point gives the lower bound v.w / |v| of the (signed) distance; once it
+// exceeds cut the pair cannot matter and the run stops with pruned = 1.
+template <bool ANY = false>
+DRC_HD __forceinline__ void gjk_run(const Shape& A, const Shape& B, GjkState& g, double cut = 1e300) {
   SV2(&S)[4] = g.S;
 #pragma unroll
   for (int i = 0; i < 4; ++i) S[i].w = S[i].a = v3(0, 0, 0);
@@ -315,10 +370,15 @@ DRC_HD __forceinline__ void gjk_run(const Shape& A, const Shape& B, GjkState& g)
   if (dot(v, v) < 1e-24) v = v3(1, 0, 0);
   int n = 0;
   g.intersect = 0;
+  g.pruned = 0;
   for (int it = 0; it < 128; ++it) {
     const SV w = sup_md(A, B, -1.0 * v);
-    const double vv = dot(v, v);
-    if (n > 0 && vv - dot(v, w.w) <= 1e-12 * sqrt(vv)) break;
+    const double vv = dot(v, v), vw = dot(v, w.w), sv = sqrt(vv);
+    if (vw > cut * sv) {
+      g.pruned = 1;
+      break;
+    }
+    if (n > 0 && vv - vw <= 1e-12 * sv) break;
     bool dup = false;
 #pragma unroll
     for (int i = 0; i < 4; ++i) dup |= i < n && S[i].w.x == w.w.x && S[i].w.y == w.w.y && S[i].w.z == w.w.z;
@@ -343,10 +403,14 @@ DRC_HD __forceinline__ void gjk_run(const Shape& A, const Shape& B, GjkState& g)
 #ifdef DRC_NARROW_DEBUG
     printf("gjk it %d add w %.17g %.17g %.17g (n=%d) vv %.6g vw %.6g\n", it, w.w.x, w.w.y, w.w.z, n, vv, dot(v, w.w));
 #endif
-    if (n == 1) n = closest_n<1>(S, &v, g.lam);
-    else if (n == 2) n = closest_n<2>(S, &v, g.lam);
-    else if (n == 3) n = closest_n<3>(S, &v, g.lam);
-    else n = closest_n<4>(S, &v, g.lam);
+    if constexpr (ANY) {
+      n = closest_any(S, n, &v, g.lam);
+    } else {
+      if (n == 1) n = closest_n<1>(S, &v, g.lam);
+      else if (n == 2) n = closest_n<2>(S, &v, g.lam);
+      else if (n == 3) n = closest_n<3>(S, &v, g.lam);
+      else n = closest_n<4>(S, &v, g.lam);
+    }
 #ifdef DRC_NARROW_DEBUG
     printf("   -> n %d v %.6g %.6g %.6g |v| %.6g\n", n, v.x, v.y, v.z, sqrt(dot(v, v)));
 #endif
@@ -789,7 +853,32 @@ DRC_HD __forceinline__ void core_segment(const Shape& s, double bound, V3* a, V3
   }
   *rad = bound;
 }
-DRC_HD __forceinline__ double seg_seg_dist(V3 p1, V3 q1, V3 p2, V3 q2) {
+// Cylinder/cylinder distance in closed form when the closest points of the
+// two axis segments are interior to both: the connecting line is then normal
+// to both axes, meets both lateral surfaces, and the swept-core (capsule)
+// bound is attained -- the exact distance GJK converges to.  Separated,
+// non-parallel pairs only; every other cylinder pair goes to GJK/EPA.
+// Oracle twin: cyl_cyl_side in oracle/drc_oracle.c (same operation order).
+DRC_HD __forceinline__ bool cyl_cyl_side(const Shape& A, const Shape& B, double* d, V3* pA, V3* pB) {
+  const V3 ua = v3(A.T[2], A.T[5], A.T[8]), ub = v3(B.T[2], B.T[5], B.T[8]);
+  const V3 p1 = v3(A.T[9], A.T[10], A.T[11]) - A.p1 * ua, p2 = v3(B.T[9], B.T[10], B.T[11]) - B.p1 * ub;
+  const V3 d1 = (2.0 * A.p1) * ua, d2 = (2.0 * B.p1) * ub, r = p1 - p2;
+  const double a = dot(d1, d1), e = dot(d2, d2), b = dot(d1, d2), c = dot(d1, r), f = dot(d2, r);
+  const double den = a * e - b * b;
+  if (!(den > 1e-12 * a * e)) return false;
+  const double s = (b * f - c * e) / den, t = (a * f - b * c) / den;
+  if (!(s > 0.0 && s < 1.0 && t > 0.0 && t < 1.0)) return false;
+  const V3 c1 = p1 + s * d1, c2 = p2 + t * d2;
+  V3 n = c2 - c1;
+  const double L = sqrt(dot(n, n)), dd = L - A.p0 - B.p0;
+  if (!(dd > 0.0)) return false;
+  n = (1.0 / L) * n;
+  *pA = c1 + A.p0 * n;
+  *pB = c2 - B.p0 * n;
+  *d = dd;
+  return true;
+}
+DRC_HD __forceinline__ double seg_seg_dist(V3 p1, V3 q1, V3 p2, V3 q2, V3* c1o = nullptr, V3* c2o = nullptr) {
   V3 d1 = q1 - p1, d2 = q2 - p2, r = p1 - p2;
   double a = dot(d1, d1), e = dot(d2, d2), f = dot(d2, r), s, t;
   if (a <= 1e-30 && e <= 1e-30) {
@@ -817,7 +906,28 @@ DRC_HD __forceinline__ double seg_seg_dist(V3 p1, V3 q1, V3 p2, V3 q2) {
     }
   }
   V3 c1 = p1 + s * d1, c2 = p2 + t * d2, dd = c1 - c2;
+  if (c1o) {
+    *c1o = c1;
+    *c2o = c2;
+  }
   return sqrt(dot(dd, dd));
+}
+
+// Lower bound on the (signed) distance of two geometries: the swept-core
+// (capsule / bounding sphere) distance, raised to the separating-axis value
+// along the core closest-point direction n,  min_B n.x - max_A n.x  (the
+// geometry lies inside its core's swept volume, so this is never below the
+// core bound).
+DRC_HD __forceinline__ double pair_lower_bound(const Shape& A, const Shape& B, double boundA, double boundB) {
+  V3 a0, a1, b0, b1, c1, c2;
+  double ra, rb;
+  core_segment(A, boundA, &a0, &a1, &ra);
+  core_segment(B, boundB, &b0, &b1, &rb);
+  const double L = seg_seg_dist(a0, a1, b0, b1, &c1, &c2), pd = L - ra - rb;
+  if (!(L > 1e-12)) return pd;
+  const V3 n = (1.0 / L) * (c2 - c1);
+  const double sat = dot(n, support(B, -1.0 * n)) - dot(n, support(A, n));
+  return fmax(pd, sat);
 }
 
 }  // namespace drc_amd

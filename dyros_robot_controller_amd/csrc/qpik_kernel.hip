@@ -1311,6 +1311,12 @@ struct IO {
   double* st_gdv;             // [narm + nv][B] grad_dot vectors (manipulability | min distance)
   const double* cf_null;      // closed-form: null_qdot / null_torque [nv][B] (may be NULL)
   int* queue;                 // per-launch work-queue counters (8, zeroed), or NULL: fixed stride
+  // lane-per-instance task stage (lane_task.hpp): instances it leaves to the
+  // wave-per-instance task_kernel; hard_mode makes task_kernel run that list
+  int* hard_list;
+  int* hard_n;
+  uint8_t* hard_flag;  // [B] 1 = instance on the hard list (QP pass over the others skips it)
+  int hard_mode;       // task_kernel / qp_kernel: 1 = run the hard list; qp_kernel: 2 = skip flagged
 };
 
 // ------------------------------------------------------------------------
@@ -1714,9 +1720,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRC_TAS
   const int64_t B = io.B;
   EpaPoly* ews = reinterpret_cast<EpaPoly*>(S + kp.kEpa);  // LDS-resident polytope
   PH_DECL
-  const InstSeq seq(B, kp.xcd_map, io.queue);
+  // hard mode: the instances the lane-per-instance stage left (grid stride)
+  const bool hard_mode = io.hard_mode != 0;
+  const InstSeq seq(hard_mode ? int64_t(*io.hard_n) : B, hard_mode ? 0 : kp.xcd_map, hard_mode ? nullptr : io.queue);
   for (int64_t j = seq.first(); j < seq.n; j = seq.next(j)) {
-    const int64_t b = seq.at(j);
+    const int64_t b = hard_mode ? int64_t(io.hard_list[j]) : seq.at(j);
     if (b >= B) continue;
     const int64_t gb = io.b0 + b, LD = io.ld;  // position in the caller's [field][B] arrays
 #ifdef DRC_PHASE_TIMING
@@ -1993,9 +2001,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRC_TAS
       const int ga = M->pair_a[p], gb = M->pair_b[p];
       Shape A{M->gtype[ga], Tg + 12 * ga, M->gparam[ga][0], M->gparam[ga][1], M->gparam[ga][2]};
       Shape Bs{M->gtype[gb], Tg + 12 * gb, M->gparam[gb][0], M->gparam[gb][1], M->gparam[gb][2]};
-      if (A.type == kSphere || Bs.type == kSphere) {
-        V3 pA, pB;
-        const double d = sphere_pair(A, Bs, &pA, &pB);
+      V3 pA, pB;
+      double d;
+      const bool closed = (A.type == kSphere || Bs.type == kSphere)
+                              ? (d = sphere_pair(A, Bs, &pA, &pB), true)
+                              : (A.type == kCylinder && Bs.type == kCylinder && cyl_cyl_side(A, Bs, &d, &pA, &pB));
+      if (closed) {
         pf[p] = 1.0;
         ub = fmin(ub, d);
         if (d < bestd) {  // p increases within this pass
@@ -2004,12 +2015,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRC_TAS
           bpA = pA;
           bpB = pB;
         }
-      } else {  // swept-core lower bound
-        V3 a0, a1, b0, b1;
-        double ra, rb;
-        core_segment(A, M->gbound[ga], &a0, &a1, &ra);
-        core_segment(Bs, M->gbound[gb], &b0, &b1, &rb);
-        pd[p] = seg_seg_dist(a0, a1, b0, b1) - ra - rb;
+      } else {  // swept-core / separating-axis lower bound
+        pd[p] = pair_lower_bound(A, Bs, M->gbound[ga], M->gbound[gb]);
         pf[p] = 0.0;
       }
     }
@@ -2050,7 +2057,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRC_TAS
     }
     wsync();
     PH(4);
-    // EPA, best-first with bounds: the swept-core bound pd[p] <= d(p) also
+    // EPA, best-first with bounds: the lower bound pd[p] <= d(p) also
     // caps the penetration depth, so pairs are expanded in increasing pd and
     // the search stops once no remaining pair can undercut the running
     // minimum (same argmin and tie rule as computing every pair).  The owning
@@ -2247,6 +2254,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRC_TAS
   }
   PH_FLUSH(0);
 }
+
+#include "lane_task.hpp"
 
 // ---- QP kernel phases ------------------------------------------------------
 template <class QD>
@@ -2977,10 +2986,14 @@ qp_kernel(const DevModel* __restrict__ M0, const KParams kp, const IO io) {
   }
   const int64_t B = io.B;
   PH_DECL
-  const InstSeq seq(B, kp.xcd_map, io.queue);
+  // hard_mode 1: the lane stage's hard list (grid stride); 2: every instance
+  // except the flagged ones (their records are still being written)
+  const bool hl = io.hard_mode == 1;
+  const InstSeq seq(hl ? int64_t(*io.hard_n) : B, hl ? 0 : kp.xcd_map, hl ? nullptr : io.queue);
   for (int64_t j = seq.first(); j < seq.n; j = seq.next(j)) {
-    const int64_t b = seq.at(j);
+    const int64_t b = hl ? int64_t(io.hard_list[j]) : seq.at(j);
     if (b >= B) continue;
+    if (io.hard_mode == 2 && io.hard_flag[b]) continue;
     const int64_t gb = io.b0 + b, LD = io.ld;  // position in the caller's [field][B] arrays
     const DevModel* M = M0;
     asm volatile("" : "+s"(M));
@@ -3200,10 +3213,15 @@ struct StreamCtx {
   int64_t pool_bytes = 0;
   // work-queue counters: [slot][kernel (task, QP)][8 XCD classes]; slots
   // 0..15 the QPIK sub-batches, 16 QPID, 17 the closed-form controllers
-  static constexpr int kQueueSlotQpid = 16, kQueueSlotCf = 17, kQueueInts = 18 * 2 * 8;
+  static constexpr int kSlotInts = 32;  // task queue 8, QP queue 8, lane-stage hard count 1
+  static constexpr int kQueueSlotQpid = 16, kQueueSlotCf = 17, kQueueInts = 18 * kSlotInts;
   int* d_queue = nullptr;
   std::vector<hipStream_t> lanes;  // concurrent sub-batches (drc_set_concurrency)
   std::vector<hipEvent_t> joins;
+  // per sub-batch: the lane stage's hard instances run their task kernel on a
+  // side stream while the QP of the other instances runs
+  std::vector<hipStream_t> sides;
+  std::vector<hipEvent_t> side_fork, side_join;
   hipEvent_t fork = nullptr;
   int* dyn_list = nullptr;  // instances whose M_inv needs the serial COD
   int64_t dyn_list_cap = 0;
@@ -3218,6 +3236,7 @@ struct drc_model_impl {
   drc_actuator_index aidx{};
   std::vector<std::unique_ptr<StreamCtx>> ctxs;  // one per caller stream seen
   int timing = 0;  // drc_debug_kernel_timing: HIP events around each launch
+  int lane_stage = 0;  // drc_debug_lane_stage: 0 off, 1 lane stage + side-stream hard path, 2 + serial hard path, 3 auto
   // timed calls: {caller-stream start, caller-stream end, per chunk: task start, task end, qp end}
   std::vector<std::vector<hipEvent_t>> events;
   // concurrent sub-batches: the batch is cut into `chunks` contiguous ranges
@@ -3277,8 +3296,12 @@ static void free_ctx(StreamCtx* c) {
   if (c->d_queue) (void)hipFree(c->d_queue);
   if (c->pool) (void)hipFree(c->pool);
   if (c->dyn_list) (void)hipFree(c->dyn_list);
+  for (hipStream_t ls : c->sides) (void)hipStreamSynchronize(ls);
   for (hipStream_t ls : c->lanes) (void)hipStreamDestroy(ls);
   for (hipEvent_t e : c->joins) (void)hipEventDestroy(e);
+  for (hipStream_t ls : c->sides) (void)hipStreamDestroy(ls);
+  for (hipEvent_t e : c->side_fork) (void)hipEventDestroy(e);
+  for (hipEvent_t e : c->side_join) (void)hipEventDestroy(e);
   if (c->fork) (void)hipEventDestroy(c->fork);
 }
 
@@ -3661,13 +3684,27 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
   const int64_t stride = (kt.rLen + 15) & ~int64_t(15);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   double* rec = nullptr;
+  int* hard = nullptr;           // lane-stage hard list, B ints
+  uint8_t* hard_flag = nullptr;  // and its per-instance flags
   StreamCtx* cx = nullptr;
+  // lane-per-instance task stage (lane_task.hpp) for the compiled joint counts
+  const DevModel& dm = m->hm.dev;
+  // (3, auto: stage-only calls, where nothing overlaps the task stage.  The
+  // default is 0: a full QPIK call is faster with the wave-per-instance
+  // kernel, which shares the CUs with the QP kernels of the other sub-batches
+  // (DESIGN.md), and stage and QPIK calls then see the same GJK witnesses)
+  const int ls = m->lane_stage;
+  const bool lane = (ls == 1 || ls == 2 || (ls == 3 && stages)) && (dm.nv == 6 || dm.nv == 7) &&
+                    dm.ncand_slots <= kMaxCandSlots;
   {
     std::lock_guard<std::mutex> g(m->mu);
     if (int r = stream_ctx(m, st, &cx)) return r;
-    if (!stages) {
-      if (int r = ensure_pool(cx, stride * B * 8)) return r;
-      rec = reinterpret_cast<double*>(cx->pool);
+    if (!stages || lane) {
+      const int64_t rec_bytes = stages ? 0 : stride * B * 8;
+      if (int r = ensure_pool(cx, rec_bytes + B * 4 + B)) return r;
+      if (!stages) rec = reinterpret_cast<double*>(cx->pool);
+      hard = reinterpret_cast<int*>(static_cast<char*>(cx->pool) + rec_bytes);
+      hard_flag = reinterpret_cast<uint8_t*>(static_cast<char*>(cx->pool) + rec_bytes + B * 4);
     }
   }
   // sub-batches: whole multiples of 16 Ki instances per chunk (each keeps the
@@ -3696,6 +3733,16 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
       cx->lanes.push_back(ls);
       cx->joins.push_back(je);
     }
+    while (lane && !stages && ls == 1 && static_cast<int>(cx->sides.size()) < S) {
+      hipStream_t ss;
+      hipEvent_t f, j;
+      HIP_TRY(hipStreamCreateWithFlags(&ss, hipStreamNonBlocking));
+      HIP_TRY(hipEventCreateWithFlags(&f, hipEventDisableTiming));
+      HIP_TRY(hipEventCreateWithFlags(&j, hipEventDisableTiming));
+      cx->sides.push_back(ss);
+      cx->side_fork.push_back(f);
+      cx->side_join.push_back(j);
+    }
     if (!cx->fork) HIP_TRY(hipEventCreateWithFlags(&cx->fork, hipEventDisableTiming));
   }
   hipEvent_t e_start = nullptr, e_end = nullptr;
@@ -3714,8 +3761,8 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
     const int64_t gq = Bc < 8192 ? Bc : 8192, gt = Bc < 8192 ? Bc : 8192;
     IO io{Bc, b0, B, q, qdot, xt, xdt, xi, xdi, out, status, iters, pose, jac, man, dist, xdd, pair,
           rec ? rec + b0 * stride : nullptr, stride};
-    int* qc = cx->d_queue + c * 16;  // c < 16 (drc_set_concurrency)
-    HIP_TRY(hipMemsetAsync(qc, 0, 16 * sizeof(int), cs));
+    int* qc = cx->d_queue + c * StreamCtx::kSlotInts;  // c < 16 (drc_set_concurrency)
+    HIP_TRY(hipMemsetAsync(qc, 0, 17 * sizeof(int), cs));
     io.queue = qc;
     hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr;
     if (timed) {
@@ -3724,27 +3771,70 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
       if (int r = mkev(&e2)) return r;
       HIP_TRY(hipEventRecord(e0, cs));
     }
-    hipLaunchKernelGGL(task_kernel<0>, dim3(static_cast<unsigned>(gt)), dim3(64),
-                       static_cast<size_t>(kt_c.lds_doubles) * sizeof(double), cs, m->d_model, kt_c, io);
-    HIP_TRY(hipGetLastError());
-    if (timed) HIP_TRY(hipEventRecord(e1, cs));
-    if (!stages) {
+    const size_t lds_t = static_cast<size_t>(kt_c.lds_doubles) * sizeof(double);
+    const size_t lds_q = stages ? 0 : static_cast<size_t>(kq_c.lds_doubles) * sizeof(double);
+    auto launch_task = [&](hipStream_t sm) -> int {
+      hipLaunchKernelGGL(task_kernel<0>, dim3(static_cast<unsigned>(gt)), dim3(64), lds_t, sm, m->d_model, kt_c, io);
+      HIP_TRY(hipGetLastError());
+      return DRC_OK;
+    };
+    auto launch_qp = [&]() -> int {
       io.queue = qc + 8;
-      const size_t lds = static_cast<size_t>(kq_c.lds_doubles) * sizeof(double);
       const dim3 g(static_cast<unsigned>(gq)), blk(64);
       // compile-time QP shapes of the bundled robots; anything else runs the
       // runtime-sized instantiation
       if (kq_c.nx == 23 && kq_c.ng == 16 && kq_c.np == 7)
-        hipLaunchKernelGGL((qp_kernel<Dims<23, 16, 7, true, true>>), g, blk, lds, cs, m->d_model, kq_c, io);  // FR3
+        hipLaunchKernelGGL((qp_kernel<Dims<23, 16, 7, true, true>>), g, blk, lds_q, cs, m->d_model, kq_c, io);  // FR3
       else if (kq_c.nx == 20 && kq_c.ng == 14 && kq_c.np == 6)
-        hipLaunchKernelGGL((qp_kernel<Dims<20, 14, 6, true, true>>), g, blk, lds, cs, m->d_model, kq_c, io);  // UR5e
+        hipLaunchKernelGGL((qp_kernel<Dims<20, 14, 6, true, true>>), g, blk, lds_q, cs, m->d_model, kq_c, io);  // UR5e
       else if (kq_c.nx == 9 && kq_c.ng == 16 && kq_c.np == 9)
-        hipLaunchKernelGGL((qp_kernel<Dims<9, 16, 9, true, true>>), g, blk, lds, cs, m->d_model, kq_c, io);  // Husky-FR3
+        hipLaunchKernelGGL((qp_kernel<Dims<9, 16, 9, true, true>>), g, blk, lds_q, cs, m->d_model, kq_c, io);  // Husky-FR3
       else if (kq_c.nx == 11 && kq_c.ng == 16 && kq_c.np == 11)
-        hipLaunchKernelGGL((qp_kernel<Dims<11, 16, 11, true, true>>), g, blk, lds, cs, m->d_model, kq_c, io);  // XLS-FR3
+        hipLaunchKernelGGL((qp_kernel<Dims<11, 16, 11, true, true>>), g, blk, lds_q, cs, m->d_model, kq_c, io);  // XLS-FR3
       else
-        hipLaunchKernelGGL((qp_kernel<Dims<0, 0, 0>>), g, blk, lds, cs, m->d_model, kq_c, io);
+        hipLaunchKernelGGL((qp_kernel<Dims<0, 0, 0>>), g, blk, lds_q, cs, m->d_model, kq_c, io);
       HIP_TRY(hipGetLastError());
+      return DRC_OK;
+    };
+    if (!lane) {  // wave-per-instance task kernel on every instance, then the QP
+      if (int r = launch_task(cs)) return r;
+      if (timed) HIP_TRY(hipEventRecord(e1, cs));
+      if (!stages)
+        if (int r = launch_qp()) return r;
+    } else {
+      // lane stage for every instance; the wave-per-instance task kernel only
+      // for the instances it hands back (hard list)
+      io.hard_list = hard + b0;
+      io.hard_n = qc + 16;
+      io.hard_flag = stages ? nullptr : hard_flag + b0;
+      const dim3 gl(static_cast<unsigned>((Bc + 63) / 64)), bl(64);
+      if (dm.nv == 7)
+        hipLaunchKernelGGL(lane_task_kernel<7>, gl, bl, 0, cs, m->d_model, kt_c, io);
+      else
+        hipLaunchKernelGGL(lane_task_kernel<6>, gl, bl, 0, cs, m->d_model, kt_c, io);
+      HIP_TRY(hipGetLastError());
+      if (timed) HIP_TRY(hipEventRecord(e1, cs));
+      io.hard_mode = 1;
+      if (stages || ls != 1) {  // hard task kernel, then one QP pass over every instance
+        if (int r = launch_task(cs)) return r;
+        io.hard_mode = 0;
+        if (!stages)
+          if (int r = launch_qp()) return r;
+      } else {
+        // hard task kernel on the side stream, overlapped with the QP of the
+        // other instances; then the QP of the hard ones
+        hipStream_t ss = cx->sides[c];
+        HIP_TRY(hipEventRecord(cx->side_fork[c], cs));
+        HIP_TRY(hipStreamWaitEvent(ss, cx->side_fork[c], 0));
+        if (int r = launch_task(ss)) return r;
+        HIP_TRY(hipEventRecord(cx->side_join[c], ss));
+        io.hard_mode = 2;
+        if (int r = launch_qp()) return r;
+        HIP_TRY(hipStreamWaitEvent(cs, cx->side_join[c], 0));
+        io.hard_mode = 1;
+        if (int r = launch_qp()) return r;
+      }
+      io.hard_mode = 0;
     }
     if (timed) HIP_TRY(hipEventRecord(e2, cs));
     if (S > 1) HIP_TRY(hipEventRecord(cx->joins[c], cs));
@@ -3821,7 +3911,7 @@ static int launch_qpid(const drc_model_impl* cm, const drc_qpik_params* params, 
   io.st_jdot = jdot;
   io.st_qpid = qpid_st;
   io.st_gdv = gdv;
-  int* qc = cx->d_queue + StreamCtx::kQueueSlotQpid * 16;
+  int* qc = cx->d_queue + StreamCtx::kQueueSlotQpid * StreamCtx::kSlotInts;
   HIP_TRY(hipMemsetAsync(qc, 0, 16 * sizeof(int), st));
   io.queue = qc;
   hipLaunchKernelGGL(task_kernel<1>, dim3(static_cast<unsigned>(grid)), dim3(64),
@@ -3899,7 +3989,7 @@ static int launch_closed_form(const drc_model_impl* cm, const drc_qpik_params* p
   io.dM = dMi;
   io.dG = dG;
   io.cf_null = nullv;
-  io.queue = cx->d_queue + StreamCtx::kQueueSlotCf * 16;
+  io.queue = cx->d_queue + StreamCtx::kQueueSlotCf * StreamCtx::kSlotInts;
   HIP_TRY(hipMemsetAsync(io.queue, 0, 8 * sizeof(int), st));
   hipLaunchKernelGGL(task_kernel<2>, dim3(static_cast<unsigned>(grid)), dim3(64),
                      static_cast<size_t>(kt.lds_doubles) * sizeof(double), st, m->d_model, kt, io);
@@ -3967,6 +4057,13 @@ int drc_set_concurrency(drc_model* m, int chunks) {
   if (!m || chunks < 1 || chunks > 16) return drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "chunks must be 1..16");
   std::lock_guard<std::mutex> g(m->mu);
   m->chunks = chunks;
+  return DRC_OK;
+}
+
+int drc_debug_lane_stage(drc_model* m, int enable) {
+  if (!m) return drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "null model");
+  std::lock_guard<std::mutex> g(m->launch_mu);
+  m->lane_stage = enable < 0 ? 0 : (enable > 3 ? 3 : enable);
   return DRC_OK;
 }
 

@@ -228,6 +228,17 @@ int drc_debug_kernel_times(drc_model* model, double* wall_ms, double* task_ms, d
  * Results do not depend on it. */
 int drc_set_concurrency(drc_model* model, int chunks);
 
+/* Task stage of drc_qpik_batch / drc_qpik_stages_batch.  0: the
+ * wave-per-instance kernel on every instance (default).  1: the lane-per-instance stage
+ * for the compiled joint counts (6, 7); the instances it hands back (EPA, COD
+ * pseudo-inverse, many GJK candidates) run the wave-per-instance kernel on a
+ * side stream while the QP of the others runs, then their QP.  2: as 1, but
+ * the hand-backs run before one QP pass.  3: the lane stage for
+ * drc_qpik_stages_batch only.  Default 0.  Results agree to rounding (GJK
+ * witness points to their ~1e-6 convergence tolerance); used by the parity
+ * tests and benchmarks. */
+int drc_debug_lane_stage(drc_model* model, int enable);
+
 const char* drc_error_string(int code);
 /* Thread-local detail of the last failing call (parse position, HIP error). */
 const char* drc_last_error(void);

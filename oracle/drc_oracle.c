@@ -706,6 +706,40 @@ static double point_box(const double* c, const Shape* s, double* qw) {
     return sd;
 }
 
+/* Cylinder/cylinder side-to-side closed form: when the closest
+ * points of the two axis segments are interior to both, the connecting line
+ * is normal to both axes and the capsule bound is attained -- the exact
+ * distance hpp-fcl's GJK (robot_data.cpp:424-494 -> fcl::distance) converges
+ * to within its tolerance.  Separated, non-parallel pairs only; kernel twin:
+ * cyl_cyl_side in qpik_device.hpp. */
+static int cyl_cyl_side(const Shape* A, const Shape* B, double* d, double* pA, double* pB) {
+    const double ua[3] = {A->T[2], A->T[5], A->T[8]}, ub[3] = {B->T[2], B->T[5], B->T[8]};
+    double p1[3], p2[3], d1[3], d2[3], r[3];
+    for (int i = 0; i < 3; ++i) {
+        p1[i] = A->T[9 + i] - A->prm[1] * ua[i];
+        p2[i] = B->T[9 + i] - B->prm[1] * ub[i];
+        d1[i] = (2.0 * A->prm[1]) * ua[i];
+        d2[i] = (2.0 * B->prm[1]) * ub[i];
+        r[i] = p1[i] - p2[i];
+    }
+    const double a = dot3(d1, d1), e = dot3(d2, d2), b = dot3(d1, d2), c = dot3(d1, r), f = dot3(d2, r);
+    const double den = a * e - b * b;
+    if (!(den > 1e-12 * a * e)) return 0;
+    const double s = (b * f - c * e) / den, t = (a * f - b * c) / den;
+    if (!(s > 0.0 && s < 1.0 && t > 0.0 && t < 1.0)) return 0;
+    double c1[3], c2[3], n[3];
+    for (int i = 0; i < 3; ++i) { c1[i] = p1[i] + s * d1[i]; c2[i] = p2[i] + t * d2[i]; n[i] = c2[i] - c1[i]; }
+    const double L = norm3(n), dd = L - A->prm[0] - B->prm[0];
+    if (!(dd > 0.0)) return 0;
+    for (int i = 0; i < 3; ++i) {
+        n[i] = (1.0 / L) * n[i];
+        pA[i] = c1[i] + A->prm[0] * n[i];
+        pB[i] = c2[i] - B->prm[0] * n[i];
+    }
+    *d = dd;
+    return 1;
+}
+
 static double shape_distance(const Shape* A, const Shape* B, double* pA, double* pB) {
     if (A->type == 0 && B->type == 0) {
         double v[3];
@@ -730,6 +764,8 @@ static double shape_distance(const Shape* A, const Shape* B, double* pA, double*
         else { memcpy(pA, ps, sizeof(ps)); memcpy(pB, q, sizeof(q)); }
         return sd - s->prm[0];
     }
+    double dside;
+    if (A->type == 1 && B->type == 1 && cyl_cyl_side(A, B, &dside, pA, pB)) return dside;
     SV S[4];
     int ns;
     double lam[4], v[3];
