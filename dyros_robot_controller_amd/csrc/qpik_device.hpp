@@ -424,15 +424,16 @@ DRC_HD __forceinline__ void gjk_run(const Shape& A, const Shape& B, GjkState& g,
 }
 // separation distance and witnesses (valid when !intersect)
 struct GjkDist {
-  int intersect;
+  int intersect, pruned;
   double dist;
   V3 pA, pB;
 };
-DRC_HD inline __noinline__ GjkDist gjk(const Shape A, const Shape B) {
+DRC_HD inline __noinline__ GjkDist gjk(const Shape A, const Shape B, double cut = 1e300) {
   GjkState g;
-  gjk_run(A, B, g);
+  gjk_run(A, B, g, cut);
   GjkDist o;
   o.intersect = g.intersect;
+  o.pruned = g.pruned;
   // witnesses: sum_i lam_i a_i and sum_i lam_i b_i (oracle accumulation order)
   V3 pA = v3(0, 0, 0), pB = v3(0, 0, 0);
 #pragma unroll

@@ -2041,8 +2041,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRC_TAS
         const int ga = M->pair_a[p], gb = M->pair_b[p];
         Shape A{M->gtype[ga], Tg + 12 * ga, M->gparam[ga][0], M->gparam[ga][1], M->gparam[ga][2]};
         Shape Bs{M->gtype[gb], Tg + 12 * gb, M->gparam[gb][0], M->gparam[gb][1], M->gparam[gb][2]};
-        const GjkDist g = gjk(A, Bs);
-        if (g.intersect) {
+        // early exit once GJK's lower bound shows the pair cannot reach ub
+        const GjkDist g = gjk(A, Bs, ub + 1e-9);
+        if (g.pruned) {
+          pf[p] = 1.0;
+        } else if (g.intersect) {
           pf[p] = 2.0;  // penetrating: EPA below
         } else {
           pf[p] = 1.0;
@@ -3461,6 +3464,13 @@ static int upload(drc_model_impl* m) {
 }
 
 // LDS plan: persistent QP region + a union of (kinematics | K^-1 | polish)
+// QPIK QP shapes with a compile-time qp_kernel instantiation (register ADMM
+// on the Schur complement); launch() dispatches on the same list
+static bool qp_compiled(int nx, int ng, int np) {
+  return (nx == 23 && ng == 16 && np == 7) || (nx == 20 && ng == 14 && np == 6) || (nx == 9 && ng == 16 && np == 9) ||
+         (nx == 11 && ng == 16 && np == 11);
+}
+
 static int plan_layout(const DevModel& M, KParams* k, bool task_only) {
   int off = 0;
   auto take = [&](int n) {
@@ -3494,6 +3504,41 @@ static int plan_layout(const DevModel& M, KParams* k, bool task_only) {
   k->oSc = take(32);
   }
   k->oU0 = off;
+  if (!task_only && k->problem == 0) {
+    // QPIK QP kernel: the union holds only what it uses -- the task record
+    // view (q, J, xdd, grad m, grad d, the mobile Jacobian, the task
+    // Jacobian), the factor (Schur blocks for the compiled shapes, K^-1
+    // otherwise) and the polish (index lists, x / y candidates; the
+    // register EQP for KKTs up to kEqpRegCap, which is also ncap: the oracle
+    // applies the same cap).  FR3: ~10 KB per wave instead of ~20.
+    int u = k->oU0;
+    auto takeu = [&](int n) {
+      int o = u;
+      u += (n + 1) & ~1;
+      return o;
+    };
+    k->kq = takeu(nv);
+    k->kJ = takeu(6 * nv);
+    k->kxdd = takeu(6);
+    k->kmg = takeu(k->narm);
+    k->kdg = takeu(nv);
+    k->kSv = takeu(3 * kMaxWheels);
+    k->kJt = takeu(6 * np);
+    const int kin_end = u;
+    const int fac_end = k->oU0 + (qp_compiled(nx, ng, np) ? np * np + ng * np + 4 * ng : nx * nx + nx * ng);
+    const int N = nx + ng < kEqpRegCap ? nx + ng : kEqpRegCap;
+    k->ncap = N;
+    k->nbuf = (N + 7) & ~7;
+    const int reg_pol = k->oU0 + 128 + m;  // Fidx/Ridx | xx | yy
+    const int lds_pol = qp_compiled(nx, ng, np) ? 0 : k->oU0 + 64 + 64 + 128 + k->nbuf * 5 + N * (N + 1) / 2;
+    int end = kin_end;
+    end = end > fac_end ? end : fac_end;
+    end = end > reg_pol ? end : reg_pol;
+    end = end > lds_pol ? end : lds_pol;
+    k->lds_doubles = end;
+    if (end * 8 > 160 * 1024) return set_err(DRC_ERR_UNSUPPORTED, "model too large for the per-wave LDS plan");
+    return DRC_OK;
+  }
   // kinematics view of the union
   int u = k->oU0;
   auto takeu = [&](int n) {
