@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <memory>
@@ -3508,9 +3509,9 @@ static int plan_layout(const DevModel& M, KParams* k, bool task_only) {
     // QPIK QP kernel: the union holds only what it uses -- the task record
     // view (q, J, xdd, grad m, grad d, the mobile Jacobian, the task
     // Jacobian), the factor (Schur blocks for the compiled shapes, K^-1
-    // otherwise) and the polish (index lists, x / y candidates; the
-    // register EQP for KKTs up to kEqpRegCap, which is also ncap: the oracle
-    // applies the same cap).  FR3: ~10 KB per wave instead of ~20.
+    // otherwise) and the polish (index lists, x / y candidates; the LDS
+    // EQP only where a KKT can exceed the register EQP's kEqpRegCap).
+    // FR3: ~10 KB per wave instead of ~20.
     int u = k->oU0;
     auto takeu = [&](int n) {
       int o = u;
@@ -3526,11 +3527,16 @@ static int plan_layout(const DevModel& M, KParams* k, bool task_only) {
     k->kJt = takeu(6 * np);
     const int kin_end = u;
     const int fac_end = k->oU0 + (qp_compiled(nx, ng, np) ? np * np + ng * np + 4 * ng : nx * nx + nx * ng);
+    // the register EQP's size; a larger reduced KKT fails that polish attempt
+    // and ADMM continues (the oracle applies the same cap).  Uncapped, the
+    // whole-body QPs (no variable bounds) solve one more instance in 65 Ki
+    // but the LDS EQP region costs ~7% throughput
     const int N = nx + ng < kEqpRegCap ? nx + ng : kEqpRegCap;
     k->ncap = N;
     k->nbuf = (N + 7) & ~7;
     const int reg_pol = k->oU0 + 128 + m;  // Fidx/Ridx | xx | yy
-    const int lds_pol = qp_compiled(nx, ng, np) ? 0 : k->oU0 + 64 + 64 + 128 + k->nbuf * 5 + N * (N + 1) / 2;
+    const int lds_pol = (qp_compiled(nx, ng, np) && N <= kEqpRegCap) ? 0
+                        : k->oU0 + 64 + 64 + 128 + k->nbuf * 5 + N * (N + 1) / 2;
     int end = kin_end;
     end = end > fac_end ? end : fac_end;
     end = end > reg_pol ? end : reg_pol;
@@ -3720,10 +3726,6 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
     if (rc) return rc;
   }
   HIP_TRY(hipSetDevice(m->device));
-  // grid-stride launches; the task kernel's grid is capped so its per-wave
-  // EPA workspaces (~60 KB each) stay modest
-  const int64_t grid = B < 8192 ? B : 8192;
-  const int64_t grid_task = B < 8192 ? B : 8192;
   // product path: per-instance task records (rLen doubles padded to whole
   // 128-B lines) in a model-owned pool; the stage API writes [field][B]
   const int64_t stride = (kt.rLen + 15) & ~int64_t(15);
@@ -3803,7 +3805,14 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
     if (S > 1) HIP_TRY(hipStreamWaitEvent(cs, cx->fork, 0));
     KParams kt_c = kt, kq_c = kq;
     kt_c.xcd_map = kq_c.xcd_map = Bc >= 16384 ? 1 : 0;
-    const int64_t gq = Bc < 8192 ? Bc : 8192, gt = Bc < 8192 ? Bc : 8192;
+    // persistent grids (work queues hand out the instances): 2048 waves per
+    // kernel and sub-batch keep every SIMD fed while each wave's prologue
+    // (kernel-argument spills, written once per wave) stays a small share of
+    // the HBM writes -- measured sweep in DESIGN.md; DRC_GRID_TASK / _QP
+    // override for such experiments
+    static const int64_t cap_t = getenv("DRC_GRID_TASK") ? atoll(getenv("DRC_GRID_TASK")) : 2048;
+    static const int64_t cap_q = getenv("DRC_GRID_QP") ? atoll(getenv("DRC_GRID_QP")) : 2048;
+    const int64_t gq = Bc < cap_q ? Bc : cap_q, gt = Bc < cap_t ? Bc : cap_t;
     IO io{Bc, b0, B, q, qdot, xt, xdt, xi, xdi, out, status, iters, pose, jac, man, dist, xdd, pair,
           rec ? rec + b0 * stride : nullptr, stride};
     int* qc = cx->d_queue + c * StreamCtx::kSlotInts;  // c < 16 (drc_set_concurrency)

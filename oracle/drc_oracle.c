@@ -1500,7 +1500,9 @@ void oracle_default_params(int kind, OracleParams* p, int exact) {
     s->adaptive_rho = 1; s->adaptive_rho_interval = 25; s->adaptive_rho_tolerance = 5;
     s->polish = exact ? 1 : 0; s->polish_refine_iter = 3; s->delta = 1e-6;
     s->exact = exact; s->eps_exact = 1e-9; s->eps_fallback = 1e-7;
-    s->polish_cap = 16;  /* the kernel's QPIK polish KKT (ncap = kEqpRegCap, register path) */
+    /* the kernel's QPIK polish KKT cap (kEqpRegCap, its register EQP): a
+     * larger reduced KKT fails that polish attempt and ADMM continues */
+    s->polish_cap = 16;
     s->polish_add_all = 1;
 }
 
