@@ -92,3 +92,45 @@ def test_gjk_separated_vs_sampling():
         assert d <= brute + 1e-12 and brute - d < 1e-2
         n += 1
     assert n > 5
+
+
+def _side_case(TA, ra, ha, TB, rb, hb):
+    """The closed-form condition of oracle/drc_oracle.c:cyl_cyl_side."""
+    ua, ub = TA[:3, 2], TB[:3, 2]
+    p1, p2 = TA[:3, 3] - ha * ua, TB[:3, 3] - hb * ub
+    d1, d2, r = 2 * ha * ua, 2 * hb * ub, p1 - p2
+    a, e, b, c, f = d1 @ d1, d2 @ d2, d1 @ d2, d1 @ r, d2 @ r
+    den = a * e - b * b
+    if not den > 1e-12 * a * e:
+        return False
+    s, t = (b * f - c * e) / den, (a * f - b * c) / den
+    return 0 < s < 1 and 0 < t < 1 and np.linalg.norm(p2 + t * d2 - p1 - s * d1) - ra - rb > 0
+
+
+def test_cylinder_side_closed_form_vs_tight_gjk():
+    """the side-to-side cylinder closed form equals the
+    distance an independent GJK (pyref, 1e-12 gap) converges to, and its
+    witnesses are the points that distance is measured between."""
+    import ctypes as C
+    rng = np.random.default_rng(3)
+    hit = 0
+    for _ in range(600):
+        TA, TB = np.eye(4), np.eye(4)
+        TA[:3, :3], TB[:3, :3] = R.so3_exp(rng.normal(size=3) * 2), R.so3_exp(rng.normal(size=3) * 2)
+        TA[:3, 3], TB[:3, 3] = rng.normal(size=3) * 0.1, rng.normal(size=3) * 0.1
+        ra, ha, rb, hb = rng.uniform(0.02, 0.06), rng.uniform(0.05, 0.2), rng.uniform(0.02, 0.06), rng.uniform(0.05, 0.2)
+        if not _side_case(TA, ra, ha, TB, rb, hb):
+            continue
+        ga, gb = dict(type=1, params=np.array([ra, ha, 0])), dict(type=1, params=np.array([rb, hb, 0]))
+        dg, pAg, pBg, inter = R.gjk_distance(ga, TA, gb, TB)
+        assert not inter
+        A12 = np.concatenate([TA[:3, :3].reshape(9), TA[:3, 3]])
+        B12 = np.concatenate([TB[:3, :3].reshape(9), TB[:3, 3]])
+        d = C.c_double()
+        pA, pB = np.zeros(3), np.zeros(3)
+        O.lib().oracle_shape_distance(1, O._ptr(A12), O._ptr(ga["params"]), 1, O._ptr(B12), O._ptr(gb["params"]),
+                                      C.byref(d), O._ptr(pA), O._ptr(pB))
+        assert abs(d.value - dg) <= 1e-10, (d.value, dg)
+        assert abs(np.linalg.norm(pB - pA) - d.value) <= 1e-12
+        hit += 1
+    assert hit >= 30

@@ -1,7 +1,11 @@
 // Host-side harness for the device narrow-phase code (compiled for the CPU,
-// no GPU needed): reads "type T(12) prm(3)" pairs on stdin, prints d pA pB.
-// Used by tests/test_narrow_host.py to check qpik_device.hpp against the
-// oracle's shape_distance.
+// no GPU needed): reads "type T(12) prm(3)" pairs on stdin, prints
+// d pA pB lb cut_pruned: the kernels' per-pair rule (sphere closed forms,
+// side-to-side cylinder closed form, else GJK / EPA), the broad-phase lower
+// bound pair_lower_bound, and whether GJK's early exit fires with a cut just
+// above the distance (it must not: its bound v.w/|v| never exceeds it).  Used by tests/test_narrow_host.py to check
+// qpik_device.hpp against the oracle's shape_distance.
+#include <cmath>
 #include <cstdio>
 #include "../dyros_robot_controller_amd/csrc/qpik_device.hpp"
 using namespace drc_amd;
@@ -20,6 +24,7 @@ int main() {
     V3 pA, pB;
     if (ta == kSphere || tb == kSphere) {
       d = sphere_pair(A, B, &pA, &pB);
+    } else if (ta == kCylinder && tb == kCylinder && cyl_cyl_side(A, B, &d, &pA, &pB)) {
     } else {
       const GjkDist g = gjk(A, B);
       if (g.intersect) {
@@ -32,6 +37,18 @@ int main() {
         pB = g.pB;
       }
     }
-    printf("%.17g %.17g %.17g %.17g %.17g %.17g %.17g\n", d, pA.x, pA.y, pA.z, pB.x, pB.y, pB.z);
+    // bounding radius of the swept core (model.cpp: sphere r, cylinder r,
+    // box |half extents|)
+    auto bound = [](int t, const double* p) {
+      return t == kBox ? std::sqrt(p[0] * p[0] + p[1] * p[1] + p[2] * p[2]) : p[0];
+    };
+    const double lb = (ta == kSphere || tb == kSphere) ? d : pair_lower_bound(A, B, bound(ta, pa), bound(tb, pb));
+    int pruned = 0;
+    if (ta != kSphere && tb != kSphere) {
+      GjkState g;
+      gjk_run(A, B, g, d + 1e-9 * (1 + std::fabs(d)));
+      pruned = g.pruned;
+    }
+    printf("%.17g %.17g %.17g %.17g %.17g %.17g %.17g %.17g %d\n", d, pA.x, pA.y, pA.z, pB.x, pB.y, pB.z, lb, pruned);
   }
 }

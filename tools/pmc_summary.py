@@ -31,17 +31,29 @@ def short(name):
     return None
 
 
-MAIN_GRID = 8192 * 64   # work-items of the bench's task/QP dispatches (grid capped at 8192 waves)
+MAIN_GRID = 2048 * 64   # work-items of the bench's task/QP dispatches (persistent grid: 2048 waves)
+
+
+def bench_rows(rows, grid_key, grid=MAIN_GRID):
+    """The bench's own task/QP dispatches: the workload generator's stage
+    launches (task kernel only) all precede the first QP dispatch, and the
+    bench's first task dispatch immediately precedes it."""
+    rows = [r for r in rows if short(r.get("Kernel_Name", "")) and int(r.get(grid_key, grid)) == grid]
+    ids = [int(r["Dispatch_Id"]) for r in rows if short(r["Kernel_Name"]) == "qp_kernel" and "Dispatch_Id" in r]
+    if not ids:
+        return rows
+    first = min(ids) - 1
+    return [r for r in rows if int(r.get("Dispatch_Id", first)) >= first]
 
 
 def counters(d, cname, grid=MAIN_GRID):
     """Per-kernel average of a counter over the bench's own dispatches (the
-    workload generator's stage launches on instance subsets have smaller grids)."""
+    workload generator's stage launches are excluded, bench_rows)."""
     per = defaultdict(list)
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
-            for row in csv.DictReader(fh):
-                if row.get("Counter_Name") != cname or int(row.get("Grid_Size", grid)) != grid:
+            for row in bench_rows(list(csv.DictReader(fh)), "Grid_Size", grid):
+                if row.get("Counter_Name") != cname:
                     continue
                 k = short(row.get("Kernel_Name", ""))
                 if k:
@@ -54,9 +66,9 @@ def trace_durations(d, grid=MAIN_GRID):
     per = defaultdict(list)
     for f in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
         with open(f) as fh:
-            for row in csv.DictReader(fh):
+            for row in bench_rows(list(csv.DictReader(fh)), "Grid_Size_X", grid):
                 k = short(row.get("Kernel_Name", ""))
-                if k and int(row["Grid_Size_X"]) == grid:
+                if k:
                     per[k].append(float(row["End_Timestamp"]) - float(row["Start_Timestamp"]))
     return {k: sum(v) / len(v) for k, v in per.items()}, {k: len(v) for k, v in per.items()}
 

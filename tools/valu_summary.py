@@ -19,6 +19,8 @@ import sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from pmc_summary import bench_rows  # noqa: E402
 
 
 def short(name):
@@ -35,9 +37,9 @@ def main():
     vals = defaultdict(lambda: defaultdict(list))
     for f in glob.glob(os.path.join(src, "**", "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
-            for row in csv.DictReader(fh):
+            for row in bench_rows(list(csv.DictReader(fh)), "Grid_Size"):   # the bench's own dispatches
                 k = short(row["Kernel_Name"])
-                if k and int(row["Grid_Size"]) == 8192 * 64:   # the bench's own dispatches
+                if k:
                     vals[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
     kern = {}
     for k, cs in vals.items():
