@@ -93,6 +93,89 @@ __device__ __forceinline__ void wave_argmin(double& v, int& idx) {
   idx = bi;
 }
 
+// Lane groups: the QPIK QP kernel packs two instances per wave (32 lanes
+// each, GS = 32); GS = 64 is the whole wave (the helpers above).  Reductions
+// stay inside a group: DPP steps never leave a row of 16 lanes, and the
+// row values of the caller's group are combined through v_readlane (which
+// reads the other group's lanes too, whatever their exec state; only the own
+// group's are used).  bcast takes a lane index uniform across the wave.
+template <int GS>
+struct Grp {
+  static_assert(GS == 64 || GS == 32, "lane groups of 32 or 64");
+  static constexpr int size = GS;
+  static __device__ __forceinline__ int lane() { return threadIdx.x & (GS - 1); }
+  static __device__ __forceinline__ bool upper() { return GS == 32 && (threadIdx.x & 32); }
+  static __device__ __forceinline__ unsigned long long ballot(bool p) {
+    const unsigned long long m = __ballot(p);
+    if constexpr (GS == 64) return m;
+    else return upper() ? (m >> 32) : (m & 0xffffffffull);
+  }
+  static __device__ __forceinline__ bool all(bool p) {
+    if constexpr (GS == 64) return __all(p);
+    else return ballot(!p) == 0;
+  }
+  static __device__ __forceinline__ bool any(bool p) {
+    if constexpr (GS == 64) return __any(p);
+    else return ballot(p) != 0;
+  }
+  static __device__ __forceinline__ double bcast(double v, int k) {
+    if constexpr (GS == 64) return rd_lane(v, k);
+    else {  // lane k of the own group through the LDS crossbar (no LDS memory)
+      const int addr = static_cast<int>(((threadIdx.x & 32) + k) << 2);
+      const long long b = __double_as_longlong(v);
+      const int lo = __builtin_amdgcn_ds_bpermute(addr, static_cast<int>(b));
+      const int hi = __builtin_amdgcn_ds_bpermute(addr, static_cast<int>(b >> 32));
+      return __hiloint2double(hi, lo);
+    }
+  }
+  template <class T>
+  static __device__ __forceinline__ T shfl(T v, int k) { return __shfl(v, k, GS); }
+  static __device__ __forceinline__ double max(double v) {
+    if constexpr (GS == 64) return wave_max(v);
+    else {
+      v = fmax(v, dpp_d<kDppQuad1032>(v));
+      v = fmax(v, dpp_d<kDppQuad2301>(v));
+      v = fmax(v, dpp_d<kDppHalfMirror>(v));
+      v = fmax(v, dpp_d<kDppMirror>(v));
+      const double a = fmax(rd_lane(v, 0), rd_lane(v, 16)), b = fmax(rd_lane(v, 32), rd_lane(v, 48));
+      return upper() ? b : a;
+    }
+  }
+  static __device__ __forceinline__ double sum(double v) {
+    if constexpr (GS == 64) return wave_sum(v);
+    else {
+      v += dpp_d<kDppQuad1032>(v);
+      v += dpp_d<kDppQuad2301>(v);
+      v += dpp_d<kDppHalfMirror>(v);
+      v += dpp_d<kDppMirror>(v);
+      const double a = rd_lane(v, 0) + rd_lane(v, 16), b = rd_lane(v, 32) + rd_lane(v, 48);
+      return upper() ? b : a;
+    }
+  }
+  static __device__ __forceinline__ void argmin(double& v, int& idx) {
+    if constexpr (GS == 64) {
+      wave_argmin(v, idx);
+    } else {
+      argmin_dpp<kDppQuad1032>(v, idx);
+      argmin_dpp<kDppQuad2301>(v, idx);
+      argmin_dpp<kDppHalfMirror>(v, idx);
+      argmin_dpp<kDppMirror>(v, idx);
+      const int r0 = upper() ? 32 : 0;  // lane index from a VGPR: read both groups' rows, select
+      double av = rd_lane(v, 0), bv = rd_lane(v, 32);
+      int ai = __builtin_amdgcn_readlane(idx, 0), bi = __builtin_amdgcn_readlane(idx, 32);
+      argmin_step(av, ai, rd_lane(v, 16), __builtin_amdgcn_readlane(idx, 16));
+      argmin_step(bv, bi, rd_lane(v, 48), __builtin_amdgcn_readlane(idx, 48));
+      v = r0 ? bv : av;
+      idx = r0 ? bi : ai;
+    }
+  }
+  static __device__ __forceinline__ void argmax(double& v, int& idx) {
+    double nv = -v;
+    argmin(nv, idx);
+    v = -nv;
+  }
+};
+
 // ------------------------------------------------------------ 3-vectors
 struct V3 {
   double x, y, z;

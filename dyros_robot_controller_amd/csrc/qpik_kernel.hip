@@ -278,11 +278,14 @@ __device__ void so3_exp(V3 w, double* R) {
 // schur: the register ADMM solves K x~ = rhs through the Schur complement of
 // K's auxiliary block (every variable past np — slacks — sits in exactly one G
 // row, so that block is diagonal): S = K_cc - K_ca D^-1 K_ac is np x np.
-template <int NX, int NG, int NP, bool REG = (NX > 0), bool SCHUR = false>
+// gs: lanes per instance (64, or 32 = two instances per wave; the QPIK
+// shapes whose n + NG Schur lanes and polish rows fit in 32).
+template <int NX, int NG, int NP, bool REG = (NX > 0), bool SCHUR = false, int GS = 64>
 struct Dims {
   static constexpr int nx = NX, ng = NG, np = NP;
   static constexpr bool reg = REG;
   static constexpr bool schur = SCHUR;
+  static constexpr int gs = GS;
 };
 #define DNX (QD::nx ? QD::nx : kp.nx)
 #define DNG (QD::ng ? QD::ng : kp.ng)
@@ -295,9 +298,10 @@ struct Dims {
 template <class QD, bool UNSCALED = true>
 __device__ __forceinline__ void residuals(const KParams& kp, double* S, const double* x, const double* z, const double* y,
                           double eps_abs, double eps_rel) {
+  using GL = Grp<QD::gs>;
   // UNSCALED = false (the polish's certification) skips the unscaled norms
   // that only adaptive rho reads (SC_PRIS .. SC_NQ keep the ADMM values)
-  const int l = lane_id(), nx = DNX, ng = DNG, np = DNP;
+  const int l = GL::lane(), nx = DNX, ng = DNG, np = DNP;
   const double *P = S + kp.oP, *G = S + kp.oG, *q = S + kp.oQ, *ab = S + kp.oAB, *D = S + kp.oD, *E = S + kp.oE;
   double pr = 0, prs = 0, nAx = 0, nz = 0, nAxs = 0, nzs = 0;
   double dr = 0, drs = 0, nPx = 0, nAty = 0, nq = 0, nPxs = 0, nAtys = 0, nqs = 0;
@@ -343,21 +347,21 @@ __device__ __forceinline__ void residuals(const KParams& kp, double* S, const do
     nAxs = fmax(nAxs, fabs(ax));
     nzs = fmax(nzs, fabs(z[row]));
   }
-  pr = wave_max(pr);
-  nAx = wave_max(nAx);
-  nz = wave_max(nz);
-  dr = wave_max(dr);
-  nPx = wave_max(nPx);
-  nAty = wave_max(nAty);
-  nq = wave_max(nq);
+  pr = GL::max(pr);
+  nAx = GL::max(nAx);
+  nz = GL::max(nz);
+  dr = GL::max(dr);
+  nPx = GL::max(nPx);
+  nAty = GL::max(nAty);
+  nq = GL::max(nq);
   if constexpr (UNSCALED) {
-    prs = wave_max(prs);
-    nAxs = wave_max(nAxs);
-    nzs = wave_max(nzs);
-    drs = wave_max(drs);
-    nPxs = wave_max(nPxs);
-    nAtys = wave_max(nAtys);
-    nqs = wave_max(nqs);
+    prs = GL::max(prs);
+    nAxs = GL::max(nAxs);
+    nzs = GL::max(nzs);
+    drs = GL::max(drs);
+    nPxs = GL::max(nPxs);
+    nAtys = GL::max(nAtys);
+    nqs = GL::max(nqs);
   }
   double c = S[kp.oSc + SC_C];
   if (l == 0) {
@@ -382,7 +386,8 @@ __device__ __forceinline__ void residuals(const KParams& kp, double* S, const do
 // K = P + sigma I + A^T diag(rho) A, inverted in place (Gauss-Jordan, SPD)
 template <class QD>
 __device__ __forceinline__ void factor_kinv(const KParams& kp, double* S) {
-  const int l = lane_id(), nx = DNX, ng = DNG, np = DNP;
+  using GL = Grp<QD::gs>;
+  const int l = GL::lane(), nx = DNX, ng = DNG, np = DNP;
   const double *P = S + kp.oP, *G = S + kp.oG, *ab = S + kp.oAB, *rho = S + kp.oRho;
   double* K = S + kp.oU0;
   if (l < nx) {
@@ -416,8 +421,9 @@ __device__ __forceinline__ void factor_kinv(const KParams& kp, double* S) {
 __device__ __forceinline__ double bcast(double v, int lane);
 template <class QD>
 __device__ __noinline__ void factor_kinv_regs(const KParams& kp, double* S) {
+  using GL = Grp<QD::gs>;
   constexpr int NX = QD::nx, NG = QD::ng, NP = QD::np;
-  const int l = lane_id();
+  const int l = GL::lane();
   const double *P = S + kp.oP, *G = S + kp.oG, *ab = S + kp.oAB, *rho = S + kp.oRho;
   double* K = S + kp.oU0;
   if (l < NX) {  // row l of K = P + sigma I + A^T diag(rho) A (LDS, as factor_kinv)
@@ -445,7 +451,7 @@ __device__ __noinline__ void factor_kinv_regs(const KParams& kp, double* S) {
     if (l != k) Kr[k] = 0.0;
 #pragma unroll
     for (int j = 0; j < NX; ++j) {
-      const double rkj = bcast(Kr[j], k);
+      const double rkj = GL::bcast(Kr[j], k);
       if (l != k) Kr[j] -= f * rkj;
     }
   }
@@ -469,8 +475,9 @@ __device__ __noinline__ void factor_kinv_regs(const KParams& kp, double* S) {
 // ------------------------------------------------------------------------
 template <class QD>
 __device__ __noinline__ void schur_setup(const KParams& kp, double* S) {
+  using GL = Grp<QD::gs>;
   constexpr int NX = QD::nx, NG = QD::ng, NP = QD::np;
-  const int l = lane_id();
+  const int l = GL::lane();
   const double *P = S + kp.oP, *G = S + kp.oG, *ab = S + kp.oAB, *rho = S + kp.oRho;
   double* Si = S + kp.oU0;             // NP x NP
   double* GS = Si + NP * NP;           // NG x NP
@@ -525,7 +532,7 @@ __device__ __noinline__ void schur_setup(const KParams& kp, double* S) {
     if (l != k) Sr[k] = 0.0;
 #pragma unroll
     for (int j = 0; j < NP; ++j) {
-      const double rkj = bcast(Sr[j], k);
+      const double rkj = GL::bcast(Sr[j], k);
       if (l != k) Sr[j] -= f * rkj;
     }
   }
@@ -534,7 +541,7 @@ __device__ __noinline__ void schur_setup(const KParams& kp, double* S) {
     for (int c = 0; c < NP; ++c) Si[l * NP + c] = Sr[c];
   }
   wsync();
-  for (int e = l; e < NG * NP; e += 64) {  // G_c S^-1
+  for (int e = l; e < NG * NP; e += GL::size) {  // G_c S^-1
     const int r = e / NP, c = e % NP;
     double sv = 0;
 #pragma unroll
@@ -553,10 +560,11 @@ __device__ __forceinline__ void factor_any(const KParams& kp, double* S) {
 
 template <class QD>
 __device__ __forceinline__ void set_rho(const KParams& kp, double* S, double rho) {
-  const int l = lane_id(), nx = DNX, ng = DNG;
+  using GL = Grp<QD::gs>;
+  const int l = GL::lane(), nx = DNX, ng = DNG;
   const double *lo = S + kp.oL, *up = S + kp.oU;
   double* rv = S + kp.oRho;
-  for (int row = l; row < nx + ng; row += 64) {
+  for (int row = l; row < nx + ng; row += GL::size) {
     double a = lo[row], b = up[row];
     bool loose = a < -kInf * kMinScaling && b > kInf * kMinScaling;
     bool eq = !loose && b - a < kRhoTol;
@@ -569,12 +577,13 @@ __device__ __forceinline__ void set_rho(const KParams& kp, double* S, double rho
 // Primal infeasibility certificate (OSQP / Banjac et al.) on the last dy
 template <class QD>
 __device__ __forceinline__ bool primal_infeasible(const KParams& kp, double* S, double eps) {
-  const int l = lane_id(), nx = DNX, ng = DNG;
+  using GL = Grp<QD::gs>;
+  const int l = GL::lane(), nx = DNX, ng = DNG;
   const double *lo = S + kp.oL, *up = S + kp.oU, *E = S + kp.oE, *dyv = S + kp.oDY, *G = S + kp.oG,
                *ab = S + kp.oAB, *D = S + kp.oD;
   double* dy = S + kp.oT1;
   double nrm = 0, lhs = 0;
-  for (int row = l; row < nx + ng; row += 64) {
+  for (int row = l; row < nx + ng; row += GL::size) {
     double d = dyv[row], a = lo[row], b = up[row];
     bool lb_inf = a < -kInf * kMinScaling, ub_inf = b > kInf * kMinScaling;
     if (lb_inf && ub_inf) d = 0;
@@ -584,8 +593,8 @@ __device__ __forceinline__ bool primal_infeasible(const KParams& kp, double* S, 
     nrm = fmax(nrm, fabs(E[row] * d));
     lhs += d > 0 ? b * d : (d < 0 ? a * d : 0.0);
   }
-  nrm = wave_max(nrm);
-  lhs = wave_sum(lhs);
+  nrm = GL::max(nrm);
+  lhs = GL::sum(lhs);
   wsync();
   if (nrm <= kDivTol || !(lhs < -eps * nrm)) return false;
   double viol = 0;
@@ -594,7 +603,7 @@ __device__ __forceinline__ bool primal_infeasible(const KParams& kp, double* S, 
     for (int i = 0; i < ng; ++i) s += G[i * nx + l] * dy[nx + i];
     viol = fabs(s / D[l]);
   }
-  viol = wave_max(viol);
+  viol = GL::max(viol);
   return viol < eps * nrm;
 }
 
@@ -617,13 +626,14 @@ __device__ __forceinline__ double bcast(double v, int lane) {
 // so the ADMM loop's register file stays free)
 template <class QD>
 __device__ __noinline__ void prep_admm_mats(const KParams& kp, double* S) {
+  using GL = Grp<QD::gs>;
   if constexpr (QD::schur) return;  // schur_setup already formed G_c S^-1
   constexpr int NX = QD::nx, NG = QD::ng;
-  const int l = lane_id();
+  const int l = GL::lane();
   const double* K = S + kp.oU0;
   double* GK = S + kp.oU0 + NX * NX;
   const double* G = S + kp.oG;
-  for (int e = l; e < NG * NX; e += 64) {
+  for (int e = l; e < NG * NX; e += GL::size) {
     const int i = e / NX, c = e % NX;
     double s = 0;
     for (int k = 0; k < NX; ++k) s += G[i * NX + k] * K[k * NX + c];
@@ -636,8 +646,9 @@ __device__ __noinline__ void prep_admm_mats(const KParams& kp, double* S) {
 template <class QD>
 __device__ __forceinline__ void load_admm_regs(const KParams& kp, const double* S, double (&Gc)[QD::ng],
                                                double (&Kr)[QD::nx], double (&GKr)[QD::nx]) {
+  using GL = Grp<QD::gs>;
   constexpr int NX = QD::nx, NG = QD::ng;
-  const int l = lane_id();
+  const int l = GL::lane();
   const double* K = S + kp.oU0;
   const double* GK = S + kp.oU0 + NX * NX;
   const double* G = S + kp.oG;
@@ -670,6 +681,7 @@ __device__ __forceinline__ void load_admm_regs(const KParams& kp, const double* 
 #endif
 template <class QD>
 __device__ __noinline__ int admm_check(const KParams& kp, double* S, int it, int check, int adapt, int* status) {
+  using GL = Grp<QD::gs>;
   double *x = S + kp.oX, *z = S + kp.oZ, *y = S + kp.oY, *sc = S + kp.oSc;
   int reload = 0;
   CK_T0();
@@ -679,7 +691,7 @@ __device__ __noinline__ int admm_check(const KParams& kp, double* S, int it, int
   if (check) {
     const bool conv = sc[SC_PRI] < sc[SC_EPSP] && sc[SC_DUA] < sc[SC_EPSD];
 #ifdef DRC_QP_DEBUG
-    if (lane_id() == 0 && it <= 200)
+    if (GL::lane() == 0 && it <= 200)
       printf("it %d rho %.4g pri %.3e/%.3e dua %.3e/%.3e x3 %.6f\n", it, sc[SC_RHO], sc[SC_PRI], sc[SC_EPSP],
              sc[SC_DUA], sc[SC_EPSD], x[3] * S[kp.oD + 3]);
 #endif
@@ -696,7 +708,7 @@ __device__ __noinline__ int admm_check(const KParams& kp, double* S, int it, int
         *status = DRC_STATUS_SOLVED;
         return 2;
       }
-      if (lane_id() == 0) sc[SC_PFAIL] += 1.0;
+      if (GL::lane() == 0) sc[SC_PFAIL] += 1.0;
       factor_any<QD>(kp, S);
       CK_T(38);  // polish used the union region
       residuals<QD>(kp, S, x, z, y, kp.s.eps_abs, kp.s.eps_rel);
@@ -717,7 +729,7 @@ __device__ __noinline__ int admm_check(const KParams& kp, double* S, int it, int
           *status = DRC_STATUS_SOLVED;
           return 2;
         }
-        if (lane_id() == 0) sc[SC_PFAIL] += 1.0;
+        if (GL::lane() == 0) sc[SC_PFAIL] += 1.0;
         factor_any<QD>(kp, S);
         CK_T(38);
       }
@@ -789,8 +801,9 @@ constexpr int kEqpRegCap = 16;
 template <class QD>
 __device__ __forceinline__ bool eqp_regs(const KParams& kp, double* S, int actb, int actg, double* xx, double* yy,
                                          unsigned long long freeMask, unsigned long long rowMask, int nF, int nR) {
+  using GL = Grp<QD::gs>;
   constexpr int NX = QD::nx, NG = QD::ng, NP = QD::np, M = NX + NG, NK = kEqpRegCap;
-  const int l = lane_id(), N = nF + nR;
+  const int l = GL::lane(), N = nF + nR;
   const double *P = S + kp.oP, *G = S + kp.oG, *q = S + kp.oQ, *ab = S + kp.oAB, *lo = S + kp.oL,
                *up = S + kp.oU;
   int* Fidx = reinterpret_cast<int*>(S + kp.oU0);  // 64 ints
@@ -822,7 +835,7 @@ __device__ __forceinline__ bool eqp_regs(const KParams& kp, double* S, int actb,
   }
   const bool hf = l < nF, hr = l >= nF && l < N;
   const int fi = hf ? Fidx[l] : 0, gi = hr ? Ridx[l - nF] : 0;
-  const double rF_ = __shfl(rF, fi, 64), rG_ = __shfl(rG, gi, 64);
+  const double rF_ = GL::shfl(rF, fi), rG_ = GL::shfl(rG, gi);
   const double rhs = hf ? rF_ : (hr ? rG_ : 0.0);
   // row l of K0: columns j < nF are the free variables, j >= nF the active rows
   double K0[NK], Ki[NK];
@@ -849,7 +862,7 @@ __device__ __forceinline__ bool eqp_regs(const KParams& kp, double* S, int actb,
 #pragma unroll
   for (int k = 0; k < NK; ++k) {
     if (k >= N) break;
-    const double piv = bcast(Ki[k], k);
+    const double piv = GL::bcast(Ki[k], k);
     if (piv == 0.0) return false;  // uniform
     if (l == k) {
       const double p = 1.0 / Ki[k];
@@ -862,7 +875,7 @@ __device__ __forceinline__ bool eqp_regs(const KParams& kp, double* S, int actb,
 #pragma unroll
     for (int j = 0; j < NK; ++j) {
       if (j >= N) break;
-      const double rkj = bcast(Ki[j], k);
+      const double rkj = GL::bcast(Ki[j], k);
       if (l != k) Ki[j] -= f * rkj;
     }
   }
@@ -871,7 +884,7 @@ __device__ __forceinline__ bool eqp_regs(const KParams& kp, double* S, int actb,
 #pragma unroll
     for (int j = 0; j < NK; ++j) {
       if (j >= N) break;
-      const double vj = bcast(v, j);
+      const double vj = GL::bcast(v, j);
       if (j & 1) s1 += A[j] * vj;
       else s0 += A[j] * vj;
     }
@@ -883,7 +896,7 @@ __device__ __forceinline__ bool eqp_regs(const KParams& kp, double* S, int actb,
     sol += apply(Ki, res);
   }
   if (hf) xx[fi] = sol;
-  for (int row = l; row < M; row += 64) yy[row] = 0.0;
+  for (int row = l; row < M; row += GL::size) yy[row] = 0.0;
   wsync();
   if (hr) yy[NX + gi] = sol;
   wsync();
@@ -911,11 +924,12 @@ __device__ __forceinline__ bool eqp_regs(const KParams& kp, double* S, int actb,
 // Flags: actb (bound row l) / actg (G row l) held by lane l.
 template <class QD>
 __device__ __forceinline__ bool eqp(const KParams& kp, double* S, int actb, int actg, double* xx, double* yy) {
-  const int l = lane_id(), nx = DNX, ng = DNG, np = DNP, m = DM;
+  using GL = Grp<QD::gs>;
+  const int l = GL::lane(), nx = DNX, ng = DNG, np = DNP, m = DM;
   const double *P = S + kp.oP, *G = S + kp.oG, *q = S + kp.oQ, *ab = S + kp.oAB, *lo = S + kp.oL,
                *up = S + kp.oU;
-  unsigned long long freeMask = __ballot(l < nx && actb == 0);
-  unsigned long long rowMask = __ballot(l < ng && actg != 0);
+  unsigned long long freeMask = GL::ballot(l < nx && actb == 0);
+  unsigned long long rowMask = GL::ballot(l < ng && actg != 0);
   const int nF = __popcll(freeMask), nR = __popcll(rowMask), N = nF + nR;
   if (N > kp.ncap) return false;  // uniform: this polish attempt fails, ADMM continues
 #ifdef DRC_PHASE_TIMING
@@ -925,6 +939,9 @@ __device__ __forceinline__ bool eqp(const KParams& kp, double* S, int actb, int 
     atomicAdd(&g_phase_cycles[42], (unsigned long long)N);
   }
 #endif
+  if constexpr (QD::gs < 64) {  // two instances per wave: register EQP only (ncap <= kEqpRegCap)
+    if (N > kEqpRegCap) return false;
+  }
   if constexpr (QD::nx > 0) {
     if (N <= kEqpRegCap) {
       const bool ok_ = eqp_regs<QD>(kp, S, actb, actg, xx, yy, freeMask, rowMask, nF, nR);
@@ -949,7 +966,7 @@ __device__ __forceinline__ bool eqp(const KParams& kp, double* S, int actb, int 
   if (l < nx) xx[l] = actb == 0 ? 0.0 : (actb < 0 ? lo[l] : up[l]) / ab[l];
   wsync();
   const double dl = kp.s.delta;
-  for (int i = l; i < N; i += 64) {  // K (packed rows i >= j) and rhs; lane i owns row i
+  for (int i = l; i < N; i += GL::size) {  // K (packed rows i >= j) and rhs; lane i owns row i
     if (i < nF) {
       int fi = Fidx[i];
       for (int j = 0; j <= i; ++j) {
@@ -982,13 +999,13 @@ __device__ __forceinline__ bool eqp(const KParams& kp, double* S, int actb, int 
   }
   wsync();
   for (int j = 0; j < N; ++j) {  // left-looking LDL^T, in place
-    for (int k = l; k < j; k += 64) vv[k] = L[pk(j, k)] * dg[k];
+    for (int k = l; k < j; k += GL::size) vv[k] = L[pk(j, k)] * dg[k];
     wsync();
     double part = 0;
-    for (int k = l; k < j; k += 64) part += L[pk(j, k)] * vv[k];
-    double dj = L[pk(j, j)] - wave_sum(part);
+    for (int k = l; k < j; k += GL::size) part += L[pk(j, k)] * vv[k];
+    double dj = L[pk(j, j)] - GL::sum(part);
     if (dj == 0.0) return false;  // uniform
-    for (int i = l; i < N; i += 64)
+    for (int i = l; i < N; i += GL::size)
       if (i > j) {
         double t = L[pk(i, j)];
         for (int k = 0; k < j; ++k) t -= L[pk(i, k)] * vv[k];
@@ -997,11 +1014,11 @@ __device__ __forceinline__ bool eqp(const KParams& kp, double* S, int actb, int 
     if (l == 0) dg[j] = dj;
     wsync();
   }
-  for (int i = l; i < N; i += 64) sol[i] = rhs[i];
+  for (int i = l; i < N; i += GL::size) sol[i] = rhs[i];
   wsync();
   ldl_solve(L, dg, N, sol);
   for (int it = 0; it < kp.s.polish_refine_iter; ++it) {
-    for (int i = l; i < N; i += 64) {
+    for (int i = l; i < N; i += GL::size) {
       double r = rhs[i];
       if (i < nF) {
         int fi = Fidx[i];
@@ -1019,13 +1036,13 @@ __device__ __forceinline__ bool eqp(const KParams& kp, double* S, int actb, int 
     }
     wsync();
     ldl_solve(L, dg, N, res);
-    for (int i = l; i < N; i += 64) sol[i] += res[i];
+    for (int i = l; i < N; i += GL::size) sol[i] += res[i];
     wsync();
   }
-  for (int i = l; i < nF; i += 64) xx[Fidx[i]] = sol[i];
-  for (int row = l; row < m; row += 64) yy[row] = 0.0;
+  for (int i = l; i < nF; i += GL::size) xx[Fidx[i]] = sol[i];
+  for (int row = l; row < m; row += GL::size) yy[row] = 0.0;
   wsync();
-  for (int k = l; k < nR; k += 64) yy[nx + Ridx[k]] = sol[nF + k];
+  for (int k = l; k < nR; k += GL::size) yy[nx + Ridx[k]] = sol[nF + k];
   wsync();
   if (l < nx && actb != 0) {  // bound multipliers from stationarity
     double g = q[l];
@@ -1050,7 +1067,8 @@ __device__ __forceinline__ bool eqp(const KParams& kp, double* S, int actb, int 
 constexpr int kPolishFeasAttempts = 4, kPolishAsIters = 24;
 template <class QD>
 __device__ __forceinline__ bool polish(const KParams& kp, double* S, bool strict) {
-  const int l = lane_id(), nx = DNX, ng = DNG, np = DNP, m = DM;
+  using GL = Grp<QD::gs>;
+  const int l = GL::lane(), nx = DNX, ng = DNG, np = DNP, m = DM;
   const double *G = S + kp.oG, *ab = S + kp.oAB, *lo = S + kp.oL, *up = S + kp.oU, *E = S + kp.oE;
   double *x = S + kp.oX, *z = S + kp.oZ, *y = S + kp.oY;
   (void)np;
@@ -1077,7 +1095,7 @@ __device__ __forceinline__ bool polish(const KParams& kp, double* S, bool strict
       // manipulability gradient of the first/last joint).  When the fixed
       // values already satisfy it strictly it is not active: drop it (the
       // oracle's qp_polish applies the same rule)
-      const unsigned long long fixed = __ballot(l < nx && actb != 0), atup = __ballot(l < nx && actb > 0);
+      const unsigned long long fixed = GL::ballot(l < nx && actb != 0), atup = GL::ballot(l < nx && actb > 0);
       if (l < ng && actg != 0) {
         const int lg = l < ng ? l : 0, row = nx + lg;
         double sf = 0, sa = 0, act = 0;
@@ -1099,8 +1117,8 @@ __device__ __forceinline__ bool polish(const KParams& kp, double* S, bool strict
         stepmax = fabs(xx[l] - xc[l]);
         xnorm = fabs(xc[l]);
       }
-      stepmax = wave_max(stepmax);
-      xnorm = wave_max(xnorm);
+      stepmax = GL::max(stepmax);
+      xnorm = GL::max(xnorm);
       if (stepmax > 1e-12 * (1 + xnorm)) {
         // ratio test along p = xx - xc over the inactive rows
         double amin = 1.0;
@@ -1126,7 +1144,7 @@ __device__ __forceinline__ bool polish(const KParams& kp, double* S, bool strict
           if (a < amin) { amin = a; blk = row; side = sd; }
         }
         int enc = blk == 0x7fffffff ? blk : blk * 4 + (side + 1);
-        wave_argmin(amin, enc);
+        GL::argmin(amin, enc);
         const double alpha = amin < 0 ? 0.0 : amin;
         wsync();
         if (l < nx) xc[l] += alpha * (xx[l] - xc[l]);
@@ -1175,11 +1193,11 @@ __device__ __forceinline__ bool polish(const KParams& kp, double* S, bool strict
         double yi = E[nx + l] * yy[nx + l] / c, viol = actg < 0 ? yi - epsd : -yi - epsd;
         if (viol > wv) { wv = viol; worst = nx + l; }
       }
-      wave_argmax(wv, worst);
+      GL::argmax(wv, worst);
       if (worst != 0x7fffffff) ok = false;
 #ifdef DRC_QP_DEBUG
       {
-        const unsigned long long fb = __ballot(l < nx && actb != 0), fg = __ballot(l < ng && actg != 0);
+        const unsigned long long fb = GL::ballot(l < nx && actb != 0), fg = GL::ballot(l < ng && actg != 0);
         if (l == 0)
           printf("polish it %d feas %d pri %.2e dua %.2e worst %d (%.2e) havefeas %d bmask %llx gmask %llx\n", it,
                  (int)feasible, pr1, dr1, worst, wv, (int)have_feas, fb, fg);
@@ -1192,7 +1210,7 @@ __device__ __forceinline__ bool polish(const KParams& kp, double* S, bool strict
     }
     if (ok) {
       if (l < nx) x[l] = xx[l];
-      for (int row = l; row < m; row += 64) {
+      for (int row = l; row < m; row += GL::size) {
         y[row] = yy[row];
         z[row] = zz[row];
       }
@@ -1232,7 +1250,7 @@ __device__ __forceinline__ bool polish(const KParams& kp, double* S, bool strict
         if (vhi > av) { av = vhi; add = row * 4 + 2; }
       }
       CK_N(45);
-      if (!__any(sb != 0 || sg != 0)) {
+      if (!GL::any(sb != 0 || sg != 0)) {
         if (worst == 0x7fffffff) break;
         if (worst < nx) { if (l == worst) actb = 0; }
         else if (l == worst - nx) actg = 0;
@@ -1240,7 +1258,7 @@ __device__ __forceinline__ bool polish(const KParams& kp, double* S, bool strict
         if (sb) actb = sb;
         if (sg) actg = sg;
       } else {
-        wave_argmax(av, add);
+        GL::argmax(av, add);
         const int row = add >> 2, sd = (add & 3) - 1;
         if (row < nx) { if (l == row) actb = sd; }
         else if (l == row - nx) actg = sd;
@@ -1286,6 +1304,37 @@ struct InstSeq {
     int v = 0;
     if (lane_id() == 0) v = atomicAdd(queue + (map ? xcd : 0), 1);
     return __builtin_amdgcn_readfirstlane(v);
+  }
+  __device__ __forceinline__ int64_t first() const { return queue ? fetch() : j0; }
+  __device__ __forceinline__ int64_t next(int64_t j) const { return queue ? fetch() : j + step; }
+  __device__ __forceinline__ int64_t at(int64_t j) const {
+    return map ? ((((j >> 4) << 3) + xcd) << 4) + (j & 15) : j;
+  }
+};
+
+// InstSeq for lane groups: each group of GS lanes is its own consumer (its
+// leader lane takes the queue position; with a fixed stride the groups of a
+// wave interleave).
+template <int GS>
+struct InstSeqG {
+  int64_t j0, step, n;
+  int xcd, map;
+  int* queue;
+  __device__ __forceinline__ InstSeqG(int64_t B, int map_, int* queue_ = nullptr) {
+    constexpr int G = 64 / GS;
+    const int g = GS == 64 ? 0 : ((threadIdx.x >> 5) & 1);
+    map = map_;
+    queue = queue_;
+    xcd = blockIdx.x & 7;
+    j0 = (map ? (blockIdx.x >> 3) : blockIdx.x) * G + g;
+    step = (map ? (gridDim.x >> 3) : gridDim.x) * G;
+    n = map ? ((B + 127) >> 7) << 4 : B;
+  }
+  __device__ __forceinline__ int64_t fetch() const {
+    int v = 0;
+    if (Grp<GS>::lane() == 0) v = atomicAdd(queue + (map ? xcd : 0), 1);
+    if constexpr (GS == 64) return __builtin_amdgcn_readfirstlane(v);
+    else return Grp<GS>::shfl(v, 0);
   }
   __device__ __forceinline__ int64_t first() const { return queue ? fetch() : j0; }
   __device__ __forceinline__ int64_t next(int64_t j) const { return queue ? fetch() : j + step; }
@@ -1389,10 +1438,11 @@ __device__ __forceinline__ void body_velocity(const DevModel* M, const double* T
 // model table for the configuration-independent drives; a caster base's
 // depends on the steer angles q[mobi_start + 2i] and is evaluated by lane 0.
 // Wave-uniform call (contains a wave barrier).
+template <int GS = 64>
 __device__ __forceinline__ const double (*mobile_jac(const DevModel* M, const KParams& kp, double* S,
                                                      const double* q))[kMaxWheels] {
   double(*Jm)[kMaxWheels] = reinterpret_cast<double(*)[kMaxWheels]>(S + kp.kSv);
-  const int l = lane_id();
+  const int l = Grp<GS>::lane();
   if (M->drive == kDriveCaster) {
     if (l == 0) mobile_fk(M, q + M->mobi_start, Jm);
   } else if (l < 3 * kMaxWheels) {
@@ -2264,7 +2314,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRC_TAS
 // ---- QP kernel phases ------------------------------------------------------
 template <class QD>
 __device__ __forceinline__ void qp_assemble(const DevModel* M, const KParams& kp, double* S, const IO& io, int64_t b) {
-  const int l = lane_id();
+  using GL = Grp<QD::gs>;
+  const int l = GL::lane();
   const int nv = kp.nv, narm = kp.narm;
   double* qv = S + kp.kq;
   double* J = S + kp.kJ;
@@ -2276,7 +2327,7 @@ __device__ __forceinline__ void qp_assemble(const DevModel* M, const KParams& kp
 #endif
   {  // task record written by task_kernel (one coalesced read)
     const double* rec = io.rec + b * io.rec_stride;
-    for (int e = l; e < kp.rLen; e += 64) {
+    for (int e = l; e < kp.rLen; e += GL::size) {
       const double v = rec[e];
       if (e < kp.rMan) J[e] = v;
       else if (e == kp.rMan) S[kp.oSc + SC_MAN] = v;
@@ -2289,7 +2340,7 @@ __device__ __forceinline__ void qp_assemble(const DevModel* M, const KParams& kp
   }
   wsync();
 #ifdef DRC_PHASE_TIMING
-  if (lane_id() == 0) atomicAdd(&g_phase_cycles[44], __builtin_amdgcn_s_memtime() - as_t0);
+  if (GL::lane() == 0) atomicAdd(&g_phase_cycles[44], __builtin_amdgcn_s_memtime() - as_t0);
 #endif
   const double bestd = S[kp.oSc + SC_DIST];
   // ---------------- QP assembly (QP_IK.cpp:69-131 / MoMa :59-128) --------
@@ -2298,12 +2349,12 @@ __device__ __forceinline__ void qp_assemble(const DevModel* M, const KParams& kp
   const double alpha = kp.alpha_cbf, man = S[kp.oSc + SC_MAN];
   double* Jt = S + kp.kJt;  // task Jacobian over the QP's task variables: 6 x np
   if (M->kind == 0) {
-    for (int e = l; e < 6 * np; e += 64) Jt[e] = J[(e / np) * nv + e % np];
+    for (int e = l; e < 6 * np; e += GL::size) Jt[e] = J[(e / np) * nv + e % np];
   } else {
     // J~ = J S  (mobile_manipulator/robot_data.cpp:407-410); S virtual block = Rz(yaw) J_mobile
     const double yaw = qv[M->virtual_start + 2], cy = cos(yaw), sy = sin(yaw);
-    const double(*Jm)[kMaxWheels] = mobile_jac(M, kp, S, qv);
-    for (int e = l; e < 6 * np; e += 64) {
+    const double(*Jm)[kMaxWheels] = mobile_jac<QD::gs>(M, kp, S, qv);
+    for (int e = l; e < 6 * np; e += GL::size) {
       const int r = e / np, a = e % np;
       double v = 0;
       const int am = a - M->act_mani_start, aw = a - M->act_mobi_start;
@@ -2320,13 +2371,13 @@ __device__ __forceinline__ void qp_assemble(const DevModel* M, const KParams& kp
     }
   }
   wsync();
-  for (int e = l; e < np * np; e += 64) {
+  for (int e = l; e < np * np; e += GL::size) {
     const int i = e / np, j = e % np;
     double s = 0;
     for (int r = 0; r < 6; ++r) s += Jt[r * np + i] * Jt[r * np + j];
     P[e] = 2.0 * s + (i == j ? kp.w_reg : 0.0);
   }
-  for (int e = l; e < ng * nx; e += 64) G[e] = 0.0;
+  for (int e = l; e < ng * nx; e += GL::size) G[e] = 0.0;
   if (l < nx) {
     double qi;
     if (l < np) {
@@ -2380,23 +2431,24 @@ __device__ __forceinline__ void qp_assemble(const DevModel* M, const KParams& kp
 // DRC_STATUS_NONFINITE or DRC_STATUS_MAX_ITER (= not yet solved)
 template <class QD>
 __device__ __forceinline__ int qp_scale(const KParams& kp, double* S) {
-  const int l = lane_id();
+  using GL = Grp<QD::gs>;
+  const int l = GL::lane();
   const int nx = DNX, ng = DNG, np = DNP, m = DM;
   double *P = S + kp.oP, *G = S + kp.oG, *qq = S + kp.oQ, *ab = S + kp.oAB, *lo = S + kp.oL, *up = S + kp.oU;
   int status = DRC_STATUS_MAX_ITER;
   {
     bool finite = true;
-    for (int e = l; e < np * np; e += 64) finite &= isfinite(P[e]);
-    for (int e = l; e < ng * nx; e += 64) finite &= isfinite(G[e]);
+    for (int e = l; e < np * np; e += GL::size) finite &= isfinite(P[e]);
+    for (int e = l; e < ng * nx; e += GL::size) finite &= isfinite(G[e]);
     if (l < nx) finite &= isfinite(qq[l]);
-    for (int row = l; row < m; row += 64) finite &= !isnan(lo[row]) && !isnan(up[row]);
-    if (!__all(finite)) status = DRC_STATUS_NONFINITE;
+    for (int row = l; row < m; row += GL::size) finite &= !isnan(lo[row]) && !isnan(up[row]);
+    if (!GL::all(finite)) status = DRC_STATUS_NONFINITE;
   }
   double *D = S + kp.oD, *E = S + kp.oE, *x = S + kp.oX, *z = S + kp.oZ, *y = S + kp.oY, *dy = S + kp.oDY;
   double* sc = S + kp.oSc;
   if (status != DRC_STATUS_NONFINITE) {
     if (l < nx) D[l] = 1.0;
-    for (int row = l; row < m; row += 64) E[row] = 1.0;
+    for (int row = l; row < m; row += GL::size) E[row] = 1.0;
     if (l == 0) sc[SC_C] = 1.0;
     double* Dt = S + kp.oT1;
     double* Et = S + kp.oT2;
@@ -2439,8 +2491,8 @@ __device__ __forceinline__ int qp_scale(const KParams& kp, double* S) {
           for (int i = 0; i < np; ++i) cn = fmax(cn, fabs(P[i * np + l]));
         qn = fabs(qq[l]);
       }
-      cn = wave_sum(cn) / nx;
-      qn = wave_max(qn);
+      cn = GL::sum(cn) / nx;
+      qn = GL::max(qn);
       qn = qn < kMinScaling ? 1.0 : (qn > kMaxScaling ? kMaxScaling : qn);
       double ct = fmax(cn, qn);
       ct = ct < kMinScaling ? 1.0 : (ct > kMaxScaling ? kMaxScaling : ct);
@@ -2452,9 +2504,9 @@ __device__ __forceinline__ int qp_scale(const KParams& kp, double* S) {
       // fixed point (as qp_scale_regs and the oracle)
       const bool ones = (l >= nx || (Dt[l] == 1.0 && Et[l] == 1.0)) && (l >= ng || Et[nx + l] == 1.0);
       wsync();
-      if (ct == 1.0 && __all(ones)) break;
+      if (ct == 1.0 && GL::all(ones)) break;
     }
-    for (int row = l; row < m; row += 64) {
+    for (int row = l; row < m; row += GL::size) {
       lo[row] = fmax(lo[row], -kInf) * E[row];
       up[row] = fmin(up[row], kInf) * E[row];
     }
@@ -2469,17 +2521,18 @@ __device__ __forceinline__ int qp_scale(const KParams& kp, double* S) {
 // qp_scale (bit-identical results); P, G, q, D, E written back at the end.
 template <class QD>
 __device__ __noinline__ int qp_scale_regs(const KParams& kp, double* S) {
+  using GL = Grp<QD::gs>;
   constexpr int NX = QD::nx, NG = QD::ng, NP = QD::np, M = NX + NG;
-  const int l = lane_id();
+  const int l = GL::lane();
   double *P = S + kp.oP, *G = S + kp.oG, *qq = S + kp.oQ, *ab = S + kp.oAB, *lo = S + kp.oL, *up = S + kp.oU;
   double *D = S + kp.oD, *E = S + kp.oE, *sc = S + kp.oSc;
   {
     bool finite = true;
-    for (int e = l; e < NP * NP; e += 64) finite &= isfinite(P[e]);
-    for (int e = l; e < NG * NX; e += 64) finite &= isfinite(G[e]);
+    for (int e = l; e < NP * NP; e += GL::size) finite &= isfinite(P[e]);
+    for (int e = l; e < NG * NX; e += GL::size) finite &= isfinite(G[e]);
     if (l < NX) finite &= isfinite(qq[l]);
-    for (int row = l; row < M; row += 64) finite &= !isnan(lo[row]) && !isnan(up[row]);
-    if (!__all(finite)) return DRC_STATUS_NONFINITE;
+    for (int row = l; row < M; row += GL::size) finite &= !isnan(lo[row]) && !isnan(up[row]);
+    if (!GL::all(finite)) return DRC_STATUS_NONFINITE;
   }
   const bool hx = l < NX, hg = l < NG, hp = l < NP;
   const int lx = hx ? l : 0, lg = hg ? l : 0, lp = hp ? l : 0;
@@ -2507,9 +2560,9 @@ __device__ __noinline__ int qp_scale_regs(const KParams& kp, double* S) {
     const double EtG = 1.0 / sqrt(clampf(sg));
     double DtA[NX], EtGA[NG];
 #pragma unroll
-    for (int c = 0; c < NX; ++c) DtA[c] = bcast(Dt, c);
+    for (int c = 0; c < NX; ++c) DtA[c] = GL::bcast(Dt, c);
 #pragma unroll
-    for (int i = 0; i < NG; ++i) EtGA[i] = bcast(EtG, i);
+    for (int i = 0; i < NG; ++i) EtGA[i] = GL::bcast(EtG, i);
     if (hp)
 #pragma unroll
       for (int c = 0; c < NP; ++c) Prow[c] *= Dt * DtA[c];
@@ -2532,8 +2585,8 @@ __device__ __noinline__ int qp_scale_regs(const KParams& kp, double* S) {
 #pragma unroll
       for (int i = 0; i < NP; ++i) cn = fmax(cn, fabs(Prow[i]));
     if (hx) qn = fabs(ql);
-    cn = wave_sum(cn) / NX;
-    qn = wave_max(qn);
+    cn = GL::sum(cn) / NX;
+    qn = GL::max(qn);
     qn = clampf(qn);
     double ct = clampf(fmax(cn, qn));
     ct = 1.0 / ct;
@@ -2544,7 +2597,7 @@ __device__ __noinline__ int qp_scale_regs(const KParams& kp, double* S) {
     cs *= ct;
     // fixed point: every factor of this pass was exactly 1, so the remaining
     // passes would repeat it bit for bit (oracle: same exit)
-    if (ct == 1.0 && __all((!hx || (Dt == 1.0 && Et == 1.0)) && (!hg || EtG == 1.0))) break;
+    if (ct == 1.0 && GL::all((!hx || (Dt == 1.0 && Et == 1.0)) && (!hg || EtG == 1.0))) break;
   }
   if (hp)
 #pragma unroll
@@ -2561,7 +2614,7 @@ __device__ __noinline__ int qp_scale_regs(const KParams& kp, double* S) {
   if (hg) E[NX + l] = EGl;
   if (l == 0) sc[SC_C] = cs;
   wsync();
-  for (int row = l; row < M; row += 64) {
+  for (int row = l; row < M; row += GL::size) {
     lo[row] = fmax(lo[row], -kInf) * E[row];
     up[row] = fmin(up[row], kInf) * E[row];
   }
@@ -2572,7 +2625,8 @@ __device__ __noinline__ int qp_scale_regs(const KParams& kp, double* S) {
 // rho, K^-1 and the ADMM iterations (+ polish); returns the status
 template <class QD>
 __device__ __forceinline__ int qp_admm(const KParams& kp, const KParams& kpl, double* S, int* iters_out) {
-  const int l = lane_id();
+  using GL = Grp<QD::gs>;
+  const int l = GL::lane();
   const int nx = DNX, ng = DNG, m = DM;
   double *G = S + kp.oG, *qq = S + kp.oQ, *ab = S + kp.oAB, *lo = S + kp.oL, *up = S + kp.oU;
   double *x = S + kp.oX, *z = S + kp.oZ, *y = S + kp.oY, *dy = S + kp.oDY;
@@ -2585,7 +2639,7 @@ __device__ __forceinline__ int qp_admm(const KParams& kp, const KParams& kpl, do
   factor_any<QD>(kpl, S);
   PHG(24);
   if (l < nx) x[l] = 0.0;
-  for (int row = l; row < m; row += 64) z[row] = y[row] = 0.0;
+  for (int row = l; row < m; row += GL::size) z[row] = y[row] = 0.0;
   wsync();
   // ---------------- OSQP: ADMM ----------------------------------------
   const double* K = S + kp.oU0;
@@ -2604,7 +2658,7 @@ __device__ __forceinline__ int qp_admm(const KParams& kp, const KParams& kpl, do
     //   core: x~_c = S^-1 r';  rows: v_r = G_r,c x~_c = (G_c S^-1)_r r'   (NP broadcasts)
     //   rows: x~_a = t_a - coef_r v_r,  (G x~)_r = v_r + g_r x~_a
     constexpr int NX = QD::nx, NG = QD::ng, NP = QD::np;
-    static_assert(NP + NG <= 64, "one lane per core variable and per G row");
+    static_assert(NP + NG <= QD::gs, "one lane per core variable and per G row");
     const double* Si = S + kp.oU0;
     const double* GS = Si + NP * NP;
     const double* dv = GS + NG * NP;
@@ -2659,7 +2713,7 @@ __device__ __forceinline__ int qp_admm(const KParams& kp, const KParams& kpl, do
       double r0 = 0, r1 = 0;
 #pragma unroll
       for (int i = 0; i < NG; ++i) {
-        const double ui = bcast(u, NP + i);
+        const double ui = GL::bcast(u, NP + i);
         if (i & 1) r1 += R[NP + i] * ui;
         else r0 += R[NP + i] * ui;
       }
@@ -2667,7 +2721,7 @@ __device__ __forceinline__ int qp_admm(const KParams& kp, const KParams& kpl, do
       double s0 = 0, s1 = 0;
 #pragma unroll
       for (int c = 0; c < NP; ++c) {
-        const double rpc = bcast(rp, c);
+        const double rpc = GL::bcast(rp, c);
         if (c & 1) s1 += R[c] * rpc;
         else s0 += R[c] * rpc;
       }
@@ -2776,7 +2830,7 @@ __device__ __forceinline__ int qp_admm(const KParams& kp, const KParams& kpl, do
       double r0 = hb ? sig * xl - q_l + ab_l * (rb * zb - yb) : 0.0, r1 = 0;
 #pragma unroll
       for (int i = 0; i < NG; ++i) {
-        const double wi = bcast(wg, i);
+        const double wi = GL::bcast(wg, i);
         if (i & 1) r1 += Gc[i] * wi;
         else r0 += Gc[i] * wi;
       }
@@ -2784,7 +2838,7 @@ __device__ __forceinline__ int qp_admm(const KParams& kp, const KParams& kpl, do
       double x0 = 0, x1 = 0, a0 = 0, a1 = 0;
 #pragma unroll
       for (int c = 0; c < NX; ++c) {
-        const double rc = bcast(rhs, c);
+        const double rc = GL::bcast(rhs, c);
         if (c & 1) {
           x1 += Kr[c] * rc;
           a1 += GKr[c] * rc;
@@ -2857,7 +2911,7 @@ __device__ __forceinline__ int qp_admm(const KParams& kp, const KParams& kpl, do
 #endif
   } else {
     for (it = 1; it <= kp.s.max_iter; ++it) {
-      for (int row = l; row < m; row += 64) w[row] = rv[row] * z[row] - y[row];
+      for (int row = l; row < m; row += GL::size) w[row] = rv[row] * z[row] - y[row];
       wsync();
       if (l < nx) {
         double r0 = sig * x[l] - qq[l] + ab[l] * w[l], r1 = 0.0;
@@ -2980,20 +3034,24 @@ qp_kernel(const DevModel* __restrict__ M0, const KParams kp, const IO io) {
   // LDS copy of the parameters for the out-of-line (rare) ADMM blocks: a
   // reference to the kernel argument itself would be copied to scratch
   __shared__ KParams kpl;
-  const int l = lane_id();
   {
     static_assert(sizeof(KParams) % 8 == 0, "KParams copied as 8-byte words");
     const uint64_t* src = reinterpret_cast<const uint64_t*>(&kp);
     uint64_t* dst = reinterpret_cast<uint64_t*>(&kpl);
-    for (int e = l; e < static_cast<int>(sizeof(KParams) / 8); e += 64) dst[e] = src[e];
+    for (int e = lane_id(); e < static_cast<int>(sizeof(KParams) / 8); e += 64) dst[e] = src[e];
     wsync();
   }
+  // QD::gs = 32: two instances per wave, each lane group on its own LDS
+  // plan (the launch allocates one per group) and its own instance sequence
+  using GL = Grp<QD::gs>;
+  const int l = GL::lane();
+  double* const Sg = S + (GL::upper() ? kp.lds_doubles : 0);
   const int64_t B = io.B;
   PH_DECL
   // hard_mode 1: the lane stage's hard list (grid stride); 2: every instance
   // except the flagged ones (their records are still being written)
   const bool hl = io.hard_mode == 1;
-  const InstSeq seq(hl ? int64_t(*io.hard_n) : B, hl ? 0 : kp.xcd_map, hl ? nullptr : io.queue);
+  const InstSeqG<QD::gs> seq(hl ? int64_t(*io.hard_n) : B, hl ? 0 : kp.xcd_map, hl ? nullptr : io.queue);
   for (int64_t j = seq.first(); j < seq.n; j = seq.next(j)) {
     const int64_t b = hl ? int64_t(io.hard_list[j]) : seq.at(j);
     if (b >= B) continue;
@@ -3001,6 +3059,7 @@ qp_kernel(const DevModel* __restrict__ M0, const KParams kp, const IO io) {
     const int64_t gb = io.b0 + b, LD = io.ld;  // position in the caller's [field][B] arrays
     const DevModel* M = M0;
     asm volatile("" : "+s"(M));
+    double* S = Sg;
     qp_assemble<QD>(M, kp, S, io, b);
     PH(0);
     int status, iters = 0;
@@ -3465,6 +3524,16 @@ static int upload(drc_model_impl* m) {
 }
 
 // LDS plan: persistent QP region + a union of (kinematics | K^-1 | polish)
+// lanes per instance of the compiled QPIK QP shapes.  32 packs two instances
+// per wave (Grp<32>: group reductions, ds_bpermute broadcasts, per-group
+// instance sequence and LDS plan; parity tests green) but measured slower on
+// FR3: 13.4 M solves/s at two waves per SIMD (spills serialise the
+// broadcasts), 12.9-13.2 M at one, against 15.7 M for 64
+#ifndef DRC_QP_GROUP
+#define DRC_QP_GROUP 64
+#endif
+constexpr int kQpGroup = DRC_QP_GROUP;
+
 // QPIK QP shapes with a compile-time qp_kernel instantiation (register ADMM
 // on the Schur complement); launch() dispatches on the same list
 static bool qp_compiled(int nx, int ng, int np) {
@@ -3541,7 +3610,7 @@ static int plan_layout(const DevModel& M, KParams* k, bool task_only) {
     end = end > fac_end ? end : fac_end;
     end = end > reg_pol ? end : reg_pol;
     end = end > lds_pol ? end : lds_pol;
-    k->lds_doubles = end;
+    k->lds_doubles = (end + 1) & ~1;  // 16-byte aligned: the second lane group's plan follows
     if (end * 8 > 160 * 1024) return set_err(DRC_ERR_UNSUPPORTED, "model too large for the per-wave LDS plan");
     return DRC_OK;
   }
@@ -3837,14 +3906,19 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
       const dim3 g(static_cast<unsigned>(gq)), blk(64);
       // compile-time QP shapes of the bundled robots; anything else runs the
       // runtime-sized instantiation
+      // (two instances per wave: one LDS plan per lane group)
       if (kq_c.nx == 23 && kq_c.ng == 16 && kq_c.np == 7)
-        hipLaunchKernelGGL((qp_kernel<Dims<23, 16, 7, true, true>>), g, blk, lds_q, cs, m->d_model, kq_c, io);  // FR3
+        hipLaunchKernelGGL((qp_kernel<Dims<23, 16, 7, true, true, kQpGroup>>), g, blk, lds_q * (64 / kQpGroup), cs,
+                           m->d_model, kq_c, io);  // FR3
       else if (kq_c.nx == 20 && kq_c.ng == 14 && kq_c.np == 6)
-        hipLaunchKernelGGL((qp_kernel<Dims<20, 14, 6, true, true>>), g, blk, lds_q, cs, m->d_model, kq_c, io);  // UR5e
+        hipLaunchKernelGGL((qp_kernel<Dims<20, 14, 6, true, true, kQpGroup>>), g, blk, lds_q * (64 / kQpGroup), cs,
+                           m->d_model, kq_c, io);  // UR5e
       else if (kq_c.nx == 9 && kq_c.ng == 16 && kq_c.np == 9)
-        hipLaunchKernelGGL((qp_kernel<Dims<9, 16, 9, true, true>>), g, blk, lds_q, cs, m->d_model, kq_c, io);  // Husky-FR3
+        hipLaunchKernelGGL((qp_kernel<Dims<9, 16, 9, true, true, kQpGroup>>), g, blk, lds_q * (64 / kQpGroup), cs,
+                           m->d_model, kq_c, io);  // Husky-FR3
       else if (kq_c.nx == 11 && kq_c.ng == 16 && kq_c.np == 11)
-        hipLaunchKernelGGL((qp_kernel<Dims<11, 16, 11, true, true>>), g, blk, lds_q, cs, m->d_model, kq_c, io);  // XLS-FR3
+        hipLaunchKernelGGL((qp_kernel<Dims<11, 16, 11, true, true, kQpGroup>>), g, blk, lds_q * (64 / kQpGroup), cs,
+                           m->d_model, kq_c, io);  // XLS-FR3
       else
         hipLaunchKernelGGL((qp_kernel<Dims<0, 0, 0>>), g, blk, lds_q, cs, m->d_model, kq_c, io);
       HIP_TRY(hipGetLastError());
