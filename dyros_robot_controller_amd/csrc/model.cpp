@@ -452,6 +452,19 @@ int build_model_from_urdf(const std::string& urdf_path, const std::string& srdf_
     m.pair_a[p] = static_cast<int16_t>(pairs[p].first);
     m.pair_b[p] = static_cast<int16_t>(pairs[p].second);
   }
+  // pair order of the wave kernel's closed-form / bound pass: by type class
+  // (sphere-sphere, sphere-cylinder, sphere-box, cylinder-cylinder,
+  // cylinder-box, box-box), pair index order within a class
+  {
+    int n = 0;
+    for (int cls = 0; cls < 6; ++cls)
+      for (int p = 0; p < m.npairs; ++p) {
+        int ta = m.gtype[m.pair_a[p]], tb = m.gtype[m.pair_b[p]];
+        if (ta > tb) std::swap(ta, tb);
+        const int c = ta == 0 ? tb : (ta == 1 ? 2 + tb : 5);  // (0,0)0 (0,1)1 (0,2)2 (1,1)3 (1,2)4 (2,2)5
+        if (c == cls) m.pair_order[n++] = static_cast<int16_t>(p);
+      }
+  }
   // GJK candidate slots of the lane-per-instance task stage: the pairs with
   // no sphere (no closed form), numbered in pair order
   m.ncand_slots = 0;

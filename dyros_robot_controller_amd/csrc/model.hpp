@@ -44,6 +44,8 @@ struct DevModel {
   int16_t cand_slot[kMaxPairs];       // pair -> GJK candidate slot (pairs without a sphere), or -1
   int16_t cand_pair[kMaxCandSlots];   // slot -> pair
   int ncand_slots;                    // non-sphere pairs (> kMaxCandSlots: lane stage not used)
+  int16_t pair_order[kMaxPairs];      // pairs grouped by shape-type class (pair index order within a class):
+                                      // the wave kernel's lanes then take same-type pairs in each round
   double J_mobile[3][kMaxWheels];  // base twist = J_mobile * wheel velocity (differential, mecanum)
   int drive;                       // DriveKind; caster: J_mobile depends on the steer angles (mobile_fk.hpp)
   double wheel_radius, wheel_offset;

@@ -1961,26 +1961,35 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRC_TAS
       // condition estimate >= 1e5) takes the serial COD path (rank by pivoted
       // QR, Moore-Penrose on the kept modes), matching DyrosMath::PinvCOD's
       // threshold semantics (math_type_define.h:563).
+      // lane i < 6 holds row i in registers; the pivot row moves by
+      // v_readlane (same element formulas as the LDS form it replaced)
       double piv_min = 1e300, det = 1;
-      if (l < 36) Ai[l] = A6[l];
-      wsync();
-      const int ii = l / 6, jj = l % 6;
+      const int lr = l < 6 ? l : 0;
+      double r6[6];
+#pragma unroll
+      for (int j = 0; j < 6; ++j) r6[j] = A6[lr * 6 + j];
+#pragma unroll
       for (int k = 0; k < 6; ++k) {
-        const double akk = Ai[k * 6 + k];
-        double nv_ = 0;
-        if (l < 36) {
-          const double aij = Ai[l], aik = Ai[ii * 6 + k], akj = Ai[k * 6 + jj];
-          if (ii == k && jj == k) nv_ = 1.0 / akk;
-          else if (ii == k) nv_ = akj / akk;
-          else if (jj == k) nv_ = -aik / akk;
-          else nv_ = aij - aik * akj / akk;
+        const double akk = bcast(r6[k], k), aik = r6[k];
+        double pk6[6];
+#pragma unroll
+        for (int j = 0; j < 6; ++j) pk6[j] = bcast(r6[j], k);
+#pragma unroll
+        for (int j = 0; j < 6; ++j) {
+          double v;
+          if (l == k && j == k) v = 1.0 / akk;
+          else if (l == k) v = pk6[j] / akk;
+          else if (j == k) v = -aik / akk;
+          else v = r6[j] - aik * pk6[j] / akk;
+          r6[j] = v;
         }
         piv_min = fmin(piv_min, akk);
         det *= akk;
-        wsync();
-        if (l < 36) Ai[l] = nv_;
-        wsync();
       }
+      if (l < 6)
+#pragma unroll
+        for (int j = 0; j < 6; ++j) Ai[l * 6 + j] = r6[j];
+      wsync();
       // kappa_2 <= |A|_F |A^-1|_F; below 1e5 the pivoted QR of PinvCOD keeps
       // every mode (|R_55|/|R_00| >= 1/kappa_2 > COD_THRESHOLD 1e-6)
       const double fa = wave_sum(l < 36 ? A6[l] * A6[l] : 0.0), fi = wave_sum(l < 36 ? Ai[l] * Ai[l] : 0.0);
@@ -2048,7 +2057,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRC_TAS
     int besti = 0x7fffffff;
     V3 bpA = v3(0, 0, 0), bpB = v3(0, 0, 0);
     double ub = 1e300;
-    for (int p = l; p < M->npairs; p += 64) {
+    // slots in type-class order (model.cpp pair_order): each round of 64 lanes
+    // runs one or two pair types instead of all of them
+    for (int sl = l; sl < M->npairs; sl += 64) {
+      const int p = M->pair_order[sl];
       const int ga = M->pair_a[p], gb = M->pair_b[p];
       Shape A{M->gtype[ga], Tg + 12 * ga, M->gparam[ga][0], M->gparam[ga][1], M->gparam[ga][2]};
       Shape Bs{M->gtype[gb], Tg + 12 * gb, M->gparam[gb][0], M->gparam[gb][1], M->gparam[gb][2]};
@@ -2060,7 +2072,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRC_TAS
       if (closed) {
         pf[p] = 1.0;
         ub = fmin(ub, d);
-        if (d < bestd) {  // p increases within this pass
+        if (d < bestd || (d == bestd && p < besti)) {  // ties -> lowest pair index
           bestd = d;
           besti = p;
           bpA = pA;
