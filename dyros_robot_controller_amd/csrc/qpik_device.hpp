@@ -6,6 +6,7 @@
 // (k, c) pairs (dJ/dq for the manipulability gradient), collision pairs
 // (narrow phase), QP variables / constraint rows (ADMM, polish).
 #pragma once
+#include <utility>
 
 #include <hip/hip_runtime.h>
 
@@ -128,6 +129,25 @@ struct Grp {
       return __hiloint2double(hi, lo);
     }
   }
+  // lane K of the own group, K a compile-time constant.  GS = 32: DPP
+  // row_newbcast puts lane K % 16 of every 16-lane row in the whole row, and
+  // v_permlane16_swap of that value with itself yields, in every row of a row
+  // pair, the even row's value (first result) and the odd row's (second):
+  // four VALU ops per double, no LDS crossbar round trip
+  template <int K>
+  static __device__ __forceinline__ double bcastc(double v) {
+    if constexpr (GS == 64) {
+      return rd_lane(v, K);
+    } else {
+      static_assert(K >= 0 && K < 32, "lane within the group");
+      const long long b = __double_as_longlong(v);
+      const int lo = __builtin_amdgcn_update_dpp(0, static_cast<int>(b), 0x150 + (K & 15), 0xF, 0xF, false);
+      const int hi = __builtin_amdgcn_update_dpp(0, static_cast<int>(b >> 32), 0x150 + (K & 15), 0xF, 0xF, false);
+      const auto pl = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+      const auto ph = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+      return K < 16 ? __hiloint2double(ph[0], pl[0]) : __hiloint2double(ph[1], pl[1]);
+    }
+  }
   template <class T>
   static __device__ __forceinline__ T shfl(T v, int k) { return __shfl(v, k, GS); }
   static __device__ __forceinline__ double max(double v) {
@@ -175,6 +195,16 @@ struct Grp {
     v = -nv;
   }
 };
+
+// compile-time loop: f(std::integral_constant<int, I>) for I = 0 .. N-1
+template <class F, int... I>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
 
 // ------------------------------------------------------------ 3-vectors
 struct V3 {

@@ -520,8 +520,8 @@ __device__ __noinline__ void schur_setup(const KParams& kp, double* S) {
   double Sr[NP];
 #pragma unroll
   for (int c = 0; c < NP; ++c) Sr[c] = Si[lr * NP + c];
-#pragma unroll
-  for (int k = 0; k < NP; ++k) {
+  static_for<NP>([&](auto K) {
+    constexpr int k = decltype(K)::value;
     if (l == k) {
       const double pv = 1.0 / Sr[k];
       Sr[k] = 1.0;
@@ -530,12 +530,12 @@ __device__ __noinline__ void schur_setup(const KParams& kp, double* S) {
     }
     const double f = Sr[k];
     if (l != k) Sr[k] = 0.0;
-#pragma unroll
-    for (int j = 0; j < NP; ++j) {
-      const double rkj = GL::bcast(Sr[j], k);
+    static_for<NP>([&](auto J) {
+      constexpr int j = decltype(J)::value;
+      const double rkj = GL::template bcastc<k>(Sr[j]);
       if (l != k) Sr[j] -= f * rkj;
-    }
-  }
+    });
+  });
   if (l < NP) {
 #pragma unroll
     for (int c = 0; c < NP; ++c) Si[l * NP + c] = Sr[c];
@@ -2571,10 +2571,8 @@ __device__ __noinline__ int qp_scale_regs(const KParams& kp, double* S) {
     for (int j = 0; j < NX; ++j) sg = fmax(sg, fabs(Grow[j]));
     const double EtG = 1.0 / sqrt(clampf(sg));
     double DtA[NX], EtGA[NG];
-#pragma unroll
-    for (int c = 0; c < NX; ++c) DtA[c] = GL::bcast(Dt, c);
-#pragma unroll
-    for (int i = 0; i < NG; ++i) EtGA[i] = GL::bcast(EtG, i);
+    static_for<NX>([&](auto C) { DtA[decltype(C)::value] = GL::template bcastc<decltype(C)::value>(Dt); });
+    static_for<NG>([&](auto I) { EtGA[decltype(I)::value] = GL::template bcastc<decltype(I)::value>(EtG); });
     if (hp)
 #pragma unroll
       for (int c = 0; c < NP; ++c) Prow[c] *= Dt * DtA[c];
@@ -2723,20 +2721,20 @@ __device__ __forceinline__ int qp_admm(const KParams& kp, const KParams& kpl, do
       }
       if (hc) loc = sig * xc - q_c + ab_c * (rc * zc - yc);
       double r0 = 0, r1 = 0;
-#pragma unroll
-      for (int i = 0; i < NG; ++i) {
-        const double ui = GL::bcast(u, NP + i);
-        if (i & 1) r1 += R[NP + i] * ui;
+      static_for<NG>([&](auto I) {
+        constexpr int i = decltype(I)::value;
+        const double ui = GL::template bcastc<NP + i>(u);
+        if constexpr (i & 1) r1 += R[NP + i] * ui;
         else r0 += R[NP + i] * ui;
-      }
+      });
       const double rp = loc + (r0 + r1);
       double s0 = 0, s1 = 0;
-#pragma unroll
-      for (int c = 0; c < NP; ++c) {
-        const double rpc = GL::bcast(rp, c);
-        if (c & 1) s1 += R[c] * rpc;
+      static_for<NP>([&](auto C) {
+        constexpr int c = decltype(C)::value;
+        const double rpc = GL::template bcastc<c>(rp);
+        if constexpr (c & 1) s1 += R[c] * rpc;
         else s0 += R[c] * rpc;
-      }
+      });
       const double sv = s0 + s1;  // core: x~_c; row: v_r = G_r,c x~_c
       if (hc) {
         const double zr = al * ab_c * sv + (1 - al) * zc;
