@@ -3535,10 +3535,10 @@ static int upload(drc_model_impl* m) {
 
 // LDS plan: persistent QP region + a union of (kinematics | K^-1 | polish)
 // lanes per instance of the compiled QPIK QP shapes.  32 packs two instances
-// per wave (Grp<32>: group reductions, ds_bpermute broadcasts, per-group
-// instance sequence and LDS plan; parity tests green) but measured slower on
-// FR3: 13.4 M solves/s at two waves per SIMD (spills serialise the
-// broadcasts), 12.9-13.2 M at one, against 15.7 M for 64
+// per wave (Grp<32>: group reductions, DPP / ds_bpermute broadcasts,
+// per-group instance sequence and LDS plan; parity tests green) but measured
+// slower on FR3: 13.7 M solves/s at two waves per SIMD, 13.4 M at one,
+// against 15.9 M for 64
 #ifndef DRC_QP_GROUP
 #define DRC_QP_GROUP 64
 #endif
