@@ -94,10 +94,6 @@ __device__ unsigned long long g_phase_cycles[64];
 #define PHG_RESET() do {} while (0)
 #endif
 
-// task-record doubles per lane of the QP kernel's prefetch (rLen <= 128 for
-// QPIK, 32-lane groups take four)
-constexpr int kRecPerLane = 4;
-
 // scalar slots in the oSc region
 enum { SC_C = 0, SC_RHO, SC_MAN, SC_DIST, SC_PAIR, SC_PRI, SC_DUA, SC_EPSP, SC_EPSD, SC_PRIS, SC_DUAS,
        SC_NAX, SC_NZ, SC_NPX, SC_NATY, SC_NQ, SC_NF, SC_NR, SC_WIN, SC_PFAIL, SC_COUNT };
@@ -1778,42 +1774,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRC_TAS
   // hard mode: the instances the lane-per-instance stage left (grid stride)
   const bool hard_mode = io.hard_mode != 0;
   const InstSeq seq(hard_mode ? int64_t(*io.hard_n) : B, hard_mode ? 0 : kp.xcd_map, hard_mode ? nullptr : io.queue);
-  // Next-instance prefetch: the queue position and the instance's inputs
-  // (lane l: q_l, qdot_l; x_target_l, xdot_target_l, x_init_l, xdot_init_l
-  // for the task velocity) are requested one instance ahead, so the atomic's
-  // and the loads' latency overlaps this instance's work instead of opening
-  // it (measured 8.6 k of 103 k cycles per FR3 instance before).
-  const int64_t LD = io.ld;
-  double pq = 0, pqd = 0, pxt = 0, pxdt = 0, pxi = 0, pxdi = 0;
-  auto prefetch = [&](int64_t jj) {
-    if (jj >= seq.n) return;
-    const int64_t bb = hard_mode ? int64_t(io.hard_list[jj]) : seq.at(jj);
-    if (bb >= B) return;
-    const int64_t g = io.b0 + bb;
-    if (l < nv) {
-      pq = io.q[l * LD + g];
-      pqd = io.qdot[l * LD + g];
-    }
-    if (kp.mode != DRC_MODE_QPIK && l < 12) pxt = io.xt[l * LD + g];
-    if (l < 6) pxdt = io.xdt[l * LD + g];
-    if (kp.mode == DRC_MODE_QPIK_CUBIC) {
-      if (l < 12) pxi = io.xi[l * LD + g];
-      if (l < 6) pxdi = io.xdi[l * LD + g];
-    }
-  };
-  int64_t jn = 0;
-  {
-    const int64_t j0 = seq.first();
-    prefetch(j0);
-    jn = j0;
-  }
-  for (int64_t j = jn; j < seq.n; j = jn) {
-    jn = seq.next(j);
-    const double cq = pq, cqd = pqd, cxt = pxt, cxdt = pxdt, cxi = pxi, cxdi = pxdi;
-    prefetch(jn);
+  for (int64_t j = seq.first(); j < seq.n; j = seq.next(j)) {
     const int64_t b = hard_mode ? int64_t(io.hard_list[j]) : seq.at(j);
     if (b >= B) continue;
-    const int64_t gb = io.b0 + b;  // position in the caller's [field][B] arrays
+    const int64_t gb = io.b0 + b, LD = io.ld;  // position in the caller's [field][B] arrays
 #ifdef DRC_PHASE_TIMING
     const unsigned long long inst_t0 = __builtin_amdgcn_s_memtime();
     unsigned long long ph_snap[8];
@@ -1828,22 +1792,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRC_TAS
     double* qv = S + kp.kq;
     double* qd = S + kp.kqd;
     if (l < nv) {
-      qv[l] = cq;
-      qd[l] = cqd;
-    }
-    {  // task-velocity inputs for lane 0's serial block (serial COD scratch, free until the manipulability stage)
-      double* tin = S + kp.kScr;
-      if (l < 12) {
-        tin[l] = cxt;
-        tin[18 + l] = cxi;
-      }
-      if (l < 6) {
-        tin[12 + l] = cxdt;
-        tin[30 + l] = cxdi;
-      }
+      qv[l] = io.q[l * LD + gb];
+      qd[l] = io.qdot[l * LD + gb];
     }
     wsync();
-    PH(8);  // (diagnostic sub-phases of phase 0 in slots 8..11)
     // ---------------- FK: local joint transforms, then the chain ------------
     double* T = S + kp.kT;  // (nv+1) x 12
     double* Zw = S + kp.kZ;  // (nv+1) x 3
@@ -1870,7 +1822,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRC_TAS
       for (int i = 0; i < 12; ++i) loc[(j - 1) * 12 + i] = Lj[i];
     }
     wsync();
-    PH(9);
     for (int j = 1; j <= nv; ++j) {  // oMi[j] = oMi[parent] * local[j]; 12 lanes
       const double* a = T + M->parent[j] * 12;
       const double* bb = loc + (j - 1) * 12;
@@ -1886,12 +1837,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRC_TAS
       if (l < 12) T[j * 12 + l] = v;
       wsync();
     }
-    PH(10);
     double* Te = S + kp.kTe;
     if (l >= 1 && l <= nv) st3(Zw + 3 * l, rot(T + 12 * l, ld3(M->axis[l])));
     if (l == 0) tmul(T + 12 * kp.frame_joint, kp.frame_place, Te);
     wsync();
-    PH(11);
     // geometry poses
     double* Tg = S + kp.kTg;
     for (int g = l; g < M->ngeom; g += 64) {
@@ -1922,18 +1871,17 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRC_TAS
     wsync();
     // ---------------- task velocity ---------------------------------------
     double* xdd = S + kp.kxdd;
-    const double* tin = S + kp.kScr;  // this instance's prefetched x_target | xdot_target | x_init | xdot_init
     if (l == 0) {
       if (kp.mode == DRC_MODE_QPIK) {
-        for (int i = 0; i < 6; ++i) xdd[i] = tin[12 + i];
+        for (int i = 0; i < 6; ++i) xdd[i] = io.xdt[i * LD + gb];
       } else {
         double xt[12], xdt[6];
-        for (int i = 0; i < 12; ++i) xt[i] = tin[i];
-        for (int i = 0; i < 6; ++i) xdt[i] = tin[12 + i];
+        for (int i = 0; i < 12; ++i) xt[i] = io.xt[i * LD + gb];
+        for (int i = 0; i < 6; ++i) xdt[i] = io.xdt[i * LD + gb];
         if (kp.mode == DRC_MODE_QPIK_CUBIC) {  // getTaskSpaceCubic (math_type_define.h:647)
           double xi[12], xdi[6], Rt[9], Ri[9];
-          for (int i = 0; i < 12; ++i) xi[i] = tin[18 + i];
-          for (int i = 0; i < 6; ++i) xdi[i] = tin[30 + i];
+          for (int i = 0; i < 12; ++i) xi[i] = io.xi[i * LD + gb];
+          for (int i = 0; i < 6; ++i) xdi[i] = io.xdi[i * LD + gb];
           for (int r = 0; r < 3; ++r)
             for (int c = 0; c < 3; ++c) {
               Rt[3 * r + c] = xt[3 * c + r];
@@ -2377,8 +2325,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRC_TAS
 
 // ---- QP kernel phases ------------------------------------------------------
 template <class QD>
-__device__ __forceinline__ void qp_assemble(const DevModel* M, const KParams& kp, double* S, const IO& io, int64_t b,
-                                            const double (&pre)[kRecPerLane]) {
+__device__ __forceinline__ void qp_assemble(const DevModel* M, const KParams& kp, double* S, const IO& io, int64_t b) {
   using GL = Grp<QD::gs>;
   const int l = GL::lane();
   const int nv = kp.nv, narm = kp.narm;
@@ -2390,13 +2337,10 @@ __device__ __forceinline__ void qp_assemble(const DevModel* M, const KParams& kp
 #ifdef DRC_PHASE_TIMING
   const unsigned long long as_t0 = __builtin_amdgcn_s_memtime();
 #endif
-  {  // task record written by task_kernel, prefetched by the kernel loop (pre[k] = element l + k * GS)
-    (void)b;
-#pragma unroll
-    for (int k = 0; k < kRecPerLane; ++k) {
-      const int e = l + k * GL::size;
-      if (e >= kp.rLen) continue;
-      const double v = pre[k];
+  {  // task record written by task_kernel (one coalesced read)
+    const double* rec = io.rec + b * io.rec_stride;
+    for (int e = l; e < kp.rLen; e += GL::size) {
+      const double v = rec[e];
       if (e < kp.rMan) J[e] = v;
       else if (e == kp.rMan) S[kp.oSc + SC_MAN] = v;
       else if (e < kp.rDist) mg[e - kp.rMan - 1] = v;
@@ -3118,24 +3062,7 @@ qp_kernel(const DevModel* __restrict__ M0, const KParams kp, const IO io) {
   // except the flagged ones (their records are still being written)
   const bool hl = io.hard_mode == 1;
   const InstSeqG<QD::gs> seq(hl ? int64_t(*io.hard_n) : B, hl ? 0 : kp.xcd_map, hl ? nullptr : io.queue);
-  // next-instance prefetch of the queue position and the task record (as in
-  // task_kernel): the atomic's and the record's latency overlap this QP
-  double pre[kRecPerLane] = {0, 0, 0, 0};
-  auto prefetch = [&](int64_t jj) {
-    if (jj >= seq.n) return;
-    const int64_t bb = hl ? int64_t(io.hard_list[jj]) : seq.at(jj);
-    if (bb >= B) return;
-    const double* rec = io.rec + bb * io.rec_stride;
-#pragma unroll
-    for (int k = 0; k < kRecPerLane; ++k)
-      if (l + k * GL::size < kp.rLen) pre[k] = rec[l + k * GL::size];
-  };
-  int64_t jn = seq.first();
-  prefetch(jn);
-  for (int64_t j = jn; j < seq.n; j = jn) {
-    jn = seq.next(j);
-    const double cur[kRecPerLane] = {pre[0], pre[1], pre[2], pre[3]};
-    prefetch(jn);
+  for (int64_t j = seq.first(); j < seq.n; j = seq.next(j)) {
     const int64_t b = hl ? int64_t(io.hard_list[j]) : seq.at(j);
     if (b >= B) continue;
     if (io.hard_mode == 2 && io.hard_flag[b]) continue;
@@ -3143,7 +3070,7 @@ qp_kernel(const DevModel* __restrict__ M0, const KParams kp, const IO io) {
     const DevModel* M = M0;
     asm volatile("" : "+s"(M));
     double* S = Sg;
-    qp_assemble<QD>(M, kp, S, io, b, cur);
+    qp_assemble<QD>(M, kp, S, io, b);
     PH(0);
     int status, iters = 0;
     if constexpr (QD::reg) status = qp_scale_regs<QD>(kpl, S);

@@ -26,9 +26,6 @@ tt, tq = v[:8], v[16:22]
 ta = v[24:28]
 print("task kernel cycles/instance: %.0f" % (tt.sum() / B))
 for n, x in zip(names_t, tt): print("  %-16s %6.1f%%  %8.0f cyc/inst" % (n, 100 * x / tt.sum(), x / B))
-sub = v[8:12]
-print("  fk sub-phases (slots 8..11, added to fk+geoms): state load %.0f, local transforms %.0f, chain %.0f, axes+frame %.0f; geometry poses %.0f cyc/inst"
-      % (sub[0] / B, sub[1] / B, sub[2] / B, sub[3] / B, tt[0] / B))
 print("qp kernel cycles/instance: %.0f" % (tq.sum() / B))
 for n, x in zip(names_q, tq): print("  %-16s %6.1f%%  %8.0f cyc/inst" % (n, 100 * x / tq.sum(), x / B))
 names_a = ["set_rho+factor", "prep+load regs", "admm iterations (+publish)", "admm_check (residuals/polish/refactor)"]
