@@ -2439,6 +2439,46 @@ __device__ __forceinline__ void qp_assemble(const DevModel* M, const KParams& kp
   wsync();
 }
 
+// Whole-body QP infeasibility certificate (exact mode, D15).  The MoMa QP has
+// no slacks and no variable bounds (mobile_manipulator/QP_IK.cpp:75-128); its
+// rows are the arm's CBF box blo <= qdot_arm <= bhi and the two gradient rows
+// g_m . qdot_arm >= r_m, g_d . qdot_arm >= r_d.  By Farkas, it is infeasible
+// iff some mu in [0, 1] has phi(mu) = max over the box of
+// (mu g_m + (1 - mu) g_d) . v - (mu r_m + (1 - mu) r_d) < 0; phi is convex
+// and piecewise linear, so its minimum sits at mu = 0, 1 or a root of a
+// component of mu g_m + (1 - mu) g_d.  Lane c evaluates candidate c on the
+// unscaled rows (before Ruiz); certified when some phi < -1e-6 (1 + scale),
+// a margin no point the certified polish accepts (residual ~1e-9) can
+// cross.  Same candidates, order of sums and margin as the oracle's
+// moma_lp_infeasible.
+template <class QD>
+__device__ __forceinline__ bool moma_lp_infeasible(const DevModel* M, const KParams& kp, const double* S) {
+  using GL = Grp<QD::gs>;
+  const int l = GL::lane();
+  const int nx = DNX, n = kp.narm, vo = M->act_mani_start;
+  const double *G = S + kp.oG, *lo = S + kp.oL + nx;
+  const double *gm = G + (2 * n) * nx + vo, *gd = G + (2 * n + 1) * nx + vo;
+  const double rm = lo[2 * n], rd = lo[2 * n + 1];
+  double mu = -1.0;
+  if (l == 0) mu = 1.0;
+  else if (l == 1) mu = 0.0;
+  else if (l < n + 2) {
+    const int i = l - 2;
+    const double den = gm[i] - gd[i];
+    if (den != 0.0) {
+      const double t = -gd[i] / den;
+      if (t > 0.0 && t < 1.0) mu = t;
+    }
+  }
+  double scale = fabs(rm) + fabs(rd), phi = -(mu * rm + (1.0 - mu) * rd);
+  for (int i = 0; i < n; ++i) {
+    const double blo = lo[i], bhi = -lo[n + i], g = mu * gm[i] + (1.0 - mu) * gd[i];
+    phi += fmax(g * blo, g * bhi);
+    scale += (fabs(gm[i]) + fabs(gd[i])) * fmax(fabs(blo), fabs(bhi));
+  }
+  return GL::any(mu >= 0.0 && phi < -1e-6 * (1.0 + scale));
+}
+
 // finiteness check + Ruiz equilibration (OSQP scaling.c); returns
 // DRC_STATUS_NONFINITE or DRC_STATUS_MAX_ITER (= not yet solved)
 template <class QD>
@@ -3072,11 +3112,15 @@ qp_kernel(const DevModel* __restrict__ M0, const KParams kp, const IO io) {
     double* S = Sg;
     qp_assemble<QD>(M, kp, S, io, b);
     PH(0);
+    const bool lp_inf = M->kind == 1 && kp.s.exact && moma_lp_infeasible<QD>(M, kp, S);
     int status, iters = 0;
     if constexpr (QD::reg) status = qp_scale_regs<QD>(kpl, S);
     else status = qp_scale<QD>(kp, S);
     PH(1);
-    if (status != DRC_STATUS_NONFINITE) status = qp_admm<QD>(kp, kpl, S, &iters);
+    if (status != DRC_STATUS_NONFINITE) {
+      if (lp_inf) status = DRC_STATUS_PRIMAL_INFEASIBLE;
+      else status = qp_admm<QD>(kp, kpl, S, &iters);
+    }
     PH(3);
     // ---------------- outputs (zero on failure, QP_IK.cpp:56-61) ------------
     const double *D = S + kp.oD, *x = S + kp.oX;
@@ -3606,11 +3650,14 @@ static int plan_layout(const DevModel& M, KParams* k, bool task_only) {
     k->kJt = takeu(6 * np);
     const int kin_end = u;
     const int fac_end = k->oU0 + (qp_compiled(nx, ng, np) ? np * np + ng * np + 4 * ng : nx * nx + nx * ng);
-    // the register EQP's size; a larger reduced KKT fails that polish attempt
-    // and ADMM continues (the oracle applies the same cap).  Uncapped, the
-    // whole-body QPs (no variable bounds) solve one more instance in 65 Ki
-    // but the LDS EQP region costs ~7% throughput
-    const int N = nx + ng < kEqpRegCap ? nx + ng : kEqpRegCap;
+    // manipulator QPs: the register EQP's size; a larger reduced KKT fails
+    // that polish attempt and ADMM continues (the oracle applies the same
+    // cap).  Whole-body QPs have no variable bounds, so every variable is free
+    // in the reduced KKT (N = nx + active rows): capped at 16 their polish
+    // fails whenever 6 (XLS-FR3) / 8 (Husky-FR3) rows are active and the
+    // instance runs to the tight ADMM fallback (up to ~3 000 iterations);
+    // they get the LDS EQP for N > 16
+    const int N = M.kind == 1 ? nx + ng : (nx + ng < kEqpRegCap ? nx + ng : kEqpRegCap);
     k->ncap = N;
     k->nbuf = (N + 7) & ~7;
     const int reg_pol = k->oU0 + 128 + m;  // Fidx/Ridx | xx | yy

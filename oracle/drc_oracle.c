@@ -1501,9 +1501,46 @@ void oracle_default_params(int kind, OracleParams* p, int exact) {
     s->polish = exact ? 1 : 0; s->polish_refine_iter = 3; s->delta = 1e-6;
     s->exact = exact; s->eps_exact = 1e-9; s->eps_fallback = 1e-7;
     /* the kernel's QPIK polish KKT cap (kEqpRegCap, its register EQP): a
-     * larger reduced KKT fails that polish attempt and ADMM continues */
-    s->polish_cap = 16;
+     * larger reduced KKT fails that polish attempt and ADMM continues.  The
+     * whole-body QP (no variable bounds) is uncapped, as the kernel's LDS EQP
+     * takes N > 16 there (D16) */
+    s->polish_cap = kind == 0 ? 16 : 0;
     s->polish_add_all = 1;
+}
+
+/* Farkas certificate for the whole-body QP (mobile_manipulator/QP_IK.cpp:
+ * 75-128: no slacks, no variable bounds).  Rows: the arm's CBF box
+ * blo_i = lg[i] <= v_i <= bhi_i = -lg[n+i], and gm.v >= lg[2n], gd.v >= lg[2n+1].
+ * Infeasible iff min over mu in [0,1] of phi(mu) = sum_i max(g_i blo_i,
+ * g_i bhi_i) - (mu rm + (1-mu) rd) < 0 with g = mu gm + (1-mu) gd; phi is
+ * convex piecewise linear, minimised at mu = 1, 0 or a root of some g_i.
+ * Certified only below -1e-6 (1 + scale) (a point the exact-mode polish
+ * accepts has residuals ~1e-9).  Test infrastructure restating the kernel's
+ * moma_lp_infeasible: same candidates, summation order and margin. */
+static int moma_lp_infeasible(int n, const double* gm, const double* gd, const double* lg) {
+    const double rm = lg[2 * n], rd = lg[2 * n + 1];
+    for (int c = 0; c < n + 2; ++c) {
+        double mu = -1.0;
+        if (c == 0) mu = 1.0;
+        else if (c == 1) mu = 0.0;
+        else {
+            int i = c - 2;
+            double den = gm[i] - gd[i];
+            if (den != 0.0) {
+                double t = -gd[i] / den;
+                if (t > 0.0 && t < 1.0) mu = t;
+            }
+        }
+        if (!(mu >= 0.0)) continue;
+        double scale = fabs(rm) + fabs(rd), phi = -(mu * rm + (1.0 - mu) * rd);
+        for (int i = 0; i < n; ++i) {
+            double blo = lg[i], bhi = -lg[n + i], g = mu * gm[i] + (1.0 - mu) * gd[i];
+            phi += fmax(g * blo, g * bhi);
+            scale += (fabs(gm[i]) + fabs(gd[i])) * fmax(fabs(blo), fabs(bhi));
+        }
+        if (phi < -1e-6 * (1.0 + scale)) return 1;
+    }
+    return 0;
 }
 
 /* dist_in (optional): the distance stage (d, grad[nv]) supplied by the caller
@@ -1633,7 +1670,16 @@ static int qpik_one_impl(const OracleModel* m, const OracleParams* p, const doub
     }
     double x[ORC_MAXX], y[ORC_MAXC];
     int iters = 0, pol = 0;
-    int st = oracle_solve_qp(nx, nc, P, qv, A, l, u, &p->solver, x, y, &iters, &pol);
+    int st;
+    /* exact mode, whole-body QP: an LP-certified infeasible instance returns
+     * PrimalInfeasible without the ADMM (the kernel's moma_lp_infeasible, D15);
+     * non-finite data keeps OSQP's check (the certificate never fires on it) */
+    if (moma && p->solver.exact &&
+        moma_lp_infeasible(m->n_arm, A + (nx + 2 * m->n_arm) * nx + m->act_mani_start,
+                           A + (nx + 2 * m->n_arm + 1) * nx + m->act_mani_start, l + nx))
+        st = ORC_PRIMAL_INFEASIBLE;
+    else
+        st = oracle_solve_qp(nx, nc, P, qv, A, l, u, &p->solver, x, y, &iters, &pol);
     /* QP_IK.cpp:53-67 / MoMa :43-57: zero on any non-Solved status */
     for (int i = 0; i < na; ++i) out[i] = st == ORC_SOLVED ? x[i] : 0.0;
     if (diag) {
