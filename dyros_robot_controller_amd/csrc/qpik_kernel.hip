@@ -685,6 +685,29 @@ __device__ __noinline__ int admm_check(const KParams& kp, double* S, int it, int
   double *x = S + kp.oX, *z = S + kp.oZ, *y = S + kp.oY, *sc = S + kp.oSc;
   int reload = 0;
   CK_T0();
+  // parity mode: a certified polish is exact whatever the ADMM residual, so
+  // the first kPolishMaxEarly checks try it before anything else (converged
+  // or not, the oracle makes exactly one polish attempt at such a check).  The
+  // polish reads only the iterate, so the ADMM residuals -- which decide
+  // convergence, the fallback and adaptive rho -- are formed only when it
+  // fails (the usual case solves here and never needs them)
+  bool early_failed = false;
+  if (check && kp.s.exact && sc[SC_PFAIL] < kPolishMaxEarly) {
+    CK_T(34);
+    const bool ok_ = polish<QD>(kp, S, true);
+    CK_T(35);
+    CK_N(36);
+    if (ok_) {
+      CK_N(37);
+      *status = DRC_STATUS_SOLVED;
+      return 2;
+    }
+    if (GL::lane() == 0) sc[SC_PFAIL] += 1.0;
+    factor_any<QD>(kp, S);
+    CK_T(38);  // polish used the union region
+    early_failed = true;
+    reload = 1;
+  }
   residuals<QD>(kp, S, x, z, y, kp.s.eps_abs, kp.s.eps_rel);
   CK_T(32);
   CK_N(33);
@@ -695,31 +718,12 @@ __device__ __noinline__ int admm_check(const KParams& kp, double* S, int it, int
       printf("it %d rho %.4g pri %.3e/%.3e dua %.3e/%.3e x3 %.6f\n", it, sc[SC_RHO], sc[SC_PRI], sc[SC_EPSP],
              sc[SC_DUA], sc[SC_EPSD], x[3] * S[kp.oD + 3]);
 #endif
-    // parity mode: a certified polish is exact whatever the ADMM residual,
-    // so try it at every check (the active set settles long before OSQP's
-    // eps_rel termination)
-    if (kp.s.exact && !conv && sc[SC_PFAIL] < kPolishMaxEarly) {
-      CK_T(34);
-      const bool ok_ = polish<QD>(kp, S, true);
-      CK_T(35);
-      CK_N(36);
-      if (ok_) {
-        CK_N(37);
-        *status = DRC_STATUS_SOLVED;
-        return 2;
-      }
-      if (GL::lane() == 0) sc[SC_PFAIL] += 1.0;
-      factor_any<QD>(kp, S);
-      CK_T(38);  // polish used the union region
-      residuals<QD>(kp, S, x, z, y, kp.s.eps_abs, kp.s.eps_rel);
-      reload = 1;
-    }
     if (conv) {
       if (!kp.s.exact) {
         *status = DRC_STATUS_SOLVED;
         return 2;
       }
-      if (sc[SC_PFAIL] < kPolishMaxTotal) {
+      if (!early_failed && sc[SC_PFAIL] < kPolishMaxTotal) {
         CK_T(34);
         const bool ok_ = polish<QD>(kp, S, true);
         CK_T(35);
@@ -3880,12 +3884,14 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
       hard_flag = reinterpret_cast<uint8_t*>(static_cast<char*>(cx->pool) + rec_bytes + B * 4);
     }
   }
-  // sub-batches: whole multiples of 16 Ki instances per chunk (each keeps the
-  // XCD-aware order, whose grids must be multiples of 8)
+  // sub-batches of >= 4 Ki instances (a chunk of >= 16 Ki keeps the XCD-aware
+  // order; smaller ones run grid-stride order): with one sub-batch the QP
+  // kernel waits for the whole task kernel, with several they overlap
+  // (Husky-FR3's 16 Ki batch)
   int S = 1;
   if (!stages)
     for (int c = m->chunks; c > 1; --c)
-      if (B / c >= 16384) {
+      if (B / c >= 4096) {
         S = c;
         break;
       }
