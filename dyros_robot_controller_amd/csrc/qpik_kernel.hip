@@ -52,6 +52,7 @@ struct KParams {
   int oP, oG, oQ, oAB, oL, oU, oD, oE, oRho, oX, oZ, oY, oDY, oXT, oZT, oT1, oT2, oRed, oSc;
   // union region (kinematics | K^-1 | polish)
   int oU0;
+  int oHi;  // whole-body polish: cached rows of (P + delta I)^-1 (persistent, nx * nx), -1 if unused
   int kT, kZ, kTe, kJ, kTg, kq, kqd, kA6, kAi, kW, kPart, kPd, kPf, kCand, kxdd, kmg, kdg, kJt, kSv, kScr, kEpa;
   int kJd, kDa, kVf, kX6, kBias, kMq, kGq;  // QPID: Jdot, arm-only Jdot, S eta, 6x6 scratch, bias | M, g
   int kGdv;                                 // QPID stage: grad_dot vectors
@@ -96,7 +97,7 @@ __device__ unsigned long long g_phase_cycles[64];
 
 // scalar slots in the oSc region
 enum { SC_C = 0, SC_RHO, SC_MAN, SC_DIST, SC_PAIR, SC_PRI, SC_DUA, SC_EPSP, SC_EPSD, SC_PRIS, SC_DUAS,
-       SC_NAX, SC_NZ, SC_NPX, SC_NATY, SC_NQ, SC_NF, SC_NR, SC_WIN, SC_PFAIL, SC_COUNT };
+       SC_NAX, SC_NZ, SC_NPX, SC_NATY, SC_NQ, SC_NF, SC_NR, SC_WIN, SC_PFAIL, SC_HIV, SC_COUNT };
 // Parity mode tries the certified polish at every termination check, but only
 // until this many attempts failed on a not-yet-converged iterate; after that
 // only at convergence (bounds the cost of slow or non-converging instances —
@@ -920,6 +921,179 @@ __device__ __forceinline__ bool eqp_regs(const KParams& kp, double* S, int actb,
   return true;
 }
 
+// Range-space form of eqp for the whole-body QPs (no variable bounds, so
+// every variable is free and the reduced KKT is [H, G_R^T; G_R, -dI] with
+// H = P + dI fixed for the instance).  Its inverse applied to (r_x, r_l):
+//   t = H^-1 r_x,  (G_R H^-1 G_R^T + dI) lam = G_R t - r_l,  x = t - H^-1 G_R^T lam
+// so a polish attempt factors only the nR x nR Schur matrix of the active rows
+// (mean 1.3 on XLS-FR3) instead of the (nx + nR)-row KKT (nx = 11).  H^-1
+// (register Gauss-Jordan, lane per row) is formed on the first attempt and
+// kept in LDS (oHi).  Lanes: l < NX hold x / row l of H^-1 / (H^-1 g_a)_l;
+// lane NX + a holds active row a: lam_a, g_a and row a of the Schur inverse.
+// Same system, refinement count and outputs as eqp's LDL^T (the oracle's
+// qp_eqp); only the rounding of the factorisation differs.
+template <class QD>
+__device__ __forceinline__ bool eqp_range(const KParams& kp, double* S, int actg, double* xx, double* yy,
+                                          unsigned long long rowMask, int nR) {
+  constexpr int NX = QD::nx, NG = QD::ng, M = NX + NG, NK = kEqpRegCap;
+  static_assert(NX + NK <= 64 && QD::gs == 64, "x lanes and active-row lanes in one wave");
+  const int l = lane_id();
+  const double *P = S + kp.oP, *G = S + kp.oG, *q = S + kp.oQ, *lo = S + kp.oL, *up = S + kp.oU;
+  double* Hi = S + kp.oHi;
+  double* sc = S + kp.oSc;
+  int* Ridx = reinterpret_cast<int*>(S + kp.oU0) + 64;
+  double* Vb = S + kp.oU0 + 256;  // [nR][NX]: H^-1 g_a
+  const double dl = kp.s.delta;
+  const bool hx = l < NX, hl = l >= NX && l < NX + nR;
+  const int lx = hx ? l : 0, a = hl ? l - NX : 0;
+  if (sc[SC_HIV] == 0.0) {  // uniform
+    double h[NX];
+#pragma unroll
+    for (int j = 0; j < NX; ++j) h[j] = P[lx * NX + j] + (j == lx ? dl : 0.0);
+#pragma unroll
+    for (int k = 0; k < NX; ++k) {
+      const double piv = rd_lane(h[k], k);
+      if (piv == 0.0) return false;  // uniform
+      if (l == k) {
+        const double p = 1.0 / h[k];
+        h[k] = 1.0;
+#pragma unroll
+        for (int j = 0; j < NX; ++j) h[j] *= p;
+      }
+      const double f = h[k];
+      if (l != k) h[k] = 0.0;
+#pragma unroll
+      for (int j = 0; j < NX; ++j) {
+        const double hkj = rd_lane(h[j], k);
+        if (l != k) h[j] -= f * hkj;
+      }
+    }
+    if (hx)
+#pragma unroll
+      for (int j = 0; j < NX; ++j) Hi[l * NX + j] = h[j];
+    wsync();
+    if (l == 0) sc[SC_HIV] = 1.0;
+  }
+  if (l < NG && actg != 0) Ridx[__popcll(rowMask & ((1ull << l) - 1))] = l;
+  // right-hand side of active row a, formed by its owner lane (the G row)
+  double rG = 0.0;
+  if (l < NG && actg != 0) rG = actg < 0 ? lo[NX + l] : up[NX + l];
+  wsync();
+  const int gi = hl ? Ridx[a] : 0;
+  const double rl = __shfl(rG, gi, 64);
+  const double rx = hx ? -q[lx] : 0.0;
+  // A1: row l of H^-1 (x lanes) or g_a (row lanes); A2: (H^-1 g_b)_l (x lanes)
+  // or row a of the Schur inverse (row lanes)
+  double A1[NX], A2[NK];
+#pragma unroll
+  for (int j = 0; j < NX; ++j) A1[j] = hl ? G[gi * NX + j] : Hi[lx * NX + j];
+  if (hx) {
+#pragma unroll
+    for (int b = 0; b < NK; ++b) {
+      if (b >= nR) break;
+      const int gb = Ridx[b];
+      double s = 0.0;
+#pragma unroll
+      for (int j = 0; j < NX; ++j) s += A1[j] * G[gb * NX + j];
+      A2[b] = s;
+      Vb[b * NX + l] = s;
+    }
+  }
+  wsync();
+  if (hl) {  // row a of G_R H^-1 G_R^T + dI
+#pragma unroll
+    for (int b = 0; b < NK; ++b) {
+      if (b >= nR) break;
+      double s = 0.0;
+#pragma unroll
+      for (int j = 0; j < NX; ++j) s += A1[j] * Vb[b * NX + j];
+      A2[b] = s + (b == a ? dl : 0.0);
+    }
+  }
+  // Gauss-Jordan inverse of the Schur matrix on lanes NX .. NX + nR - 1
+  // (symmetric positive definite: nonzero pivots in natural order)
+#pragma unroll
+  for (int k = 0; k < NK; ++k) {
+    if (k >= nR) break;
+    const double piv = rd_lane(A2[k], NX + k);
+    if (piv == 0.0) return false;  // uniform
+    if (l == NX + k) {
+      const double p = 1.0 / A2[k];
+      A2[k] = 1.0;
+#pragma unroll
+      for (int j = 0; j < NK; ++j) A2[j] *= p;
+    }
+    const double f = A2[k];
+    if (hl && l != NX + k) A2[k] = 0.0;
+#pragma unroll
+    for (int j = 0; j < NK; ++j) {
+      if (j >= nR) break;
+      const double rkj = rd_lane(A2[j], NX + k);
+      if (hl && l != NX + k) A2[j] -= f * rkj;
+    }
+  }
+  // K^-1 (vx on x lanes, vl on row lanes) -> (x on x lanes, lam on row lanes)
+  auto solve = [&](double vx, double vl, double& ox, double& ol) {
+    double t0 = 0, t1 = 0;
+#pragma unroll
+    for (int j = 0; j < NX; ++j) {
+      const double v = rd_lane(vx, j);
+      if (j & 1) t1 += A1[j] * v;
+      else t0 += A1[j] * v;
+    }
+    const double t = t0 + t1;  // x lanes: (H^-1 vx)_l
+    double s0 = 0, s1 = 0;
+#pragma unroll
+    for (int j = 0; j < NX; ++j) {
+      const double v = rd_lane(t, j);
+      if (j & 1) s1 += A1[j] * v;
+      else s0 += A1[j] * v;
+    }
+    const double sr = s0 + s1 - vl;  // row lanes: (G_R t - vl)_a
+    double lam = 0;
+#pragma unroll
+    for (int b = 0; b < NK; ++b) {
+      if (b >= nR) break;
+      lam += A2[b] * rd_lane(sr, NX + b);
+    }
+    double xc = t;
+#pragma unroll
+    for (int b = 0; b < NK; ++b) {
+      if (b >= nR) break;
+      xc -= A2[b] * rd_lane(lam, NX + b);
+    }
+    ox = xc;
+    ol = lam;
+  };
+  double sx, sl;
+  solve(rx, rl, sx, sl);
+  for (int it = 0; it < kp.s.polish_refine_iter; ++it) {
+    // residual against the unregularised KKT [P, G_R^T; G_R, 0]
+    double px = 0, gl = 0;
+#pragma unroll
+    for (int j = 0; j < NX; ++j) {
+      const double xj = rd_lane(sx, j);
+      px += P[lx * NX + j] * xj;
+      gl += A1[j] * xj;  // row lanes: g_a . x
+    }
+#pragma unroll
+    for (int b = 0; b < NK; ++b) {
+      if (b >= nR) break;
+      px += G[Ridx[b] * NX + lx] * rd_lane(sl, NX + b);
+    }
+    double dx, dlam;
+    solve(rx - px, rl - gl, dx, dlam);
+    sx += dx;
+    sl += dlam;
+  }
+  if (hx) xx[l] = sx;
+  for (int row = l; row < M; row += 64) yy[row] = 0.0;
+  wsync();
+  if (hl) yy[NX + gi] = sl;
+  wsync();
+  return true;
+}
+
 // Equality-constrained QP on the flagged rows (OSQP polish's reduced KKT):
 // bound-active variables are fixed at their bound (eliminated exactly), the
 // active G rows enter [P_FF + dI, G_RF^T; G_RF, -dI] solved by a packed
@@ -945,6 +1119,15 @@ __device__ __forceinline__ bool eqp(const KParams& kp, double* S, int actb, int 
 #endif
   if constexpr (QD::gs < 64) {  // two instances per wave: register EQP only (ncap <= kEqpRegCap)
     if (N > kEqpRegCap) return false;
+  }
+  if constexpr (QD::nx > 0 && QD::nx == QD::np && QD::gs == 64) {  // whole-body shapes: range-space form
+    if (kp.oHi >= 0 && nF == QD::nx && nR <= kEqpRegCap) {
+      const bool ok_ = eqp_range<QD>(kp, S, actg, xx, yy, rowMask, nR);
+#ifdef DRC_PHASE_TIMING
+      if (l == 0) atomicAdd(&g_phase_cycles[40], __builtin_amdgcn_s_memtime() - eq_t0);
+#endif
+      return ok_;
+    }
   }
   if constexpr (QD::nx > 0) {
     if (N <= kEqpRegCap) {
@@ -2688,7 +2871,10 @@ __device__ __forceinline__ int qp_admm(const KParams& kp, const KParams& kpl, do
   int status = DRC_STATUS_MAX_ITER;
   (void)G;
   PHG_DECL
-  if (l == 0) sc[SC_PFAIL] = 0.0;
+  if (l == 0) {
+    sc[SC_PFAIL] = 0.0;
+    sc[SC_HIV] = 0.0;  // the polish's cached (P + delta I)^-1 is formed on first use
+  }
   set_rho<QD>(kp, S, kp.s.rho);
   factor_any<QD>(kpl, S);
   PHG(24);
@@ -3631,6 +3817,8 @@ static int plan_layout(const DevModel& M, KParams* k, bool task_only) {
   k->oRed = take(64);
   k->oSc = take(32);
   }
+  k->oHi = -1;
+  if (!task_only && k->problem == 0 && M.kind == 1 && qp_compiled(nx, ng, np)) k->oHi = take(nx * nx);
   k->oU0 = off;
   if (!task_only && k->problem == 0) {
     // QPIK QP kernel: the union holds only what it uses -- the task record

@@ -3,17 +3,18 @@ import os, sys, ctypes as C
 os.environ["DRC_AMD_LIB"] = "libdrc_amd_timing.so"
 sys.path.insert(0, "tests"); sys.path.insert(0, "oracle"); sys.path.insert(0, ".")
 import numpy as np, torch
-from _common import make_manipulator, step_inputs
-from dyros_robot_controller_amd import manipulator, _capi
+import bench
+from dyros_robot_controller_amd import BUNDLED, make_robot, manipulator, mobile_manipulator, _capi
 dev = torch.device("cuda", 0)
 robot = sys.argv[1] if len(sys.argv) > 1 else "fr3"
 B = int(sys.argv[2]) if len(sys.argv) > 2 else 65536
-rd = make_manipulator(robot, dev)
-q, qd, xt, xdt = step_inputs(rd, robot, 7, B, dev, stress=True)
-ctrl = manipulator.RobotController(0.001, rd)
+spec = BUNDLED[robot]
+rd = make_robot(robot, dev)
+mod = manipulator if spec["kind"] == "manipulator" else mobile_manipulator
+ctrl = mod.RobotController(0.001, rd, solver_mode="exact")
+_, args, _ = bench.make_inputs(rd, robot, B, 12345, 0, dev)   # bench.py's workload (stress tiers)
 _capi.lib().drc_set_concurrency(rd.model.handle, 1)  # one sub-batch: per-instance cycles without overlap
-link = "fr3_link8" if robot == "fr3" else "tool0"
-args = [torch.as_tensor(a, device=dev) for a in (q, qd, xt, xdt)]
+link = spec["link"]
 ctrl.QPIK_step_batch(*args, link); torch.cuda.synchronize()
 buf = (C.c_ulonglong * 64)()
 _capi.lib().drc_debug_phase_cycles(buf, 1)
