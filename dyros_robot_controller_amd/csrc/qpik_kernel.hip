@@ -1128,6 +1128,7 @@ __device__ __forceinline__ bool eqp(const KParams& kp, double* S, int actb, int 
 #endif
       return ok_;
     }
+    if (kp.oHi >= 0) return false;  // no LDS LDL^T region in this plan (never reached: no variable bounds)
   }
   if constexpr (QD::nx > 0) {
     if (N <= kEqpRegCap) {
@@ -2157,17 +2158,17 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRC_TAS
       for (int j = 0; j < 6; ++j) r6[j] = A6[lr * 6 + j];
 #pragma unroll
       for (int k = 0; k < 6; ++k) {
-        const double akk = bcast(r6[k], k), aik = r6[k];
+        const double akk = bcast(r6[k], k), aik = r6[k], ia = 1.0 / akk;  // one FP64 divide per pivot
         double pk6[6];
 #pragma unroll
         for (int j = 0; j < 6; ++j) pk6[j] = bcast(r6[j], k);
 #pragma unroll
         for (int j = 0; j < 6; ++j) {
           double v;
-          if (l == k && j == k) v = 1.0 / akk;
-          else if (l == k) v = pk6[j] / akk;
-          else if (j == k) v = -aik / akk;
-          else v = r6[j] - aik * pk6[j] / akk;
+          if (l == k && j == k) v = ia;
+          else if (l == k) v = pk6[j] * ia;
+          else if (j == k) v = -aik * ia;
+          else v = r6[j] - aik * (pk6[j] * ia);
           r6[j] = v;
         }
         piv_min = fmin(piv_min, akk);
@@ -3853,7 +3854,10 @@ static int plan_layout(const DevModel& M, KParams* k, bool task_only) {
     k->ncap = N;
     k->nbuf = (N + 7) & ~7;
     const int reg_pol = k->oU0 + 128 + m;  // Fidx/Ridx | xx | yy
-    const int lds_pol = (qp_compiled(nx, ng, np) && N <= kEqpRegCap) ? 0
+    // (compiled whole-body shapes solve every polish KKT in range-space form,
+    // eqp_range: its H^-1 g_a buffer instead of the LDS LDL^T's)
+    const int lds_pol = k->oHi >= 0 ? k->oU0 + 256 + kEqpRegCap * nx
+                        : (qp_compiled(nx, ng, np) && N <= kEqpRegCap) ? 0
                         : k->oU0 + 64 + 64 + 128 + k->nbuf * 5 + N * (N + 1) / 2;
     int end = kin_end;
     end = end > fac_end ? end : fac_end;
