@@ -1983,6 +1983,17 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRC_TAS
       qv[l] = io.q[l * LD + gb];
       qd[l] = io.qdot[l * LD + gb];
     }
+    // task targets, one value per lane (lanes 0-11 x_target, 12-17 xdot_target,
+    // 18-29 x_init, 30-35 xdot_init): issued here so their latency overlaps the
+    // FK; the task-velocity stage reads them by v_readlane
+    double tgt = 0.0;
+    if (l < 12) {
+      if (kp.mode != DRC_MODE_QPIK) tgt = io.xt[l * LD + gb];
+    } else if (l < 18) {
+      tgt = io.xdt[(l - 12) * LD + gb];
+    } else if (l < 36 && kp.mode == DRC_MODE_QPIK_CUBIC) {
+      tgt = l < 30 ? io.xi[(l - 18) * LD + gb] : io.xdi[(l - 30) * LD + gb];
+    }
     wsync();
     // ---------------- FK: local joint transforms, then the chain ------------
     double* T = S + kp.kT;  // (nv+1) x 12
@@ -2059,17 +2070,21 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRC_TAS
     wsync();
     // ---------------- task velocity ---------------------------------------
     double* xdd = S + kp.kxdd;
+    // getVelocity = J qdot (robot_data.cpp:419-422), row r on lane r
+    double jq = 0.0;
+    if (l < 6)
+      for (int c = 0; c < nv; ++c) jq += J[l * nv + c] * qd[c];
     if (l == 0) {
       if (kp.mode == DRC_MODE_QPIK) {
-        for (int i = 0; i < 6; ++i) xdd[i] = io.xdt[i * LD + gb];
+        for (int i = 0; i < 6; ++i) xdd[i] = rd_lane(tgt, 12 + i);
       } else {
         double xt[12], xdt[6];
-        for (int i = 0; i < 12; ++i) xt[i] = io.xt[i * LD + gb];
-        for (int i = 0; i < 6; ++i) xdt[i] = io.xdt[i * LD + gb];
+        for (int i = 0; i < 12; ++i) xt[i] = rd_lane(tgt, i);
+        for (int i = 0; i < 6; ++i) xdt[i] = rd_lane(tgt, 12 + i);
         if (kp.mode == DRC_MODE_QPIK_CUBIC) {  // getTaskSpaceCubic (math_type_define.h:647)
           double xi[12], xdi[6], Rt[9], Ri[9];
-          for (int i = 0; i < 12; ++i) xi[i] = io.xi[i * LD + gb];
-          for (int i = 0; i < 6; ++i) xdi[i] = io.xdi[i * LD + gb];
+          for (int i = 0; i < 12; ++i) xi[i] = rd_lane(tgt, 18 + i);
+          for (int i = 0; i < 6; ++i) xdi[i] = rd_lane(tgt, 30 + i);
           for (int r = 0; r < 3; ++r)
             for (int c = 0; c < 3; ++c) {
               Rt[3 * r + c] = xt[3 * c + r];
@@ -2118,11 +2133,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRC_TAS
         for (int i = 0; i < 3; ++i)
           phi = phi + cross(v3(xt[3 * i], xt[3 * i + 1], xt[3 * i + 2]), v3(Te[i], Te[3 + i], Te[6 + i]));
         e[3] = -0.5 * phi.x; e[4] = -0.5 * phi.y; e[5] = -0.5 * phi.z;
-        for (int r = 0; r < 6; ++r) {  // getVelocity = J qdot (robot_data.cpp:419-422)
-          double s = 0;
-          for (int c = 0; c < nv; ++c) s += J[r * nv + c] * qd[c];
-          xdot[r] = s;
-        }
+        for (int r = 0; r < 6; ++r) xdot[r] = rd_lane(jq, r);
         for (int i = 0; i < 6; ++i)
           xdd[i] = kp.kp[i] * e[i] + kp.kv[i] * (xdt[i] - xdot[i]) + kp.ff * xdt[i];
       }
