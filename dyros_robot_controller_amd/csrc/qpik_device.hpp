@@ -803,6 +803,127 @@ DRC_HD __forceinline__ void epa_grow(EpaPoly* E, const SV w, int best, FaceMask 
   E->freel[C.nfree++] = best;
   C.store(E);
 }
+// Wave form of epa_grow (the task kernel).  The lane-serial horizon walk only
+// allocates the new faces' slots, vertices and adjacency (epa_grow_walk); the
+// wave then forms their normals and offsets and runs epa_newface's validity
+// tests one face per lane (epa_face_geometry), and the walking lane commits or
+// rolls back (epa_grow_finish).  Same slots, adjacency, face data and
+// decisions as epa_grow: a face that fails its test makes the step roll back
+// either way (epa_grow stops the walk there, this form finishes the walk
+// first; the rollback restores the same alive set and EPA stops).
+DRC_HD __forceinline__ int epa_newslot(EpaPoly* E, EpaCtl& C, int a, int b, int c) {
+  int f;
+  if (C.nfree > 0) {
+    f = E->freel[--C.nfree];
+  } else if (C.nf < kEpaMaxF) {
+    f = C.nf++;
+  } else {
+    C.fail = 1;
+    return -1;
+  }
+  E->newl[C.nnew++] = f;
+  E->fv[f][0] = a;
+  E->fv[f][1] = b;
+  E->fv[f][2] = c;
+  return f;
+}
+// epa_newface's geometry and tests for slot f (any lane)
+DRC_HD __forceinline__ bool epa_face_geometry(EpaPoly* E, int f, double fdmin) {
+  const V3 va_ = epa_vw(E, E->fv[f][0]);
+  V3 nn = cross(epa_vw(E, E->fv[f][1]) - va_, epa_vw(E, E->fv[f][2]) - va_);
+  const double L = sqrt(dot(nn, nn));
+  if (!(L > 1e-300)) {
+    E->alive[f] = 0;
+    return false;
+  }
+  nn = v3(nn.x / L, nn.y / L, nn.z / L);
+  const double fd = dot(nn, va_);
+  st3(E->fn[f], nn);
+  E->fd[f] = fd;
+  if (fd < -1e-12 || fd < fdmin - 1e-12) {
+    E->alive[f] = 0;
+    return false;
+  }
+  E->alive[f] = 1;
+  return true;
+}
+DRC_HD __forceinline__ bool epa_walk_all(EpaPoly* E, EpaCtl& C, int w, int best, FaceMask vis) {
+  FaceMask done{0, 0};
+  done.set(best);
+  for (int j = 0; j < 3; ++j) {
+    E->stk[0] = E->adj[best][j];
+    int sp = 1;
+    while (sp > 0) {
+      const int ent = E->stk[sp - 1];
+      const int f = ent & 0xffff, e = (ent >> 16) & 0xff, st = ent >> 24;
+      if (st == 0) {
+        if (done.has(f)) {
+          --sp;
+          continue;
+        }
+        const int e1 = e == 2 ? 0 : e + 1;
+        if (!vis.has(f)) {  // horizon edge
+          const int nf = epa_newslot(E, C, E->fv[f][e1], E->fv[f][e], w);
+          if (nf < 0) return false;
+          epa_bind(E, nf, 0, f, e);
+          if (C.hcf >= 0) epa_bind(E, C.hcf, 1, nf, 2);
+          else C.hff = nf;
+          C.hcf = nf;
+          ++C.hnf;
+          --sp;
+          continue;
+        }
+        done.set(f);
+        E->stk[sp - 1] = f | (e << 16) | (1 << 24);
+        if (sp >= kEpaMaxF) return false;
+        E->stk[sp++] = E->adj[f][e1];
+      } else if (st == 1) {
+        const int e2 = e == 0 ? 2 : e - 1;
+        E->stk[sp - 1] = f | (e << 16) | (2 << 24);
+        if (sp >= kEpaMaxF) return false;
+        E->stk[sp++] = E->adj[f][e2];
+      } else {
+        E->alive[f] = 0;
+        E->deadl[C.ndead++] = f;
+        --sp;
+      }
+    }
+  }
+  return true;
+}
+DRC_HD __forceinline__ void epa_grow_walk(EpaPoly* E, const SV w, int best, FaceMask vis) {
+  EpaCtl C;
+  C.load(E);
+  const int wi = C.nv;
+  st3(E->vw[wi], w.w);
+  st3(E->va[wi], w.a);
+  C.nv++;
+  C.hcf = -1;
+  C.hff = -1;
+  C.hnf = 0;
+  C.ndead = 0;
+  C.nnew = 0;
+  C.fdmin = E->fd[best];
+  if (!epa_walk_all(E, C, wi, best, vis)) C.hnf = -1;  // invalid walk: epa_grow_finish rolls back
+  C.store(E);
+}
+DRC_HD __forceinline__ void epa_grow_finish(EpaPoly* E, int best, bool geom_fail) {
+  EpaCtl C;
+  C.load(E);
+  if (C.hnf < 3 || C.fail || geom_fail) {  // roll back to the last closed polytope
+    for (int i = 0; i < C.nnew; ++i) E->alive[E->newl[i]] = 0;
+    for (int i = 0; i < C.ndead; ++i) E->alive[E->deadl[i]] = 1;
+    C.nv--;
+    C.store(E);
+    E->stop = 1;
+    return;
+  }
+  epa_bind(E, C.hcf, 1, C.hff, 2);
+  E->alive[best] = 0;
+  for (int i = 0; i < C.ndead; ++i) E->freel[C.nfree++] = E->deadl[i];
+  E->freel[C.nfree++] = best;
+  C.store(E);
+}
 // one expansion step (lane-serial form, host harness)
 DRC_HD inline void epa_step(const Shape& A, const Shape& B, EpaPoly* E, int best) {
   const SV w = sup_md(A, B, ld3(E->fn[best]));

@@ -2405,7 +2405,18 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRC_TAS
           FaceMask vis;  // visibility of every face for w, one bit per face
           vis.lo = __ballot(l < ews->nf && epa_sees(ews, l, w.w));
           vis.hi = __ballot(l + 64 < ews->nf && epa_sees(ews, l + 64, w.w));
-          if (l == ln) epa_grow(ews, w, fb, vis);
+          // horizon walk on one lane (slots, adjacency), the new faces'
+          // normals and validity tests one per lane, then commit / roll back
+          if (l == ln) epa_grow_walk(ews, w, fb, vis);
+          wsync();
+          {
+            const double fdmin = ews->fd[fb];
+            bool gfail = false;
+            for (int i = l; i < ews->nnew; i += 64) gfail |= !epa_face_geometry(ews, ews->newl[i], fdmin);
+            gfail = __any(gfail);
+            wsync();
+            if (l == ln) epa_grow_finish(ews, fb, gfail);
+          }
           wsync();
 #ifdef DRC_PHASE_TIMING
           epa_t[2] += __builtin_amdgcn_s_memtime() - te2;
