@@ -111,3 +111,16 @@ def test_broad_phase_bound_and_gjk_cut(harness):
     assert np.all(lb <= d + 1e-12), (lb - d).max()
     assert np.mean(d - lb < 0.25 * np.abs(d) + 1e-3) > 0.3  # informative, not just -inf
     assert not pruned.any(), np.nonzero(pruned)
+
+
+def test_epa_wave_form_matches_serial(harness):
+    """The task kernel's EPA growth (horizon walk on one lane, the new faces'
+    geometry and validity tests one per lane, then commit or roll back:
+    epa_grow_walk / epa_face_geometry / epa_grow_finish) returns the
+    lane-serial epa_grow's depth and witnesses bit for bit on every
+    penetrating pair, including the vertex-cap and rolled-back steps."""
+    pairs = random_pairs(4000, 13)
+    dev = run_harness(harness, pairs)
+    pen = dev[:, 0] < 0
+    assert pen.sum() > 500
+    assert np.all(dev[:, 9] == 1), np.nonzero(dev[:, 9] != 1)
