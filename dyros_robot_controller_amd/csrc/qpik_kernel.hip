@@ -4102,10 +4102,11 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
   // order; smaller ones run grid-stride order): with one sub-batch the QP
   // kernel waits for the whole task kernel, with several they overlap
   // (Husky-FR3's 16 Ki batch)
+  static const int64_t min_sub = getenv("DRC_MIN_SUBBATCH") ? atoll(getenv("DRC_MIN_SUBBATCH")) : 4096;
   int S = 1;
   if (!stages)
     for (int c = m->chunks; c > 1; --c)
-      if (B / c >= 4096) {
+      if (B / c >= min_sub) {
         S = c;
         break;
       }
