@@ -505,15 +505,13 @@ __device__ __noinline__ void schur_setup(const KParams& kp, double* S) {
     wt[l] = w;
   }
   wsync();
-  if (l < NP) {  // row l of S
+  for (int e = l; e < NP * NP; e += GL::size) {  // entry (i, c) of S, one per lane
+    const int i = e / NP, c = e % NP;
+    double sv = P[i * NP + c];
+    if (c == i) sv += sig + rho[i] * ab[i] * ab[i];
 #pragma unroll
-    for (int c = 0; c < NP; ++c) {
-      double sv = P[l * NP + c];
-      if (c == l) sv += sig + rho[l] * ab[l] * ab[l];
-#pragma unroll
-      for (int r = 0; r < NG; ++r) sv += wt[r] * G[r * NX + l] * G[r * NX + c];
-      Si[l * NP + c] = sv;
-    }
+    for (int r = 0; r < NG; ++r) sv += wt[r] * G[r * NX + i] * G[r * NX + c];
+    Si[e] = sv;
   }
   wsync();
   // Gauss-Jordan in registers, lane l holding row l (S is SPD)
