@@ -464,6 +464,10 @@ int build_model_from_urdf(const std::string& urdf_path, const std::string& srdf_
         const int c = ta == 0 ? tb : (ta == 1 ? 2 + tb : 5);  // (0,0)0 (0,1)1 (0,2)2 (1,1)3 (1,2)4 (2,2)5
         if (c == cls) m.pair_order[n++] = static_cast<int16_t>(p);
       }
+    for (int sl = 0; sl < m.npairs; ++sl) {
+      m.slot_a[sl] = m.pair_a[m.pair_order[sl]];
+      m.slot_b[sl] = m.pair_b[m.pair_order[sl]];
+    }
   }
   // GJK candidate slots of the lane-per-instance task stage: the pairs with
   // no sphere (no closed form), numbered in pair order

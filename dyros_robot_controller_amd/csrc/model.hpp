@@ -46,6 +46,7 @@ struct DevModel {
   int ncand_slots;                    // non-sphere pairs (> kMaxCandSlots: lane stage not used)
   int16_t pair_order[kMaxPairs];      // pairs grouped by shape-type class (pair index order within a class):
                                       // the wave kernel's lanes then take same-type pairs in each round
+  int16_t slot_a[kMaxPairs], slot_b[kMaxPairs];  // pair_a / pair_b of pair_order[slot]: one load level less
   double J_mobile[3][kMaxWheels];  // base twist = J_mobile * wheel velocity (differential, mecanum)
   int drive;                       // DriveKind; caster: J_mobile depends on the steer angles (mobile_fk.hpp)
   double wheel_radius, wheel_offset;

@@ -2257,8 +2257,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRC_TAS
     // slots in type-class order (model.cpp pair_order): each round of 64 lanes
     // runs one or two pair types instead of all of them
     for (int sl = l; sl < M->npairs; sl += 64) {
-      const int p = M->pair_order[sl];
-      const int ga = M->pair_a[p], gb = M->pair_b[p];
+      const int p = M->pair_order[sl], ga = M->slot_a[sl], gb = M->slot_b[sl];
       Shape A{M->gtype[ga], Tg + 12 * ga, M->gparam[ga][0], M->gparam[ga][1], M->gparam[ga][2]};
       Shape Bs{M->gtype[gb], Tg + 12 * gb, M->gparam[gb][0], M->gparam[gb][1], M->gparam[gb][2]};
       V3 pA, pB;
