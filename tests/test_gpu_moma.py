@@ -85,3 +85,32 @@ def test_moma_single_instance_split(cuda):
         np.testing.assert_array_equal(vm, eta[a.mobi_start:a.mobi_start + W])
         np.testing.assert_array_equal(va, eta[a.mani_start:a.mani_start + 7])
     assert vm.shape == (W,) and va.shape == (7,)
+
+
+@pytest.mark.parametrize("robot", ["husky_fr3", "xls_fr3"])
+def test_moma_lp_certificate_on_device(cuda, robot):
+    """D15 on the device: the whole-body instances the oracle's Farkas
+    certificate proves infeasible come back PrimalInfeasible after 0 ADMM
+    iterations with zero output, the same instances as the oracle's (fed the
+    device's distance stage, so both judge the same rows); every other
+    instance runs the ADMM (iterations > 0) and no instance runs past 100
+    iterations (D16: no polish-cap tail)."""
+    import torch
+    rd = make_moma(robot, cuda)
+    ctrl = MM.RobotController(0.001, rd, solver_mode="exact")
+    B = 2048
+    q, qd, xt, xdt = moma_step_inputs(rd, robot, 12, B, cuda, stress=True)
+    iters = torch.zeros(B, dtype=torch.int32, device=cuda)
+    out, status = ctrl.QPIK_step_batch(q, qd, xt, xdt, LINK[robot], iters=iters)
+    out, status, iters = out.cpu().numpy(), status.cpu().numpy(), iters.cpu().numpy()
+    st = stage_pose(rd.model, cuda, q, qd, LINK[robot])
+    pm, om, spec = O.load(robot)
+    par = O.default_params(1, exact=True)
+    _, ost, oit = O.qpik_batch_dist(om, par, q, qd, xt, xdt, np.ascontiguousarray(st["dist"]), nthreads=8)
+    cert_dev = (status == O.PRIMAL_INFEASIBLE) & (iters == 0)
+    cert_orc = (ost == O.PRIMAL_INFEASIBLE) & (oit == 0)
+    assert cert_dev.sum() >= 3
+    np.testing.assert_array_equal(cert_dev, cert_orc)
+    assert np.all(out[:, cert_dev] == 0)
+    assert np.all(iters[~cert_dev] > 0)
+    assert iters.max() <= 100, iters.max()
