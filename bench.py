@@ -11,12 +11,20 @@
 One "step" = one control cycle of the batch through the product path
 (drc_qpik_batch: task-space kernel + QP kernel), inputs resident in HBM,
 SURVEY §8d's workload including the three 10 % stress tiers.  Multi-GPU: one
-process per GPU (torchrun), instances sharded as contiguous ranges with no
-data-path collective; weak scaling by default (--batch per GPU), strong
-scaling with --global-batch.  A barrier and a max-reduction of the timed
-region are the only collectives.
+process per GPU, instances sharded as contiguous ranges with no data-path
+collective; weak scaling by default (--batch per GPU), strong scaling with
+--global-batch.  A barrier and a max-reduction of the timed region are the
+only collectives.  ``--gpus N`` without a torchrun environment starts the N
+ranks itself (dist.launch_if_needed); under torchrun, WORLD_SIZE must equal N.
+
+Besides the headline line (exact mode), a single-GPU run reports, outside the
+timed region: the same batch at the reference's OSQP settings
+(``reference_settings``), the BASELINE config-2 batch of 4 096
+(``batch_4096``), and the latency of the reference's per-cycle call — one
+synchronous QPIKCubic through the host entry (``latency_b1``, p50 / p99).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--robot fr3] [--batch B | --global-batch G]
+                    [--solver exact|osqp_default] [--no-extras] [--no-cpu-baseline]
 """
 import argparse
 import json
@@ -29,8 +37,12 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+from dyros_robot_controller_amd import dist as ddist  # noqa: E402  (no torch / GPU at import)
+
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 FP64_VECTOR_PEAK_TFS = 78.6    # AMD spec, FP64 vector
+CLOCK_GHZ = 2.4                # MI355X peak engine clock (MI355X_MICROARCH.md)
+WAVE_SLOTS = 256 * 4 * 2       # CUs x SIMDs x waves per SIMD at the kernels' 256-VGPR budget
 DEFAULT_BATCH = {"fr3": 65536, "ur5e": 65536, "husky_fr3": 16384, "xls_fr3": 65536, "caster_fr3": 65536}
 METRIC = "QP-IK solves/s (FR3 7-DoF, batch 65k) + achieved HBM GB/s vs peak"
 
@@ -120,6 +132,79 @@ def load_profile(name, robot, B):
     return None
 
 
+def timed_steps(torch, step, steps, warmup):
+    """Warm-up, then ``steps`` calls bracketed by synchronisation: seconds per
+    call (host wall clock over the whole run)."""
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps
+
+
+def iter_stats(iters, status):
+    it = iters.cpu().numpy()
+    return {"non_solved": int((status != 1).sum().item()), "admm_iters_mean": float(it.mean()),
+            "admm_iters_p99_max": [float(np.percentile(it, 99)), int(it.max())]}
+
+
+def latency_b1(rd, robot, q, qd, xt, xdt, solver, calls=400, warmup=20):
+    """The reference's per-cycle call (examples/C++/src/fr3_controller.cpp:122-134,
+    one QPIKCubic per 1 kHz control cycle): one instance through the
+    synchronous host entry drc_qpik_host (what the C++ facade's QPIKCubic
+    calls), wall time per call on the host, p50 / p99 / max."""
+    import ctypes as C
+    from dyros_robot_controller_amd import BUNDLED, _capi, manipulator
+    link = BUNDLED[robot]["link"]
+    p = manipulator.QPIKParamsBuilder(rd.model, exact=(solver == "exact")).params(
+        link, _capi.MODE_QPIK_CUBIC, t=0.3, t0=0.0, duration=1.0)
+    col = lambda a: np.ascontiguousarray(a[:, :1])
+    q1, qd1, xt1, xdt1 = col(q), col(qd), col(xt), col(xdt)
+    xi1, xdi1 = xt1.copy(), np.zeros_like(xdt1)
+    xi1[9:] -= 0.02                                  # start 2 cm away: the cubic is mid-profile at t = 0.3
+    out = np.zeros((rd.model.actuated_dof, 1))
+    st, it = np.zeros(1, np.int32), np.zeros(1, np.int32)
+    dp = lambda a: a.ctypes.data_as(C.POINTER(C.c_double))
+    ip = lambda a: a.ctypes.data_as(C.POINTER(C.c_int))
+    lib, h = _capi.lib(), rd.model.handle
+    ts = []
+    for k in range(warmup + calls):
+        t0 = time.perf_counter()
+        rc = lib.drc_qpik_host(h, C.byref(p), C.c_int64(1), dp(q1), dp(qd1), dp(xt1), dp(xdt1), dp(xi1), dp(xdi1),
+                               dp(out), ip(st), ip(it))
+        t1 = time.perf_counter()
+        _capi.check(rc)
+        if k >= warmup:
+            ts.append(t1 - t0)
+    ts = np.array(ts) * 1e6
+    return {"call": "QPIKCubic, B = 1, drc_qpik_host (host buffers in and out, synchronous)",
+            "p50_us": float(np.percentile(ts, 50)), "p99_us": float(np.percentile(ts, 99)),
+            "max_us": float(ts.max()), "calls": calls, "status": int(st[0]), "admm_iters": int(it[0]),
+            "cycle_budget_us": 1000.0}
+
+
+def dry_run(args):
+    """Launcher / sharding / reduction rehearsal without a GPU (tests): every
+    rank reports its shard through the same collectives the bench uses."""
+    import torch.distributed as dist
+    rank, world, _ = ddist.env_rank()
+    backend = os.environ.get("DRC_DIST_BACKEND", "gloo")
+    if world > 1:
+        ddist.init(backend)
+    B = args.batch or DEFAULT_BATCH[args.robot]
+    offset, cnt = ddist.shard_global(rank, world, args.global_batch) if args.global_batch else ddist.shard(rank, B)
+    wall, n_cnt, off_mean = ddist.reduce_stats(0.001 * (rank + 1), cnt, offset, world)
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "ranks_reporting": world, "instances": int(n_cnt),
+                          "max_wall": wall, "mean_offset": off_mean}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -128,25 +213,36 @@ def main():
     ap.add_argument("--robot", default="fr3", choices=sorted(DEFAULT_BATCH))
     ap.add_argument("--batch", type=int, default=None, help="instances per GPU (weak scaling)")
     ap.add_argument("--global-batch", type=int, default=None, help="fixed total instances (strong scaling)")
+    ap.add_argument("--solver", default="exact", choices=("exact", "osqp_default"),
+                    help="exact: certified optimum (parity contract); osqp_default: the reference's OSQP settings")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true", help="skip reference_settings / batch_4096 / latency_b1")
     ap.add_argument("--chunks", type=int, default=3, help="concurrent sub-batches per call")
     ap.add_argument("--task-stage", type=int, default=0, choices=(0, 1, 2),
                     help="0 wave-per-instance task kernel (default), 1 lane stage + side-stream hand-backs, "
                          "2 lane stage + serial hand-backs (drc_debug_lane_stage)")
+    ap.add_argument("--dry-run", action="store_true", help="launcher and collectives only (no GPU)")
     args = ap.parse_args()
+
+    rc = ddist.launch_if_needed(args.gpus, os.path.abspath(__file__), sys.argv[1:])
+    if rc is not None:          # this process launched the ranks; it never touched the GPU
+        sys.exit(rc)
+    if args.dry_run:
+        return dry_run(args)
 
     import torch
     import torch.distributed as dist
 
-    from dyros_robot_controller_amd import BUNDLED, _capi, dist as ddist, make_robot
+    from dyros_robot_controller_amd import BUNDLED, _capi, make_robot
     from dyros_robot_controller_amd import manipulator, mobile_manipulator
     rank, world, local = ddist.env_rank()
     backend = os.environ.get("DRC_DIST_BACKEND", "nccl")   # gloo: rehearse N ranks on one GPU
-    if world > 1:
-        torch.cuda.set_device(local % max(torch.cuda.device_count(), 1))
-        ddist.init(backend, torch.device("cuda", local) if backend == "nccl" else None)
-    dev = torch.device("cuda", local % max(torch.cuda.device_count(), 1))
+    ndev = max(torch.cuda.device_count(), 1)
+    dev = torch.device("cuda", local % ndev)
     torch.cuda.set_device(dev)
+    if world > 1:
+        ddist.init(backend, dev if backend == "nccl" else None)
+    red_dev = dev if backend == "nccl" else "cpu"
 
     robot = args.robot
     spec = BUNDLED[robot]
@@ -159,7 +255,7 @@ def main():
         scaling, total_per_step = "weak", B * world
     rd = make_robot(robot, dev)
     mod = manipulator if spec["kind"] == "manipulator" else mobile_manipulator
-    ctrl = mod.RobotController(0.001, rd, solver_mode="exact")
+    ctrl = mod.RobotController(0.001, rd, solver_mode=args.solver)
     (q, qd, xt, xdt), (dq, dqd, dxt, dxdt), tiers = make_inputs(rd, robot, B, 12345, offset, dev)
     iters = torch.zeros(B, dtype=torch.int32, device=dev)
     link = spec["link"]
@@ -200,8 +296,7 @@ def main():
     # concurrent sub-batches); task/qp: summed per-sub-batch kernel durations
     kernel_ms, task_ms, qp_ms = tw.value / ncall, tk.value / ncall, tq.value / ncall
     wall, n_bad, it_mean = ddist.reduce_stats(wall, float((status != 1).sum().item()),
-                                              float(iters.double().mean().item()), world,
-                                              dev if backend == "nccl" else "cpu")
+                                              float(iters.double().mean().item()), world, red_dev)
 
     if rank == 0:
         dof, act = rd.model.dof, rd.model.actuated_dof
@@ -226,18 +321,25 @@ def main():
         valu = load_profile("valu_counters_%s.json" % robot, robot, B)
         if valu:   # counter-based FP64 work per call (tools/valu_summary.py over rocprofv3 --pmc passes)
             f = valu["fp64_flops_per_step"]
-            roof["fp64_valu"] = {"achieved_tflops": f / (kernel_ms * 1e-3) / 1e12, "peak_tflops": FP64_VECTOR_PEAK_TFS,
-                                 "frac": f / (kernel_ms * 1e-3) / 1e12 / FP64_VECTOR_PEAK_TFS,
-                                 "fp64_flops_per_step": f, "lane_efficiency": valu.get("lane_efficiency"),
+            eff = valu.get("lane_efficiency") or 0.0
+            issued = f / (kernel_ms * 1e-3) / 1e12
+            roof["fp64_valu"] = {"issued_tflops": issued, "executed_tflops": issued * eff,
+                                 "peak_tflops": FP64_VECTOR_PEAK_TFS,
+                                 "issued_frac": issued / FP64_VECTOR_PEAK_TFS,
+                                 "executed_frac": issued * eff / FP64_VECTOR_PEAK_TFS,
+                                 "fp64_flops_issued_per_step": f, "lane_efficiency": eff,
+                                 "note": "issued counts 64 lanes per FP64 instruction; executed = issued x lane "
+                                         "efficiency (active lanes); neither is algorithmic work",
                                  "source": "profiles/valu_counters_%s.json" % robot}
         line = {
             "metric": METRIC, "value": value, "unit": "solves/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": scaling,
             "vs_baseline": None, "dtype": "f64", "data": "synthetic (SURVEY 8d workload with the stress tiers)",
-            "config": {"workload": "%s QPIKStep (exact: certified OSQP polish), %d instances per GPU%s"
-                                   % (robot.upper(), B, ", global batch %d" % args.global_batch
-                                      if args.global_batch else ""),
-                       "robot": robot, "batch_per_gpu": B, "global_batch": total_per_step,
+            "config": {"workload": "%s QPIKStep (%s), %d instances per GPU%s"
+                                   % (robot.upper(), "exact: certified OSQP polish" if args.solver == "exact"
+                                      else "reference OSQP settings: eps 1e-3, no polish", B,
+                                      ", global batch %d" % args.global_batch if args.global_batch else ""),
+                       "robot": robot, "batch_per_gpu": B, "global_batch": total_per_step, "solver": args.solver,
                        "parallelism": "dp%d (instances sharded, no data-path collective)" % world,
                        "task_stage": ["wave-per-instance", "lane-per-instance + side-stream hand-backs",
                                       "lane-per-instance + serial hand-backs"][args.task_stage]},
@@ -246,11 +348,56 @@ def main():
             "admm_iters_p99_max": [float(np.percentile(iters.cpu().numpy(), 99)), int(iters.max().item())],
             "stress_tiers": tiers,
         }
+        if world == 1 and not args.no_extras:
+            extras(torch, args, rd, mod, robot, link, q, qd, xt, xdt, dq, dqd, dxt, dxdt, line)
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(robot, q, qd, xt, xdt)
         print(json.dumps(line), flush=True)
     if world > 1:
+        dist.barrier()
         dist.destroy_process_group()
+
+
+def extras(torch, args, rd, mod, robot, link, q, qd, xt, xdt, dq, dqd, dxt, dxdt, line):
+    """Single-GPU side measurements, outside the headline's timed region."""
+    B = dq.shape[1]
+    other = "osqp_default" if args.solver == "exact" else "exact"
+    ctrl_o = mod.RobotController(0.001, rd, solver_mode=other)
+    it_o = torch.zeros(B, dtype=torch.int32, device=dq.device)
+    res = {}
+    s = timed_steps(torch, lambda: res.update(r=ctrl_o.QPIK_step_batch(dq, dqd, dxt, dxdt, link, iters=it_o)),
+                    args.steps, 2)
+    line["reference_settings" if other == "osqp_default" else "exact_settings"] = dict(
+        solver=other, value=B / s, unit="solves/s", ms_per_step=1e3 * s, **iter_stats(it_o, res["r"][1]))
+    # BASELINE config 2: batch 4 096 (first instances of the same workload)
+    nb = min(4096, B)
+    sub = [t[:, :nb].contiguous() for t in (dq, dqd, dxt, dxdt)]
+    ctrl = mod.RobotController(0.001, rd, solver_mode=args.solver)
+    it_s = torch.zeros(nb, dtype=torch.int32, device=dq.device)
+    s = timed_steps(torch, lambda: res.update(r=ctrl.QPIK_step_batch(*sub, link, iters=it_s)), max(args.steps, 20), 3)
+    line["batch_%d" % nb] = dict(value=nb / s, unit="solves/s", ms_per_step=1e3 * s, **iter_stats(it_s, res["r"][1]))
+    line["latency_b1"] = latency_b1(rd, robot, q, qd, xt, xdt, args.solver)
+    # latency roof: one instance alone on the chip (B = 1 device time) bounds a
+    # wave-per-instance design at WAVE_SLOTS / latency solves/s
+    import ctypes as C
+    from dyros_robot_controller_amd import _capi
+    one = [t[:, :1].contiguous() for t in (dq, dqd, dxt, dxdt)]
+    it1 = torch.zeros(1, dtype=torch.int32, device=dq.device)
+    timed_steps(torch, lambda: ctrl.QPIK_step_batch(*one, link, iters=it1), 1, 10)
+    lib, h = _capi.lib(), rd.model.handle
+    _capi.check(lib.drc_debug_kernel_timing(h, 1))
+    timed_steps(torch, lambda: ctrl.QPIK_step_batch(*one, link, iters=it1), 100, 0)
+    tw, tk, tq, nc = C.c_double(), C.c_double(), C.c_double(), C.c_int()
+    _capi.check(lib.drc_debug_kernel_times(h, C.byref(tw), C.byref(tk), C.byref(tq), C.byref(nc)))
+    _capi.check(lib.drc_debug_kernel_timing(h, 0))
+    lat = (tk.value + tq.value) / max(nc.value, 1) * 1e-3          # task + QP kernel of one instance, seconds
+    roof = WAVE_SLOTS / lat
+    line["roofline"]["latency_roof"] = {
+        "instance_latency_us": 1e6 * lat, "call_us": 1e3 * tw.value / max(nc.value, 1), "wave_slots": WAVE_SLOTS,
+        "solves_per_s": roof, "frac": line["value"] / roof,
+        "note": "one instance alone on the GPU: task + QP kernel durations (HIP events, B = 1); a wave-per-instance "
+                "design with WAVE_SLOTS instances in flight (two 256-VGPR waves per SIMD) cannot beat "
+                "WAVE_SLOTS / latency"}
 
 
 if __name__ == "__main__":

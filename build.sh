@@ -1,11 +1,25 @@
 #!/bin/bash
 # Builds the product library (gfx950) and the oracle checker library.
+# The HIP translation units compile in parallel (one hipcc per unit), then link.
 set -e
 cd "$(dirname "$0")"
 HIPCC=${HIPCC:-/opt/rocm/bin/hipcc}
-$HIPCC --offload-arch=gfx950 -O3 -fPIC -shared -std=c++17 -Wall -Wno-unused-function \
-  dyros_robot_controller_amd/csrc/qpik_kernel.hip dyros_robot_controller_amd/csrc/dynamics.hip dyros_robot_controller_amd/csrc/model.cpp \
-  -o dyros_robot_controller_amd/libdrc_amd.so -Wl,-rpath,/opt/rocm/lib
+CSRC=dyros_robot_controller_amd/csrc
+OBJ=build/obj${DRC_VARIANT:+_$DRC_VARIANT}
+OUT=${DRC_OUT:-dyros_robot_controller_amd/libdrc_amd.so}
+mkdir -p "$OBJ"
+FLAGS="--offload-arch=gfx950 -O3 -fPIC -std=c++17 -Wall -Wno-unused-function $DRC_EXTRA_FLAGS"
+pids=()
+for src in task_kernel.hip qp_kernel.hip qpid_kernel.hip dynamics.hip api.cpp model.cpp; do
+  $HIPCC $FLAGS -c $CSRC/$src -o "$OBJ/${src%.*}.o" &
+  pids+=($!)
+done
+rc=0
+for p in "${pids[@]}"; do wait "$p" || rc=1; done
+[ $rc -eq 0 ] || { echo "build.sh: a HIP translation unit failed to compile" >&2; exit 1; }
+$HIPCC --offload-arch=gfx950 -shared -fPIC "$OBJ"/task_kernel.o "$OBJ"/qp_kernel.o "$OBJ"/qpid_kernel.o \
+  "$OBJ"/dynamics.o "$OBJ"/api.o "$OBJ"/model.o -o "$OUT" -Wl,-rpath,/opt/rocm/lib
+[ -n "$DRC_VARIANT" ] && exit 0
 make -s -C oracle
 mkdir -p dyros_robot_controller_amd/python
 # C++ facade + pybind11 module with the reference's module/class names (host code only)

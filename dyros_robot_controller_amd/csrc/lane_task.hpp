@@ -1,4 +1,4 @@
-// Lane-per-instance task stage of QPIK (included by qpik_kernel.hip).
+// Lane-per-instance task stage of QPIK (included by task_kernel.hip).
 //
 // The wave-per-instance task_kernel spends most of its time in phases that
 // use a handful of lanes (the FK chain, the 6x6 manipulability algebra, one
@@ -222,6 +222,7 @@ lane_task_kernel(const DevModel* __restrict__ M, const KParams kp, const IO io) 
   LPH(50);
   LCNT(56, hard && !why_int);
   LCNT(57, why_int);
+  (void)why_int;  // counted in the timing build only
   LCNT(58, true);
 #ifdef DRC_PHASE_TIMING
   atomicAdd(&g_phase_cycles[60], (unsigned long long)ncand);

@@ -1,0 +1,31 @@
+// Host-side launchers of the kernel translation units (task_kernel.hip,
+// qp_kernel.hip, qpid_kernel.hip), called by the C-ABI in api.cpp.  Each
+// returns the hipError_t of its launch (0 = hipSuccess).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "kernel_common.hpp"
+
+namespace drc_amd {
+
+// task_kernel<problem>: 0 QPIK stage, 1 QPID stage, 2 closed-form CLIK / OSF
+int launch_task_kernel(int problem, unsigned grid, size_t lds, hipStream_t st, const DevModel* m, const KParams& kp,
+                       const IO& io);
+// lane-per-instance task stage (nv = 6 or 7)
+int launch_lane_task_kernel(int nv, unsigned grid, hipStream_t st, const DevModel* m, const KParams& kp,
+                            const IO& io);
+// QPIK shapes with a compile-time qp_kernel instantiation (register Schur ADMM)
+bool qp_compiled(int nx, int ng, int np);
+// qp_kernel for kp's shape; lds = one lane group's plan
+int launch_qp_kernel(unsigned grid, size_t lds, hipStream_t st, const DevModel* m, const KParams& kp, const IO& io);
+int launch_qpid_kernel(unsigned grid, size_t lds, hipStream_t st, const DevModel* m, const KParams& kp, const IO& io);
+
+#ifdef DRC_PHASE_TIMING
+// diagnostic build: add each unit's phase slots to out[64]
+int phase_cycles_task(unsigned long long* out, int reset);
+int phase_cycles_qp(unsigned long long* out, int reset);
+int phase_cycles_qpid(unsigned long long* out, int reset);
+#endif
+
+}  // namespace drc_amd

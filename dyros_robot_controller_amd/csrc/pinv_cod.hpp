@@ -1,5 +1,5 @@
 // DyrosMath::PinvCOD (math_type_define.h:563-570) as a serial device routine,
-// shared by the manipulability stage (6x6 JJ^T, qpik_kernel.hip) and the
+// shared by the manipulability stage (6x6 JJ^T, task_kernel.hip) and the
 // dynamics kernel (M, S^T M S; dynamics.hip) for the rare inputs whose full rank
 // the fast paths cannot certify.
 #pragma once

@@ -1,0 +1,102 @@
+// QP stage of the QP-IK hot path: one wavefront
+// per instance assembles the QP of QP_IK.cpp:69-131 (MoMa QP_IK.cpp:59-128)
+// from the task record and solves it with the OSQP ADMM of qp_solver.hpp.
+// Compile-time shapes for the bundled robots (register Schur ADMM), a
+// runtime-sized instantiation for anything else.
+#include "kernel_common.hpp"
+#include "launch.hpp"
+#include "qp_solver.hpp"
+
+namespace drc_amd {
+
+
+// QP kernel: assembles and solves the QP of each instance from the task
+// record written by task_kernel.
+#ifndef DRC_QP_WAVES
+#define DRC_QP_WAVES 2
+#endif
+template <class QD>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRC_QP_WAVES, 8)))
+qp_kernel(const DevModel* __restrict__ M0, const KParams kp, const IO io) {
+  extern __shared__ __attribute__((aligned(16))) double S[];
+  // LDS copy of the parameters for the out-of-line (rare) ADMM blocks: a
+  // reference to the kernel argument itself would be copied to scratch
+  __shared__ KParams kpl;
+  {
+    static_assert(sizeof(KParams) % 8 == 0, "KParams copied as 8-byte words");
+    const uint64_t* src = reinterpret_cast<const uint64_t*>(&kp);
+    uint64_t* dst = reinterpret_cast<uint64_t*>(&kpl);
+    for (int e = lane_id(); e < static_cast<int>(sizeof(KParams) / 8); e += 64) dst[e] = src[e];
+    wsync();
+  }
+  // QD::gs = 32: two instances per wave, each lane group on its own LDS
+  // plan (the launch allocates one per group) and its own instance sequence
+  using GL = Grp<QD::gs>;
+  const int l = GL::lane();
+  double* const Sg = S + (GL::upper() ? kp.lds_doubles : 0);
+  const int64_t B = io.B;
+  PH_DECL
+  // hard_mode 1: the lane stage's hard list (grid stride); 2: every instance
+  // except the flagged ones (their records are still being written)
+  const bool hl = io.hard_mode == 1;
+  const InstSeqG<QD::gs> seq(hl ? int64_t(*io.hard_n) : B, hl ? 0 : kp.xcd_map, hl ? nullptr : io.queue);
+  for (int64_t j = seq.first(); j < seq.n; j = seq.next(j)) {
+    const int64_t b = hl ? int64_t(io.hard_list[j]) : seq.at(j);
+    if (b >= B) continue;
+    if (io.hard_mode == 2 && io.hard_flag[b]) continue;
+    const int64_t gb = io.b0 + b, LD = io.ld;  // position in the caller's [field][B] arrays
+    const DevModel* M = M0;
+    asm volatile("" : "+s"(M));
+    double* S = Sg;
+    qp_assemble<QD>(M, kp, S, io, b);
+    PH(0);
+    const bool lp_inf = M->kind == 1 && kp.s.exact && moma_lp_infeasible<QD>(M, kp, S);
+    int status, iters = 0;
+    if constexpr (QD::reg) status = qp_scale_regs<QD>(kpl, S);
+    else status = qp_scale<QD>(kp, S);
+    PH(1);
+    if (status != DRC_STATUS_NONFINITE) {
+      if (lp_inf) status = DRC_STATUS_PRIMAL_INFEASIBLE;
+      else status = qp_admm<QD>(kp, kpl, S, &iters);
+    }
+    PH(3);
+    // ---------------- outputs (zero on failure, QP_IK.cpp:56-61) ------------
+    const double *D = S + kp.oD, *x = S + kp.oX;
+    if (l < kp.na) io.out[(int64_t)l * LD + gb] = status == DRC_STATUS_SOLVED ? D[l] * x[l] : 0.0;
+    if (l == 0) {
+      io.status[gb] = status;
+      if (io.iters) io.iters[gb] = iters;
+    }
+    wsync();
+    PH(5);
+  }
+  PH_FLUSH(16);
+}
+
+
+bool qp_compiled(int nx, int ng, int np) {
+  return (nx == 23 && ng == 16 && np == 7) || (nx == 20 && ng == 14 && np == 6) || (nx == 9 && ng == 16 && np == 9) ||
+         (nx == 11 && ng == 16 && np == 11);
+}
+
+int launch_qp_kernel(unsigned grid, size_t lds, hipStream_t st, const DevModel* m, const KParams& kp, const IO& io) {
+  const dim3 g(grid), blk(64);
+  const size_t lg = lds * (64 / kQpGroup);  // one LDS plan per lane group
+  if (kp.nx == 23 && kp.ng == 16 && kp.np == 7)  // FR3
+    hipLaunchKernelGGL((qp_kernel<Dims<23, 16, 7, true, true, kQpGroup>>), g, blk, lg, st, m, kp, io);
+  else if (kp.nx == 20 && kp.ng == 14 && kp.np == 6)  // UR5e
+    hipLaunchKernelGGL((qp_kernel<Dims<20, 14, 6, true, true, kQpGroup>>), g, blk, lg, st, m, kp, io);
+  else if (kp.nx == 9 && kp.ng == 16 && kp.np == 9)  // Husky-FR3
+    hipLaunchKernelGGL((qp_kernel<Dims<9, 16, 9, true, true, kQpGroup>>), g, blk, lg, st, m, kp, io);
+  else if (kp.nx == 11 && kp.ng == 16 && kp.np == 11)  // XLS-FR3
+    hipLaunchKernelGGL((qp_kernel<Dims<11, 16, 11, true, true, kQpGroup>>), g, blk, lg, st, m, kp, io);
+  else  // any other model: runtime-sized shapes
+    hipLaunchKernelGGL((qp_kernel<Dims<0, 0, 0>>), g, blk, lds, st, m, kp, io);
+  return hipGetLastError();
+}
+
+#ifdef DRC_PHASE_TIMING
+DRC_PHASE_EXPORT(phase_cycles_qp)
+#endif
+
+}  // namespace drc_amd

@@ -6,9 +6,72 @@ owns instances [r * B, (r + 1) * B) of the global batch (weak scaling, B per
 rank).  The only collectives are the benchmark's barrier and the reduction
 of its timing / status counters (max of the timed region, sums of counts).
 torch.distributed is the transport: "nccl" (RCCL over xGMI) on the GPUs,
-"gloo" for the CPU tests.
+"gloo" for the CPU tests.  ``bench.py --gpus N`` run without torchrun starts
+its N ranks itself (``launch_if_needed``).
 """
 import os
+import socket
+import subprocess
+import sys
+import time
+
+
+def free_port():
+    """An unused TCP port on 127.0.0.1 for the rendezvous."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n, argv, extra_env=None, poll_s=0.2):
+    """Launch ``n`` ranks of ``argv`` (one process per GPU, as torchrun would:
+    RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT set)
+    and wait for them.  The caller must not have touched the GPU: the ranks are
+    fresh child processes (fork + exec of a new interpreter), never an exec of
+    the caller.  When one rank fails, the others are terminated (by their own
+    PIDs) so none is left waiting in a collective.  Returns the first non-zero
+    exit status, or 0."""
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ)
+        env.update(extra_env or {})
+        env.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen(argv, env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for o in live:
+                    o.terminate()
+        time.sleep(poll_s)
+    for p in procs:
+        p.wait()
+    return rc
+
+
+def launch_if_needed(n_gpus, script, args):
+    """bench.py's launcher: when ``--gpus N`` > 1 and no torchrun environment is
+    present, run N ranks of ``script`` with the same arguments and return their
+    exit status; None when this process is already a rank (or N = 1).  Raises
+    when the torchrun world size contradicts ``--gpus``."""
+    world = os.environ.get("WORLD_SIZE")
+    if world is not None:
+        if int(world) != n_gpus:
+            raise SystemExit("bench: --gpus %d but WORLD_SIZE=%s" % (n_gpus, world))
+        return None
+    if n_gpus <= 1:
+        return None
+    return spawn_ranks(n_gpus, [sys.executable, "-u", script] + list(args))
 
 
 def env_rank():

@@ -18,5 +18,11 @@ d = json.load(open(sys.argv[1])); ro = d["roofline"]
 print(d["config"]["robot"], "%.3fM" % (d["value"] / 1e6), "ms", round(d["ms_per_step"], 3), "task",
       round(ro["task_kernel_ms_sum"], 3), "qp", round(ro["qp_kernel_ms_sum"], 3), "nonsolved", d["non_solved"],
       "iters", round(d["admm_iters_mean"], 3), d["admm_iters_p99_max"])
+if "latency_b1" in d:
+    rs, sb, lb, lr = d["reference_settings"], d["batch_4096"], d["latency_b1"], ro["latency_roof"]
+    print("  osqp_default %.3fM nonsolved %d iters %s | B=4096 %.3fM | B=1 p50 %.0f us p99 %.0f us | "
+          "instance latency %.0f us, roof %.2fM (frac %.2f)" % (rs["value"] / 1e6, rs["non_solved"],
+          rs["admm_iters_p99_max"], sb["value"] / 1e6, lb["p50_us"], lb["p99_us"], lr["instance_latency_us"],
+          lr["solves_per_s"] / 1e6, lr["frac"]))
 PY
 done
