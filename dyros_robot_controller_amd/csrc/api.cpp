@@ -25,11 +25,16 @@
 namespace drc_amd {
 
 // Per-stream scratch of a model: the task-record pool, the work-queue
-// counters and the fork/join lanes.  Calls on one stream are ordered by that
-// stream, so they may share it; calls on two streams get disjoint contexts
-// (the C-ABI's "reentrant per stream", include/drc_amd.h).
+// counters and the COD list.  Calls on one stream are ordered by that stream,
+// so they may share it; calls on two streams get disjoint contexts (the
+// C-ABI's "reentrant per stream", include/drc_amd.h).  At most kMaxStreamCtx
+// contexts are kept: a new stream beyond that evicts the least recently used
+// one (after a device synchronisation), and drc_model_release_stream frees a
+// stream's context at once, so a caller cycling through streams holds a
+// bounded amount of device memory.
 struct StreamCtx {
   hipStream_t stream = nullptr;
+  uint64_t last_use = 0;
   void* pool = nullptr;  // task records / QPID dynamics / OSF M^-1, g
   int64_t pool_bytes = 0;
   // work-queue counters: [slot][kernel (task, QP)][8 XCD classes]; slots
@@ -37,6 +42,18 @@ struct StreamCtx {
   static constexpr int kSlotInts = 32;  // task queue 8, QP queue 8, lane-stage hard count 1
   static constexpr int kQueueSlotQpid = 16, kQueueSlotCf = 17, kQueueInts = 18 * kSlotInts;
   int* d_queue = nullptr;
+  int* dyn_list = nullptr;  // instances whose M_inv needs the serial COD
+  int64_t dyn_list_cap = 0;
+};
+constexpr size_t kMaxStreamCtx = 8;
+
+// Fork/join streams of the concurrent sub-batches, shared by every caller
+// stream of a model: a process gets 4 hardware queues (GPU_MAX_HW_QUEUES), so
+// the internal streams do not multiply with the caller's streams.  Calls are
+// enqueued under the model's launch mutex, so an event is recorded and waited
+// on by one call before the next re-records it; work of two caller streams on
+// one lane runs in order (each call on its own context's scratch).
+struct Lanes {
   std::vector<hipStream_t> lanes;  // concurrent sub-batches (drc_set_concurrency)
   std::vector<hipEvent_t> joins;
   // per sub-batch: the lane stage's hard instances run their task kernel on a
@@ -44,8 +61,6 @@ struct StreamCtx {
   std::vector<hipStream_t> sides;
   std::vector<hipEvent_t> side_fork, side_join;
   hipEvent_t fork = nullptr;
-  int* dyn_list = nullptr;  // instances whose M_inv needs the serial COD
-  int64_t dyn_list_cap = 0;
 };
 
 struct drc_model_impl {
@@ -55,7 +70,9 @@ struct drc_model_impl {
   drc_kinematic_param kparam{};
   drc_joint_index jidx{};
   drc_actuator_index aidx{};
-  std::vector<std::unique_ptr<StreamCtx>> ctxs;  // one per caller stream seen
+  std::vector<std::unique_ptr<StreamCtx>> ctxs;  // one per caller stream seen (at most kMaxStreamCtx)
+  uint64_t ctx_tick = 0;
+  Lanes ln;
   int timing = 0;  // drc_debug_kernel_timing: HIP events around each launch
   int lane_stage = 0;  // drc_debug_lane_stage: 0 off, 1 lane stage + side-stream hard path, 2 + serial hard path, 3 auto
   // timed calls: {caller-stream start, caller-stream end, per chunk: task start, task end, qp end}
@@ -89,15 +106,49 @@ static int set_err(int code, const std::string& msg) {
     if (e_ != hipSuccess) return set_err(DRC_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
   } while (0)
 
-// The scratch context of `st` (created on first use; caller holds m->mu).
+static void free_ctx(StreamCtx* c) {
+  if (c->d_queue) (void)hipFree(c->d_queue);
+  if (c->pool) (void)hipFree(c->pool);
+  if (c->dyn_list) (void)hipFree(c->dyn_list);
+  c->d_queue = nullptr;
+  c->pool = nullptr;
+  c->dyn_list = nullptr;
+}
+
+// A tuning knob from the environment: its integer value when set and
+// parsable, clamped to >= lo; otherwise the default.
+static int64_t env_int(const char* name, int64_t def, int64_t lo) {
+  const char* v = getenv(name);
+  if (!v || !*v) return def;
+  char* end = nullptr;
+  const long long x = strtoll(v, &end, 10);
+  if (end == v) return def;
+  return x < lo ? lo : x;
+}
+
+// The scratch context of `st` (created on first use; the caller holds
+// m->launch_mu and m->mu, so no launch still being enqueued uses an evicted
+// context).  Beyond kMaxStreamCtx streams the least recently used context is
+// freed after the device has drained (its stream may already be destroyed,
+// so the device, not the stream, is synchronised).
 static int stream_ctx(drc_model_impl* m, hipStream_t st, StreamCtx** out) {
   for (auto& c : m->ctxs)
     if (c->stream == st) {
+      c->last_use = ++m->ctx_tick;
       *out = c.get();
       return DRC_OK;
     }
+  if (m->ctxs.size() >= kMaxStreamCtx) {
+    size_t lru = 0;
+    for (size_t i = 1; i < m->ctxs.size(); ++i)
+      if (m->ctxs[i]->last_use < m->ctxs[lru]->last_use) lru = i;
+    HIP_TRY(hipDeviceSynchronize());
+    free_ctx(m->ctxs[lru].get());
+    m->ctxs.erase(m->ctxs.begin() + static_cast<std::ptrdiff_t>(lru));
+  }
   std::unique_ptr<StreamCtx> c(new StreamCtx());
   c->stream = st;
+  c->last_use = ++m->ctx_tick;
   HIP_TRY(hipMalloc(&c->d_queue, StreamCtx::kQueueInts * sizeof(int)));
   *out = c.get();
   m->ctxs.push_back(std::move(c));
@@ -112,11 +163,8 @@ static int ensure_pool(StreamCtx* c, int64_t bytes) {
   c->pool_bytes = bytes;
   return DRC_OK;
 }
-static void free_ctx(StreamCtx* c) {
+static void free_lanes(Lanes* c) {
   for (hipStream_t ls : c->lanes) (void)hipStreamSynchronize(ls);
-  if (c->d_queue) (void)hipFree(c->d_queue);
-  if (c->pool) (void)hipFree(c->pool);
-  if (c->dyn_list) (void)hipFree(c->dyn_list);
   for (hipStream_t ls : c->sides) (void)hipStreamSynchronize(ls);
   for (hipStream_t ls : c->lanes) (void)hipStreamDestroy(ls);
   for (hipEvent_t e : c->joins) (void)hipEventDestroy(e);
@@ -581,7 +629,7 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
   // order; smaller ones run grid-stride order): with one sub-batch the QP
   // kernel waits for the whole task kernel, with several they overlap
   // (Husky-FR3's 16 Ki batch)
-  static const int64_t min_sub = getenv("DRC_MIN_SUBBATCH") ? atoll(getenv("DRC_MIN_SUBBATCH")) : 4096;
+  static const int64_t min_sub = env_int("DRC_MIN_SUBBATCH", 4096, 1);
   int S = 1;
   if (!stages)
     for (int c = m->chunks; c > 1; --c)
@@ -598,25 +646,25 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
   };
   {
     std::lock_guard<std::mutex> g(m->mu);
-    while (static_cast<int>(cx->lanes.size()) < S) {
+    while (static_cast<int>(m->ln.lanes.size()) < S) {
       hipStream_t ls;
       hipEvent_t je;
       HIP_TRY(hipStreamCreateWithFlags(&ls, hipStreamNonBlocking));
       HIP_TRY(hipEventCreateWithFlags(&je, hipEventDisableTiming));
-      cx->lanes.push_back(ls);
-      cx->joins.push_back(je);
+      m->ln.lanes.push_back(ls);
+      m->ln.joins.push_back(je);
     }
-    while (lane && !stages && ls == 1 && static_cast<int>(cx->sides.size()) < S) {
+    while (lane && !stages && ls == 1 && static_cast<int>(m->ln.sides.size()) < S) {
       hipStream_t ss;
       hipEvent_t f, j;
       HIP_TRY(hipStreamCreateWithFlags(&ss, hipStreamNonBlocking));
       HIP_TRY(hipEventCreateWithFlags(&f, hipEventDisableTiming));
       HIP_TRY(hipEventCreateWithFlags(&j, hipEventDisableTiming));
-      cx->sides.push_back(ss);
-      cx->side_fork.push_back(f);
-      cx->side_join.push_back(j);
+      m->ln.sides.push_back(ss);
+      m->ln.side_fork.push_back(f);
+      m->ln.side_join.push_back(j);
     }
-    if (!cx->fork) HIP_TRY(hipEventCreateWithFlags(&cx->fork, hipEventDisableTiming));
+    if (!m->ln.fork) HIP_TRY(hipEventCreateWithFlags(&m->ln.fork, hipEventDisableTiming));
   }
   hipEvent_t e_start = nullptr, e_end = nullptr;
   if (timed) {
@@ -624,11 +672,11 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
     if (int r = mkev(&e_end)) return r;
     HIP_TRY(hipEventRecord(e_start, st));
   }
-  if (S > 1) HIP_TRY(hipEventRecord(cx->fork, st));
+  if (S > 1) HIP_TRY(hipEventRecord(m->ln.fork, st));
   for (int c = 0; c < S; ++c) {
     const int64_t b0 = B * c / S, b1 = B * (c + 1) / S, Bc = b1 - b0;
-    hipStream_t cs = S > 1 ? cx->lanes[c] : st;
-    if (S > 1) HIP_TRY(hipStreamWaitEvent(cs, cx->fork, 0));
+    hipStream_t cs = S > 1 ? m->ln.lanes[c] : st;
+    if (S > 1) HIP_TRY(hipStreamWaitEvent(cs, m->ln.fork, 0));
     KParams kt_c = kt, kq_c = kq;
     kt_c.xcd_map = kq_c.xcd_map = Bc >= 16384 ? 1 : 0;
     // persistent grids (work queues hand out the instances): 2048 waves per
@@ -636,8 +684,10 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
     // (kernel-argument spills, written once per wave) stays a small share of
     // the HBM writes -- measured sweep in DESIGN.md; DRC_GRID_TASK / _QP
     // override for such experiments
-    static const int64_t cap_t = getenv("DRC_GRID_TASK") ? atoll(getenv("DRC_GRID_TASK")) : 2048;
-    static const int64_t cap_q = getenv("DRC_GRID_QP") ? atoll(getenv("DRC_GRID_QP")) : 2048;
+    // (clamped to >= 8 and a multiple of 8: with the XCD-aware order every
+    // residue class blockIdx & 7 needs waves to drain its queue)
+    static const int64_t cap_t = env_int("DRC_GRID_TASK", 2048, 8) & ~int64_t(7);
+    static const int64_t cap_q = env_int("DRC_GRID_QP", 2048, 8) & ~int64_t(7);
     const int64_t gq = Bc < cap_q ? Bc : cap_q, gt = Bc < cap_t ? Bc : cap_t;
     IO io{Bc, b0, B, q, qdot, xt, xdt, xi, xdi, out, status, iters, pose, jac, man, dist, xdd, pair,
           rec ? rec + b0 * stride : nullptr, stride};
@@ -687,24 +737,24 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
       } else {
         // hard task kernel on the side stream, overlapped with the QP of the
         // other instances; then the QP of the hard ones
-        hipStream_t ss = cx->sides[c];
-        HIP_TRY(hipEventRecord(cx->side_fork[c], cs));
-        HIP_TRY(hipStreamWaitEvent(ss, cx->side_fork[c], 0));
+        hipStream_t ss = m->ln.sides[c];
+        HIP_TRY(hipEventRecord(m->ln.side_fork[c], cs));
+        HIP_TRY(hipStreamWaitEvent(ss, m->ln.side_fork[c], 0));
         if (int r = launch_task(ss)) return r;
-        HIP_TRY(hipEventRecord(cx->side_join[c], ss));
+        HIP_TRY(hipEventRecord(m->ln.side_join[c], ss));
         io.hard_mode = 2;
         if (int r = launch_qp()) return r;
-        HIP_TRY(hipStreamWaitEvent(cs, cx->side_join[c], 0));
+        HIP_TRY(hipStreamWaitEvent(cs, m->ln.side_join[c], 0));
         io.hard_mode = 1;
         if (int r = launch_qp()) return r;
       }
       io.hard_mode = 0;
     }
     if (timed) HIP_TRY(hipEventRecord(e2, cs));
-    if (S > 1) HIP_TRY(hipEventRecord(cx->joins[c], cs));
+    if (S > 1) HIP_TRY(hipEventRecord(m->ln.joins[c], cs));
   }
   if (S > 1)
-    for (int c = 0; c < S; ++c) HIP_TRY(hipStreamWaitEvent(st, cx->joins[c], 0));
+    for (int c = 0; c < S; ++c) HIP_TRY(hipStreamWaitEvent(st, m->ln.joins[c], 0));
   if (timed) {
     HIP_TRY(hipEventRecord(e_end, st));
     std::lock_guard<std::mutex> g(m->mu);
@@ -1010,10 +1060,29 @@ int drc_model_create_mobile_manipulator(const drc_kinematic_param* param, const 
   return DRC_OK;
 }
 
+int drc_model_release_stream(drc_model* m, void* stream) {
+  using drc_amd::set_err;
+  if (!m) return drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "null model");
+  std::lock_guard<std::mutex> launch_lock(m->launch_mu);
+  std::lock_guard<std::mutex> g(m->mu);
+  HIP_TRY(hipSetDevice(m->device));
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  for (size_t i = 0; i < m->ctxs.size(); ++i)
+    if (m->ctxs[i]->stream == st) {
+      HIP_TRY(hipStreamSynchronize(st));  // the stream is still valid: its work on the context drains first
+      drc_amd::free_ctx(m->ctxs[i].get());
+      m->ctxs.erase(m->ctxs.begin() + static_cast<std::ptrdiff_t>(i));
+      break;
+    }
+  return DRC_OK;
+}
+
 void drc_model_destroy(drc_model* m) {
   if (!m) return;
   (void)hipSetDevice(m->device);
+  (void)hipDeviceSynchronize();
   for (auto& c : m->ctxs) drc_amd::free_ctx(c.get());
+  drc_amd::free_lanes(&m->ln);
   if (m->d_model) (void)hipFree(m->d_model);
   if (m->hstream) (void)hipStreamSynchronize(m->hstream), (void)hipStreamDestroy(m->hstream);
   if (m->stage) (void)hipFree(m->stage);

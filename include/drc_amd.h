@@ -12,10 +12,12 @@
  *    a [F][B] array is at ptr[f * B + b].  All batched pointers are DEVICE
  *    pointers owned by the caller (HBM resident); `stream` is a hipStream_t
  *    (NULL = default stream).  Calls are asynchronous on that stream.  A
- *    model keeps its per-call scratch (task records, work-queue counters,
- *    fork/join lanes) per caller stream, so calls on one model from several
- *    streams run concurrently without sharing scratch, and calls from several
- *    host threads are safe (each call's launches are enqueued as a unit).
+ *    model keeps its per-call scratch (task records, work-queue counters)
+ *    per caller stream (at most 8 streams; see drc_model_release_stream), so
+ *    calls on one model from several streams never share scratch, and calls
+ *    from several host threads are safe (each call's launches are enqueued as
+ *    a unit).  The internal fork/join streams of the concurrent sub-batches
+ *    are per model, shared by the caller streams.
  *  - Poses are 12 doubles: R column-major (9) then p (3) — Eigen::Affine3d
  *    `linear()` memory order followed by `translation()`.
  *  - Velocities / twists are [v(3); w(3)] in the world frame
@@ -227,6 +229,15 @@ int drc_debug_kernel_times(drc_model* model, double* wall_ms, double* task_ms, d
  * streams forked from and joined back to the caller's stream (default 3).
  * Results do not depend on it. */
 int drc_set_concurrency(drc_model* model, int chunks);
+
+/* Frees the per-stream scratch (task-record pool, work-queue counters) the
+ * model keeps for `stream`, after the stream's queued work has finished; call
+ * it before destroying a stream the model was used on.  A model keeps at most
+ * 8 such contexts in any case (the least recently used one is freed when a
+ * ninth stream appears), so a caller cycling through streams cannot grow it
+ * without bound.  No-op for a stream the model has not seen.  (Reference: no
+ * counterpart — the reference's OSQP solver object is per controller.) */
+int drc_model_release_stream(drc_model* model, void* stream);
 
 /* Task stage of drc_qpik_batch / drc_qpik_stages_batch.  0: the
  * wave-per-instance kernel on every instance (default).  1: the lane-per-instance stage

@@ -2,8 +2,9 @@
 bounds) in exact mode: the LP infeasibility certificate (D15) and the
 uncapped polish KKT (D16) of oracle/drc_oracle.c, which the kernel mirrors.
 
-- every certified instance is infeasible by an independent LP (scipy HiGHS on
-  the same rows) and comes back PrimalInfeasible after 0 ADMM iterations;
+- every certified instance is infeasible by an independent feasibility LP
+  (pyref.feasible: scipy's HiGHS on the same rows, not the certificate's
+  candidate scan) and comes back PrimalInfeasible after 0 ADMM iterations;
 - every LP-infeasible instance with a margin is certified;
 - with both rules the stress-tier workload has no ADMM tail (the capped polish
   left solved instances running ~3 000 iterations and infeasible ones to

@@ -68,3 +68,20 @@ def test_simple_qp_exact():
     st, x, y, it, pol = O.solve_qp(P, qv, A, l, u, O.default_params(1, exact=True).solver)
     assert st == O.SOLVED
     np.testing.assert_allclose(x, [0.3, 0.7], atol=1e-9)    # OSQP README example
+
+
+def test_polish_cap_changes_iterations_not_outputs():
+    """The manipulator polish KKT cap of 16 (the kernel's register EQP, copied
+    into the oracle) is a cost rule, not a numerical one: with the cap removed
+    (polish_cap = 0, the LDS LDL^T for every size) the certified optimum is the
+    same within 1e-6 on every instance, statuses identical, and the cap can
+    only add ADMM iterations (a too-large KKT skips that polish attempt)."""
+    pm, om, q, qd, xt, xdt, link = _instances("fr3", 13, 300)
+    par = O.default_params(0, exact=True)
+    assert par.solver.polish_cap == 16
+    o16, s16, it16 = O.qpik_batch(om, par, q, qd, xt, xdt, nthreads=4)
+    par.solver.polish_cap = 0
+    o0, s0, it0 = O.qpik_batch(om, par, q, qd, xt, xdt, nthreads=4)
+    np.testing.assert_array_equal(s16, s0)
+    assert np.abs(o16 - o0).max() <= 1e-6
+    assert np.all(it16 >= it0)
