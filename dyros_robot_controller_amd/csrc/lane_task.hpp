@@ -133,6 +133,7 @@ lane_task_kernel(const DevModel* __restrict__ M, const KParams kp, const IO io) 
   // the argmin, so pruning it leaves the result of computing every pair.
   double bestd = 1.7976931348623157e308, ub = 1e300;
   int besti = 0x7fffffff;
+  bool bgjk = false;  // the running best came from GJK (refined below, D17)
   V3 bpA = v3(0, 0, 0), bpB = v3(0, 0, 0);
   uint64_t cmask[kLaneCandWords];
 #pragma unroll
@@ -156,6 +157,7 @@ lane_task_kernel(const DevModel* __restrict__ M, const KParams kp, const IO io) 
       if (d < bestd) {
         bestd = d;
         besti = p;
+        bgjk = false;
         bpA = pA;
         bpB = pB;
       }
@@ -214,6 +216,7 @@ lane_task_kernel(const DevModel* __restrict__ M, const KParams kp, const IO io) 
       if (gd < bestd || (gd == bestd && p < besti)) {
         bestd = gd;
         besti = p;
+        bgjk = true;
         bpA = gA;
         bpB = gB;
       }
@@ -232,6 +235,15 @@ lane_task_kernel(const DevModel* __restrict__ M, const KParams kp, const IO io) 
     io.hard_list[k] = static_cast<int>(b);
     if (io.hard_flag) io.hard_flag[b] = 1;
     return;
+  }
+  if (bgjk) {  // the winner's GJK witnesses sharpened to the exact critical point (D17)
+    const int ga = M->pair_a[besti], gb_ = M->pair_b[besti];
+    double TA[12], TB[12];
+    lane_geom<NV>(M, T, ga, true, TA);
+    lane_geom<NV>(M, T, gb_, true, TB);
+    const Shape A{M->gtype[ga], TA, M->gparam[ga][0], M->gparam[ga][1], M->gparam[ga][2]};
+    const Shape Bs{M->gtype[gb_], TB, M->gparam[gb_][0], M->gparam[gb_][1], M->gparam[gb_][2]};
+    refine_witness(A, Bs, &bestd, &bpA, &bpB);
   }
   // ---------------- joint axes, Jacobian, distance gradient ----------------
   V3 z[NV], pj[NV];

@@ -460,6 +460,12 @@ DRC_HD __forceinline__ int closest_any(SV2 (&S)[4], int n, V3* v, double (&lam)[
   return k;
 }
 
+// Support-gap stop tolerances (metres; oracle: GJK_TOL / EPA_TOL).  The
+// winning pair's witnesses are refined to the exact critical point afterwards
+// (refine_witness, D17), so GJK / EPA only decide the argmin and the basin:
+// EPA stops at hpp-fcl's default epa_tolerance, GJK at 1e-9.
+constexpr double kGjkTol = 1e-9, kEpaTol = 1e-6;
+
 // GJK on the cores (same iteration, tolerances and duplicate test as
 // oracle/drc_oracle.c:gjk).  The simplex stays in registers.  ANY: the
 // closest-point step for per-lane simplex sizes (closest_any).
@@ -491,7 +497,7 @@ DRC_HD __forceinline__ void gjk_run(const Shape& A, const Shape& B, GjkState& g,
       g.pruned = 1;
       break;
     }
-    if (n > 0 && vv - vw <= 1e-12 * sv) break;
+    if (n > 0 && vv - vw <= kGjkTol * sv) break;
     bool dup = false;
 #pragma unroll
     for (int i = 0; i < 4; ++i) dup |= i < n && S[i].w.x == w.w.x && S[i].w.y == w.w.y && S[i].w.z == w.w.z;
@@ -766,7 +772,7 @@ DRC_HD __forceinline__ void epa_init(const Shape A, const Shape B, EpaPoly* E) {
 // w in direction n_best: support gap below tolerance or vertex cap reached.
 // The duplicate-vertex test is separate so a wave can spread it over lanes.
 DRC_HD __forceinline__ bool epa_gap_stop(const EpaPoly* E, int best, const SV& w) {
-  return dot(ld3(E->fn[best]), w.w) - E->fd[best] <= 1e-12 || E->nv >= kEpaMaxV;
+  return dot(ld3(E->fn[best]), w.w) - E->fd[best] <= kEpaTol || E->nv >= kEpaMaxV;
 }
 DRC_HD __forceinline__ bool epa_is_dup(const EpaPoly* E, int i, const SV& w) {
   const V3 d = w.w - epa_vw(E, i);
@@ -1073,6 +1079,320 @@ DRC_HD __forceinline__ double sphere_pair(const Shape& A, const Shape& B, V3* pA
   return sd - s.p0;
 }
 
+// ------------------------------------------------------------ witness refinement
+// DESIGN.md D17 (oracle twin: refine_witness in oracle/drc_oracle.c, same
+// features, rules and tolerances).  The GJK / EPA witnesses of the winning
+// pair converge only to ~sqrt(gap) / the EPA vertex cap, so implementations
+// whose iterations differ by rounding disagree by up to ~1e-5 there, and the
+// distance gradient n^T (J_B(pB) - J_A(pA)), n = (pB - pA)/|pB - pA|, with
+// them.  The exact witnesses are a critical point of |X_A(u_A) - X_B(u_B)|^2
+// over the surface features the estimates lie on -- cylinder side (theta, z),
+// cap (x, y), rim (theta); box face / edge / vertex (the free coordinates) --
+// which Newton reaches quadratically from either implementation's estimate.
+// Accepted when the point lies inside its features, n* = (pB - pA)/sd is in
+// A's normal cone and -n* in B's, and sd moves by <= 1e-6; otherwise the
+// estimates stay (parallel flat features: witnesses not unique).
+// Register-only form: the parameter counts (0-2 per feature) are template
+// arguments, so the Newton system, the feature tangents and the parameters
+// stay in VGPRs (no private arrays, no scratch frame in the task kernel).
+enum : int { kFtSide = 0, kFtCap = 1, kFtRim = 2, kFtBox = 3 };
+struct Feat {
+  int kind;
+  double s;
+  int fx, fy, fz;  // box: 0 free, +-1 the face sign of that axis
+  DRC_HD __forceinline__ int fix(int i) const { return i == 0 ? fx : (i == 1 ? fy : fz); }
+  DRC_HD __forceinline__ void set_fix(int i, int v) {
+    if (i == 0) fx = v;
+    else if (i == 1) fy = v;
+    else fz = v;
+  }
+  DRC_HD __forceinline__ int nparam() const {
+    return kind == kFtRim ? 1 : (kind == kFtBox ? (fx == 0) + (fy == 0) + (fz == 0) : 2);
+  }
+};
+constexpr double kRwTau = 1e-4, kRwPivot = 1e-9, kRwStep = 1e-12, kRwCone = 1e-9, kRwDMove = 1e-5;
+
+DRC_HD __forceinline__ double v3c(V3 v, int i) { return i == 0 ? v.x : (i == 1 ? v.y : v.z); }
+DRC_HD __forceinline__ V3 v3e(int i) { return v3(i == 0, i == 1, i == 2); }
+
+DRC_HD __forceinline__ void rw_classify(const Shape& s, V3 x, Feat* f) {
+  f->fx = f->fy = f->fz = 0;
+  f->s = x.z > 0 ? 1.0 : -1.0;
+  if (s.type == kCylinder) {
+    const double r = s.p0, h = s.p1, rho = sqrt(x.x * x.x + x.y * x.y);
+    if (fabs(x.z) > h - kRwTau && rho > r - kRwTau) f->kind = kFtRim;
+    else if (fabs(x.z) > h - kRwTau) f->kind = kFtCap;
+    else f->kind = kFtSide;
+    return;
+  }
+  f->kind = kFtBox;
+  int any = 0, im = 0;
+  double best = -1;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const double xi = v3c(x, i), hi = i == 0 ? s.p0 : (i == 1 ? s.p1 : s.p2);
+    const int fi = fabs(xi) > hi - kRwTau ? (xi > 0 ? 1 : -1) : 0;
+    f->set_fix(i, fi);
+    any |= fi != 0;
+    const double t = fabs(xi) / hi;
+    if (t > best) {
+      best = t;
+      im = i;
+    }
+  }
+  if (!any) f->set_fix(im, v3c(x, im) > 0 ? 1 : -1);
+}
+// parameters (u0, u1) of feature f at the local point x
+DRC_HD __forceinline__ void rw_params(const Feat& f, V3 x, double* u0, double* u1) {
+  if (f.kind == kFtSide || f.kind == kFtRim) {
+    *u0 = atan2(x.y, x.x);
+    *u1 = x.z;
+  } else if (f.kind == kFtCap) {
+    *u0 = x.x;
+    *u1 = x.y;
+  } else {
+    int k = 0;
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+      if (!f.fix(i)) {
+        if (k == 0) *u0 = v3c(x, i);
+        else *u1 = v3c(x, i);
+        ++k;
+      }
+  }
+}
+// world point, unit-speed tangents t0, t1 and the theta curvature vector c0
+// (arc-length derivatives; the other parameters are linear)
+DRC_HD __forceinline__ V3 rw_eval(const Shape& s, const Feat& f, double u0, double u1, V3* t0, V3* t1, V3* c0) {
+  V3 x, a = v3(0, 0, 0), b = v3(0, 0, 0), c = v3(0, 0, 0);
+  if (f.kind == kFtSide || f.kind == kFtRim) {
+    const double r = s.p0, cs = cos(u0), sn = sin(u0);
+    x = v3(r * cs, r * sn, f.kind == kFtSide ? u1 : f.s * s.p1);
+    a = v3(-sn, cs, 0);
+    c = v3(-cs / r, -sn / r, 0);
+    b = v3(0, 0, 1);
+  } else if (f.kind == kFtCap) {
+    x = v3(u0, u1, f.s * s.p1);
+    a = v3(1, 0, 0);
+    b = v3(0, 1, 0);
+  } else {
+    double xl[3];
+    int k = 0;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const double hi = i == 0 ? s.p0 : (i == 1 ? s.p1 : s.p2);
+      const int fi = f.fix(i);
+      xl[i] = fi ? fi * hi : (k == 0 ? u0 : u1);
+      if (!fi) {
+        if (k == 0) a = v3e(i);
+        else b = v3e(i);
+        ++k;
+      }
+    }
+    x = v3(xl[0], xl[1], xl[2]);
+  }
+  *t0 = rot(s.T, a);
+  *t1 = rot(s.T, b);
+  *c0 = rot(s.T, c);
+  return xform(s.T, x);
+}
+DRC_HD __forceinline__ void rw_step(const Shape& s, const Feat& f, double* u0, double* u1, double d0, double d1) {
+  if (f.kind == kFtSide || f.kind == kFtRim) {
+    *u0 += d0 / s.p0;
+    if (f.kind == kFtSide) *u1 += d1;
+  } else {
+    *u0 += d0;
+    *u1 += d1;
+  }
+}
+// Newton on grad |X_A - X_B|^2 = 0 with MA + MB <= 4 unknowns (compile-time);
+// false when degenerate or not converged.  Same system, pivoting and stop
+// rule as the oracle's rw_newton.
+template <int MA, int MB>
+DRC_HD __forceinline__ bool rw_newton_t(const Shape& A, const Feat& fA, double* uA0, double* uA1, const Shape& B, const Feat& fB,
+                               double* uB0, double* uB1, V3* XA, V3* XB) {
+  constexpr int M = MA + MB;
+  for (int it = 0; it < 20; ++it) {
+    V3 tA0, tA1, cA, tB0, tB1, cB;
+    *XA = rw_eval(A, fA, *uA0, *uA1, &tA0, &tA1, &cA);
+    *XB = rw_eval(B, fB, *uB0, *uB1, &tB0, &tB1, &cB);
+    if constexpr (M == 0) {
+      return true;
+    } else {
+      const V3 D = *XA - *XB;
+      V3 J[M];
+#pragma unroll
+      for (int i = 0; i < MA; ++i) J[i] = i == 0 ? tA0 : tA1;
+#pragma unroll
+      for (int i = 0; i < MB; ++i) J[MA + i] = -1.0 * (i == 0 ? tB0 : tB1);
+      double H[M][M + 1];
+#pragma unroll
+      for (int i = 0; i < M; ++i) {
+#pragma unroll
+        for (int j = 0; j < M; ++j) H[i][j] = dot(J[i], J[j]);
+        H[i][M] = -dot(J[i], D);
+      }
+      if constexpr (MA > 0) H[0][0] += dot(D, cA);  // theta curvature (index 0 only)
+      if constexpr (MB > 0) H[MA][MA] -= dot(D, cB);
+#pragma unroll
+      for (int c = 0; c < M; ++c) {  // Gaussian elimination, partial pivoting (swaps by selects)
+        double pv = fabs(H[c][c]);
+        int p = c;
+#pragma unroll
+        for (int r = c + 1; r < M; ++r)
+          if (fabs(H[r][c]) > pv) {
+            pv = fabs(H[r][c]);
+            p = r;
+          }
+        if (!(pv > kRwPivot)) return false;
+#pragma unroll
+        for (int r = c + 1; r < M; ++r)
+          if (r == p)
+#pragma unroll
+            for (int j = 0; j <= M; ++j) {
+              const double t = H[c][j];
+              H[c][j] = H[r][j];
+              H[r][j] = t;
+            }
+#pragma unroll
+        for (int r = c + 1; r < M; ++r) {
+          const double g = H[r][c] / H[c][c];
+#pragma unroll
+          for (int j = c; j <= M; ++j) H[r][j] -= g * H[c][j];
+        }
+      }
+      double du[M], mx = 0;
+#pragma unroll
+      for (int r = M - 1; r >= 0; --r) {
+        double t = H[r][M];
+#pragma unroll
+        for (int j = r + 1; j < M; ++j) t -= H[r][j] * du[j];
+        du[r] = t / H[r][r];
+        mx = fmax(mx, fabs(du[r]));
+      }
+      rw_step(A, fA, uA0, uA1, MA > 0 ? du[0] : 0.0, MA > 1 ? du[MA > 1 ? 1 : 0] : 0.0);
+      rw_step(B, fB, uB0, uB1, MB > 0 ? du[MA] : 0.0, MB > 1 ? du[MB > 1 ? MA + 1 : MA] : 0.0);
+      if (mx <= kRwStep) {
+        *XA = rw_eval(A, fA, *uA0, *uA1, &tA0, &tA1, &cA);
+        *XB = rw_eval(B, fB, *uB0, *uB1, &tB0, &tB1, &cB);
+        return true;
+      }
+    }
+  }
+  return false;
+}
+DRC_HD __forceinline__ bool rw_newton(const Shape& A, const Feat& fA, double* uA0, double* uA1, const Shape& B, const Feat& fB,
+                             double* uB0, double* uB1, V3* XA, V3* XB) {
+  const int k = 3 * fA.nparam() + fB.nparam();
+  switch (k) {
+    case 0: return rw_newton_t<0, 0>(A, fA, uA0, uA1, B, fB, uB0, uB1, XA, XB);
+    case 1: return rw_newton_t<0, 1>(A, fA, uA0, uA1, B, fB, uB0, uB1, XA, XB);
+    case 2: return rw_newton_t<0, 2>(A, fA, uA0, uA1, B, fB, uB0, uB1, XA, XB);
+    case 3: return rw_newton_t<1, 0>(A, fA, uA0, uA1, B, fB, uB0, uB1, XA, XB);
+    case 4: return rw_newton_t<1, 1>(A, fA, uA0, uA1, B, fB, uB0, uB1, XA, XB);
+    case 5: return rw_newton_t<1, 2>(A, fA, uA0, uA1, B, fB, uB0, uB1, XA, XB);
+    case 6: return rw_newton_t<2, 0>(A, fA, uA0, uA1, B, fB, uB0, uB1, XA, XB);
+    case 7: return rw_newton_t<2, 1>(A, fA, uA0, uA1, B, fB, uB0, uB1, XA, XB);
+    default: return rw_newton_t<2, 2>(A, fA, uA0, uA1, B, fB, uB0, uB1, XA, XB);
+  }
+}
+// outside the feature's domain: move to the bounding feature (true)
+DRC_HD __forceinline__ bool rw_domain(const Shape& s, Feat* f, double u0, double u1) {
+  if (f->kind == kFtSide && fabs(u1) > s.p1) {
+    f->kind = kFtRim;
+    f->s = u1 > 0 ? 1 : -1;
+    return true;
+  }
+  if (f->kind == kFtCap && u0 * u0 + u1 * u1 > s.p0 * s.p0) {
+    f->kind = kFtRim;
+    return true;
+  }
+  if (f->kind == kFtBox) {
+    int k = 0;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      if (f->fix(i)) continue;
+      const double hi = i == 0 ? s.p0 : (i == 1 ? s.p1 : s.p2), ui = k == 0 ? u0 : u1;
+      if (fabs(ui) > hi) {
+        f->set_fix(i, ui > 0 ? 1 : -1);
+        return true;
+      }
+      ++k;
+    }
+  }
+  return false;
+}
+// the outward normal nrm in the normal cone of f at u: -1 impossible, 1
+// feature moves to a neighbour, 0 holds
+DRC_HD __forceinline__ int rw_cone(const Shape& s, Feat* f, double u0, V3 nrm) {
+  const V3 ax = v3(s.T[2], s.T[5], s.T[8]);
+  if (f->kind == kFtBox) {
+    const int nfix = (f->fx != 0) + (f->fy != 0) + (f->fz != 0);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int fi = f->fix(i);
+      if (!fi) continue;
+      const V3 e = v3(s.T[i], s.T[3 + i], s.T[6 + i]);
+      if (fi * dot(nrm, e) < -kRwCone) {
+        if (nfix == 1) return -1;  // no face left
+        f->set_fix(i, 0);
+        return 1;
+      }
+    }
+    return 0;
+  }
+  if (f->kind == kFtCap) return f->s * dot(nrm, ax) > 0 ? 0 : -1;
+  const V3 rad = rot(s.T, v3(cos(u0), sin(u0), 0));
+  const double a = dot(nrm, rad), b = f->s * dot(nrm, ax);
+  if (f->kind == kFtSide) return a > 0 ? 0 : -1;
+  if (a < -kRwCone) {
+    f->kind = kFtCap;
+    return 1;
+  }
+  if (b < -kRwCone) {
+    f->kind = kFtSide;
+    return 1;
+  }
+  return 0;
+}
+// sharpens (d, pA, pB) in place; false: the estimates stay
+DRC_HD inline __noinline__ bool refine_witness(const Shape A, const Shape B, double* d, V3* pA, V3* pB) {
+  Feat fA, fB;
+  double uA0 = 0, uA1 = 0, uB0 = 0, uB1 = 0;
+  const V3 cA = v3(A.T[9], A.T[10], A.T[11]), cB = v3(B.T[9], B.T[10], B.T[11]);
+  const V3 xA = rotT(A.T, *pA - cA), xB = rotT(B.T, *pB - cB);
+  rw_classify(A, xA, &fA);
+  rw_classify(B, xB, &fB);
+  rw_params(fA, xA, &uA0, &uA1);
+  rw_params(fB, xB, &uB0, &uB1);
+  const double sgn = *d < 0 ? -1.0 : 1.0;
+  for (int round = 0; round < 4; ++round) {
+    V3 XA, XB;
+    if (!rw_newton(A, fA, &uA0, &uA1, B, fB, &uB0, &uB1, &XA, &XB)) return false;
+    int ca = rw_domain(A, &fA, uA0, uA1), cb = rw_domain(B, &fB, uB0, uB1);
+    if (!ca && !cb) {
+      const V3 D = XB - XA;
+      const double L = sqrt(dot(D, D));
+      if (!(L > 1e-12)) return false;
+      const double sd = sgn * L;
+      const V3 n = v3(D.x / sd, D.y / sd, D.z / sd), nb = v3(-n.x, -n.y, -n.z);
+      ca = rw_cone(A, &fA, uA0, n);
+      cb = rw_cone(B, &fB, uB0, nb);
+      if (ca < 0 || cb < 0) return false;
+      if (!ca && !cb) {
+        if (!(fabs(sd - *d) <= kRwDMove)) return false;
+        *d = sd;
+        *pA = XA;
+        *pB = XB;
+        return true;
+      }
+    }
+    rw_params(fA, rotT(A.T, XA - cA), &uA0, &uA1);
+    rw_params(fB, rotT(B.T, XB - cB), &uB0, &uB1);
+  }
+  return false;
+}
+
 // Lower bound on the distance of two geometries via their swept cores:
 // cylinder -> axis segment (radius r), box -> centre point (bounding radius),
 // sphere -> centre.  Exact closed form for segment/segment.
@@ -1116,7 +1436,11 @@ DRC_HD __forceinline__ bool cyl_cyl_side(const Shape& A, const Shape& B, double*
 DRC_HD __forceinline__ double seg_seg_dist(V3 p1, V3 q1, V3 p2, V3 q2, V3* c1o = nullptr, V3* c2o = nullptr) {
   V3 d1 = q1 - p1, d2 = q2 - p2, r = p1 - p2;
   double a = dot(d1, d1), e = dot(d2, d2), f = dot(d2, r), s, t;
-  if (a <= 1e-30 && e <= 1e-30) {
+  if (a <= 1e-30 && e <= 1e-30) {  // two points (box / box cores): the closest points are the points
+    if (c1o) {
+      *c1o = p1;
+      *c2o = p2;
+    }
     return sqrt(dot(r, r));
   }
   if (a <= 1e-30) {

@@ -689,6 +689,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRC_TAS
     double* pf = S + kp.kPf;
     double bestd = 1.7976931348623157e308;
     int besti = 0x7fffffff;
+    int bhow = 0;  // how the running best was found: 0 closed form, 1 GJK, 2 EPA
     V3 bpA = v3(0, 0, 0), bpB = v3(0, 0, 0);
     double ub = 1e300;
     // slots in type-class order (model.cpp pair_order): each round of 64 lanes
@@ -708,6 +709,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRC_TAS
         if (d < bestd || (d == bestd && p < besti)) {  // ties -> lowest pair index
           bestd = d;
           besti = p;
+          bhow = 0;
           bpA = pA;
           bpB = pB;
         }
@@ -748,6 +750,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRC_TAS
           if (g.dist < bestd || (g.dist == bestd && p < besti)) {
             bestd = g.dist;
             besti = p;
+            bhow = 1;
             bpA = g.pA;
             bpB = g.pB;
           }
@@ -816,6 +819,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRC_TAS
               if (d < bestd || (d == bestd && p < besti)) {
                 bestd = d;
                 besti = p;
+                bhow = 2;
                 bpA = ld3(ews->out);
                 bpB = ld3(ews->out + 3);
               }
@@ -857,15 +861,27 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRC_TAS
     double* dgv = S + kp.kdg;
     double* red = S + kp.oRed;
     if (myi == besti && myi < M->npairs) {  // the winning lane publishes its witnesses
+      double dref = myd;
+      if (bhow) {  // GJK / EPA estimates sharpened to the exact critical point (D17)
+        const int ga = M->pair_a[myi], gb = M->pair_b[myi];
+        const Shape A{M->gtype[ga], Tg + 12 * ga, M->gparam[ga][0], M->gparam[ga][1], M->gparam[ga][2]};
+        const Shape Bs{M->gtype[gb], Tg + 12 * gb, M->gparam[gb][0], M->gparam[gb][1], M->gparam[gb][2]};
+#ifndef DRC_NO_REFINE
+        refine_witness(A, Bs, &dref, &bpA, &bpB);
+#else
+        (void)A, (void)Bs;
+#endif
+      }
       st3(red, bpA);
       st3(red + 3, bpB);
+      S[kp.oSc + SC_DIST] = dref;
     }
     if (l == 0) {
-      S[kp.oSc + SC_DIST] = bestd;
+      if (besti >= M->npairs) S[kp.oSc + SC_DIST] = bestd;
       S[kp.oSc + SC_PAIR] = besti;
     }
-    (void)myd;
     wsync();
+    bestd = S[kp.oSc + SC_DIST];
     PH(6);
     if (l < nv) {  // grad d = n^T (J_B(pB) - J_A(pA)), sign flipped when penetrating
       double g = 0;

@@ -485,6 +485,15 @@ static int closest_simplex(SV* S, int n, double* v, double* lam_out) {
     return k;
 }
 
+/* Stop tolerances (support gaps, metres).  The winning pair's witnesses are
+ * refined to the exact critical point afterwards (refine_witness, D17), so
+ * GJK / EPA only have to decide the argmin and land in the right basin:
+ * EPA stops at hpp-fcl's default epa_tolerance (1e-6), GJK at 1e-9 (the
+ * argmin of pairs closer than that is a tie at the reference's own
+ * tolerance).  Kernel twins: kGjkTol / kEpaTol in qpik_device.hpp. */
+#define GJK_TOL 1e-9
+#define EPA_TOL 1e-6
+
 /* GJK on the cores.  Returns 1 when the origin is enclosed (penetration). */
 static int gjk(const Shape* A, const Shape* B, SV* S, int* ns, double* lam, double* v) {
     sub3(A->T + 9, B->T + 9, v);
@@ -495,7 +504,7 @@ static int gjk(const Shape* A, const Shape* B, SV* S, int* ns, double* lam, doub
         SV w;
         sup_md(A, B, nv, &w);
         double vv = dot3(v, v);
-        if (n > 0 && vv - dot3(v, w.w) <= 1e-12 * sqrt(vv)) break;
+        if (n > 0 && vv - dot3(v, w.w) <= GJK_TOL * sqrt(vv)) break;
         int dup = 0;
         for (int i = 0; i < n; ++i) if (S[i].w[0] == w.w[0] && S[i].w[1] == w.w[1] && S[i].w[2] == w.w[2]) dup = 1;
         /* a repeated support point before the gap test passed: the simplex
@@ -614,7 +623,7 @@ static double epa(const Shape* A, const Shape* B, SV* S, int ns, double* pA, dou
                 if (E.alive[f] && E.fd[f] < bd) { bd = E.fd[f]; best = f; }
             SV w;
             sup_md(A, B, E.fn[best], &w);
-            if (dot3(E.fn[best], w.w) - E.fd[best] <= 1e-12 || E.nv >= EPA_MAXV) break;
+            if (dot3(E.fn[best], w.w) - E.fd[best] <= EPA_TOL || E.nv >= EPA_MAXV) break;
             int dupv = 0;
             for (int i = 0; i < E.nv; ++i) {
                 double d[3];
@@ -740,7 +749,238 @@ static int cyl_cyl_side(const Shape* A, const Shape* B, double* d, double* pA, d
     return 1;
 }
 
-static double shape_distance(const Shape* A, const Shape* B, double* pA, double* pB) {
+/* ------------------------------------------------------------------------
+ * Witness refinement.  GJK's witness points converge only to
+ * ~sqrt(gap) and EPA's to its vertex cap, so two implementations whose
+ * iterations differ by rounding return witnesses up to ~1e-5 apart, and the
+ * gradient n^T (J_B(pB) - J_A(pA)) with n = (pB - pA)/|pB - pA|
+ * (robot_data.cpp:476-494) inherits the difference.  The exact witnesses are
+ * a critical point of |X_A(u_A) - X_B(u_B)|^2 over the surface features the
+ * approximate witnesses lie on -- cylinder side (theta, z), cap (x, y), rim
+ * (theta); box face / edge / vertex (the free coordinates) -- and Newton
+ * converges to it quadratically from the GJK / EPA estimate (the same point
+ * from any nearby start).  Accepted only when the solution lies inside its
+ * features, n* = (pB - pA) / sd lies in A's normal cone and -n* in B's, and
+ * sd moves by at most 1e-6; otherwise the GJK / EPA witnesses stay (parallel
+ * flat features: the witnesses are not unique).  Kernel twin: refine_witness
+ * in qpik_device.hpp (same features, rules and tolerances).
+ * ------------------------------------------------------------------------ */
+enum { FT_SIDE = 0, FT_CAP = 1, FT_RIM = 2, FT_BOX = 3 };
+typedef struct Feat { int kind; double s; int fix[3]; } Feat;  /* box: fix[i] = 0 free, +-1 face sign */
+
+#define RW_TAU 1e-4       /* feature classification tolerance on the GJK / EPA witness  */
+#define RW_PIVOT 1e-9     /* smallest Newton pivot (unit-speed parameters): else degenerate */
+#define RW_STEP 1e-12     /* Newton stops after a step this small                        */
+#define RW_CONE 1e-9      /* normal-cone slack                                           */
+#define RW_DMOVE 1e-5     /* largest accepted change of the signed distance (EPA gap 1e-6) */
+
+static void rw_classify(const Shape* s, const double* x, Feat* f) {
+    if (s->type == 1) {
+        const double r = s->prm[0], h = s->prm[1], rho = sqrt(x[0] * x[0] + x[1] * x[1]);
+        f->s = x[2] > 0 ? 1.0 : -1.0;
+        if (fabs(x[2]) > h - RW_TAU && rho > r - RW_TAU) f->kind = FT_RIM;
+        else if (fabs(x[2]) > h - RW_TAU) f->kind = FT_CAP;
+        else f->kind = FT_SIDE;
+        return;
+    }
+    f->kind = FT_BOX;
+    int any = 0, im = 0;
+    double best = -1;
+    for (int i = 0; i < 3; ++i) {
+        f->fix[i] = fabs(x[i]) > s->prm[i] - RW_TAU ? (x[i] > 0 ? 1 : -1) : 0;
+        any |= f->fix[i] != 0;
+        const double t = fabs(x[i]) / s->prm[i];
+        if (t > best) { best = t; im = i; }
+    }
+    if (!any) f->fix[im] = x[im] > 0 ? 1 : -1;
+}
+/* parameters of feature f at the local point x */
+static int rw_params(const Shape* s, const Feat* f, const double* x, double* u) {
+    switch (f->kind) {
+    case FT_SIDE: u[0] = atan2(x[1], x[0]); u[1] = x[2]; return 2;
+    case FT_RIM: u[0] = atan2(x[1], x[0]); return 1;
+    case FT_CAP: u[0] = x[0]; u[1] = x[1]; return 2;
+    default: {
+        int k = 0;
+        for (int i = 0; i < 3; ++i) if (!f->fix[i]) u[k++] = x[i];
+        (void)s;
+        return k;
+    }
+    }
+}
+/* world point, unit-speed tangents t[k] and curvature vectors c[k] (theta:
+ * arc-length derivatives; all other parameters are linear) */
+static void rw_eval(const Shape* s, const Feat* f, const double* u, double* X, double t[2][3], double c[2][3]) {
+    double x[3], tl[2][3] = {{0, 0, 0}, {0, 0, 0}}, cl[2][3] = {{0, 0, 0}, {0, 0, 0}};
+    int k = 0;
+    if (f->kind == FT_SIDE || f->kind == FT_RIM) {
+        const double r = s->prm[0], cs = cos(u[0]), sn = sin(u[0]);
+        x[0] = r * cs; x[1] = r * sn; x[2] = f->kind == FT_SIDE ? u[1] : f->s * s->prm[1];
+        tl[0][0] = -sn; tl[0][1] = cs;
+        cl[0][0] = -cs / r; cl[0][1] = -sn / r;
+        if (f->kind == FT_SIDE) tl[1][2] = 1;
+        k = f->kind == FT_SIDE ? 2 : 1;
+    } else if (f->kind == FT_CAP) {
+        x[0] = u[0]; x[1] = u[1]; x[2] = f->s * s->prm[1];
+        tl[0][0] = 1; tl[1][1] = 1;
+        k = 2;
+    } else {
+        for (int i = 0; i < 3; ++i) {
+            if (f->fix[i]) { x[i] = f->fix[i] * s->prm[i]; continue; }
+            x[i] = u[k];
+            tl[k][i] = 1;
+            ++k;
+        }
+    }
+    matvec3(s->T, x, X);
+    X[0] += s->T[9]; X[1] += s->T[10]; X[2] += s->T[11];
+    for (int j = 0; j < k; ++j) { matvec3(s->T, tl[j], t[j]); matvec3(s->T, cl[j], c[j]); }
+}
+/* theta parameters move by the arc-length step / r */
+static void rw_step(const Shape* s, const Feat* f, double* u, const double* du) {
+    if (f->kind == FT_SIDE || f->kind == FT_RIM) {
+        u[0] += du[0] / s->prm[0];
+        if (f->kind == FT_SIDE) u[1] += du[1];
+    } else {
+        const int k = f->kind == FT_CAP ? 2 : (!f->fix[0]) + (!f->fix[1]) + (!f->fix[2]);
+        for (int j = 0; j < k; ++j) u[j] += du[j];
+    }
+}
+/* Newton on grad |X_A - X_B|^2 = 0.  Returns 1 converged, 0 degenerate / not converged. */
+static int rw_newton(const Shape* A, const Feat* fA, double* uA, int mA, const Shape* B, const Feat* fB, double* uB,
+                     int mB, double* XA, double* XB) {
+    const int m = mA + mB;
+    for (int it = 0; it < 20; ++it) {
+        double tA[2][3], cA[2][3], tB[2][3], cB[2][3], D[3], J[4][3], H[4][5];
+        rw_eval(A, fA, uA, XA, tA, cA);
+        rw_eval(B, fB, uB, XB, tB, cB);
+        sub3(XA, XB, D);
+        if (m == 0) return 1;
+        for (int i = 0; i < mA; ++i) memcpy(J[i], tA[i], sizeof(J[i]));
+        for (int i = 0; i < mB; ++i) for (int c = 0; c < 3; ++c) J[mA + i][c] = -tB[i][c];
+        for (int i = 0; i < m; ++i) {
+            for (int j = 0; j < m; ++j) H[i][j] = dot3(J[i], J[j]);
+            H[i][m] = -dot3(J[i], D);
+        }
+        H[0][0] += mA > 0 ? dot3(D, cA[0]) : -dot3(D, cB[0]);   /* theta curvature terms (index 0 only) */
+        if (mA > 0 && mB > 0) H[mA][mA] -= dot3(D, cB[0]);
+        /* Gaussian elimination, partial pivoting */
+        for (int c = 0; c < m; ++c) {
+            int p = c;
+            for (int r = c + 1; r < m; ++r) if (fabs(H[r][c]) > fabs(H[p][c])) p = r;
+            if (!(fabs(H[p][c]) > RW_PIVOT)) return 0;
+            if (p != c) for (int j = 0; j <= m; ++j) { const double t = H[c][j]; H[c][j] = H[p][j]; H[p][j] = t; }
+            for (int r = c + 1; r < m; ++r) {
+                const double g = H[r][c] / H[c][c];
+                for (int j = c; j <= m; ++j) H[r][j] -= g * H[c][j];
+            }
+        }
+        double du[4], mx = 0;
+        for (int r = m - 1; r >= 0; --r) {
+            double t = H[r][m];
+            for (int j = r + 1; j < m; ++j) t -= H[r][j] * du[j];
+            du[r] = t / H[r][r];
+            mx = fmax(mx, fabs(du[r]));
+        }
+        rw_step(A, fA, uA, du);
+        rw_step(B, fB, uB, du + mA);
+        if (mx <= RW_STEP) {
+            rw_eval(A, fA, uA, XA, tA, cA);
+            rw_eval(B, fB, uB, XB, tB, cB);
+            return 1;
+        }
+    }
+    return 0;
+}
+/* Outside the feature's domain: move to the bounding feature (returns 1). */
+static int rw_domain(const Shape* s, Feat* f, const double* u) {
+    if (f->kind == FT_SIDE && fabs(u[1]) > s->prm[1]) { f->kind = FT_RIM; f->s = u[1] > 0 ? 1 : -1; return 1; }
+    if (f->kind == FT_CAP && u[0] * u[0] + u[1] * u[1] > s->prm[0] * s->prm[0]) { f->kind = FT_RIM; return 1; }
+    if (f->kind == FT_BOX) {
+        int k = 0;
+        for (int i = 0; i < 3; ++i) {
+            if (f->fix[i]) continue;
+            if (fabs(u[k]) > s->prm[i]) { f->fix[i] = u[k] > 0 ? 1 : -1; return 1; }
+            ++k;
+        }
+    }
+    return 0;
+}
+/* The outward normal nrm must lie in the normal cone of feature f at u.
+ * Returns -1 when it cannot (refinement fails), 1 when the feature moves to a
+ * neighbour (rim -> cap / side, box face -> edge ...), 0 when it holds. */
+static int rw_cone(const Shape* s, Feat* f, const double* u, const double* nrm) {
+    const double ax[3] = {s->T[2], s->T[5], s->T[8]};
+    if (f->kind == FT_BOX) {
+        for (int i = 0; i < 3; ++i) {
+            if (!f->fix[i]) continue;
+            const double e[3] = {s->T[i], s->T[3 + i], s->T[6 + i]};
+            if (f->fix[i] * dot3(nrm, e) < -RW_CONE) {
+                if ((f->fix[0] != 0) + (f->fix[1] != 0) + (f->fix[2] != 0) == 1) return -1;  /* no face left */
+                f->fix[i] = 0;
+                return 1;
+            }
+        }
+        return 0;
+    }
+    if (f->kind == FT_CAP) return f->s * dot3(nrm, ax) > 0 ? 0 : -1;
+    const double rl[3] = {cos(u[0]), sin(u[0]), 0};
+    double rad[3];
+    matvec3(s->T, rl, rad);
+    const double a = dot3(nrm, rad), b = f->s * dot3(nrm, ax);
+    if (f->kind == FT_SIDE) return a > 0 ? 0 : -1;
+    if (a < -RW_CONE) { f->kind = FT_CAP; return 1; }
+    if (b < -RW_CONE) { f->kind = FT_SIDE; return 1; }
+    return 0;
+}
+/* feature parameters at the world point X */
+static int rw_reparam(const Shape* s, const Feat* f, const double* X, double* u) {
+    double t[3], x[3];
+    sub3(X, s->T + 9, t);
+    matTvec3(s->T, t, x);
+    return rw_params(s, f, x, u);
+}
+static int refine_witness(const Shape* A, const Shape* B, double* d, double* pA, double* pB) {
+    Feat fA, fB;
+    double xA[3], xB[3], t[3], uA[2], uB[2];
+    sub3(pA, A->T + 9, t); matTvec3(A->T, t, xA);
+    sub3(pB, B->T + 9, t); matTvec3(B->T, t, xB);
+    rw_classify(A, xA, &fA);
+    rw_classify(B, xB, &fB);
+    int mA = rw_params(A, &fA, xA, uA), mB = rw_params(B, &fB, xB, uB);
+    const double sgn = *d < 0 ? -1.0 : 1.0;
+    for (int round = 0; round < 4; ++round) {
+        double XA[3], XB[3], D[3], n[3], nb[3];
+        if (!rw_newton(A, &fA, uA, mA, B, &fB, uB, mB, XA, XB)) return 0;
+        int ca = rw_domain(A, &fA, uA), cb = rw_domain(B, &fB, uB);
+        if (!ca && !cb) {
+            sub3(XB, XA, D);
+            const double L = norm3(D);
+            if (!(L > 1e-12)) return 0;
+            const double sd = sgn * L;
+            for (int c = 0; c < 3; ++c) { n[c] = D[c] / sd; nb[c] = -n[c]; }
+            ca = rw_cone(A, &fA, uA, n);
+            cb = rw_cone(B, &fB, uB, nb);
+            if (ca < 0 || cb < 0) return 0;
+            if (!ca && !cb) {
+                if (!(fabs(sd - *d) <= RW_DMOVE)) return 0;
+                *d = sd;
+                memcpy(pA, XA, sizeof(XA));
+                memcpy(pB, XB, sizeof(XB));
+                return 1;
+            }
+        }
+        mA = rw_reparam(A, &fA, XA, uA);
+        mB = rw_reparam(B, &fB, XB, uB);
+    }
+    return 0;
+}
+
+/* signed distance and witnesses of one pair; *how: 0 closed form (sphere
+ * pairs, cylinder sides), 1 GJK, 2 EPA -- the latter two are what
+ * refine_witness sharpens */
+static double shape_distance(const Shape* A, const Shape* B, double* pA, double* pB, int* how) {
+    *how = 0;
     if (A->type == 0 && B->type == 0) {
         double v[3];
         sub3(B->T + 9, A->T + 9, v);
@@ -769,7 +1009,8 @@ static double shape_distance(const Shape* A, const Shape* B, double* pA, double*
     SV S[4];
     int ns;
     double lam[4], v[3];
-    if (gjk(A, B, S, &ns, lam, v)) return epa(A, B, S, ns, pA, pB);
+    if (gjk(A, B, S, &ns, lam, v)) { *how = 2; return epa(A, B, S, ns, pA, pB); }
+    *how = 1;
     for (int c = 0; c < 3; ++c) {
         pA[c] = 0; pB[c] = 0;
         for (int i = 0; i < ns; ++i) { pA[c] += lam[i] * S[i].a[c]; pB[c] += lam[i] * S[i].b[c]; }
@@ -797,12 +1038,15 @@ static void min_distance_w(const OracleModel* m, const Kin* k, double* dist, dou
     Shape sh[ORC_MAXG];
     for (int g = 0; g < m->ngeom; ++g) make_shape(m, k, g, &sh[g]);
     double best = 1.7976931348623157e308, bpA[3] = {0}, bpB[3] = {0};
-    int bi = -1;
+    int bi = -1, bhow = 0;
     for (int p = 0; p < m->npairs; ++p) {
         double pA[3], pB[3];
-        double d = shape_distance(&sh[m->pair_a[p]], &sh[m->pair_b[p]], pA, pB);
-        if (d < best) { best = d; bi = p; memcpy(bpA, pA, sizeof(pA)); memcpy(bpB, pB, sizeof(pB)); }
+        int how;
+        double d = shape_distance(&sh[m->pair_a[p]], &sh[m->pair_b[p]], pA, pB, &how);
+        if (d < best) { best = d; bi = p; bhow = how; memcpy(bpA, pA, sizeof(pA)); memcpy(bpB, pB, sizeof(pB)); }
     }
+    /* the winner's GJK / EPA witnesses sharpened to the exact critical point (D17) */
+    if (bi >= 0 && bhow) refine_witness(&sh[m->pair_a[bi]], &sh[m->pair_b[bi]], &best, bpA, bpB);
     *dist = best;
     *pair_out = bi;
     memcpy(wA, bpA, sizeof(bpA));
@@ -2119,7 +2363,9 @@ void oracle_pair_distance(const OracleModel* m, const double* q, int pair, doubl
     Shape a, b;
     make_shape(m, &k, m->pair_a[pair], &a);
     make_shape(m, &k, m->pair_b[pair], &b);
-    *d = shape_distance(&a, &b, pA, pB);
+    int how;
+    *d = shape_distance(&a, &b, pA, pB, &how);
+    if (how) refine_witness(&a, &b, d, pA, pB);
 }
 /* narrow phase on two free shapes (T: R row-major then p), for checking the
  * device narrow-phase code in isolation */
@@ -2129,7 +2375,28 @@ void oracle_shape_distance(int ta, const double* TA, const double* prmA, int tb,
     a.type = ta; b.type = tb;
     memcpy(a.T, TA, sizeof(a.T)); memcpy(b.T, TB, sizeof(b.T));
     memcpy(a.prm, prmA, sizeof(a.prm)); memcpy(b.prm, prmB, sizeof(b.prm));
-    *d = shape_distance(&a, &b, pA, pB);
+    int how;
+    *d = shape_distance(&a, &b, pA, pB, &how);
+    if (how) refine_witness(&a, &b, d, pA, pB);
+}
+/* the pair's raw GJK / EPA result, without the witness refinement (tests) */
+void oracle_pair_distance_raw(const OracleModel* m, const double* q, int pair, double* d, double* pA, double* pB,
+                              int* how) {
+    Kin k;
+    kin_fk(m, q, &k);
+    Shape a, b;
+    make_shape(m, &k, m->pair_a[pair], &a);
+    make_shape(m, &k, m->pair_b[pair], &b);
+    *d = shape_distance(&a, &b, pA, pB, how);
+}
+/* the raw GJK / EPA result without the witness refinement (tests) */
+void oracle_shape_distance_raw(int ta, const double* TA, const double* prmA, int tb, const double* TB,
+                               const double* prmB, double* d, double* pA, double* pB, int* how) {
+    Shape a, b;
+    a.type = ta; b.type = tb;
+    memcpy(a.T, TA, sizeof(a.T)); memcpy(b.T, TB, sizeof(b.T));
+    memcpy(a.prm, prmA, sizeof(a.prm)); memcpy(b.prm, prmB, sizeof(b.prm));
+    *d = shape_distance(&a, &b, pA, pB, how);
 }
 void oracle_manipulability(const OracleModel* m, const double* q, double* man, double* grad) {
     Kin k;

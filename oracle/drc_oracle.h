@@ -172,6 +172,12 @@ void oracle_min_distance(const OracleModel* m, const double* q, double* dist, do
 void oracle_pair_distance(const OracleModel* m, const double* q, int pair, double* d, double* pA, double* pB);
 void oracle_shape_distance(int ta, const double* TA, const double* prmA, int tb, const double* TB,
                            const double* prmB, double* d, double* pA, double* pB);
+/* raw GJK / EPA results without the witness refinement (D17), for tests;
+ * how: 0 closed form, 1 GJK, 2 EPA */
+void oracle_pair_distance_raw(const OracleModel* m, const double* q, int pair, double* d, double* pA, double* pB,
+                              int* how);
+void oracle_shape_distance_raw(int ta, const double* TA, const double* prmA, int tb, const double* TB,
+                               const double* prmB, double* d, double* pA, double* pB, int* how);
 void oracle_manipulability(const OracleModel* m, const double* q, double* man, double* grad);
 int oracle_solve_qp(int nx, int nc, const double* P, const double* qv, const double* A,
                     const double* l, const double* u, const OracleSettings* s,

@@ -327,6 +327,17 @@ def pair_distance(om, q, pair):
     return d.value, pA, pB
 
 
+def pair_distance_raw(om, q, pair):
+    """The pair's GJK / EPA result before the witness refinement (D17): (d, pA, pB, how)
+    with how 0 closed form, 1 GJK, 2 EPA."""
+    d = C.c_double()
+    how = C.c_int()
+    pA, pB = np.zeros(3), np.zeros(3)
+    lib().oracle_pair_distance_raw(C.byref(om), _ptr(np.ascontiguousarray(q, float)), C.c_int(pair), C.byref(d),
+                                   _ptr(pA), _ptr(pB), C.byref(how))
+    return d.value, pA, pB, how.value
+
+
 def manipulability(om, q):
     m = C.c_double()
     n = om.n_arm if om.kind == 1 else om.nv

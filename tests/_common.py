@@ -103,7 +103,7 @@ def narrow_phase_close(om, q, d_dev, dg_dev):
     d, dg, _ = O.min_distance(om, q)
     if abs(d_dev - d) > (1e-9 if d > 0 else 1e-6):
         return False
-    if np.max(np.abs(dg_dev - dg)) <= (1e-5 if d > 0 else 2e-2):
+    if np.max(np.abs(dg_dev - dg)) <= 1e-6:   # exact witnesses on both sides (D17)
         return True
     return nonsmooth_min_distance(om, q)
 

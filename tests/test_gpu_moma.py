@@ -49,7 +49,7 @@ def test_moma_stages_match_oracle(cuda, robot):
         assert narrow_phase_close(om, q[:, b], st["dist"][0, b], st["dist"][1:, b]), b
 
 
-EXPECTED_OFF = {"husky_fr3": 0, "xls_fr3": 0, "caster_fr3": 2}   # measured end-to-end count beyond 1e-4 (assert_qpik_parity)
+EXPECTED_OFF = {"husky_fr3": 0, "xls_fr3": 0, "caster_fr3": 0}   # measured end-to-end count beyond 1e-4 (assert_qpik_parity)
 
 
 @pytest.mark.parametrize("robot", ROBOTS)

@@ -94,8 +94,10 @@ def test_many_streams_bounded_scratch(cuda):
         np.testing.assert_array_equal(out.cpu().numpy(), ro)
         np.testing.assert_array_equal(st.cpu().numpy(), rs)
         mem.append(used())
-    grown = mem[-1] - mem[7]                    # 16 more streams past the 8-context cap
-    assert grown < 8 * 2 ** 20, (grown, mem)
+    # 16 more streams past the 8-context cap: only the HIP stream objects
+    # themselves (~1 MB each) may add, not 16 more ~10.5 MB pools
+    grown = mem[-1] - mem[7]
+    assert grown < 48 * 2 ** 20, (grown, mem)
     before = used()
     for s in streams:
         _capi.check(_capi.lib().drc_model_release_stream(rd.model.handle, C.c_void_p(s.cuda_stream)))

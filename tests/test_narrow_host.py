@@ -59,14 +59,21 @@ def run_harness(exe, pairs):
     return np.array([[float(x) for x in ln.split()] for ln in res.stdout.strip().splitlines()])
 
 
-def oracle_dist(pairs):
+def oracle_dist(pairs, raw=True):
+    """The oracle's narrow phase: raw GJK / EPA (raw=True) or with the witness
+    refinement (D17)."""
     import ctypes as C
     out = []
     for ta, TA, pa, tb, TB, pb in pairs:
         d = C.c_double()
+        how = C.c_int()
         pA, pB = np.zeros(3), np.zeros(3)
-        O.lib().oracle_shape_distance(ta, O._ptr(TA), O._ptr(pa), tb, O._ptr(TB), O._ptr(pb),
-                                      C.byref(d), O._ptr(pA), O._ptr(pB))
+        if raw:
+            O.lib().oracle_shape_distance_raw(ta, O._ptr(TA), O._ptr(pa), tb, O._ptr(TB), O._ptr(pb),
+                                              C.byref(d), O._ptr(pA), O._ptr(pB), C.byref(how))
+        else:
+            O.lib().oracle_shape_distance(ta, O._ptr(TA), O._ptr(pa), tb, O._ptr(TB), O._ptr(pb),
+                                          C.byref(d), O._ptr(pA), O._ptr(pB))
         out.append(np.concatenate([[d.value], pA, pB]))
     return np.array(out)
 
@@ -78,23 +85,23 @@ def test_device_narrow_phase_matches_oracle(harness):
     pen = ref[:, 0] < 0
     assert 0.2 < pen.mean() < 0.8  # both GJK and EPA exercised
     err = np.abs(dev[:, 0] - ref[:, 0])
-    # separated: GJK converges to 1e-12 relative on both sides
-    assert err[~pen].max() <= 1e-9, err[~pen].max()
-    # penetrating: identical EPA decisions agree to 1e-9 unless the polytope
-    # hits its vertex cap on a deep curved contact; there both sides stop
-    # within hpp-fcl's default EPA tolerance (1e-6) of the true depth
-    assert err[pen].max() <= 1e-6, err[pen].max()
-    assert np.mean(err[pen] <= 1e-9) >= 0.99
-    # witnesses: flat-flat contacts admit a face of witnesses, so compare the
-    # separation vector pB - pA (unique).  GJK stops on a 1e-12 distance gap,
-    # which leaves the direction accurate to ~sqrt(gap * d) ~ 1e-7; EPA's
-    # 1e-12 face gap likewise.  Most pairs agree to the last bits.
+    # raw estimates (before the D17 refinement, test below): separated, GJK
+    # stops at a 1e-9 support gap on both sides; penetrating, identical EPA
+    # decisions agree to 1e-9 unless rounding changes a step, and both sides
+    # stop within the EPA tolerance (1e-6, hpp-fcl's default) of the depth
+    assert err[~pen].max() <= 2e-9, err[~pen].max()
+    assert err[pen].max() <= 2e-6, err[pen].max()
+    assert np.mean(err[pen] <= 1e-9) >= 0.97
+    # raw witnesses: flat-flat contacts admit a face of witnesses, so compare
+    # the separation vector pB - pA (unique).  GJK's 1e-9 gap leaves the
+    # direction accurate to ~sqrt(gap * d); EPA's 1e-6 gap likewise -- the
+    # footprint the D17 refinement removes (test_witness_refinement_matches_oracle)
     sep = dev[:, 4:7] - dev[:, 1:4]
     sep_ref = ref[:, 4:7] - ref[:, 1:4]
     serr = np.abs(sep - sep_ref).max(axis=1)
-    assert serr[~pen].max() <= 1e-6, serr[~pen].max()
+    assert serr[~pen].max() <= 1e-4, serr[~pen].max()
     assert np.median(serr[~pen]) <= 1e-12
-    assert serr[pen].max() <= 5e-5, serr[pen].max()
+    assert serr[pen].max() <= 1e-3, serr[pen].max()
     assert np.quantile(serr[pen], 0.9) <= 1e-7
 
 
@@ -124,3 +131,30 @@ def test_epa_wave_form_matches_serial(harness):
     pen = dev[:, 0] < 0
     assert pen.sum() > 500
     assert np.all(dev[:, 9] == 1), np.nonzero(dev[:, 9] != 1)
+
+
+def test_witness_refinement_matches_oracle(harness):
+    """D17: the device refine_witness and the oracle's land on the same
+    critical point from their own GJK / EPA estimates -- distance and
+    separation vector to rounding, where the raw estimates differ by up to
+    ~1e-5 -- and they accept / reject the same pairs."""
+    pairs = random_pairs(4000, 17)
+    dev = run_harness(harness, pairs)
+    ref = oracle_dist(pairs, raw=False)
+    raw = oracle_dist(pairs, raw=True)
+    acc_dev = dev[:, 17] == 1
+    acc_ref = np.any(ref[:, 1:] != raw[:, 1:], axis=1) | (ref[:, 0] != raw[:, 0])
+    assert acc_dev.sum() > 1000
+    # the oracle may return a refined point bit-identical to its estimate (box vertices)
+    assert np.all(acc_ref <= acc_dev)
+    d_err = np.abs(dev[acc_dev, 10] - ref[acc_dev, 0])
+    assert d_err.max() <= 1e-12, d_err.max()
+    sep = dev[acc_dev, 14:17] - dev[acc_dev, 11:14]
+    sep_ref = ref[acc_dev, 4:7] - ref[acc_dev, 1:4]
+    assert np.abs(sep - sep_ref).max() <= 1e-12, np.abs(sep - sep_ref).max()
+    w_err = np.maximum(np.abs(dev[acc_dev, 11:14] - ref[acc_dev, 1:4]).max(1),
+                       np.abs(dev[acc_dev, 14:17] - ref[acc_dev, 4:7]).max(1))
+    assert np.quantile(w_err, 0.99) <= 1e-12, np.quantile(w_err, 0.99)
+    # rejected on the device -> the oracle kept its estimate as well
+    rej = ~acc_dev & (dev[:, 0] == dev[:, 10])
+    assert np.all(~acc_ref[rej])

@@ -76,7 +76,15 @@ int main() {
       gjk_run(A, B, g, d + 1e-9 * (1 + std::fabs(d)));
       pruned = g.pruned;
     }
-    printf("%.17g %.17g %.17g %.17g %.17g %.17g %.17g %.17g %d %d\n", d, pA.x, pA.y, pA.z, pB.x, pB.y, pB.z, lb, pruned,
-           wave_same);
+    // witness refinement of GJK / EPA results (D17)
+    double dr = d;
+    V3 rA = pA, rB = pB;
+    int refined = 0;
+    if (ta != kSphere && tb != kSphere && !(ta == kCylinder && tb == kCylinder && cyl_cyl_side(A, B, &dr, &rA, &rB))) {
+      dr = d;
+      refined = refine_witness(A, B, &dr, &rA, &rB) ? 1 : 0;
+    }
+    printf("%.17g %.17g %.17g %.17g %.17g %.17g %.17g %.17g %d %d %.17g %.17g %.17g %.17g %.17g %.17g %.17g %d\n", d,
+           pA.x, pA.y, pA.z, pB.x, pB.y, pB.z, lb, pruned, wave_same, dr, rA.x, rA.y, rA.z, rB.x, rB.y, rB.z, refined);
   }
 }
