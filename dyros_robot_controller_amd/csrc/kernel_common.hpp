@@ -68,7 +68,7 @@ struct KParams {
 
 // scalar slots in the oSc region
 enum { SC_C = 0, SC_RHO, SC_MAN, SC_DIST, SC_PAIR, SC_PRI, SC_DUA, SC_EPSP, SC_EPSD, SC_PRIS, SC_DUAS,
-       SC_NAX, SC_NZ, SC_NPX, SC_NATY, SC_NQ, SC_NF, SC_NR, SC_WIN, SC_PFAIL, SC_HIV, SC_COUNT };
+       SC_NAX, SC_NZ, SC_NPX, SC_NATY, SC_NQ, SC_NF, SC_NR, SC_WIN, SC_PFAIL, SC_HIV, SC_HOW, SC_COUNT };
 // Parity mode tries the certified polish at every termination check, but only
 // until this many attempts failed on a not-yet-converged iterate; after that
 // only at convergence (bounds the cost of slow or non-converging instances —

@@ -1092,9 +1092,13 @@ DRC_HD __forceinline__ double sphere_pair(const Shape& A, const Shape& B, V3* pA
 // Accepted when the point lies inside its features, n* = (pB - pA)/sd is in
 // A's normal cone and -n* in B's, and sd moves by <= 1e-6; otherwise the
 // estimates stay (parallel flat features: witnesses not unique).
-// Register-only form: the parameter counts (0-2 per feature) are template
-// arguments, so the Newton system, the feature tangents and the parameters
-// stay in VGPRs (no private arrays, no scratch frame in the task kernel).
+// Device form: register-only and compact (the task kernel calls it once per
+// instance on one lane, so its code size matters more than its FLOPs).  One
+// 4-unknown Newton system for every feature pair (absent parameters get
+// identity rows), and the angle of a side / rim point is kept as its unit
+// radial vector (c, s) moved by the retraction normalize(r + delta t / r): no
+// transcendental calls.  The oracle's form (angles, variable-size system)
+// converges to the same critical point.
 enum : int { kFtSide = 0, kFtCap = 1, kFtRim = 2, kFtBox = 3 };
 struct Feat {
   int kind;
@@ -1110,12 +1114,17 @@ struct Feat {
     return kind == kFtRim ? 1 : (kind == kFtBox ? (fx == 0) + (fy == 0) + (fz == 0) : 2);
   }
 };
+// feature parameters: side (c, s, z), rim (c, s), cap (x, y), box (first, second free coordinate)
+struct FParam {
+  double a, b, c;
+};
 constexpr double kRwTau = 1e-4, kRwPivot = 1e-9, kRwStep = 1e-12, kRwCone = 1e-9, kRwDMove = 1e-5;
 
 DRC_HD __forceinline__ double v3c(V3 v, int i) { return i == 0 ? v.x : (i == 1 ? v.y : v.z); }
 DRC_HD __forceinline__ V3 v3e(int i) { return v3(i == 0, i == 1, i == 2); }
+DRC_HD __forceinline__ double shp(const Shape& s, int i) { return i == 0 ? s.p0 : (i == 1 ? s.p1 : s.p2); }
 
-DRC_HD __forceinline__ void rw_classify(const Shape& s, V3 x, Feat* f) {
+DRC_HD inline void rw_classify(const Shape& s, V3 x, Feat* f) {
   f->fx = f->fy = f->fz = 0;
   f->s = x.z > 0 ? 1.0 : -1.0;
   if (s.type == kCylinder) {
@@ -1128,9 +1137,8 @@ DRC_HD __forceinline__ void rw_classify(const Shape& s, V3 x, Feat* f) {
   f->kind = kFtBox;
   int any = 0, im = 0;
   double best = -1;
-#pragma unroll
   for (int i = 0; i < 3; ++i) {
-    const double xi = v3c(x, i), hi = i == 0 ? s.p0 : (i == 1 ? s.p1 : s.p2);
+    const double xi = v3c(x, i), hi = shp(s, i);
     const int fi = fabs(xi) > hi - kRwTau ? (xi > 0 ? 1 : -1) : 0;
     f->set_fix(i, fi);
     any |= fi != 0;
@@ -1142,47 +1150,48 @@ DRC_HD __forceinline__ void rw_classify(const Shape& s, V3 x, Feat* f) {
   }
   if (!any) f->set_fix(im, v3c(x, im) > 0 ? 1 : -1);
 }
-// parameters (u0, u1) of feature f at the local point x
-DRC_HD __forceinline__ void rw_params(const Feat& f, V3 x, double* u0, double* u1) {
+// parameters of feature f at the local point x
+DRC_HD inline FParam rw_params(const Feat& f, V3 x) {
+  FParam u{0, 0, 0};
   if (f.kind == kFtSide || f.kind == kFtRim) {
-    *u0 = atan2(x.y, x.x);
-    *u1 = x.z;
+    const double rho = sqrt(x.x * x.x + x.y * x.y);
+    u.a = rho > 0 ? x.x / rho : 1.0;
+    u.b = rho > 0 ? x.y / rho : 0.0;
+    u.c = x.z;
   } else if (f.kind == kFtCap) {
-    *u0 = x.x;
-    *u1 = x.y;
+    u.a = x.x;
+    u.b = x.y;
   } else {
     int k = 0;
-#pragma unroll
     for (int i = 0; i < 3; ++i)
       if (!f.fix(i)) {
-        if (k == 0) *u0 = v3c(x, i);
-        else *u1 = v3c(x, i);
+        if (k == 0) u.a = v3c(x, i);
+        else u.b = v3c(x, i);
         ++k;
       }
   }
+  return u;
 }
-// world point, unit-speed tangents t0, t1 and the theta curvature vector c0
-// (arc-length derivatives; the other parameters are linear)
-DRC_HD __forceinline__ V3 rw_eval(const Shape& s, const Feat& f, double u0, double u1, V3* t0, V3* t1, V3* c0) {
+// world point, unit-speed tangents t0, t1 (zero where the feature has fewer
+// parameters) and the curvature vector c0 of the first (angle: arc length)
+DRC_HD inline V3 rw_eval(const Shape& s, const Feat& f, const FParam& u, V3* t0, V3* t1, V3* c0) {
   V3 x, a = v3(0, 0, 0), b = v3(0, 0, 0), c = v3(0, 0, 0);
   if (f.kind == kFtSide || f.kind == kFtRim) {
-    const double r = s.p0, cs = cos(u0), sn = sin(u0);
-    x = v3(r * cs, r * sn, f.kind == kFtSide ? u1 : f.s * s.p1);
-    a = v3(-sn, cs, 0);
-    c = v3(-cs / r, -sn / r, 0);
-    b = v3(0, 0, 1);
+    const double r = s.p0;
+    x = v3(r * u.a, r * u.b, f.kind == kFtSide ? u.c : f.s * s.p1);
+    a = v3(-u.b, u.a, 0);
+    c = v3(-u.a / r, -u.b / r, 0);
+    if (f.kind == kFtSide) b = v3(0, 0, 1);
   } else if (f.kind == kFtCap) {
-    x = v3(u0, u1, f.s * s.p1);
+    x = v3(u.a, u.b, f.s * s.p1);
     a = v3(1, 0, 0);
     b = v3(0, 1, 0);
   } else {
     double xl[3];
     int k = 0;
-#pragma unroll
     for (int i = 0; i < 3; ++i) {
-      const double hi = i == 0 ? s.p0 : (i == 1 ? s.p1 : s.p2);
       const int fi = f.fix(i);
-      xl[i] = fi ? fi * hi : (k == 0 ? u0 : u1);
+      xl[i] = fi ? fi * shp(s, i) : (k == 0 ? u.a : u.b);
       if (!fi) {
         if (k == 0) a = v3e(i);
         else b = v3e(i);
@@ -1196,124 +1205,104 @@ DRC_HD __forceinline__ V3 rw_eval(const Shape& s, const Feat& f, double u0, doub
   *c0 = rot(s.T, c);
   return xform(s.T, x);
 }
-DRC_HD __forceinline__ void rw_step(const Shape& s, const Feat& f, double* u0, double* u1, double d0, double d1) {
-  if (f.kind == kFtSide || f.kind == kFtRim) {
-    *u0 += d0 / s.p0;
-    if (f.kind == kFtSide) *u1 += d1;
+DRC_HD __forceinline__ void rw_step(const Shape& s, const Feat& f, FParam* u, double d0, double d1) {
+  if (f.kind == kFtSide || f.kind == kFtRim) {  // rotate the radial vector by the arc d0 (retraction)
+    const double w = d0 / s.p0, ca = u->a - w * u->b, sa = u->b + w * u->a, n = 1.0 / sqrt(ca * ca + sa * sa);
+    u->a = ca * n;
+    u->b = sa * n;
+    if (f.kind == kFtSide) u->c += d1;
   } else {
-    *u0 += d0;
-    *u1 += d1;
+    u->a += d0;
+    u->b += d1;
   }
 }
-// Newton on grad |X_A - X_B|^2 = 0 with MA + MB <= 4 unknowns (compile-time);
-// false when degenerate or not converged.  Same system, pivoting and stop
-// rule as the oracle's rw_newton.
-template <int MA, int MB>
-DRC_HD __forceinline__ bool rw_newton_t(const Shape& A, const Feat& fA, double* uA0, double* uA1, const Shape& B, const Feat& fB,
-                               double* uB0, double* uB1, V3* XA, V3* XB) {
-  constexpr int M = MA + MB;
+// Newton on grad |X_A - X_B|^2 = 0 (unknowns A0 A1 B0 B1; absent ones get
+// identity rows); false when degenerate or not converged.
+DRC_HD inline bool rw_newton(const Shape& A, const Feat& fA, FParam* uA, const Shape& B, const Feat& fB, FParam* uB,
+                             V3* XA, V3* XB) {
+  const int mA = fA.nparam(), mB = fB.nparam();
+  const bool act[4] = {mA > 0, mA > 1, mB > 0, mB > 1};
+#pragma unroll 1
   for (int it = 0; it < 20; ++it) {
     V3 tA0, tA1, cA, tB0, tB1, cB;
-    *XA = rw_eval(A, fA, *uA0, *uA1, &tA0, &tA1, &cA);
-    *XB = rw_eval(B, fB, *uB0, *uB1, &tB0, &tB1, &cB);
-    if constexpr (M == 0) {
-      return true;
-    } else {
-      const V3 D = *XA - *XB;
-      V3 J[M];
+    *XA = rw_eval(A, fA, *uA, &tA0, &tA1, &cA);
+    *XB = rw_eval(B, fB, *uB, &tB0, &tB1, &cB);
+    if (mA + mB == 0) return true;
+    const V3 D = *XA - *XB;
+    const V3 J[4] = {tA0, tA1, -1.0 * tB0, -1.0 * tB1};
+    double H[4][5];
 #pragma unroll
-      for (int i = 0; i < MA; ++i) J[i] = i == 0 ? tA0 : tA1;
+    for (int i = 0; i < 4; ++i) {
 #pragma unroll
-      for (int i = 0; i < MB; ++i) J[MA + i] = -1.0 * (i == 0 ? tB0 : tB1);
-      double H[M][M + 1];
+      for (int j = 0; j < 4; ++j) H[i][j] = act[i] && act[j] ? dot(J[i], J[j]) : (i == j ? 1.0 : 0.0);
+      H[i][4] = act[i] ? -dot(J[i], D) : 0.0;
+    }
+    if (act[0]) H[0][0] += dot(D, cA);  // angle curvature (first parameter only)
+    if (act[2]) H[2][2] -= dot(D, cB);
 #pragma unroll
-      for (int i = 0; i < M; ++i) {
+    for (int c = 0; c < 4; ++c) {  // Gaussian elimination, partial pivoting (swaps by selects)
+      double pv = fabs(H[c][c]);
+      int p = c;
 #pragma unroll
-        for (int j = 0; j < M; ++j) H[i][j] = dot(J[i], J[j]);
-        H[i][M] = -dot(J[i], D);
-      }
-      if constexpr (MA > 0) H[0][0] += dot(D, cA);  // theta curvature (index 0 only)
-      if constexpr (MB > 0) H[MA][MA] -= dot(D, cB);
-#pragma unroll
-      for (int c = 0; c < M; ++c) {  // Gaussian elimination, partial pivoting (swaps by selects)
-        double pv = fabs(H[c][c]);
-        int p = c;
-#pragma unroll
-        for (int r = c + 1; r < M; ++r)
-          if (fabs(H[r][c]) > pv) {
-            pv = fabs(H[r][c]);
-            p = r;
-          }
-        if (!(pv > kRwPivot)) return false;
-#pragma unroll
-        for (int r = c + 1; r < M; ++r)
-          if (r == p)
-#pragma unroll
-            for (int j = 0; j <= M; ++j) {
-              const double t = H[c][j];
-              H[c][j] = H[r][j];
-              H[r][j] = t;
-            }
-#pragma unroll
-        for (int r = c + 1; r < M; ++r) {
-          const double g = H[r][c] / H[c][c];
-#pragma unroll
-          for (int j = c; j <= M; ++j) H[r][j] -= g * H[c][j];
+      for (int r = c + 1; r < 4; ++r)
+        if (fabs(H[r][c]) > pv) {
+          pv = fabs(H[r][c]);
+          p = r;
         }
-      }
-      double du[M], mx = 0;
+      if (!(pv > kRwPivot)) return false;
 #pragma unroll
-      for (int r = M - 1; r >= 0; --r) {
-        double t = H[r][M];
+      for (int r = c + 1; r < 4; ++r)
+        if (r == p)
 #pragma unroll
-        for (int j = r + 1; j < M; ++j) t -= H[r][j] * du[j];
-        du[r] = t / H[r][r];
-        mx = fmax(mx, fabs(du[r]));
+          for (int j = 0; j < 5; ++j) {
+            const double t = H[c][j];
+            H[c][j] = H[r][j];
+            H[r][j] = t;
+          }
+      const double ip = 1.0 / H[c][c];
+#pragma unroll
+      for (int r = c + 1; r < 4; ++r) {
+        const double g = H[r][c] * ip;
+#pragma unroll
+        for (int j = c; j < 5; ++j) H[r][j] -= g * H[c][j];
       }
-      rw_step(A, fA, uA0, uA1, MA > 0 ? du[0] : 0.0, MA > 1 ? du[MA > 1 ? 1 : 0] : 0.0);
-      rw_step(B, fB, uB0, uB1, MB > 0 ? du[MA] : 0.0, MB > 1 ? du[MB > 1 ? MA + 1 : MA] : 0.0);
-      if (mx <= kRwStep) {
-        *XA = rw_eval(A, fA, *uA0, *uA1, &tA0, &tA1, &cA);
-        *XB = rw_eval(B, fB, *uB0, *uB1, &tB0, &tB1, &cB);
-        return true;
-      }
+    }
+    double du[4], mx = 0;
+#pragma unroll
+    for (int r = 3; r >= 0; --r) {
+      double t = H[r][4];
+#pragma unroll
+      for (int j = r + 1; j < 4; ++j) t -= H[r][j] * du[j];
+      du[r] = t / H[r][r];
+      mx = fmax(mx, fabs(du[r]));
+    }
+    rw_step(A, fA, uA, du[0], du[1]);
+    rw_step(B, fB, uB, du[2], du[3]);
+    if (mx <= kRwStep) {
+      *XA = rw_eval(A, fA, *uA, &tA0, &tA1, &cA);
+      *XB = rw_eval(B, fB, *uB, &tB0, &tB1, &cB);
+      return true;
     }
   }
   return false;
 }
-DRC_HD __forceinline__ bool rw_newton(const Shape& A, const Feat& fA, double* uA0, double* uA1, const Shape& B, const Feat& fB,
-                             double* uB0, double* uB1, V3* XA, V3* XB) {
-  const int k = 3 * fA.nparam() + fB.nparam();
-  switch (k) {
-    case 0: return rw_newton_t<0, 0>(A, fA, uA0, uA1, B, fB, uB0, uB1, XA, XB);
-    case 1: return rw_newton_t<0, 1>(A, fA, uA0, uA1, B, fB, uB0, uB1, XA, XB);
-    case 2: return rw_newton_t<0, 2>(A, fA, uA0, uA1, B, fB, uB0, uB1, XA, XB);
-    case 3: return rw_newton_t<1, 0>(A, fA, uA0, uA1, B, fB, uB0, uB1, XA, XB);
-    case 4: return rw_newton_t<1, 1>(A, fA, uA0, uA1, B, fB, uB0, uB1, XA, XB);
-    case 5: return rw_newton_t<1, 2>(A, fA, uA0, uA1, B, fB, uB0, uB1, XA, XB);
-    case 6: return rw_newton_t<2, 0>(A, fA, uA0, uA1, B, fB, uB0, uB1, XA, XB);
-    case 7: return rw_newton_t<2, 1>(A, fA, uA0, uA1, B, fB, uB0, uB1, XA, XB);
-    default: return rw_newton_t<2, 2>(A, fA, uA0, uA1, B, fB, uB0, uB1, XA, XB);
-  }
-}
 // outside the feature's domain: move to the bounding feature (true)
-DRC_HD __forceinline__ bool rw_domain(const Shape& s, Feat* f, double u0, double u1) {
-  if (f->kind == kFtSide && fabs(u1) > s.p1) {
+DRC_HD inline bool rw_domain(const Shape& s, Feat* f, const FParam& u) {
+  if (f->kind == kFtSide && fabs(u.c) > s.p1) {
     f->kind = kFtRim;
-    f->s = u1 > 0 ? 1 : -1;
+    f->s = u.c > 0 ? 1 : -1;
     return true;
   }
-  if (f->kind == kFtCap && u0 * u0 + u1 * u1 > s.p0 * s.p0) {
+  if (f->kind == kFtCap && u.a * u.a + u.b * u.b > s.p0 * s.p0) {
     f->kind = kFtRim;
     return true;
   }
   if (f->kind == kFtBox) {
     int k = 0;
-#pragma unroll
     for (int i = 0; i < 3; ++i) {
       if (f->fix(i)) continue;
-      const double hi = i == 0 ? s.p0 : (i == 1 ? s.p1 : s.p2), ui = k == 0 ? u0 : u1;
-      if (fabs(ui) > hi) {
+      const double ui = k == 0 ? u.a : u.b;
+      if (fabs(ui) > shp(s, i)) {
         f->set_fix(i, ui > 0 ? 1 : -1);
         return true;
       }
@@ -1324,11 +1313,10 @@ DRC_HD __forceinline__ bool rw_domain(const Shape& s, Feat* f, double u0, double
 }
 // the outward normal nrm in the normal cone of f at u: -1 impossible, 1
 // feature moves to a neighbour, 0 holds
-DRC_HD __forceinline__ int rw_cone(const Shape& s, Feat* f, double u0, V3 nrm) {
+DRC_HD inline int rw_cone(const Shape& s, Feat* f, const FParam& u, V3 nrm) {
   const V3 ax = v3(s.T[2], s.T[5], s.T[8]);
   if (f->kind == kFtBox) {
     const int nfix = (f->fx != 0) + (f->fy != 0) + (f->fz != 0);
-#pragma unroll
     for (int i = 0; i < 3; ++i) {
       const int fi = f->fix(i);
       if (!fi) continue;
@@ -1342,7 +1330,7 @@ DRC_HD __forceinline__ int rw_cone(const Shape& s, Feat* f, double u0, V3 nrm) {
     return 0;
   }
   if (f->kind == kFtCap) return f->s * dot(nrm, ax) > 0 ? 0 : -1;
-  const V3 rad = rot(s.T, v3(cos(u0), sin(u0), 0));
+  const V3 rad = rot(s.T, v3(u.a, u.b, 0));
   const double a = dot(nrm, rad), b = f->s * dot(nrm, ax);
   if (f->kind == kFtSide) return a > 0 ? 0 : -1;
   if (a < -kRwCone) {
@@ -1358,26 +1346,25 @@ DRC_HD __forceinline__ int rw_cone(const Shape& s, Feat* f, double u0, V3 nrm) {
 // sharpens (d, pA, pB) in place; false: the estimates stay
 DRC_HD inline __noinline__ bool refine_witness(const Shape A, const Shape B, double* d, V3* pA, V3* pB) {
   Feat fA, fB;
-  double uA0 = 0, uA1 = 0, uB0 = 0, uB1 = 0;
   const V3 cA = v3(A.T[9], A.T[10], A.T[11]), cB = v3(B.T[9], B.T[10], B.T[11]);
   const V3 xA = rotT(A.T, *pA - cA), xB = rotT(B.T, *pB - cB);
   rw_classify(A, xA, &fA);
   rw_classify(B, xB, &fB);
-  rw_params(fA, xA, &uA0, &uA1);
-  rw_params(fB, xB, &uB0, &uB1);
+  FParam uA = rw_params(fA, xA), uB = rw_params(fB, xB);
   const double sgn = *d < 0 ? -1.0 : 1.0;
+#pragma unroll 1
   for (int round = 0; round < 4; ++round) {
     V3 XA, XB;
-    if (!rw_newton(A, fA, &uA0, &uA1, B, fB, &uB0, &uB1, &XA, &XB)) return false;
-    int ca = rw_domain(A, &fA, uA0, uA1), cb = rw_domain(B, &fB, uB0, uB1);
+    if (!rw_newton(A, fA, &uA, B, fB, &uB, &XA, &XB)) return false;
+    int ca = rw_domain(A, &fA, uA), cb = rw_domain(B, &fB, uB);
     if (!ca && !cb) {
       const V3 D = XB - XA;
       const double L = sqrt(dot(D, D));
       if (!(L > 1e-12)) return false;
       const double sd = sgn * L;
       const V3 n = v3(D.x / sd, D.y / sd, D.z / sd), nb = v3(-n.x, -n.y, -n.z);
-      ca = rw_cone(A, &fA, uA0, n);
-      cb = rw_cone(B, &fB, uB0, nb);
+      ca = rw_cone(A, &fA, uA, n);
+      cb = rw_cone(B, &fB, uB, nb);
       if (ca < 0 || cb < 0) return false;
       if (!ca && !cb) {
         if (!(fabs(sd - *d) <= kRwDMove)) return false;
@@ -1387,8 +1374,8 @@ DRC_HD inline __noinline__ bool refine_witness(const Shape A, const Shape B, dou
         return true;
       }
     }
-    rw_params(fA, rotT(A.T, XA - cA), &uA0, &uA1);
-    rw_params(fB, rotT(B.T, XB - cB), &uB0, &uB1);
+    uA = rw_params(fA, rotT(A.T, XA - cA));
+    uB = rw_params(fB, rotT(B.T, XB - cB));
   }
   return false;
 }

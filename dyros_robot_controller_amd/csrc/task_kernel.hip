@@ -860,30 +860,29 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRC_TAS
     wave_argmin(bestd, besti);
     double* dgv = S + kp.kdg;
     double* red = S + kp.oRed;
-    if (myi == besti && myi < M->npairs) {  // the winning lane publishes its witnesses
-      double dref = myd;
-      if (bhow) {  // GJK / EPA estimates sharpened to the exact critical point (D17)
-        const int ga = M->pair_a[myi], gb = M->pair_b[myi];
-        const Shape A{M->gtype[ga], Tg + 12 * ga, M->gparam[ga][0], M->gparam[ga][1], M->gparam[ga][2]};
-        const Shape Bs{M->gtype[gb], Tg + 12 * gb, M->gparam[gb][0], M->gparam[gb][1], M->gparam[gb][2]};
-#ifndef DRC_NO_REFINE
-        refine_witness(A, Bs, &dref, &bpA, &bpB);
+    // The winning pair's GJK / EPA witnesses are refined to the exact critical
+    // point (D17).  The QPIK stage does it after the task data are written,
+    // where little is live across the call (in place, the call's register
+    // saves and frame slowed every instance: measured); QPID's extras read
+    // the witnesses, so QPID refines here.
+    auto refine_winner = [&]() {
+      const int ga = M->pair_a[besti], gb = M->pair_b[besti];
+      const Shape A{M->gtype[ga], Tg + 12 * ga, M->gparam[ga][0], M->gparam[ga][1], M->gparam[ga][2]};
+      const Shape Bs{M->gtype[gb], Tg + 12 * gb, M->gparam[gb][0], M->gparam[gb][1], M->gparam[gb][2]};
+      double dref = S[kp.oSc + SC_DIST];
+      V3 rA = ld3(red), rB = ld3(red + 3);
+#ifdef DRC_NO_REFINE  // diagnostic build: the raw GJK / EPA witnesses
+      if (false && refine_witness(A, Bs, &dref, &rA, &rB)) {
 #else
-        (void)A, (void)Bs;
+      if (refine_witness(A, Bs, &dref, &rA, &rB)) {
 #endif
+        st3(red, rA);
+        st3(red + 3, rB);
+        S[kp.oSc + SC_DIST] = dref;
       }
-      st3(red, bpA);
-      st3(red + 3, bpB);
-      S[kp.oSc + SC_DIST] = dref;
-    }
-    if (l == 0) {
-      if (besti >= M->npairs) S[kp.oSc + SC_DIST] = bestd;
-      S[kp.oSc + SC_PAIR] = besti;
-    }
-    wsync();
-    bestd = S[kp.oSc + SC_DIST];
-    PH(6);
-    if (l < nv) {  // grad d = n^T (J_B(pB) - J_A(pA)), sign flipped when penetrating
+    };
+    // grad d = n^T (J_B(pB) - J_A(pA)) for joint l + 1, sign flipped when penetrating
+    auto dist_grad = [&](double dd) {
       double g = 0;
       if (besti < M->npairs) {
         const int jA = M->gparent[M->pair_a[besti]], jB = M->gparent[M->pair_b[besti]];
@@ -896,10 +895,31 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRC_TAS
         if (jA > 0 && (M->anc[jA] & (1u << l))) cA = rev ? cross(z, pA - pj) : z;
         if (jB > 0 && (M->anc[jB] & (1u << l))) cB = rev ? cross(z, pB - pj) : z;
         g = dot(n, cB - cA);
-        if (bestd < 0) g = -g;
+        if (dd < 0) g = -g;
       }
-      dgv[l] = g;
+      return g;
+    };
+    if (myi == besti && myi < M->npairs) {  // the winning lane publishes its witnesses
+      st3(red, bpA);
+      st3(red + 3, bpB);
+      S[kp.oSc + SC_DIST] = myd;
+      S[kp.oSc + SC_HOW] = bhow;
     }
+    if (l == 0) {
+      if (besti >= M->npairs) {
+        S[kp.oSc + SC_DIST] = bestd;
+        S[kp.oSc + SC_HOW] = 0;
+      }
+      S[kp.oSc + SC_PAIR] = besti;
+    }
+    wsync();
+    if constexpr (PROBLEM == 1) {
+      if (l == 0 && S[kp.oSc + SC_HOW] != 0) refine_winner();
+      wsync();
+    }
+    bestd = S[kp.oSc + SC_DIST];
+    PH(6);
+    if (l < nv) dgv[l] = dist_grad(bestd);
     wsync();
     if constexpr (PROBLEM == 1) qpid_task_extras(M, kp, S, bestd, besti, io.st_gdv != nullptr);
     PH(7);
@@ -960,6 +980,23 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRC_TAS
       }
     }
     wsync();
+    if constexpr (PROBLEM == 0) {  // late refinement of the winner (D17): patch d and grad d
+      if (S[kp.oSc + SC_HOW] != 0) {
+        if (l == 0) refine_winner();
+        wsync();
+        const double dd = S[kp.oSc + SC_DIST];
+        const double g = l < nv ? dist_grad(dd) : 0.0;
+        if (io.rec) {
+          double* rec = io.rec + b * io.rec_stride;
+          if (l == 0) rec[kp.rDist] = dd;
+          if (l < nv) rec[kp.rDist + 1 + l] = g;
+        } else if (io.st_dist) {
+          if (l == 0) io.st_dist[gb] = dd;
+          if (l < nv) io.st_dist[(int64_t)(1 + l) * LD + gb] = g;
+        }
+        wsync();
+      }
+    }
   }
   PH_FLUSH(0);
 }
