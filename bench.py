@@ -381,23 +381,29 @@ def extras(torch, args, rd, mod, robot, link, q, qd, xt, xdt, dq, dqd, dxt, dxdt
     # wave-per-instance design at WAVE_SLOTS / latency solves/s
     import ctypes as C
     from dyros_robot_controller_amd import _capi
-    one = [t[:, :1].contiguous() for t in (dq, dqd, dxt, dxdt)]
-    it1 = torch.zeros(1, dtype=torch.int32, device=dq.device)
-    timed_steps(torch, lambda: ctrl.QPIK_step_batch(*one, link, iters=it1), 1, 10)
+    # mean over the first 32 instances, each alone on the GPU (B = 1 calls)
     lib, h = _capi.lib(), rd.model.handle
+    it1 = torch.zeros(1, dtype=torch.int32, device=dq.device)
+    ones = [[t[:, k:k + 1].contiguous() for t in (dq, dqd, dxt, dxdt)] for k in range(32)]
+    for one in ones:
+        ctrl.QPIK_step_batch(*one, link, iters=it1)
+    torch.cuda.synchronize()
     _capi.check(lib.drc_debug_kernel_timing(h, 1))
-    timed_steps(torch, lambda: ctrl.QPIK_step_batch(*one, link, iters=it1), 100, 0)
+    for one in ones:
+        for _ in range(3):
+            ctrl.QPIK_step_batch(*one, link, iters=it1)
+    torch.cuda.synchronize()
     tw, tk, tq, nc = C.c_double(), C.c_double(), C.c_double(), C.c_int()
     _capi.check(lib.drc_debug_kernel_times(h, C.byref(tw), C.byref(tk), C.byref(tq), C.byref(nc)))
     _capi.check(lib.drc_debug_kernel_timing(h, 0))
-    lat = (tk.value + tq.value) / max(nc.value, 1) * 1e-3          # task + QP kernel of one instance, seconds
+    lat = (tk.value + tq.value) / max(nc.value, 1) * 1e-3          # task + QP kernel(s) of one instance, seconds
     roof = WAVE_SLOTS / lat
     line["roofline"]["latency_roof"] = {
         "instance_latency_us": 1e6 * lat, "call_us": 1e3 * tw.value / max(nc.value, 1), "wave_slots": WAVE_SLOTS,
         "solves_per_s": roof, "frac": line["value"] / roof,
-        "note": "one instance alone on the GPU: task + QP kernel durations (HIP events, B = 1); a wave-per-instance "
-                "design with WAVE_SLOTS instances in flight (two 256-VGPR waves per SIMD) cannot beat "
-                "WAVE_SLOTS / latency"}
+        "note": "mean over the batch's first 32 instances, each alone on the GPU (B = 1 calls, kernel durations by "
+                "HIP events): a wave-per-instance design with WAVE_SLOTS instances in flight (two 256-VGPR waves per "
+                "SIMD) cannot beat WAVE_SLOTS / latency if instances ran at their isolated latency"}
 
 
 if __name__ == "__main__":

@@ -10,14 +10,14 @@ OUT=${DRC_OUT:-dyros_robot_controller_amd/libdrc_amd.so}
 mkdir -p "$OBJ"
 FLAGS="--offload-arch=gfx950 -O3 -fPIC -std=c++17 -Wall -Wno-unused-function $DRC_EXTRA_FLAGS"
 pids=()
-for src in task_kernel.hip qp_kernel.hip qpid_kernel.hip dynamics.hip api.cpp model.cpp; do
+for src in task_kernel.hip qp_kernel.hip fused_kernel.hip qpid_kernel.hip dynamics.hip api.cpp model.cpp; do
   $HIPCC $FLAGS -c $CSRC/$src -o "$OBJ/${src%.*}.o" &
   pids+=($!)
 done
 rc=0
 for p in "${pids[@]}"; do wait "$p" || rc=1; done
 [ $rc -eq 0 ] || { echo "build.sh: a HIP translation unit failed to compile" >&2; exit 1; }
-$HIPCC --offload-arch=gfx950 -shared -fPIC "$OBJ"/task_kernel.o "$OBJ"/qp_kernel.o "$OBJ"/qpid_kernel.o \
+$HIPCC --offload-arch=gfx950 -shared -fPIC "$OBJ"/task_kernel.o "$OBJ"/qp_kernel.o "$OBJ"/fused_kernel.o "$OBJ"/qpid_kernel.o \
   "$OBJ"/dynamics.o "$OBJ"/api.o "$OBJ"/model.o -o "$OUT" -Wl,-rpath,/opt/rocm/lib
 [ -n "$DRC_VARIANT" ] && exit 0
 make -s -C oracle

@@ -38,7 +38,7 @@ EXPORTED_SYMBOLS = (
     "drc_model_info", "drc_model_limits", "drc_model_find_frame", "drc_model_mobile_fk_jacobian",
     "drc_mobile_fk_jacobian", "drc_mobile_ik_jacobian",
     "drc_default_qpik_params", "drc_qpik_batch", "drc_qpik_stages_batch", "drc_debug_kernel_timing",
-    "drc_debug_kernel_times", "drc_set_concurrency", "drc_model_release_stream", "drc_debug_lane_stage", "drc_qpik_host", "drc_qpik_stages_host",
+    "drc_debug_kernel_times", "drc_set_concurrency", "drc_set_fusion", "drc_model_release_stream", "drc_debug_lane_stage", "drc_qpik_host", "drc_qpik_stages_host",
     "drc_dynamics_batch", "drc_dynamics_host", "drc_joint_torque_step_batch", "drc_joint_torque_step_host",
     "drc_default_qpid_params", "drc_qpid_batch", "drc_qpid_stages_batch", "drc_qpid_host",
     "drc_qpid_stages_host", "drc_clik_batch", "drc_osf_batch", "drc_closed_form_host",
@@ -133,6 +133,7 @@ def _load():
     lib.drc_debug_lane_stage.argtypes = [vp, C.c_int]
     lib.drc_set_concurrency.argtypes = [vp, C.c_int]
     lib.drc_model_release_stream.argtypes = [vp, vp]
+    lib.drc_set_fusion.argtypes = [vp, C.c_int]
     lib.drc_qpik_host.argtypes = [vp, C.POINTER(QPIKParams), C.c_int64, dp, dp, dp, dp, dp, dp, dp, ip, ip]
     lib.drc_qpik_stages_host.argtypes = [vp, C.POINTER(QPIKParams), C.c_int64, dp, dp, dp, dp, dp, dp,
                                          dp, dp, dp, dp, ip, dp]

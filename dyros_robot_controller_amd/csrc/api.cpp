@@ -84,6 +84,9 @@ struct drc_model_impl {
   // 1 / 2 / 3 / 4 chunks = 7.3 / 8.5 / 8.9 / 7.3 M solves/s; 3 lanes plus the
   // caller's stream fit the 4 hardware queues a process gets by default)
   int chunks = 3;
+  // fused task + QP kernel for the compiled QPIK shapes and small batches
+  // (fused_kernel.hip; drc_set_fusion): one launch per call, the record in LDS
+  int fused = 1;
   // host-buffer entry points: device staging + an internal stream
   std::mutex host_mu;
   void* stage = nullptr;
@@ -630,8 +633,15 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
   // kernel waits for the whole task kernel, with several they overlap
   // (Husky-FR3's 16 Ki batch)
   static const int64_t min_sub = env_int("DRC_MIN_SUBBATCH", 4096, 1);
+  // fused for small batches only: it wins where a call is one or two
+  // instances per wave (B <= 8 Ki: FR3 +10-20 %, XLS-FR3 +20-30 %) and loses
+  // to the overlapped sub-batch pipeline above (FR3 B = 65 536: 14.3 M vs
+  // 17.6 M solves/s; tools/fusion_sweep.py)
+  static const int64_t fuse_max = env_int("DRC_FUSE_MAX", 8192, 0);
+  const bool fuse =
+      m->fused && !stages && !lane && B <= fuse_max && kQpGroup == 64 && qp_compiled(kq.nx, kq.ng, kq.np);
   int S = 1;
-  if (!stages)
+  if (!stages && !fuse)
     for (int c = m->chunks; c > 1; --c)
       if (B / c >= min_sub) {
         S = c;
@@ -714,7 +724,18 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
       HIP_TRY(static_cast<hipError_t>(launch_qp_kernel(static_cast<unsigned>(gq), lds_q, cs, m->d_model, kq_c, io)));
       return DRC_OK;
     };
-    if (!lane) {  // wave-per-instance task kernel on every instance, then the QP
+    if (fuse) {  // one fused task + QP kernel, the record in LDS
+      static const int64_t cap_f = env_int("DRC_GRID_FUSED", 2048, 8) & ~int64_t(7);
+      const int64_t gf = Bc < cap_f ? Bc : cap_f;
+      const int rec_doubles = (kt_c.rLen + 1) & ~1;
+      const size_t lds_f =
+          static_cast<size_t>((kt_c.lds_doubles > kq_c.lds_doubles ? kt_c.lds_doubles : kq_c.lds_doubles) + rec_doubles) *
+          sizeof(double);
+      io.queue = qc;
+      HIP_TRY(static_cast<hipError_t>(
+          launch_fused_kernel(static_cast<unsigned>(gf), lds_f, cs, m->d_model, kt_c, kq_c, io)));
+      if (timed) HIP_TRY(hipEventRecord(e1, cs));
+    } else if (!lane) {  // wave-per-instance task kernel on every instance, then the QP
       if (int r = launch_task(cs)) return r;
       if (timed) HIP_TRY(hipEventRecord(e1, cs));
       if (!stages)
@@ -953,6 +974,13 @@ int drc_debug_kernel_times(drc_model* m, double* wall_ms, double* task_ms, doubl
   *wall_ms = tw;
   *task_ms = t0;
   *qp_ms = t1;
+  return DRC_OK;
+}
+
+int drc_set_fusion(drc_model* m, int enable) {
+  if (!m) return drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "null model");
+  std::lock_guard<std::mutex> g(m->launch_mu);
+  m->fused = enable != 0;
   return DRC_OK;
 }
 

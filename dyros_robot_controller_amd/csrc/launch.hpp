@@ -20,12 +20,17 @@ bool qp_compiled(int nx, int ng, int np);
 // qp_kernel for kp's shape; lds = one lane group's plan
 int launch_qp_kernel(unsigned grid, size_t lds, hipStream_t st, const DevModel* m, const KParams& kp, const IO& io);
 int launch_qpid_kernel(unsigned grid, size_t lds, hipStream_t st, const DevModel* m, const KParams& kp, const IO& io);
+// fused task + QP kernel (compiled QPIK shapes; hipErrorInvalidValue otherwise);
+// lds = both plans' maximum plus the record slot
+int launch_fused_kernel(unsigned grid, size_t lds, hipStream_t st, const DevModel* m, const KParams& kt,
+                        const KParams& kq, const IO& io);
 
 #ifdef DRC_PHASE_TIMING
 // diagnostic build: add each unit's phase slots to out[64]
 int phase_cycles_task(unsigned long long* out, int reset);
 int phase_cycles_qp(unsigned long long* out, int reset);
 int phase_cycles_qpid(unsigned long long* out, int reset);
+int phase_cycles_fused(unsigned long long* out, int reset);
 #endif
 
 }  // namespace drc_amd

@@ -32,10 +32,8 @@ qp_kernel(const DevModel* __restrict__ M0, const KParams kp, const IO io) {
   // QD::gs = 32: two instances per wave, each lane group on its own LDS
   // plan (the launch allocates one per group) and its own instance sequence
   using GL = Grp<QD::gs>;
-  const int l = GL::lane();
   double* const Sg = S + (GL::upper() ? kp.lds_doubles : 0);
   const int64_t B = io.B;
-  PH_DECL
   // hard_mode 1: the lane stage's hard list (grid stride); 2: every instance
   // except the flagged ones (their records are still being written)
   const bool hl = io.hard_mode == 1;
@@ -44,33 +42,8 @@ qp_kernel(const DevModel* __restrict__ M0, const KParams kp, const IO io) {
     const int64_t b = hl ? int64_t(io.hard_list[j]) : seq.at(j);
     if (b >= B) continue;
     if (io.hard_mode == 2 && io.hard_flag[b]) continue;
-    const int64_t gb = io.b0 + b, LD = io.ld;  // position in the caller's [field][B] arrays
-    const DevModel* M = M0;
-    asm volatile("" : "+s"(M));
-    double* S = Sg;
-    qp_assemble<QD>(M, kp, S, io, b);
-    PH(0);
-    const bool lp_inf = M->kind == 1 && kp.s.exact && moma_lp_infeasible<QD>(M, kp, S);
-    int status, iters = 0;
-    if constexpr (QD::reg) status = qp_scale_regs<QD>(kpl, S);
-    else status = qp_scale<QD>(kp, S);
-    PH(1);
-    if (status != DRC_STATUS_NONFINITE) {
-      if (lp_inf) status = DRC_STATUS_PRIMAL_INFEASIBLE;
-      else status = qp_admm<QD>(kp, kpl, S, &iters);
-    }
-    PH(3);
-    // ---------------- outputs (zero on failure, QP_IK.cpp:56-61) ------------
-    const double *D = S + kp.oD, *x = S + kp.oX;
-    if (l < kp.na) io.out[(int64_t)l * LD + gb] = status == DRC_STATUS_SOLVED ? D[l] * x[l] : 0.0;
-    if (l == 0) {
-      io.status[gb] = status;
-      if (io.iters) io.iters[gb] = iters;
-    }
-    wsync();
-    PH(5);
+    qp_instance<QD>(M0, kp, kpl, io, Sg, b);
   }
-  PH_FLUSH(16);
 }
 
 

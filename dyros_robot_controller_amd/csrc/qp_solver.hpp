@@ -1873,4 +1873,41 @@ __device__ __forceinline__ int qp_admm(const KParams& kp, const KParams& kpl, do
   return status;
 }
 
+// One instance b of the QP stage on this lane group (S: its LDS plan kp; kpl:
+// an LDS copy of kp for the out-of-line ADMM blocks): assembly from the task
+// record, Ruiz scaling, ADMM + certified polish, outputs (zero on failure,
+// QP_IK.cpp:56-61).  Used by qp_kernel and the fused task + QP kernel.
+template <class QD>
+__device__ __forceinline__ void qp_instance(const DevModel* __restrict__ M0, const KParams& kp, const KParams& kpl,
+                                            const IO& io, double* S, int64_t b) {
+  using GL = Grp<QD::gs>;
+  const int l = GL::lane();
+  PH_DECL
+  const int64_t gb = io.b0 + b, LD = io.ld;  // position in the caller's [field][B] arrays
+  const DevModel* M = M0;
+  asm volatile("" : "+s"(M));
+  qp_assemble<QD>(M, kp, S, io, b);
+  PH(0);
+  const bool lp_inf = M->kind == 1 && kp.s.exact && moma_lp_infeasible<QD>(M, kp, S);
+  int status, iters = 0;
+  if constexpr (QD::reg) status = qp_scale_regs<QD>(kpl, S);
+  else status = qp_scale<QD>(kp, S);
+  PH(1);
+  if (status != DRC_STATUS_NONFINITE) {
+    if (lp_inf) status = DRC_STATUS_PRIMAL_INFEASIBLE;
+    else status = qp_admm<QD>(kp, kpl, S, &iters);
+  }
+  PH(3);
+  // ---------------- outputs (zero on failure, QP_IK.cpp:56-61) ------------
+  const double *D = S + kp.oD, *x = S + kp.oX;
+  if (l < kp.na) io.out[(int64_t)l * LD + gb] = status == DRC_STATUS_SOLVED ? D[l] * x[l] : 0.0;
+  if (l == 0) {
+    io.status[gb] = status;
+    if (io.iters) io.iters[gb] = iters;
+  }
+  wsync();
+  PH(5);
+  PH_FLUSH(16);
+}
+
 }  // namespace drc_amd

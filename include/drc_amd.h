@@ -230,6 +230,15 @@ int drc_debug_kernel_times(drc_model* model, double* wall_ms, double* task_ms, d
  * Results do not depend on it. */
 int drc_set_concurrency(drc_model* model, int chunks);
 
+/* Fused task + QP kernel for the QP shapes the library compiles (the bundled
+ * FR3, UR5e, Husky-FR3, XLS-FR3 layouts) and batches of up to 8 192
+ * instances: 1 (default) runs such a drc_qpik_batch call as one kernel whose
+ * waves take an instance through the task stage and the QP before the next,
+ * the task record kept in LDS; 0 always runs the task-kernel -> QP-kernel
+ * pipeline (drc_set_concurrency sub-batches), as larger batches do.  Results
+ * agree to rounding (the compiler forms FMAs per kernel). */
+int drc_set_fusion(drc_model* model, int enable);
+
 /* Frees the per-stream scratch (task-record pool, work-queue counters) the
  * model keeps for `stream`, after the stream's queued work has finished; call
  * it before destroying a stream the model was used on.  A model keeps at most

@@ -15,10 +15,10 @@ timeout -k 10 420 python3 bench.py $ARGS > $OUT/bench.json 2> $OUT/bench.err
 cat $OUT/bench.json
 cd /tmp
 export TMPDIR=/tmp
-timeout -k 10 420 rocprofv3 --kernel-trace --stats -f csv -d $OUT/kt -o kt -- python3 $ROOT/bench.py --steps 5 --warmup 2 --no-cpu-baseline $ARGS > $OUT/kt.log 2>&1
+timeout -k 10 420 rocprofv3 --kernel-trace --stats -f csv -d $OUT/kt -o kt -- python3 $ROOT/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-extras $ARGS > $OUT/kt.log 2>&1
 echo "kernel trace done"
-timeout -k 10 420 rocprofv3 --pmc FETCH_SIZE -f csv -d $OUT/fetch -o fetch -- python3 $ROOT/bench.py --steps 3 --warmup 1 --no-cpu-baseline $ARGS > $OUT/fetch.log 2>&1
+timeout -k 10 420 rocprofv3 --pmc FETCH_SIZE -f csv -d $OUT/fetch -o fetch -- python3 $ROOT/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-extras $ARGS > $OUT/fetch.log 2>&1
 echo "fetch pass done"
-timeout -k 10 420 rocprofv3 --pmc WRITE_SIZE -f csv -d $OUT/write -o write -- python3 $ROOT/bench.py --steps 3 --warmup 1 --no-cpu-baseline $ARGS > $OUT/write.log 2>&1
+timeout -k 10 420 rocprofv3 --pmc WRITE_SIZE -f csv -d $OUT/write -o write -- python3 $ROOT/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-extras $ARGS > $OUT/write.log 2>&1
 echo "write pass done"
 bash $ROOT/tools/valu_pass.sh $TAG $ARGS

@@ -14,6 +14,6 @@ B="SQ_WAVES SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VALU_INT64 SQ_INS
 i=0
 for G in "$A" "$B"; do
   i=$((i+1))
-  timeout -s KILL 150 rocprofv3 --pmc $G -f csv -d $OUT/p$i -o p$i -- python3 $ROOT/bench.py --steps 2 --warmup 1 --no-cpu-baseline "$@" > $OUT/p$i.log 2>&1
+  timeout -s KILL 150 rocprofv3 --pmc $G -f csv -d $OUT/p$i -o p$i -- python3 $ROOT/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-extras "$@" > $OUT/p$i.log 2>&1
   echo "valu pass $i done"
 done
