@@ -54,10 +54,32 @@ def algorithmic_bytes(dof, actuated):
     return (2 * dof + 12 + 6) * 8 + actuated * 8 + 4
 
 
-def flops_per_solve(iters):
-    """SURVEY §8(d) static estimate for FR3-sized problems (52k setup +
-    1.3k per ADMM iteration); the counter-based figure is roofline.fp64_valu."""
-    return 52e3 + 1.3e3 * iters
+def algorithmic_flops(robot, solver, q, qd, xt, xdt, n=256):
+    """FP64 operations per solve of the algorithm itself, counted, not
+    estimated: the oracle's C restatement built with every double replaced by
+    a counting type (oracle/flopcount.hpp, count_build.cpp) runs a strided
+    sample of the same batch with the same settings and the kernels' pruned
+    narrow phase (oracle min_distance_pruned -- same argmin as all pairs).
+    + - * / sqrt count 1 each; sin / cos / atan2 / acos are reported apart.
+    The QP linear algebra is the dense reduced-KKT restatement (what the QP
+    kernel runs), so structural zeros of A are counted."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    _, om, spec = O.load(robot)
+    par = O.default_params(spec["kind"], exact=(solver == "exact"))
+    idx = np.unique(np.linspace(0, q.shape[1] - 1, n).astype(np.int64))
+    pick = lambda a: np.ascontiguousarray(a[:, idx])
+    with O.counting_build():
+        O.set_pruned_narrow_phase(True)
+        try:
+            O.flop_counts(reset=True)
+            O.qpik_batch(om, par, pick(q), pick(qd), pick(xt), pick(xdt), nthreads=1)
+            fl, tr = O.flop_counts(reset=True)
+        finally:
+            O.set_pruned_narrow_phase(False)
+    return {"flops_per_solve": fl / len(idx), "transcendentals_per_solve": tr / len(idx),
+            "sample": "%d instances, every %d-th of the batch" % (len(idx), max(1, q.shape[1] // n)),
+            "source": "oracle/count_build.cpp (counting build of oracle/drc_oracle.c, pruned narrow phase)"}
 
 
 def make_inputs(rd, robot, B, seed, offset, dev):
@@ -307,7 +329,8 @@ def main():
         per_launch_bytes = bps * B
         achieved = per_launch_bytes / (kernel_ms * 1e-3) / 1e9
         traffic = load_profile("pmc_traffic_%s.json" % robot, robot, B) or load_profile("pmc_traffic.json", robot, B)
-        fl = flops_per_solve(it_mean) * B / (kernel_ms * 1e-3) / 1e12
+        alg = algorithmic_flops(robot, args.solver, q, qd, xt, xdt)
+        fl = alg["flops_per_solve"] * B / (kernel_ms * 1e-3) / 1e12
         roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS, "traffic": traffic.get("hbm_bytes_per_step") if traffic else None,
                 "kernel": "drc_qpik_batch call (task_kernel + qp_kernel per sub-batch, %d concurrent sub-batches)"
@@ -315,9 +338,8 @@ def main():
                 "bytes_per_solve": bps, "bytes_per_launch": per_launch_bytes,
                 "kernel_ms": kernel_ms, "task_kernel_ms_sum": task_ms, "qp_kernel_ms_sum": qp_ms,
                 "step_event_ms": step_event_ms,
-                "fp64_valu_estimate": {"achieved_tflops": fl, "peak_tflops": FP64_VECTOR_PEAK_TFS,
-                                       "frac": fl / FP64_VECTOR_PEAK_TFS,
-                                       "flops_per_solve": flops_per_solve(it_mean)}}
+                "fp64_algorithmic": dict(alg, achieved_tflops=fl, peak_tflops=FP64_VECTOR_PEAK_TFS,
+                                         frac=fl / FP64_VECTOR_PEAK_TFS)}
         valu = load_profile("valu_counters_%s.json" % robot, robot, B)
         if valu:   # counter-based FP64 work per call (tools/valu_summary.py over rocprofv3 --pmc passes)
             f = valu["fp64_flops_per_step"]

@@ -1,0 +1,11 @@
+// ORACLE / TEST INFRASTRUCTURE ONLY: the FLOP-counting build of drc_oracle.c
+// (see flopcount.hpp).  Same C-ABI as libdrc_oracle.so plus the counters.
+#include "flopcount.hpp"
+std::atomic<unsigned long long> g_flops{0}, g_trans{0};
+extern "C" {
+#include "drc_oracle.c"
+void oracle_flop_counts(unsigned long long* flops, unsigned long long* trans, int reset) {
+  *flops = reset ? g_flops.exchange(0) : g_flops.load();
+  *trans = reset ? g_trans.exchange(0) : g_trans.load();
+}
+}

@@ -1033,8 +1033,171 @@ static void min_distance(const OracleModel* m, const Kin* k, double* dist, doubl
     double wA[3], wB[3];
     min_distance_w(m, k, dist, grad, pair_out, wA, wB);
 }
+/* ---- the kernel's pruned narrow phase (FLOP count; same argmin) ---------- */
+/* Segment / segment closest points (the kernel's seg_seg_dist). */
+static double seg_seg(const double* p1, const double* q1, const double* p2, const double* q2, double* c1, double* c2) {
+    double d1[3], d2[3], r[3];
+    sub3(q1, p1, d1); sub3(q2, p2, d2); sub3(p1, p2, r);
+    const double a = dot3(d1, d1), e = dot3(d2, d2), f = dot3(d2, r);
+    double s, t;
+    if (a <= 1e-30 && e <= 1e-30) { s = 0; t = 0; }
+    else if (a <= 1e-30) { s = 0; t = fmin(fmax(f / e, 0.0), 1.0); }
+    else {
+        const double c = dot3(d1, r);
+        if (e <= 1e-30) { t = 0; s = fmin(fmax(-c / a, 0.0), 1.0); }
+        else {
+            const double b = dot3(d1, d2), den = a * e - b * b;
+            s = den > 0 ? fmin(fmax((b * f - c * e) / den, 0.0), 1.0) : 0.0;
+            t = (b * s + f) / e;
+            if (t < 0) { t = 0; s = fmin(fmax(-c / a, 0.0), 1.0); }
+            else if (t > 1) { t = 1; s = fmin(fmax((b - c) / a, 0.0), 1.0); }
+        }
+    }
+    double dd[3];
+    for (int i = 0; i < 3; ++i) { c1[i] = p1[i] + s * d1[i]; c2[i] = p2[i] + t * d2[i]; dd[i] = c1[i] - c2[i]; }
+    return norm3(dd);
+}
+/* Swept-core lower bound of the signed distance raised to the separating-axis
+ * value along the cores' closest-point direction (kernel: pair_lower_bound). */
+static double pair_lower_bound(const Shape* A, const Shape* B) {
+    double a0[3], a1[3], b0[3], b1[3], c1[3], c2[3];
+    const Shape* S2[2] = {A, B};
+    double* ends[2][2] = {{a0, a1}, {b0, b1}};
+    double rad[2];
+    for (int k = 0; k < 2; ++k) {
+        const Shape* s = S2[k];
+        for (int i = 0; i < 3; ++i) { ends[k][0][i] = s->T[9 + i]; ends[k][1][i] = s->T[9 + i]; }
+        if (s->type == 1) {
+            const double ax[3] = {s->T[2], s->T[5], s->T[8]};
+            for (int i = 0; i < 3; ++i) { ends[k][0][i] -= s->prm[1] * ax[i]; ends[k][1][i] += s->prm[1] * ax[i]; }
+            rad[k] = s->prm[0];
+        } else if (s->type == 2) {
+            rad[k] = sqrt(s->prm[0] * s->prm[0] + s->prm[1] * s->prm[1] + s->prm[2] * s->prm[2]);
+        } else {
+            rad[k] = s->prm[0];
+        }
+    }
+    const double L = seg_seg(a0, a1, b0, b1, c1, c2), pd = L - rad[0] - rad[1];
+    if (!(L > 1e-12)) return pd;
+    double n[3], mn[3], sa[3], sb[3];
+    for (int i = 0; i < 3; ++i) { n[i] = (c2[i] - c1[i]) / L; mn[i] = -n[i]; }
+    support(A, n, sa);
+    support(B, mn, sb);
+    return fmax(pd, dot3(n, sb) - dot3(n, sa));
+}
+/* GJK that stops once its lower bound v.w/|v| exceeds `cut` (the kernel's
+ * early exit): returns 0 separated, 1 penetrating, 2 pruned. */
+static int gjk_cut(const Shape* A, const Shape* B, SV* S, int* ns, double* lam, double* v, double cut) {
+    sub3(A->T + 9, B->T + 9, v);
+    if (dot3(v, v) < 1e-24) { v[0] = 1; v[1] = 0; v[2] = 0; }
+    int n = 0;
+    for (int it = 0; it < 128; ++it) {
+        double nv[3] = {-v[0], -v[1], -v[2]};
+        SV w;
+        sup_md(A, B, nv, &w);
+        const double vv = dot3(v, v), vw = dot3(v, w.w), sv = sqrt(vv);
+        if (vw > cut * sv) { *ns = n; return 2; }
+        if (n > 0 && vv - vw <= GJK_TOL * sv) break;
+        int dup = 0;
+        for (int i = 0; i < n; ++i) if (S[i].w[0] == w.w[0] && S[i].w[1] == w.w[1] && S[i].w[2] == w.w[2]) dup = 1;
+        if (dup) { if (vw <= 0) { *ns = n; return 1; } break; }
+        S[n++] = w;
+        n = closest_simplex(S, n, v, lam);
+        if (n == 4 || dot3(v, v) < 1e-24) { *ns = n; return 1; }
+    }
+    *ns = n;
+    return 0;
+}
+/* getMinDistance's argmin by the kernel's algorithm (task_stage.hpp): closed
+ * forms for every pair they cover, the lower bound for the rest, GJK (with
+ * the early exit) only where the bound can still reach the closed-form
+ * minimum, EPA best-first in increasing bound order while a bound can still
+ * undercut the running minimum.  Pruning only drops pairs that provably cannot
+ * be the argmin, so the result is min_distance_w's (tests/test_oracle_distance.py). */
+static void min_distance_pruned(const OracleModel* m, const Kin* k, double* dist, double* grad, int* pair_out,
+                                double* wA, double* wB) {
+    Shape sh[ORC_MAXG];
+    for (int g = 0; g < m->ngeom; ++g) make_shape(m, k, g, &sh[g]);
+    static __thread double pd[ORC_MAXP];
+    static __thread int st[ORC_MAXP];  /* 0 done, 1 candidate, 2 penetrating */
+    double best = 1.7976931348623157e308, bpA[3] = {0}, bpB[3] = {0}, ub = 1e300;
+    int bi = -1, bhow = 0;
+    for (int p = 0; p < m->npairs; ++p) {
+        const Shape *A = &sh[m->pair_a[p]], *B = &sh[m->pair_b[p]];
+        double pA[3], pB[3], d;
+        int closed = 0;
+        if (A->type == 0 || B->type == 0) { int how; d = shape_distance(A, B, pA, pB, &how); closed = 1; }
+        else if (A->type == 1 && B->type == 1 && cyl_cyl_side(A, B, &d, pA, pB)) closed = 1;
+        st[p] = 0;
+        if (closed) {
+            ub = fmin(ub, d);
+            if (d < best || (d == best && p < bi)) { best = d; bi = p; bhow = 0; memcpy(bpA, pA, sizeof(pA)); memcpy(bpB, pB, sizeof(pB)); }
+        } else {
+            pd[p] = pair_lower_bound(A, B);
+            st[p] = 1;
+        }
+    }
+    for (int p = 0; p < m->npairs; ++p) {
+        if (st[p] != 1) continue;
+        st[p] = 0;
+        if (!(pd[p] - 1e-9 <= ub)) continue;
+        SV S[4];
+        int ns;
+        double lam[4], v[3];
+        const int r = gjk_cut(&sh[m->pair_a[p]], &sh[m->pair_b[p]], S, &ns, lam, v, ub + 1e-9);
+        if (r == 2) continue;
+        if (r == 1) { st[p] = 2; continue; }
+        double pA[3] = {0, 0, 0}, pB[3] = {0, 0, 0}, dd[3];
+        for (int c = 0; c < 3; ++c) for (int i = 0; i < ns; ++i) { pA[c] += lam[i] * S[i].a[c]; pB[c] += lam[i] * S[i].b[c]; }
+        sub3(pA, pB, dd);
+        const double d = norm3(dd);
+        if (d < best || (d == best && p < bi)) { best = d; bi = p; bhow = 1; memcpy(bpA, pA, sizeof(pA)); memcpy(bpB, pB, sizeof(pB)); }
+    }
+    for (;;) {  /* EPA best-first */
+        int cp = -1;
+        for (int p = 0; p < m->npairs; ++p)
+            if (st[p] == 2 && (cp < 0 || pd[p] < pd[cp])) cp = p;
+        if (cp < 0 || pd[cp] > best || (pd[cp] == best && cp > bi)) break;
+        st[cp] = 0;
+        const Shape *A = &sh[m->pair_a[cp]], *B = &sh[m->pair_b[cp]];
+        SV S[4];
+        int ns;
+        double lam[4], v[3], pA[3], pB[3];
+        gjk(A, B, S, &ns, lam, v);
+        const double d = epa(A, B, S, ns, pA, pB);
+        if (d < best || (d == best && cp < bi)) { best = d; bi = cp; bhow = 2; memcpy(bpA, pA, sizeof(pA)); memcpy(bpB, pB, sizeof(pB)); }
+    }
+    if (bi >= 0 && bhow) refine_witness(&sh[m->pair_a[bi]], &sh[m->pair_b[bi]], &best, bpA, bpB);
+    *dist = best;
+    *pair_out = bi;
+    memcpy(wA, bpA, sizeof(bpA));
+    memcpy(wB, bpB, sizeof(bpB));
+    const int nv = m->nv;
+    memset(grad, 0, nv * sizeof(double));
+    if (bi < 0) return;
+    int jA = m->gparent[m->pair_a[bi]], jB = m->gparent[m->pair_b[bi]];
+    double n[3];
+    sub3(bpB, bpA, n);
+    const double L = norm3(n);
+    n[0] /= L; n[1] /= L; n[2] /= L;
+    double JA[6 * ORC_MAXJ], JB[6 * ORC_MAXJ];
+    point_jacobian(m, k, jA, bpA, JA);
+    point_jacobian(m, k, jB, bpB, JB);
+    for (int c = 0; c < nv; ++c) {
+        double s2 = 0;
+        for (int i = 0; i < 3; ++i) s2 += n[i] * (JB[i * nv + c] - JA[i * nv + c]);
+        grad[c] = best < 0 ? -s2 : s2;
+    }
+}
+/* 1: min_distance_w (all pairs, the reference's computeDistances loop) is
+ * replaced by the pruned search above in every oracle entry point (tests and
+ * the FLOP count set it; the default is the reference's all-pairs loop) */
+static int g_pruned_narrow_phase = 0;
+void oracle_set_pruned_narrow_phase(int on) { g_pruned_narrow_phase = on; }
+
 static void min_distance_w(const OracleModel* m, const Kin* k, double* dist, double* grad, int* pair_out,
                            double* wA, double* wB) {
+    if (g_pruned_narrow_phase) { min_distance_pruned(m, k, dist, grad, pair_out, wA, wB); return; }
     Shape sh[ORC_MAXG];
     for (int g = 0; g < m->ngeom; ++g) make_shape(m, k, g, &sh[g]);
     double best = 1.7976931348623157e308, bpA[3] = {0}, bpB[3] = {0};

@@ -174,6 +174,10 @@ void oracle_shape_distance(int ta, const double* TA, const double* prmA, int tb,
                            const double* prmB, double* d, double* pA, double* pB);
 /* raw GJK / EPA results without the witness refinement (D17), for tests;
  * how: 0 closed form, 1 GJK, 2 EPA */
+/* 1: getMinDistance's argmin by the kernel's pruned algorithm (closed forms,
+ * lower bounds, GJK early exit, best-first EPA) instead of the reference's
+ * all-pairs loop; same result.  Used by the FLOP count. */
+void oracle_set_pruned_narrow_phase(int on);
 void oracle_pair_distance_raw(const OracleModel* m, const double* q, int pair, double* d, double* pA, double* pB,
                               int* how);
 void oracle_shape_distance_raw(int ta, const double* TA, const double* prmA, int tb, const double* TB,

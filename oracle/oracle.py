@@ -103,24 +103,61 @@ class OracleDiag(C.Structure):
 _lib = None
 
 
+def _load(name, target):
+    so = os.path.join(HERE, name)
+    if not os.path.exists(so):
+        subprocess.check_call(["make", "-s", "-C", HERE, target])
+    L = C.CDLL(so)
+    d = C.POINTER(C.c_double)
+    L.oracle_qpik_one.restype = C.c_int
+    L.oracle_qpik_batch.restype = C.c_int64
+    L.oracle_qpik_batch.argtypes = [C.POINTER(OracleModel), C.POINTER(OracleParams), C.c_int64,
+                                    d, d, d, d, d, d, d, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.c_int]
+    L.oracle_qpik_batch_dist.restype = C.c_int64
+    L.oracle_qpik_batch_dist.argtypes = [C.POINTER(OracleModel), C.POINTER(OracleParams), C.c_int64,
+                                         d, d, d, d, d, d, d, d, d, C.POINTER(C.c_int32),
+                                         C.POINTER(C.c_int32), C.c_int]
+    L.oracle_solve_qp.restype = C.c_int
+    return L
+
+
 def lib():
     global _lib
     if _lib is None:
-        so = os.path.join(HERE, "libdrc_oracle.so")
-        if not os.path.exists(so):
-            subprocess.check_call(["make", "-s", "-C", HERE])
-        _lib = C.CDLL(so)
-        d = C.POINTER(C.c_double)
-        _lib.oracle_qpik_one.restype = C.c_int
-        _lib.oracle_qpik_batch.restype = C.c_int64
-        _lib.oracle_qpik_batch.argtypes = [C.POINTER(OracleModel), C.POINTER(OracleParams), C.c_int64,
-                                           d, d, d, d, d, d, d, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.c_int]
-        _lib.oracle_qpik_batch_dist.restype = C.c_int64
-        _lib.oracle_qpik_batch_dist.argtypes = [C.POINTER(OracleModel), C.POINTER(OracleParams), C.c_int64,
-                                                d, d, d, d, d, d, d, d, d, C.POINTER(C.c_int32),
-                                                C.POINTER(C.c_int32), C.c_int]
-        _lib.oracle_solve_qp.restype = C.c_int
+        _lib = _load("libdrc_oracle.so", "all")
     return _lib
+
+
+class counting_build:
+    """Context manager: inside it every wrapper of this module runs
+    libdrc_oracle_count.so, the build of drc_oracle.c whose double arithmetic
+    is counted (flopcount.hpp); the timing build is restored on exit."""
+
+    def __enter__(self):
+        global _lib
+        self._prev = _lib
+        _lib = _load("libdrc_oracle_count.so", "count")
+        return _lib
+
+    def __exit__(self, *exc):
+        global _lib
+        _lib = self._prev
+        return False
+
+
+def flop_counts(reset=True):
+    """(flops, transcendentals) counted in this process since the last reset
+    (counting build only)."""
+    f, t = C.c_ulonglong(), C.c_ulonglong()
+    lib().oracle_flop_counts(C.byref(f), C.byref(t), C.c_int(1 if reset else 0))
+    return f.value, t.value
+
+
+def set_pruned_narrow_phase(on):
+    """1: the oracle's getMinDistance runs the kernel's pruned search (closed
+    forms, lower bounds, GJK early exit, best-first EPA) instead of every pair.
+    Same argmin; the FLOP count uses it."""
+    lib().oracle_set_pruned_narrow_phase(C.c_int(1 if on else 0))
 
 
 def _se3_to12(T):

@@ -51,3 +51,29 @@ def test_single_gpu_runs_in_process():
 def test_world_size_must_match_gpus():
     p = _run(["--gpus", "2", "--dry-run"], env_extra={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"}, drop=())
     assert p.returncode != 0 and "WORLD_SIZE" in p.stderr
+
+
+def test_algorithmic_flop_count():
+    """bench.py's roofline FLOPs come from the counting build of the oracle
+    (pruned narrow phase): positive, reproducible, and the pruned search does
+    less work than the all-pairs loop on the same sample."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import bench
+    import oracle as O
+    from dyros_robot_controller_amd import workload
+    pm, om, spec = O.load("fr3")
+    q, qd = workload.joint_states(pm.lower, pm.upper, pm.vel, 3, 64)
+    xt = np.stack([O.fk_pose(om, q[:, b])[0] for b in range(64)], 1)
+    xt[9:] += 0.01
+    xdt = np.zeros((6, 64))
+    a = bench.algorithmic_flops("fr3", "exact", q, qd, xt, xdt, n=16)
+    b = bench.algorithmic_flops("fr3", "exact", q, qd, xt, xdt, n=16)
+    assert a == b and a["flops_per_solve"] > 1e4
+    par = O.default_params(spec["kind"], exact=True)
+    idx = np.unique(np.linspace(0, 63, 16).astype(np.int64))
+    with O.counting_build():
+        O.flop_counts(reset=True)
+        O.qpik_batch(om, par, *[np.ascontiguousarray(v[:, idx]) for v in (q, qd, xt, xdt)])
+        full, _ = O.flop_counts(reset=True)
+    assert a["flops_per_solve"] < full / len(idx)

@@ -134,3 +134,25 @@ def test_cylinder_side_closed_form_vs_tight_gjk():
         assert abs(np.linalg.norm(pB - pA) - d.value) <= 1e-12
         hit += 1
     assert hit >= 30
+
+
+def test_pruned_narrow_phase_matches_all_pairs():
+    """The kernel's pruned search (oracle min_distance_pruned: closed forms,
+    lower bounds, GJK early exit, best-first EPA) returns the all-pairs
+    argmin bit for bit -- the FLOP count (tools/flop_count.py) runs it."""
+    pen = 0
+    try:
+        for robot in ("fr3", "ur5e", "husky_fr3", "xls_fr3", "caster_fr3"):
+            pm, om, _ = O.load(robot)
+            q, _ = workload.joint_states(pm.lower, pm.upper, pm.vel, 11, 96)
+            for b in range(q.shape[1]):
+                O.set_pruned_narrow_phase(False)
+                d0, g0, p0 = O.min_distance(om, q[:, b])
+                O.set_pruned_narrow_phase(True)
+                d1, g1, p1 = O.min_distance(om, q[:, b])
+                assert (d1, p1) == (d0, p0), (robot, b)
+                assert np.array_equal(g1, g0), (robot, b)
+                pen += d0 < 0
+    finally:
+        O.set_pruned_narrow_phase(False)
+    assert pen > 0  # the EPA branch was exercised
