@@ -20,6 +20,8 @@ for p in "${pids[@]}"; do wait "$p" || rc=1; done
 $HIPCC --offload-arch=gfx950 -shared -fPIC "$OBJ"/task_kernel.o "$OBJ"/qp_kernel.o "$OBJ"/fused_kernel.o "$OBJ"/qpid_kernel.o \
   "$OBJ"/dynamics.o "$OBJ"/api.o "$OBJ"/model.o -o "$OUT" -Wl,-rpath,/opt/rocm/lib
 [ -n "$DRC_VARIANT" ] && exit 0
+# test-only: the narrow-phase device code on one wave per pair (tests/test_gpu_narrow.py)
+$HIPCC $FLAGS -shared tests/gpu_narrow.hip -o tests/_narrow_gpu.so
 make -s -C oracle all count
 mkdir -p dyros_robot_controller_amd/python
 # C++ facade + pybind11 module with the reference's module/class names (host code only)

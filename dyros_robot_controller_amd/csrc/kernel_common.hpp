@@ -387,6 +387,182 @@ __device__ __forceinline__ double bcast(double v, int lane) {
   return __hiloint2double(hi, lo);
 }
 
+// Wave forms of det_lu6 and pinv_cod6 (the ill-conditioned JJ^T path of
+// every near-singular instance, formerly ~0.6 M cycles on one lane): the same
+// operation sequences with the 6 rows / columns in registers of lanes 0..5,
+// pivots and broadcasts by v_readlane, the six triangular solves one per lane.
+// Bit-identical to the serial forms (tests/test_gpu_parity.py near-singular
+// tier).  Call with the whole wave; results are wave-uniform.
+__device__ __forceinline__ double det_lu6_wave(const double* A) {
+  const int l = lane_id(), lr = l < 6 ? l : 0;
+  double r[6];
+#pragma unroll
+  for (int j = 0; j < 6; ++j) r[j] = A[lr * 6 + j];
+  double det = 1;
+#pragma unroll
+  for (int c = 0; c < 6; ++c) {
+    double col[6];
+#pragma unroll
+    for (int i = c; i < 6; ++i) col[i] = bcast(r[c], i);
+    int p = c;  // first row of maximal |M[r][c]| (serial scan)
+#pragma unroll
+    for (int i = c + 1; i < 6; ++i)
+      if (fabs(col[i]) > fabs(col[p])) p = i;
+    p = __builtin_amdgcn_readfirstlane(p);
+    double pv = col[c];
+#pragma unroll
+    for (int i = c + 1; i < 6; ++i) pv = p == i ? col[i] : pv;
+    if (pv == 0) return 0;
+    if (p != c) {
+#pragma unroll
+      for (int j = 0; j < 6; ++j) {
+        const double rc = bcast(r[j], c), rp = bcast(r[j], p);
+        r[j] = l == c ? rp : (l == p ? rc : r[j]);
+      }
+      det = -det;
+    }
+    det *= pv;
+    double pr[6];
+#pragma unroll
+    for (int j = c; j < 6; ++j) pr[j] = bcast(r[j], c);
+    if (l > c && l < 6) {
+      const double f = r[c] / pr[c];
+#pragma unroll
+      for (int j = c; j < 6; ++j) r[j] -= f * pr[j];
+    }
+  }
+  return det;
+}
+// rank_cpqr6 with column j in lane j
+__device__ __forceinline__ int rank_cpqr6_wave(const double* A) {
+  const int l = lane_id(), lc = l < 6 ? l : 0;
+  double m[6], piv[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) m[i] = A[i * 6 + lc];
+  double maxpiv = 0;
+  bool done = false;
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    if (done) {
+      piv[k] = 0;
+      continue;
+    }
+    double cn = 0;
+#pragma unroll
+    for (int i = k; i < 6; ++i) cn += m[i] * m[i];
+    double cv[6];
+#pragma unroll
+    for (int j = k; j < 6; ++j) cv[j] = bcast(cn, j);
+    int p = k;
+#pragma unroll
+    for (int j = k + 1; j < 6; ++j)
+      if (cv[j] > cv[p]) p = j;
+    p = __builtin_amdgcn_readfirstlane(p);
+    double cp = cv[k];
+#pragma unroll
+    for (int j = k + 1; j < 6; ++j) cp = p == j ? cv[j] : cp;
+    if (p != k)
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        const double mk = bcast(m[i], k), mp = bcast(m[i], p);
+        m[i] = l == k ? mp : (l == p ? mk : m[i]);
+      }
+    const double nrm = sqrt(cp);
+    piv[k] = nrm;
+    maxpiv = fmax(maxpiv, nrm);
+    if (nrm == 0) {
+      done = true;
+      continue;
+    }
+    double v[6];
+#pragma unroll
+    for (int i = k; i < 6; ++i) v[i] = bcast(m[i], k);
+    const double alpha = v[k] > 0 ? -nrm : nrm;
+    v[k] -= alpha;
+    double vn = 0;
+#pragma unroll
+    for (int i = k; i < 6; ++i) vn += v[i] * v[i];
+    if (vn > 0 && l >= k && l < 6) {
+      double sm = 0;
+#pragma unroll
+      for (int i = k; i < 6; ++i) sm += v[i] * m[i];
+      sm = 2 * sm / vn;
+#pragma unroll
+      for (int i = k; i < 6; ++i) m[i] -= sm * v[i];
+    }
+  }
+  int r = 0;
+#pragma unroll
+  for (int k = 0; k < 6; ++k) r += piv[k] > 1e-6 * maxpiv;
+  return r;
+}
+// pinv_cod6: rank, Cholesky (row i in lane i), the six column solves one per
+// lane against L in LDS (ws[0..35]); rank-deficient / not-PD -> the serial
+// COD on lane 0
+__device__ __forceinline__ void pinv_cod6_wave(const double* A, double* X, double* ws) {
+  const int l = lane_id(), lr = l < 6 ? l : 0;
+  bool ok = rank_cpqr6_wave(A) == 6;
+  if (ok) {
+    double Lr[6];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) Lr[j] = A[lr * 6 + j];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      double rj[6];
+#pragma unroll
+      for (int k = 0; k <= j; ++k) rj[k] = bcast(Lr[k], j);
+      double sv = rj[j];
+#pragma unroll
+      for (int k = 0; k < j; ++k) sv -= rj[k] * rj[k];
+      if (!(sv > 0)) {
+        ok = false;
+        break;
+      }
+      const double d = sqrt(sv);
+      if (l == j) Lr[j] = d;
+      if (l > j && l < 6) {
+        double t = Lr[j];
+#pragma unroll
+        for (int k = 0; k < j; ++k) t -= Lr[k] * rj[k];
+        Lr[j] = t / d;
+      }
+    }
+    if (ok) {
+      if (l < 6)
+#pragma unroll
+        for (int j = 0; j < 6; ++j) ws[l * 6 + j] = Lr[j];
+      wsync();
+      if (l < 6) {
+        const double* L = ws;
+        double e[6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) e[i] = i == l ? 1.0 : 0.0;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+          double t = e[i];
+#pragma unroll
+          for (int k = 0; k < i; ++k) t -= L[i * 6 + k] * e[k];
+          e[i] = t / L[i * 6 + i];
+        }
+#pragma unroll
+        for (int i = 5; i >= 0; --i) {
+          double t = e[i];
+#pragma unroll
+          for (int k = i + 1; k < 6; ++k) t -= L[k * 6 + i] * e[k];
+          e[i] = t / L[i * 6 + i];
+        }
+#pragma unroll
+        for (int i = 0; i < 6; ++i) X[i * 6 + l] = e[i];
+      }
+      wsync();
+      return;
+    }
+  }
+  if (l == 0) pinv_cod_serial(A, 6, 1, X, ws);
+  wsync();
+}
+
+
 // Register EQP of the polish (eqp_regs): reduced KKTs of up to this many rows
 // are solved lane-per-row in registers; the LDS plan sizes follow it.
 constexpr int kEqpRegCap = 16;

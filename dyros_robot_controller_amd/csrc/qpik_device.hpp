@@ -567,16 +567,22 @@ DRC_HD inline __noinline__ GjkDist gjk(const Shape A, const Shape B, double cut 
   return o;
 }
 
-// Expanding polytope (EPA) with face adjacency (Bullet/libccd style): the
-// visible region is flood-filled from the closest face across shared edges
-// (explicit DFS stack, same visiting order as the recursive oracle), so the
-// horizon is a single loop and the polytope stays a closed 2-manifold even
-// when flat features (cylinder caps, box faces) make the support mapping
-// degenerate.  The polytope lives in LDS.  Per step the wave computes the
-// closest face, the support point, the stop tests and the visibility of
-// every face (one bit per face); one lane then walks the horizon with the
-// visited/visible bits in registers and packed adjacency (one LDS word per
-// edge).  Same caps and decisions as oracle/drc_oracle.c:epa.
+// Expanding polytope (EPA) with face adjacency (Bullet/libccd style).  The
+// polytope lives in LDS.  One expansion step from the closest face `best` by
+// the support point w (oracle/drc_oracle.c:epa_grow_canon, same decisions):
+//  - the removed region C is the connected component of `best` among the
+//    alive faces that see w (what btGjkEpa2's recursive flood fill kills);
+//  - its horizon (edges of C faces whose neighbour is outside C) must be one
+//    simple cycle of >= 3 edges; the new faces (start, end, w) take slots in
+//    cycle order from the edge of smallest key 3 face + edge: free list first
+//    (last freed first), then fresh slots;
+//  - every new face must be non-degenerate, keep the origin inside and not
+//    undercut `best` (EPA's lower bound never decreases);
+//  - C is freed in ascending slot order, `best` last.
+// A failed step leaves the polytope unchanged and EPA stops.  The task kernel
+// runs a step on the whole wave (epa_grow_wave: component by ballots, horizon
+// compaction, cycle order by pointer jumping, one new face per lane);
+// epa_grow_canon is the lane-serial form (host harness, single-lane use).
 // caps: hpp-fcl's GJKSolver defaults (epa_max_vertex_num 64,
 // epa_max_face_num 128, epa_max_iterations 255), mirrored by the oracle
 constexpr int kEpaMaxV = 64, kEpaMaxF = 128;
@@ -586,33 +592,12 @@ struct EpaPoly {
   double fn[kEpaMaxF][3], fd[kEpaMaxF];
   double out[6];
   int32_t adj[kEpaMaxF][3];  // neighbour across edge e: face | (its edge << 16)
-  int32_t stk[kEpaMaxF];     // DFS stack: face | edge << 16 | state << 24
+  int32_t hl[kEpaMaxV];      // a step's horizon edges: face | (edge << 16)
+  int32_t vout[kEpaMaxV], vin[kEpaMaxV];  // horizon edge leaving / entering each vertex
   int16_t fv[kEpaMaxF][3];
-  int16_t freel[kEpaMaxF], deadl[kEpaMaxF], newl[kEpaMaxF];  // recycled slots; this pass's kills / births
+  int16_t freel[kEpaMaxF];  // recycled slots, last freed first
   int8_t alive[kEpaMaxF];
-  int nv, nf, hcf, hff, hnf, fail, stop, nfree, ndead, nnew;
-  double fdmin;  // distance of the face being expanded: new faces may not undercut it
-};
-// scalar state of a step, kept in registers while one lane grows the hull
-struct EpaCtl {
-  int nv, nf, hcf, hff, hnf, fail, nfree, ndead, nnew;
-  double fdmin;
-  DRC_HD __forceinline__ void load(const EpaPoly* E) {
-    nv = E->nv; nf = E->nf; hcf = E->hcf; hff = E->hff; hnf = E->hnf; fail = E->fail;
-    nfree = E->nfree; ndead = E->ndead; nnew = E->nnew; fdmin = E->fdmin;
-  }
-  DRC_HD __forceinline__ void store(EpaPoly* E) const {
-    E->nv = nv; E->nf = nf; E->hcf = hcf; E->hff = hff; E->hnf = hnf; E->fail = fail;
-    E->nfree = nfree; E->ndead = ndead; E->nnew = nnew; E->fdmin = fdmin;
-  }
-};
-struct FaceMask {
-  uint64_t lo, hi;
-  DRC_HD __forceinline__ bool has(int f) const { return f < 64 ? (lo >> f) & 1ull : (hi >> (f - 64)) & 1ull; }
-  DRC_HD __forceinline__ void set(int f) {
-    if (f < 64) lo |= 1ull << f;
-    else hi |= 1ull << (f - 64);
-  }
+  int nv, nf, fail, stop, nfree;
 };
 DRC_HD __forceinline__ V3 epa_vw(const EpaPoly* E, int i) { return v3(E->vw[i][0], E->vw[i][1], E->vw[i][2]); }
 DRC_HD __forceinline__ V3 epa_va(const EpaPoly* E, int i) { return v3(E->va[i][0], E->va[i][1], E->va[i][2]); }
@@ -625,93 +610,44 @@ DRC_HD __forceinline__ void epa_addv(EpaPoly* E, V3 w, V3 a) {
 DRC_HD __forceinline__ bool epa_sees(const EpaPoly* E, int f, V3 w) {
   return !(dot(ld3(E->fn[f]), w) - E->fd[f] < -1e-12);
 }
-DRC_HD __forceinline__ int epa_newface(EpaPoly* E, EpaCtl& C, int a, int b, int c) {
-  int f;
-  if (C.nfree > 0) {
-    f = E->freel[--C.nfree];
-  } else if (C.nf < kEpaMaxF) {
-    f = C.nf++;
-  } else {
-    C.fail = 1;
-    return -1;
-  }
-  E->newl[C.nnew++] = f;
-  E->fv[f][0] = a;
-  E->fv[f][1] = b;
-  E->fv[f][2] = c;
+// normal and offset of the face (a, b, c); false if degenerate, seeing the
+// origin from outside or closer than fdmin (oracle epa_newface / epa_grow_canon)
+DRC_HD __forceinline__ bool epa_face_plane(const EpaPoly* E, int a, int b, int c, double fdmin, V3* n, double* fd) {
   const V3 va_ = epa_vw(E, a);
   V3 nn = cross(epa_vw(E, b) - va_, epa_vw(E, c) - va_);
   const double L = sqrt(dot(nn, nn));
-  if (!(L > 1e-300)) {
-    C.fail = 1;
-    E->alive[f] = 0;
-    return -1;
-  }
+  if (!(L > 1e-300)) return false;
   nn = v3(nn.x / L, nn.y / L, nn.z / L);  // same rounding as the oracle
-  const double fd = dot(nn, va_);
-  st3(E->fn[f], nn);
-  E->fd[f] = fd;
-  // the origin must stay inside (Bullet's EPA_INSIDE_EPS test): a face that
-  // sees it from outside means the hull went non-convex numerically.  And
-  // EPA's lower bound never decreases: a new face closer to the origin than
-  // the face it replaces is a rounding artefact of a near-coplanar support
-  if (fd < -1e-12 || fd < C.fdmin - 1e-12) {
-    C.fail = 1;
-    E->alive[f] = 0;
+  *n = nn;
+  *fd = dot(nn, va_);
+  return !(*fd < -1e-12 || *fd < fdmin - 1e-12);
+}
+// initial tetrahedron face (lane-serial)
+DRC_HD __forceinline__ int epa_newface(EpaPoly* E, int a, int b, int c) {
+  int f;
+  if (E->nfree > 0) {
+    f = E->freel[--E->nfree];
+  } else if (E->nf < kEpaMaxF) {
+    f = E->nf++;
+  } else {
+    E->fail = 1;
     return -1;
   }
-  E->alive[f] = 1;
-  return f;
+  E->fv[f][0] = a;
+  E->fv[f][1] = b;
+  E->fv[f][2] = c;
+  V3 n;
+  double fd;
+  const bool ok = epa_face_plane(E, a, b, c, -1e300, &n, &fd);
+  st3(E->fn[f], n);
+  E->fd[f] = fd;
+  E->alive[f] = ok;
+  if (!ok) E->fail = 1;
+  return ok ? f : -1;
 }
 DRC_HD __forceinline__ void epa_bind(EpaPoly* E, int f0, int e0, int f1, int e1) {
   E->adj[f0][e0] = f1 | (e1 << 16);
   E->adj[f1][e1] = f0 | (e0 << 16);
-}
-// iterative form of btGjkEpa2::expand over the three edges of `best`; `vis`
-// holds epa_sees() of every face for the new vertex w (computed up front)
-DRC_HD __forceinline__ bool epa_expand_all(EpaPoly* E, EpaCtl& C, int w, int best, FaceMask vis) {
-  FaceMask done{0, 0};  // oracle: fpass[f] == pass
-  done.set(best);
-  for (int j = 0; j < 3; ++j) {
-    E->stk[0] = E->adj[best][j];
-    int sp = 1;
-    while (sp > 0) {
-      const int ent = E->stk[sp - 1];
-      const int f = ent & 0xffff, e = (ent >> 16) & 0xff, st = ent >> 24;
-      if (st == 0) {
-        if (done.has(f)) {
-          --sp;
-          continue;
-        }
-        const int e1 = e == 2 ? 0 : e + 1;
-        if (!vis.has(f)) {  // horizon edge: new face on (f's e1 vertex, e vertex, w)
-          const int nf = epa_newface(E, C, E->fv[f][e1], E->fv[f][e], w);
-          if (nf < 0) return false;
-          epa_bind(E, nf, 0, f, e);
-          if (C.hcf >= 0) epa_bind(E, C.hcf, 1, nf, 2);
-          else C.hff = nf;
-          C.hcf = nf;
-          ++C.hnf;
-          --sp;
-          continue;
-        }
-        done.set(f);
-        E->stk[sp - 1] = f | (e << 16) | (1 << 24);
-        if (sp >= kEpaMaxF) return false;
-        E->stk[sp++] = E->adj[f][e1];
-      } else if (st == 1) {
-        const int e2 = e == 0 ? 2 : e - 1;
-        E->stk[sp - 1] = f | (e << 16) | (2 << 24);
-        if (sp >= kEpaMaxF) return false;
-        E->stk[sp++] = E->adj[f][e2];
-      } else {
-        E->alive[f] = 0;
-        E->deadl[C.ndead++] = f;
-        --sp;
-      }
-    }
-  }
-  return true;
 }
 // rerun GJK and build the initial tetrahedron from its final simplex
 // (lane-serial)
@@ -722,11 +658,6 @@ DRC_HD __forceinline__ void epa_init(const Shape A, const Shape B, EpaPoly* E) {
   E->nf = 0;
   E->fail = 0;
   E->nfree = 0;
-  E->nnew = 0;
-  E->ndead = 0;
-  E->hcf = E->hff = -1;
-  E->hnf = 0;
-  E->fdmin = -1e300;
   for (int i = 0; i < 4; ++i)
     if (i < g.n) epa_addv(E, g.S[i].w, g.S[i].a);
   for (int di = 0; di < 6 && E->nv < 4; ++di) {
@@ -753,11 +684,8 @@ DRC_HD __forceinline__ void epa_init(const Shape A, const Shape B, EpaPoly* E) {
       }
     }
   }
-  EpaCtl C;
-  C.load(E);
-  const int t0 = epa_newface(E, C, 0, 1, 2), t1 = epa_newface(E, C, 1, 0, 3), t2 = epa_newface(E, C, 2, 1, 3),
-            t3 = epa_newface(E, C, 0, 2, 3);
-  C.store(E);
+  const int t0 = epa_newface(E, 0, 1, 2), t1 = epa_newface(E, 1, 0, 3), t2 = epa_newface(E, 2, 1, 3),
+            t3 = epa_newface(E, 0, 2, 3);
   if (!E->fail) {
     epa_bind(E, t0, 0, t1, 0);
     epa_bind(E, t0, 1, t2, 0);
@@ -778,171 +706,97 @@ DRC_HD __forceinline__ bool epa_is_dup(const EpaPoly* E, int i, const SV& w) {
   const V3 d = w.w - epa_vw(E, i);
   return fabs(d.x) <= 1e-14 && fabs(d.y) <= 1e-14 && fabs(d.z) <= 1e-14;
 }
-// grow the polytope by w from face `best` (lane-serial; vis from the wave);
-// sets E->stop when the expansion is inconsistent (rolled back to the last
-// closed polytope)
-DRC_HD __forceinline__ void epa_grow(EpaPoly* E, const SV w, int best, FaceMask vis) {
-  EpaCtl C;
-  C.load(E);
-  const int wi = C.nv;
+DRC_HD __forceinline__ int epa_next_edge(int e) { return e == 2 ? 0 : e + 1; }
+// lane-serial step (see the header comment); sets E->stop on failure
+DRC_HD inline void epa_grow_canon(EpaPoly* E, const SV w, int best) {
+  bool inC[kEpaMaxF];
+  int hf[kEpaMaxV], he[kEpaMaxV], ord[kEpaMaxV], slot[kEpaMaxV];
+  const int wi = E->nv, nf = E->nf;
   st3(E->vw[wi], w.w);
   st3(E->va[wi], w.a);
-  C.nv++;
-  C.hcf = -1;
-  C.hff = -1;
-  C.hnf = 0;
-  C.ndead = 0;
-  C.nnew = 0;
-  C.fdmin = E->fd[best];
-  const bool valid = epa_expand_all(E, C, wi, best, vis);
-  if (!valid || C.hnf < 3 || C.fail) {  // roll back to the last closed polytope
-    for (int i = 0; i < C.nnew; ++i) E->alive[E->newl[i]] = 0;
-    for (int i = 0; i < C.ndead; ++i) E->alive[E->deadl[i]] = 1;
-    C.nv--;
-    C.store(E);
-    E->stop = 1;
-    return;
-  }
-  epa_bind(E, C.hcf, 1, C.hff, 2);
-  E->alive[best] = 0;
-  for (int i = 0; i < C.ndead; ++i) E->freel[C.nfree++] = E->deadl[i];
-  E->freel[C.nfree++] = best;
-  C.store(E);
-}
-// Wave form of epa_grow (the task kernel).  The lane-serial horizon walk only
-// allocates the new faces' slots, vertices and adjacency (epa_grow_walk); the
-// wave then forms their normals and offsets and runs epa_newface's validity
-// tests one face per lane (epa_face_geometry), and the walking lane commits or
-// rolls back (epa_grow_finish).  Same slots, adjacency, face data and
-// decisions as epa_grow: a face that fails its test makes the step roll back
-// either way (epa_grow stops the walk there, this form finishes the walk
-// first; the rollback restores the same alive set and EPA stops).
-DRC_HD __forceinline__ int epa_newslot(EpaPoly* E, EpaCtl& C, int a, int b, int c) {
-  int f;
-  if (C.nfree > 0) {
-    f = E->freel[--C.nfree];
-  } else if (C.nf < kEpaMaxF) {
-    f = C.nf++;
-  } else {
-    C.fail = 1;
-    return -1;
-  }
-  E->newl[C.nnew++] = f;
-  E->fv[f][0] = a;
-  E->fv[f][1] = b;
-  E->fv[f][2] = c;
-  return f;
-}
-// epa_newface's geometry and tests for slot f (any lane)
-DRC_HD __forceinline__ bool epa_face_geometry(EpaPoly* E, int f, double fdmin) {
-  const V3 va_ = epa_vw(E, E->fv[f][0]);
-  V3 nn = cross(epa_vw(E, E->fv[f][1]) - va_, epa_vw(E, E->fv[f][2]) - va_);
-  const double L = sqrt(dot(nn, nn));
-  if (!(L > 1e-300)) {
-    E->alive[f] = 0;
-    return false;
-  }
-  nn = v3(nn.x / L, nn.y / L, nn.z / L);
-  const double fd = dot(nn, va_);
-  st3(E->fn[f], nn);
-  E->fd[f] = fd;
-  if (fd < -1e-12 || fd < fdmin - 1e-12) {
-    E->alive[f] = 0;
-    return false;
-  }
-  E->alive[f] = 1;
-  return true;
-}
-DRC_HD __forceinline__ bool epa_walk_all(EpaPoly* E, EpaCtl& C, int w, int best, FaceMask vis) {
-  FaceMask done{0, 0};
-  done.set(best);
-  for (int j = 0; j < 3; ++j) {
-    E->stk[0] = E->adj[best][j];
-    int sp = 1;
-    while (sp > 0) {
-      const int ent = E->stk[sp - 1];
-      const int f = ent & 0xffff, e = (ent >> 16) & 0xff, st = ent >> 24;
-      if (st == 0) {
-        if (done.has(f)) {
-          --sp;
-          continue;
+  for (int f = 0; f < nf; ++f) inC[f] = f == best;
+  for (bool grown = true; grown;) {
+    grown = false;
+    for (int f = 0; f < nf; ++f) {
+      if (inC[f] || !E->alive[f] || !epa_sees(E, f, w.w)) continue;
+      for (int e = 0; e < 3; ++e)
+        if (inC[E->adj[f][e] & 0xffff]) {
+          inC[f] = true;
+          grown = true;
+          break;
         }
-        const int e1 = e == 2 ? 0 : e + 1;
-        if (!vis.has(f)) {  // horizon edge
-          const int nf = epa_newslot(E, C, E->fv[f][e1], E->fv[f][e], w);
-          if (nf < 0) return false;
-          epa_bind(E, nf, 0, f, e);
-          if (C.hcf >= 0) epa_bind(E, C.hcf, 1, nf, 2);
-          else C.hff = nf;
-          C.hcf = nf;
-          ++C.hnf;
-          --sp;
-          continue;
-        }
-        done.set(f);
-        E->stk[sp - 1] = f | (e << 16) | (1 << 24);
-        if (sp >= kEpaMaxF) return false;
-        E->stk[sp++] = E->adj[f][e1];
-      } else if (st == 1) {
-        const int e2 = e == 0 ? 2 : e - 1;
-        E->stk[sp - 1] = f | (e << 16) | (2 << 24);
-        if (sp >= kEpaMaxF) return false;
-        E->stk[sp++] = E->adj[f][e2];
-      } else {
-        E->alive[f] = 0;
-        E->deadl[C.ndead++] = f;
-        --sp;
-      }
     }
   }
-  return true;
-}
-DRC_HD __forceinline__ void epa_grow_walk(EpaPoly* E, const SV w, int best, FaceMask vis) {
-  EpaCtl C;
-  C.load(E);
-  const int wi = C.nv;
-  st3(E->vw[wi], w.w);
-  st3(E->va[wi], w.a);
-  C.nv++;
-  C.hcf = -1;
-  C.hff = -1;
-  C.hnf = 0;
-  C.ndead = 0;
-  C.nnew = 0;
-  C.fdmin = E->fd[best];
-  if (!epa_walk_all(E, C, wi, best, vis)) C.hnf = -1;  // invalid walk: epa_grow_finish rolls back
-  C.store(E);
-}
-DRC_HD __forceinline__ void epa_grow_finish(EpaPoly* E, int best, bool geom_fail) {
-  EpaCtl C;
-  C.load(E);
-  if (C.hnf < 3 || C.fail || geom_fail) {  // roll back to the last closed polytope
-    for (int i = 0; i < C.nnew; ++i) E->alive[E->newl[i]] = 0;
-    for (int i = 0; i < C.ndead; ++i) E->alive[E->deadl[i]] = 1;
-    C.nv--;
-    C.store(E);
+  for (int v = 0; v < kEpaMaxV; ++v) E->vout[v] = E->vin[v] = -1;
+  int H = 0;
+  bool ok = true;
+  for (int c = 0; c < nf && ok; ++c) {
+    if (!inC[c]) continue;
+    for (int e = 0; e < 3 && ok; ++e) {
+      if (inC[E->adj[c][e] & 0xffff]) continue;
+      const int a = E->fv[c][e], b = E->fv[c][epa_next_edge(e)];
+      if (H >= kEpaMaxV || E->vout[a] >= 0 || E->vin[b] >= 0) {
+        ok = false;
+        break;
+      }
+      E->vout[a] = H;
+      E->vin[b] = H;
+      hf[H] = c;
+      he[H] = e;
+      ++H;
+    }
+  }
+  ok = ok && H >= 3;
+  int cur = 0;
+  for (int k = 0; k < H && ok; ++k) {
+    if (cur < 0 || (k > 0 && cur == 0)) ok = false;
+    else {
+      ord[k] = cur;
+      cur = E->vout[E->fv[hf[cur]][epa_next_edge(he[cur])]];
+    }
+  }
+  ok = ok && cur == 0 && H <= E->nfree + (kEpaMaxF - nf);
+  const double fdmin = E->fd[best];
+  for (int k = 0; k < H && ok; ++k) {
+    const int h = ord[k], c = hf[h], e = he[h];
+    V3 n;
+    double fd;
+    ok = epa_face_plane(E, E->fv[c][e], E->fv[c][epa_next_edge(e)], wi, fdmin, &n, &fd);
+    slot[k] = k < E->nfree ? E->freel[E->nfree - 1 - k] : nf + (k - E->nfree);
+  }
+  if (!ok) {
     E->stop = 1;
     return;
   }
-  epa_bind(E, C.hcf, 1, C.hff, 2);
+  for (int k = 0; k < H; ++k) {
+    const int f = slot[k], h = ord[k], c = hf[h], e = he[h];
+    const int a = E->fv[c][e], b = E->fv[c][epa_next_edge(e)];
+    V3 n;
+    double fd;
+    epa_face_plane(E, a, b, wi, fdmin, &n, &fd);
+    st3(E->fn[f], n);
+    E->fd[f] = fd;
+    E->fv[f][0] = a;
+    E->fv[f][1] = b;
+    E->fv[f][2] = wi;
+    const int g = E->adj[c][e];
+    E->adj[f][0] = g;
+    E->adj[g & 0xffff][g >> 16] = f;
+    E->adj[f][1] = slot[(k + 1) % H] | (2 << 16);
+    E->adj[f][2] = slot[(k + H - 1) % H] | (1 << 16);
+  }
+  const int nfree0 = E->nfree > H ? E->nfree - H : 0;
+  if (H > E->nfree) E->nf = nf + (H - E->nfree);
+  E->nfree = nfree0;
+  for (int c = 0; c < nf; ++c)
+    if (inC[c] && c != best) {
+      E->alive[c] = 0;
+      E->freel[E->nfree++] = c;
+    }
   E->alive[best] = 0;
-  for (int i = 0; i < C.ndead; ++i) E->freel[C.nfree++] = E->deadl[i];
-  E->freel[C.nfree++] = best;
-  C.store(E);
-}
-// one expansion step (lane-serial form, host harness)
-DRC_HD inline void epa_step(const Shape& A, const Shape& B, EpaPoly* E, int best) {
-  const SV w = sup_md(A, B, ld3(E->fn[best]));
-  bool stop = epa_gap_stop(E, best, w);
-  for (int i = 0; !stop && i < E->nv; ++i) stop = epa_is_dup(E, i, w);
-  if (stop) {
-    E->stop = 1;
-    return;
-  }
-  FaceMask vis{0, 0};
-  for (int f = 0; f < E->nf; ++f)
-    if (epa_sees(E, f, w.w)) vis.set(f);
-  epa_grow(E, w, best, vis);
+  E->freel[E->nfree++] = best;
+  for (int k = 0; k < H; ++k) E->alive[slot[k]] = 1;
+  E->nv = wi + 1;
 }
 // witness points on the closest face (lane-serial); returns -depth
 DRC_HD __forceinline__ double epa_finish(EpaPoly* E, int best) {
@@ -959,6 +813,214 @@ DRC_HD __forceinline__ double epa_finish(EpaPoly* E, int best) {
   st3(E->out + 3, l0 * (aa - aw) + l1 * (ba - bw) + l2 * (ca - cw));
   return -bd;
 }
+// Wave form of epa_grow_canon (the task kernel; every lane calls it with the
+// same w and best).  Lane l owns faces l and l + 64 and, after compaction,
+// horizon edge l.  Same slots, adjacency, face data, free list and decisions.
+__device__ __forceinline__ void epa_grow_wave(EpaPoly* E, const SV& w, int best) {
+  const int l = threadIdx.x & 63;
+  const int nf = E->nf, wi = E->nv, nfree = E->nfree;
+  if (l == 0) {
+    st3(E->vw[wi], w.w);
+    st3(E->va[wi], w.a);
+  }
+  E->vout[l] = -1;
+  E->vin[l] = -1;
+  const int f0 = l, f1 = l + 64;
+  const bool h0 = f0 < nf, h1 = f1 < nf;
+  const bool s0 = h0 && E->alive[f0] && epa_sees(E, f0, w.w);
+  const bool s1 = h1 && E->alive[f1] && epa_sees(E, f1, w.w);
+  int n0[3], n1[3];
+#pragma unroll
+  for (int e = 0; e < 3; ++e) {
+    n0[e] = h0 ? E->adj[f0][e] : 0;
+    n1[e] = h1 ? E->adj[f1][e] : 0;
+  }
+  auto in = [](uint64_t lo, uint64_t hi, int f) -> bool {
+    return f < 64 ? (lo >> f) & 1ull : (hi >> (f - 64)) & 1ull;
+  };
+  uint64_t clo = best < 64 ? 1ull << best : 0ull, chi = best < 64 ? 0ull : 1ull << (best - 64);
+  for (;;) {  // component of best among the visible faces, one ring per round
+    const bool j0 = s0 && !in(clo, chi, f0) &&
+                    (in(clo, chi, n0[0] & 0xffff) || in(clo, chi, n0[1] & 0xffff) || in(clo, chi, n0[2] & 0xffff));
+    const bool j1 = s1 && !in(clo, chi, f1) &&
+                    (in(clo, chi, n1[0] & 0xffff) || in(clo, chi, n1[1] & 0xffff) || in(clo, chi, n1[2] & 0xffff));
+    const uint64_t nlo = clo | __ballot(j0), nhi = chi | __ballot(j1);
+    if (nlo == clo && nhi == chi) break;
+    clo = nlo;
+    chi = nhi;
+  }
+  // horizon edges (c, e), compacted in (edge slot j, lane) order
+  const bool c0 = in(clo, chi, f0), c1 = in(clo, chi, f1);
+  bool hz[6];
+#pragma unroll
+  for (int e = 0; e < 3; ++e) {
+    hz[e] = c0 && !in(clo, chi, n0[e] & 0xffff);
+    hz[3 + e] = c1 && !in(clo, chi, n1[e] & 0xffff);
+  }
+  const uint64_t below = (1ull << l) - 1;
+  int H = 0;
+  int pos[6];
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    const uint64_t m = __ballot(hz[j]);
+    pos[j] = H + __popcll(m & below);
+    H += __popcll(m);
+  }
+  wsync();  // vout / vin cleared, vertex wi stored
+  bool bad = H < 3 || H > kEpaMaxV || H > nfree + (kEpaMaxF - nf);
+  if (!bad) {
+#pragma unroll
+    for (int j = 0; j < 6; ++j)
+      if (hz[j]) {
+        const int c = j < 3 ? f0 : f1, e = j % 3;
+        E->hl[pos[j]] = c | (e << 16);
+        E->vout[E->fv[c][e]] = pos[j];
+        E->vin[E->fv[c][epa_next_edge(e)]] = pos[j];
+      }
+  }
+  wsync();
+  const bool own = l < H && !bad;
+  int hc = 0, he_ = 0, a = 0, b = 0, nx = 0, pv = 0;
+  if (own) {
+    const int hv = E->hl[l];
+    hc = hv & 0xffff;
+    he_ = hv >> 16;
+    a = E->fv[hc][he_];
+    b = E->fv[hc][epa_next_edge(he_)];
+    nx = E->vout[b];
+    pv = E->vin[a];
+    // a vertex starting or ending two edges (the other write won), or an end
+    // with no continuation: not one simple cycle
+    bad = E->vout[a] != l || E->vin[b] != l || nx < 0 || pv < 0;
+  }
+  bad = __any(bad);
+  // cycle position relative to the edge of smallest key (pointer jumping)
+  double key = own ? double(3 * hc + he_) : 1e300;
+  int s = l;
+  wave_argmin(key, s);
+  int d = (own && l != s) ? 1 : 0, p = own ? (l == s ? s : nx) : l;
+#pragma unroll
+  for (int r = 0; r < 6; ++r) {
+    const int dp = __shfl(d, p, 64), pp = __shfl(p, p, 64);
+    d += dp;
+    p = pp;
+  }
+  bad = __any(bad || (own && p != s));
+  int slot = 0;
+  bool gbad = bad;
+  V3 nn = v3(0, 0, 0);
+  double fd = 0;
+  if (own && !bad) {
+    const int k = d == 0 ? 0 : H - d;
+    slot = k < nfree ? E->freel[nfree - 1 - k] : nf + (k - nfree);
+    gbad = !epa_face_plane(E, a, b, wi, E->fd[best], &nn, &fd);
+  }
+  if (__any(gbad)) {
+    if (l == 0) E->stop = 1;
+    wsync();
+    return;
+  }
+  const int snx = __shfl(slot, nx, 64), spv = __shfl(slot, pv, 64);
+  const int g = own ? E->adj[hc][he_] : 0;
+  // C's faces, ascending, then best: positions in the new free list
+  const uint64_t rlo = clo & ~(best < 64 ? 1ull << best : 0ull), rhi = chi & ~(best < 64 ? 0ull : 1ull << (best - 64));
+  const int nC = __popcll(rlo) + __popcll(rhi), nfree0 = nfree > H ? nfree - H : 0;
+  wsync();  // every free-list read (slots) before the free list is rewritten
+  if (own) {
+    st3(E->fn[slot], nn);
+    E->fd[slot] = fd;
+    E->fv[slot][0] = a;
+    E->fv[slot][1] = b;
+    E->fv[slot][2] = wi;
+    E->adj[slot][0] = g;
+    E->adj[g & 0xffff][g >> 16] = slot;
+    E->adj[slot][1] = snx | (2 << 16);
+    E->adj[slot][2] = spv | (1 << 16);
+    E->alive[slot] = 1;
+  }
+  if (in(rlo, rhi, f0)) {
+    E->alive[f0] = 0;
+    E->freel[nfree0 + __popcll(rlo & below)] = f0;
+  }
+  if (in(rlo, rhi, f1)) {
+    E->alive[f1] = 0;
+    E->freel[nfree0 + __popcll(rlo) + __popcll(rhi & below)] = f1;
+  }
+  if (l == 0) {
+    E->alive[best] = 0;
+    E->freel[nfree0 + nC] = best;
+    E->nfree = nfree0 + nC + 1;
+    if (H > nfree) E->nf = nf + (H - nfree);
+    E->nv = wi + 1;
+  }
+  wsync();
+}
+// EPA on the whole wave for one penetrating pair: lane ln seeds the polytope
+// from GJK's simplex; per step the wave takes the closest alive face, the
+// support point and the stop tests, then grows (epa_grow_wave).  Returns the
+// signed distance (-depth) on every lane; lane ln leaves the witnesses in
+// E->out.  Same steps and result as epa_serial.  st (timing builds): steps,
+// cycles in face scan, support + tests, growth.
+__device__ __forceinline__ double epa_run_wave(const Shape& A, const Shape& B, EpaPoly* E, int ln,
+                                               unsigned long long* st = nullptr) {
+  const int l = threadIdx.x & 63;
+  if (l == ln) epa_init(A, B, E);
+  wsync();
+  double dres = 0;
+  for (int it = 0; it <= 255; ++it) {
+    unsigned long long t0 = 0, t1 = 0;
+    if (st) {
+      st[0] = it;
+      t0 = __builtin_amdgcn_s_memtime();
+    }
+    bool stop = E->stop || it == 255;
+    double fdm = 1e300;
+    int fb = 0x7fffffff;
+    for (int f = l; f < E->nf; f += 64)
+      if (E->alive[f] && E->fd[f] < fdm) {
+        fdm = E->fd[f];
+        fb = f;
+      }
+    wave_argmin(fdm, fb);
+    if (fb == 0x7fffffff) {  // no alive face (failed seed): the oracle takes face 0
+      fb = 0;
+      stop = true;
+    }
+    if (st) {
+      t1 = __builtin_amdgcn_s_memtime();
+      st[1] += t1 - t0;
+    }
+    SV w;
+    if (!stop) {  // support, gap and duplicate tests on the whole wave
+      w = sup_md(A, B, ld3(E->fn[fb]));
+      stop = epa_gap_stop(E, fb, w);
+      if (!stop) {
+        bool dup = false;
+        for (int i = l; i < E->nv; i += 64) dup |= epa_is_dup(E, i, w);
+        stop = __any(dup);
+      }
+    }
+    if (stop) {
+      if (l == ln) dres = epa_finish(E, fb);
+      break;
+    }
+    if (st) t0 = __builtin_amdgcn_s_memtime(), st[2] += t0 - t1;
+    epa_grow_wave(E, w, fb);
+    if (st) st[3] += __builtin_amdgcn_s_memtime() - t0;
+  }
+  return __shfl(dres, ln, 64);
+}
+// one expansion step (lane-serial form, host harness)
+DRC_HD inline void epa_step(const Shape& A, const Shape& B, EpaPoly* E, int best) {
+  const SV w = sup_md(A, B, ld3(E->fn[best]));
+  bool stop = epa_gap_stop(E, best, w);
+  for (int i = 0; !stop && i < E->nv; ++i) stop = epa_is_dup(E, i, w);
+  if (stop) {
+    E->stop = 1;
+    return;
+  }
+  epa_grow_canon(E, w, best);
+}
 // closest alive face by a serial scan (host / oracle-style reference)
 DRC_HD inline int epa_best_serial(const EpaPoly* E) {
   int best = -1;
@@ -973,18 +1035,9 @@ DRC_HD inline int epa_best_serial(const EpaPoly* E) {
 // lane-serial driver (host harness and single-lane use)
 DRC_HD inline double epa_serial(const Shape& A, const Shape& B, EpaPoly* E) {
   epa_init(A, B, E);
-  for (int it = 0; it < 255 && !E->stop; ++it) {
-#ifdef DRC_NARROW_DEBUG
-    const int bb = epa_best_serial(E);
-    const SV ww = sup_md(A, B, ld3(E->fn[bb]));
-    printf("epa it %d best %d fd %.12g gap %.3g nv %d nf %d\n", it, bb, E->fd[bb], dot(ld3(E->fn[bb]), ww.w) - E->fd[bb], E->nv, E->nf);
-#endif
-    epa_step(A, B, E, epa_best_serial(E));
-  }
-#ifdef DRC_NARROW_DEBUG
-  printf("epa end stop %d fail %d nv %d\n", E->stop, E->fail, E->nv);
-#endif
-  return epa_finish(E, epa_best_serial(E));
+  for (int it = 0; it < 255 && !E->stop; ++it) epa_step(A, B, E, epa_best_serial(E));
+  const int bb = epa_best_serial(E);
+  return epa_finish(E, bb < 0 ? 0 : bb);
 }
 
 // signed distance + closest surface point of a solid cylinder / box

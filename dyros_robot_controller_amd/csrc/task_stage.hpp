@@ -352,10 +352,7 @@ __device__ __noinline__ void closed_form_stage(const DevModel* M, const KParams&
       A6[l] = s;
     }
     wsync();
-    if (!inv6_certified(A6, Ai)) {
-      if (l == 0) pinv_cod6(A6, Ai, ws);
-      wsync();
-    }
+    if (!inv6_certified(A6, Ai)) pinv_cod6_wave(A6, Ai, ws);
     for (int e = l; e < 6 * nv; e += 64) {
       const int i = e / nv, c = e % nv;
       double s = 0;
@@ -619,11 +616,9 @@ __device__ __forceinline__ void task_instance(const DevModel* __restrict__ M0, c
     // every mode (|R_55|/|R_00| >= 1/kappa_2 > COD_THRESHOLD 1e-6)
     const double fa = wave_sum(l < 36 ? A6[l] * A6[l] : 0.0), fi = wave_sum(l < 36 ? Ai[l] * Ai[l] : 0.0);
     if (!(piv_min > 0) || !(fa * fi < 1e10)) {  // uniform
-      if (l == 0) {
-        double* ws = S + kp.kScr;
-        S[kp.oSc + SC_MAN] = sqrt(det_lu6(A6, ws));
-        pinv_cod6(A6, Ai, ws);
-      }
+      const double dt = det_lu6_wave(A6);
+      pinv_cod6_wave(A6, Ai, S + kp.kScr);
+      if (l == 0) S[kp.oSc + SC_MAN] = sqrt(dt);
     } else if (l == 0) {
       S[kp.oSc + SC_MAN] = sqrt(det);
     }
@@ -772,71 +767,17 @@ __device__ __forceinline__ void task_instance(const DevModel* __restrict__ M0, c
       const int p = cp, ln = p & 63, ga = M->pair_a[p], gb = M->pair_b[p];
       const Shape A{M->gtype[ga], Tg + 12 * ga, M->gparam[ga][0], M->gparam[ga][1], M->gparam[ga][2]};
       const Shape Bs{M->gtype[gb], Tg + 12 * gb, M->gparam[gb][0], M->gparam[gb][1], M->gparam[gb][2]};
-      if (l == ln) epa_init(A, Bs, ews);
-      wsync();
-      double dres = 0;
-      PH_ONLY(epa_calls++;)
-      for (int it = 0; it <= 255; ++it) {
-        PH_ONLY(epa_steps++; if ((unsigned long long)it > epa_maxsteps) epa_maxsteps = it;
-                const unsigned long long te0 = __builtin_amdgcn_s_memtime();)
-        bool stop = ews->stop || it == 255;
-        double fdm = 1e300;
-        int fb = 0x7fffffff;
-        for (int f = l; f < ews->nf; f += 64)
-          if (ews->alive[f] && ews->fd[f] < fdm) {
-            fdm = ews->fd[f];
-            fb = f;
-          }
-        wave_argmin(fdm, fb);
-        if (fb == 0x7fffffff) {  // no alive face (failed seed): oracle takes face 0
-          fb = 0;
-          stop = true;
-        }
-        PH_ONLY(const unsigned long long te1 = __builtin_amdgcn_s_memtime(); epa_t[0] += te1 - te0;)
-        SV w;
-        if (!stop) {  // support, gap and duplicate tests on the whole wave
-          w = sup_md(A, Bs, ld3(ews->fn[fb]));
-          stop = epa_gap_stop(ews, fb, w);
-          if (!stop) {
-            bool dup = false;
-            for (int i = l; i < ews->nv; i += 64) dup |= epa_is_dup(ews, i, w);
-            stop = __any(dup);
-          }
-        }
-        if (stop) {
-          if (l == ln) {
-            const double d = epa_finish(ews, fb);
-            dres = d;
-            if (d < bestd || (d == bestd && p < besti)) {
-              bestd = d;
-              besti = p;
-              bhow = 2;
-              bpA = ld3(ews->out);
-              bpB = ld3(ews->out + 3);
-            }
-          }
-          break;
-        }
-        PH_ONLY(const unsigned long long te2 = __builtin_amdgcn_s_memtime(); epa_t[1] += te2 - te1;)
-        FaceMask vis;  // visibility of every face for w, one bit per face
-        vis.lo = __ballot(l < ews->nf && epa_sees(ews, l, w.w));
-        vis.hi = __ballot(l + 64 < ews->nf && epa_sees(ews, l + 64, w.w));
-        // horizon walk on one lane (slots, adjacency), the new faces'
-        // normals and validity tests one per lane, then commit / roll back
-        if (l == ln) epa_grow_walk(ews, w, fb, vis);
-        wsync();
-        {
-          const double fdmin = ews->fd[fb];
-          bool gfail = false;
-          for (int i = l; i < ews->nnew; i += 64) gfail |= !epa_face_geometry(ews, ews->newl[i], fdmin);
-          gfail = __any(gfail);
-          wsync();
-          if (l == ln) epa_grow_finish(ews, fb, gfail);
-        }
-        wsync();
-        PH_ONLY(epa_t[2] += __builtin_amdgcn_s_memtime() - te2;)
+      PH_ONLY(epa_calls++; unsigned long long est[4] = {0, 0, 0, 0};)
+      const double dall = epa_run_wave(A, Bs, ews, ln PH_ONLY(, est));
+      PH_ONLY(epa_steps += est[0]; if (est[0] > epa_maxsteps) epa_maxsteps = est[0];
+              epa_t[0] += est[1]; epa_t[1] += est[2]; epa_t[2] += est[3];)
+      if (l == ln && (dall < bestd || (dall == bestd && p < besti))) {
+        bestd = dall;
+        besti = p;
+        bhow = 2;
+        bpA = ld3(ews->out);
+        bpB = ld3(ews->out + 3);
       }
-      const double dall = __shfl(dres, ln, 64);
       if (dall < gbd || (dall == gbd && p < gbi)) {
         gbd = dall;
         gbi = p;

@@ -530,11 +530,10 @@ static int gjk(const Shape* A, const Shape* B, SV* S, int* ns, double* lam, doub
 typedef struct Epa {
     SV V[EPA_MAXV];
     int nv, nf, pass;
-    int fv[EPA_MAXF][3], ff[EPA_MAXF][3], fe[EPA_MAXF][3], fpass[EPA_MAXF], alive[EPA_MAXF];
+    int fv[EPA_MAXF][3], ff[EPA_MAXF][3], fe[EPA_MAXF][3], alive[EPA_MAXF];
     double fn[EPA_MAXF][3], fd[EPA_MAXF];
-    int freel[EPA_MAXF], deadl[EPA_MAXF], newl[EPA_MAXF];  /* recycled slots; this pass's kills / births */
-    int hcf, hff, hnf, fail, nfree, ndead, nnew;
-    double fdmin;  /* distance of the face being expanded: new faces may not undercut it */
+    int freel[EPA_MAXF];  /* recycled slots, last freed first */
+    int fail, nfree;
 } Epa;
 
 static int epa_newface(Epa* E, int a, int b, int c) {
@@ -542,9 +541,8 @@ static int epa_newface(Epa* E, int a, int b, int c) {
     if (E->nfree > 0) f = E->freel[--E->nfree];
     else if (E->nf < EPA_MAXF) f = E->nf++;
     else { E->fail = 1; return -1; }
-    E->newl[E->nnew++] = f;
     E->fv[f][0] = a; E->fv[f][1] = b; E->fv[f][2] = c;
-    E->alive[f] = 1; E->fpass[f] = 0;
+    E->alive[f] = 1;
     double e1[3], e2[3], nn[3];
     sub3(E->V[b].w, E->V[a].w, e1);
     sub3(E->V[c].w, E->V[a].w, e2);
@@ -556,43 +554,115 @@ static int epa_newface(Epa* E, int a, int b, int c) {
     /* the origin must stay inside (Bullet's EPA_INSIDE_EPS test): a face
      * that sees it from outside means the hull went non-convex numerically */
     if (E->fd[f] < -1e-12) { E->fail = 1; E->alive[f] = 0; return -1; }
-    /* EPA's lower bound never decreases: a new face closer to the origin than
-     * the face it replaces is a rounding artefact of a near-coplanar support */
-    if (E->fd[f] < E->fdmin - 1e-12) { E->fail = 1; E->alive[f] = 0; return -1; }
     return f;
 }
 static void epa_bind(Epa* E, int f0, int e0, int f1, int e1) {
     E->ff[f0][e0] = f1; E->fe[f0][e0] = e1;
     E->ff[f1][e1] = f0; E->fe[f1][e1] = e0;
 }
-/* recursive horizon walk (btGjkEpa2::expand) */
-static int epa_expand(Epa* E, int w, int f, int e) {
-    static const int i1m3[3] = {1, 2, 0}, i2m3[3] = {2, 0, 1};
-    if (E->fpass[f] == E->pass) return 1;
-    const int e1 = i1m3[e];
-    if (dot3(E->fn[f], E->V[w].w) - E->fd[f] < -1e-12) {
-        int nf = epa_newface(E, E->fv[f][e1], E->fv[f][e], w);
-        if (nf < 0) return 0;
-        epa_bind(E, nf, 0, f, e);
-        if (E->hcf >= 0) epa_bind(E, E->hcf, 1, nf, 2); else E->hff = nf;
-        E->hcf = nf;
-        ++E->hnf;
-        return 1;
+/* One expansion step from face `best` by the new vertex wi (btGjkEpa2::expand's
+ * result, in the order the task kernel's wave form produces it -- kernel twin:
+ * epa_grow_canon / the wave form in task_stage.hpp):
+ *  - the removed region C is the connected component of `best` among the
+ *    alive faces that see w (exactly the faces the recursive flood fill from
+ *    `best` visits and kills);
+ *  - the horizon is every edge (c, e) of a face c in C whose neighbour is not
+ *    in C; it must be a single simple cycle (each vertex starts and ends at
+ *    most one edge, one cycle through all of them) of >= 3 edges;
+ *  - the new faces (start, end, w) of the horizon edges take slots in cycle
+ *    order from the edge of smallest key 3c + e: the free list first (last
+ *    freed first), then fresh slots;
+ *  - every new face passes epa_newface's tests (non-degenerate, origin
+ *    inside, no closer than `best`);
+ *  - the faces of C are freed in ascending slot order, `best` last.
+ * Any failure leaves the polytope as it was.  Returns 1 when committed. */
+static int epa_grow_canon(Epa* E, int wi, int best) {
+    static __thread int inC[EPA_MAXF], hc[EPA_MAXV], he[EPA_MAXV], outv[EPA_MAXV], inv[EPA_MAXV], ord[EPA_MAXV];
+    static __thread int slot[EPA_MAXV];
+    const double* w = E->V[wi].w;
+    for (int f = 0; f < E->nf; ++f) inC[f] = 0;
+    inC[best] = 1;
+    for (int grown = 1; grown;) {  /* component of best among visible faces */
+        grown = 0;
+        for (int f = 0; f < E->nf; ++f) {
+            if (inC[f] || !E->alive[f] || dot3(E->fn[f], w) - E->fd[f] < -1e-12) continue;
+            for (int e = 0; e < 3; ++e)
+                if (inC[E->ff[f][e]]) { inC[f] = 1; grown = 1; break; }
+        }
     }
-    const int e2 = i2m3[e];
-    E->fpass[f] = E->pass;
-    if (epa_expand(E, w, E->ff[f][e1], E->fe[f][e1]) && epa_expand(E, w, E->ff[f][e2], E->fe[f][e2])) {
-        E->alive[f] = 0;
-        E->deadl[E->ndead++] = f;
-        return 1;
+    int H = 0;
+    for (int v = 0; v < EPA_MAXV; ++v) { outv[v] = -1; inv[v] = -1; }
+    for (int c = 0; c < E->nf; ++c) {
+        if (!inC[c]) continue;
+        for (int e = 0; e < 3; ++e) {
+            if (inC[E->ff[c][e]]) continue;
+            if (H >= EPA_MAXV) return 0;
+            const int a = E->fv[c][e], b = E->fv[c][e == 2 ? 0 : e + 1];
+            if (outv[a] >= 0 || inv[b] >= 0) return 0;  /* not a simple cycle */
+            outv[a] = H; inv[b] = H;
+            hc[H] = c; he[H] = e; ++H;
+        }
     }
-    return 0;
+    if (H < 3) return 0;
+    /* cycle order from edge 0 (smallest key: c ascending, then e) */
+    int cur = 0;
+    for (int k = 0; k < H; ++k) {
+        if (cur < 0 || (k > 0 && cur == 0)) return 0;
+        ord[k] = cur;
+        cur = outv[E->fv[hc[cur]][he[cur] == 2 ? 0 : he[cur] + 1]];
+    }
+    if (cur != 0) return 0;
+    if (H > E->nfree + (EPA_MAXF - E->nf)) return 0;
+    const double fdmin = E->fd[best];
+    for (int k = 0; k < H; ++k) {
+        const int f = k < E->nfree ? E->freel[E->nfree - 1 - k] : E->nf + (k - E->nfree);
+        const int h = ord[k], c = hc[h], e = he[h];
+        const int a = E->fv[c][e], b = E->fv[c][e == 2 ? 0 : e + 1];
+        double e1[3], e2[3], nn[3], fn[3];
+        sub3(E->V[b].w, E->V[a].w, e1);
+        sub3(w, E->V[a].w, e2);
+        cross3(e1, e2, nn);
+        const double L = norm3(nn);
+        if (!(L > 1e-300)) return 0;
+        for (int i = 0; i < 3; ++i) fn[i] = nn[i] / L;
+        const double fd = dot3(fn, E->V[a].w);
+        if (fd < -1e-12 || fd < fdmin - 1e-12) return 0;
+        slot[k] = f;
+    }
+    /* commit */
+    for (int k = 0; k < H; ++k) {
+        const int f = slot[k], h = ord[k], c = hc[h], e = he[h];
+        const int a = E->fv[c][e], b = E->fv[c][e == 2 ? 0 : e + 1];
+        double e1[3], e2[3], nn[3];
+        sub3(E->V[b].w, E->V[a].w, e1);
+        sub3(w, E->V[a].w, e2);
+        cross3(e1, e2, nn);
+        const double L = norm3(nn);
+        for (int i = 0; i < 3; ++i) E->fn[f][i] = nn[i] / L;
+        E->fd[f] = dot3(E->fn[f], E->V[a].w);
+        E->fv[f][0] = a; E->fv[f][1] = b; E->fv[f][2] = wi;
+        /* edge 0 faces the outer neighbour, edge 1 the next new face, edge 2 the previous */
+        const int g = E->ff[c][e], ge = E->fe[c][e];
+        E->ff[f][0] = g; E->fe[f][0] = ge;
+        E->ff[g][ge] = f; E->fe[g][ge] = 0;
+        E->ff[f][1] = slot[(k + 1) % H]; E->fe[f][1] = 2;
+        E->ff[f][2] = slot[(k + H - 1) % H]; E->fe[f][2] = 1;
+    }
+    const int nf0 = E->nf, nfree0 = E->nfree > H ? E->nfree - H : 0;
+    if (H > E->nfree) E->nf += H - E->nfree;
+    E->nfree = nfree0;
+    for (int c = 0; c < nf0; ++c)
+        if (inC[c] && c != best) { E->alive[c] = 0; E->freel[E->nfree++] = c; }
+    E->alive[best] = 0;
+    E->freel[E->nfree++] = best;
+    for (int k = 0; k < H; ++k) E->alive[slot[k]] = 1;
+    return 1;
 }
 
 static double epa(const Shape* A, const Shape* B, SV* S, int ns, double* pA, double* pB) {
     static const double dirs[6][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}, {-1, 0, 0}, {0, -1, 0}, {0, 0, -1}};
     static __thread Epa E;
-    E.nv = ns; E.nf = 0; E.pass = 0; E.fail = 0; E.nfree = 0; E.nnew = 0; E.fdmin = -INFINITY;
+    E.nv = ns; E.nf = 0; E.fail = 0; E.nfree = 0;
     for (int i = 0; i < ns; ++i) E.V[i] = S[i];
     for (int di = 0; di < 6 && E.nv < 4; ++di) {
         SV w;
@@ -633,21 +703,10 @@ static double epa(const Shape* A, const Shape* B, SV* S, int ns, double* pA, dou
             if (dupv) break;
             int wi = E.nv;
             E.V[E.nv++] = w;
-            E.pass++;
-            E.hcf = -1; E.hff = -1; E.hnf = 0; E.ndead = 0; E.nnew = 0; E.fdmin = E.fd[best];
-            E.fpass[best] = E.pass;
-            int valid = 1;
-            for (int j = 0; j < 3 && valid; ++j) valid = epa_expand(&E, wi, E.ff[best][j], E.fe[best][j]);
-            if (!valid || E.hnf < 3 || E.fail) {  /* roll back to the last closed polytope */
-                for (int i = 0; i < E.nnew; ++i) E.alive[E.newl[i]] = 0;
-                for (int i = 0; i < E.ndead; ++i) E.alive[E.deadl[i]] = 1;
+            if (!epa_grow_canon(&E, wi, best)) {  /* rolled back: the last closed polytope */
                 E.nv--;
                 break;
             }
-            epa_bind(&E, E.hcf, 1, E.hff, 2);
-            E.alive[best] = 0;
-            for (int i = 0; i < E.ndead; ++i) E.freel[E.nfree++] = E.deadl[i];
-            E.freel[E.nfree++] = best;
         }
     }
     double bd = INFINITY;

@@ -1,0 +1,50 @@
+"""The task kernel's narrow phase on the GPU, pair by pair: GJK and the wave
+form of EPA (epa_run_wave / epa_grow_wave, the functions task_stage.hpp
+runs) on one wavefront per random shape pair (tests/gpu_narrow.hip), against
+the oracle's raw GJK / EPA (oracle/drc_oracle.c epa_grow_canon: the same
+expansion rule).  About half the pairs penetrate."""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+from test_narrow_host import oracle_dist, random_pairs
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pytestmark = pytest.mark.gpu
+
+
+def _run(pairs):
+    so = os.path.join(ROOT, "tests", "_narrow_gpu.so")
+    if not os.path.exists(so):
+        raise RuntimeError("tests/_narrow_gpu.so missing: run build.sh")
+    lib = C.CDLL(so)
+    buf = np.zeros((len(pairs), 32))
+    for i, (ta, TA, pa, tb, TB, pb) in enumerate(pairs):
+        buf[i] = np.concatenate([[ta], TA, pa, [tb], TB, pb])
+    out = np.zeros((len(pairs), 8))
+    dp = lambda a: a.ctypes.data_as(C.POINTER(C.c_double))
+    assert lib.drc_test_narrow(dp(buf), C.c_int(len(pairs)), dp(out)) == 0
+    return out
+
+
+def test_gpu_gjk_epa_match_oracle():
+    # no sphere pairs: those take the closed forms in the kernels
+    pairs = [p for p in random_pairs(6000, 23) if p[0] != 0 and p[3] != 0]
+    dev = _run(pairs)
+    ref = oracle_dist(pairs)
+    pen = dev[:, 7] == 1
+    assert pen.sum() > 800 and (~pen).sum() > 800
+    assert np.array_equal(pen, ref[:, 0] < 0)
+    err = np.abs(dev[:, 0] - ref[:, 0])
+    # separated: both GJKs stop at a 1e-9 support gap; penetrating: the same
+    # expansion decisions, so depths agree to rounding unless rounding flips a
+    # step, and both stop within the EPA tolerance (1e-6) of the depth
+    assert err[~pen].max() <= 2e-9, err[~pen].max()
+    assert err[pen].max() <= 2e-6, err[pen].max()
+    assert np.mean(err[pen] <= 1e-12) >= 0.95, np.mean(err[pen] <= 1e-12)
+    sep = dev[:, 4:7] - dev[:, 1:4]
+    sep_ref = ref[:, 4:7] - ref[:, 1:4]
+    serr = np.abs(sep - sep_ref).max(axis=1)
+    assert np.quantile(serr[pen], 0.9) <= 1e-9, np.quantile(serr[pen], 0.9)
