@@ -1490,6 +1490,181 @@ __device__ __noinline__ int qp_scale_regs(const KParams& kp, double* S) {
   return DRC_STATUS_MAX_ITER;
 }
 
+// The Schur-complement register ADMM loop (QD::schur shapes), out of line so
+// its register file holds only the loop's state: inlined into the kernel, the
+// values live across it (assembly, scaling, polish) pushed it into VGPR and
+// SGPR spills inside the iteration.  Reads its parameters from the LDS copy
+// kpl.  Returns the iteration count as qp_admm's loop leaves it.
+template <class QD>
+__device__ __noinline__ int admm_loop_schur(const KParams& kpl, double* S, int* status_out) {
+  using GL = Grp<QD::gs>;
+  const int l = GL::lane();
+  const KParams& kp = kpl;
+  double *qq = S + kp.oQ, *ab = S + kp.oAB, *lo = S + kp.oL, *up = S + kp.oU;
+  double *x = S + kp.oX, *z = S + kp.oZ, *y = S + kp.oY, *dy = S + kp.oDY;
+  const double* rv = S + kp.oRho;
+  const double sig = kp.s.sigma, al = kp.s.alpha;
+  const int max_iter = kp.s.max_iter, check_every = kp.s.check_termination;
+  const int adapt_every = kp.s.adaptive_rho && kp.s.adaptive_rho_interval > 0 ? kp.s.adaptive_rho_interval : 0;
+  int status = *status_out;
+  int it;
+  PHG_DECL
+  // Lane roles: l < NP core variable l (and its bound row); NP + r < NP + NG:
+  // G row r together with its auxiliary variable a(r) and that variable's
+  // bound row.  R[] holds, on core lanes, row l of S^-1 then column l of
+  // G_c; on row lanes, row r of G_c S^-1.  Per iteration:
+  //   rows: t_a = r_a / d_a, u_r = w_r - rho_r g_r t_a       (w = rho z - y)
+  //   core: r'_c = sigma x_c - q_c + ab_c w_b + sum_r G_rc u_r   (NG broadcasts)
+  //   core: x~_c = S^-1 r';  rows: v_r = G_r,c x~_c = (G_c S^-1)_r r'   (NP broadcasts)
+  //   rows: x~_a = t_a - coef_r v_r,  (G x~)_r = v_r + g_r x~_a
+  constexpr int NX = QD::nx, NG = QD::ng, NP = QD::np;
+  static_assert(NP + NG <= QD::gs, "one lane per core variable and per G row");
+  const double* Si = S + kp.oU0;
+  const double* GS = Si + NP * NP;
+  const double* dv = GS + NG * NP;
+  const double* cf = dv + NG;
+  const int* aux = reinterpret_cast<const int*>(cf + 2 * NG);
+  const double* G = S + kp.oG;
+  double R[NP + NG];
+  const bool hc = l < NP, hr = l >= NP && l < NP + NG;
+  const int rr_ = hr ? l - NP : 0, lc_ = hc ? l : 0;
+  auto load_regs = [&]() {
+    if (hc) {
+#pragma unroll
+      for (int c = 0; c < NP; ++c) R[c] = Si[lc_ * NP + c];
+#pragma unroll
+      for (int i = 0; i < NG; ++i) R[NP + i] = G[i * NX + lc_];
+    } else {
+#pragma unroll
+      for (int c = 0; c < NP; ++c) R[c] = GS[rr_ * NP + c];
+#pragma unroll
+      for (int i = 0; i < NG; ++i) R[NP + i] = 0.0;
+    }
+  };
+  load_regs();
+  PHG(25);
+  PH_ACC(tchk);
+  const int a_ = hr ? aux[rr_] : -1;           // auxiliary variable of row r (or -1)
+  const bool ha = a_ >= 0;
+  const int ia = ha ? a_ : 0, ig = NX + rr_;   // its bound row, the G row
+  // core lane: its bound row; row lane: the G row and the aux bound row
+  const double ab_c = ab[lc_], q_c = qq[lc_], lo_c = lo[lc_], up_c = up[lc_];
+  const double g_r = ha ? G[rr_ * NX + ia] : 0.0, ab_a = ab[ia], q_a = qq[ia];
+  const double lo_a = lo[ia], up_a = up[ia], lo_g = lo[ig], up_g = up[ig];
+  double d_r = dv[rr_], c_r = cf[rr_];
+  double rc = rv[lc_], ra = rv[ia], rg = rv[ig];
+  double irc = 1.0 / rc, ira = 1.0 / ra, irg = 1.0 / rg;  // y / rho as a product in the loop
+  double xc = 0, zc = 0, yc = 0, dyc = 0, xa = 0, za = 0, ya = 0, dya = 0, zg = 0, yg = 0, dyg = 0;
+  for (it = 1; it <= max_iter; ++it) {
+    double u = 0, ta = 0, loc = 0;
+    if (hr) {
+      const double wg = rg * zg - yg;
+      if (ha) {
+        const double r_a = sig * xa - q_a + ab_a * (ra * za - ya) + g_r * wg;
+        ta = r_a * d_r;  // d_r holds 1 / d_a
+        u = wg - rg * g_r * ta;
+      } else {
+        u = wg;
+      }
+    }
+    if (hc) loc = sig * xc - q_c + ab_c * (rc * zc - yc);
+    double r0 = 0, r1 = 0;
+    static_for<NG>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      const double ui = GL::template bcastc<NP + i>(u);
+      if constexpr (i & 1) r1 += R[NP + i] * ui;
+      else r0 += R[NP + i] * ui;
+    });
+    const double rp = loc + (r0 + r1);
+    double s0 = 0, s1 = 0;
+    static_for<NP>([&](auto C) {
+      constexpr int c = decltype(C)::value;
+      const double rpc = GL::template bcastc<c>(rp);
+      if constexpr (c & 1) s1 += R[c] * rpc;
+      else s0 += R[c] * rpc;
+    });
+    const double sv = s0 + s1;  // core: x~_c; row: v_r = G_r,c x~_c
+    if (hc) {
+      const double zr = al * ab_c * sv + (1 - al) * zc;
+      double zn = zr + yc * irc;
+      zn = fmin(fmax(zn, lo_c), up_c);
+      dyc = rc * (zr - zn);
+      yc += dyc;
+      zc = zn;
+      xc = al * sv + (1 - al) * xc;
+    }
+    if (hr) {
+      const double xta = ha ? ta - c_r * sv : 0.0;
+      {  // G row
+        const double zr = al * (sv + g_r * xta) + (1 - al) * zg;
+        double zn = zr + yg * irg;
+        zn = fmin(fmax(zn, lo_g), up_g);
+        dyg = rg * (zr - zn);
+        yg += dyg;
+        zg = zn;
+      }
+      if (ha) {  // bound row of the aux variable
+        const double zr = al * ab_a * xta + (1 - al) * za;
+        double zn = zr + ya * ira;
+        zn = fmin(fmax(zn, lo_a), up_a);
+        dya = ra * (zr - zn);
+        ya += dya;
+        za = zn;
+        xa = al * xta + (1 - al) * xa;
+      }
+    }
+    const bool check = check_every > 0 && it % check_every == 0;
+    const bool adapt = adapt_every > 0 && it % adapt_every == 0;
+    if (!(check || adapt) && it < max_iter) continue;
+    // publish the iterate for the (LDS) residual / polish / rho code
+    if (hc) {
+      x[l] = xc;
+      z[l] = zc;
+      y[l] = yc;
+      dy[l] = dyc;
+    }
+    if (hr) {
+      z[ig] = zg;
+      y[ig] = yg;
+      dy[ig] = dyg;
+      if (ha) {
+        x[ia] = xa;
+        z[ia] = za;
+        y[ia] = ya;
+        dy[ia] = dya;
+      }
+    }
+    wsync();
+    if (!(check || adapt)) continue;  // last iteration: published for the output
+    PH_STAMP(tc0);
+    const int act = admm_check<QD>(kpl, S, it, check, adapt, &status);
+    PH_ACC_SINCE(tchk, tc0);
+    if (act == 2) break;
+    load_regs();  // S^-1 / rho may have changed, the iterate may be polished
+    d_r = dv[rr_];
+    c_r = cf[rr_];
+    rc = rv[lc_];
+    ra = rv[ia];
+    rg = rv[ig];
+    irc = 1.0 / rc;
+    ira = 1.0 / ra;
+    irg = 1.0 / rg;
+    xc = x[lc_];
+    zc = z[lc_];
+    yc = y[lc_];
+    xa = x[ia];
+    za = z[ia];
+    ya = y[ia];
+    zg = z[ig];
+    yg = y[ig];
+  }
+  PHG(26);
+  PH_ADD(27, tchk);        // termination checks out of the loop's slot
+  PH_ADD(26, 0ull - tchk);
+  *status_out = status;
+  return it;
+}
+
 // rho, K^-1 and the ADMM iterations (+ polish); returns the status
 template <class QD>
 __device__ __forceinline__ int qp_admm(const KParams& kp, const KParams& kpl, double* S, int* iters_out) {
@@ -1520,158 +1695,7 @@ __device__ __forceinline__ int qp_admm(const KParams& kp, const KParams& kpl, do
   const double sig = kp.s.sigma, al = kp.s.alpha;
   int it;
   if constexpr (QD::schur) {
-    // Lane roles: l < NP core variable l (and its bound row); NP + r < NP + NG:
-    // G row r together with its auxiliary variable a(r) and that variable's
-    // bound row.  R[] holds, on core lanes, row l of S^-1 then column l of
-    // G_c; on row lanes, row r of G_c S^-1.  Per iteration:
-    //   rows: t_a = r_a / d_a, u_r = w_r - rho_r g_r t_a       (w = rho z - y)
-    //   core: r'_c = sigma x_c - q_c + ab_c w_b + sum_r G_rc u_r   (NG broadcasts)
-    //   core: x~_c = S^-1 r';  rows: v_r = G_r,c x~_c = (G_c S^-1)_r r'   (NP broadcasts)
-    //   rows: x~_a = t_a - coef_r v_r,  (G x~)_r = v_r + g_r x~_a
-    constexpr int NX = QD::nx, NG = QD::ng, NP = QD::np;
-    static_assert(NP + NG <= QD::gs, "one lane per core variable and per G row");
-    const double* Si = S + kp.oU0;
-    const double* GS = Si + NP * NP;
-    const double* dv = GS + NG * NP;
-    const double* cf = dv + NG;
-    const int* aux = reinterpret_cast<const int*>(cf + 2 * NG);
-    const double* G = S + kp.oG;
-    double R[NP + NG];
-    const bool hc = l < NP, hr = l >= NP && l < NP + NG;
-    const int rr_ = hr ? l - NP : 0, lc_ = hc ? l : 0;
-    auto load_regs = [&]() {
-      if (hc) {
-#pragma unroll
-        for (int c = 0; c < NP; ++c) R[c] = Si[lc_ * NP + c];
-#pragma unroll
-        for (int i = 0; i < NG; ++i) R[NP + i] = G[i * NX + lc_];
-      } else {
-#pragma unroll
-        for (int c = 0; c < NP; ++c) R[c] = GS[rr_ * NP + c];
-#pragma unroll
-        for (int i = 0; i < NG; ++i) R[NP + i] = 0.0;
-      }
-    };
-    load_regs();
-    PHG(25);
-    PH_ACC(tchk);
-    const int a_ = hr ? aux[rr_] : -1;           // auxiliary variable of row r (or -1)
-    const bool ha = a_ >= 0;
-    const int ia = ha ? a_ : 0, ig = NX + rr_;   // its bound row, the G row
-    // core lane: its bound row; row lane: the G row and the aux bound row
-    const double ab_c = ab[lc_], q_c = qq[lc_], lo_c = lo[lc_], up_c = up[lc_];
-    const double g_r = ha ? G[rr_ * NX + ia] : 0.0, ab_a = ab[ia], q_a = qq[ia];
-    const double lo_a = lo[ia], up_a = up[ia], lo_g = lo[ig], up_g = up[ig];
-    double d_r = dv[rr_], c_r = cf[rr_];
-    double rc = rv[lc_], ra = rv[ia], rg = rv[ig];
-    double irc = 1.0 / rc, ira = 1.0 / ra, irg = 1.0 / rg;  // y / rho as a product in the loop
-    double xc = 0, zc = 0, yc = 0, dyc = 0, xa = 0, za = 0, ya = 0, dya = 0, zg = 0, yg = 0, dyg = 0;
-    for (it = 1; it <= kp.s.max_iter; ++it) {
-      double u = 0, ta = 0, loc = 0;
-      if (hr) {
-        const double wg = rg * zg - yg;
-        if (ha) {
-          const double r_a = sig * xa - q_a + ab_a * (ra * za - ya) + g_r * wg;
-          ta = r_a * d_r;  // d_r holds 1 / d_a
-          u = wg - rg * g_r * ta;
-        } else {
-          u = wg;
-        }
-      }
-      if (hc) loc = sig * xc - q_c + ab_c * (rc * zc - yc);
-      double r0 = 0, r1 = 0;
-      static_for<NG>([&](auto I) {
-        constexpr int i = decltype(I)::value;
-        const double ui = GL::template bcastc<NP + i>(u);
-        if constexpr (i & 1) r1 += R[NP + i] * ui;
-        else r0 += R[NP + i] * ui;
-      });
-      const double rp = loc + (r0 + r1);
-      double s0 = 0, s1 = 0;
-      static_for<NP>([&](auto C) {
-        constexpr int c = decltype(C)::value;
-        const double rpc = GL::template bcastc<c>(rp);
-        if constexpr (c & 1) s1 += R[c] * rpc;
-        else s0 += R[c] * rpc;
-      });
-      const double sv = s0 + s1;  // core: x~_c; row: v_r = G_r,c x~_c
-      if (hc) {
-        const double zr = al * ab_c * sv + (1 - al) * zc;
-        double zn = zr + yc * irc;
-        zn = fmin(fmax(zn, lo_c), up_c);
-        dyc = rc * (zr - zn);
-        yc += dyc;
-        zc = zn;
-        xc = al * sv + (1 - al) * xc;
-      }
-      if (hr) {
-        const double xta = ha ? ta - c_r * sv : 0.0;
-        {  // G row
-          const double zr = al * (sv + g_r * xta) + (1 - al) * zg;
-          double zn = zr + yg * irg;
-          zn = fmin(fmax(zn, lo_g), up_g);
-          dyg = rg * (zr - zn);
-          yg += dyg;
-          zg = zn;
-        }
-        if (ha) {  // bound row of the aux variable
-          const double zr = al * ab_a * xta + (1 - al) * za;
-          double zn = zr + ya * ira;
-          zn = fmin(fmax(zn, lo_a), up_a);
-          dya = ra * (zr - zn);
-          ya += dya;
-          za = zn;
-          xa = al * xta + (1 - al) * xa;
-        }
-      }
-      const bool check = kp.s.check_termination > 0 && it % kp.s.check_termination == 0;
-      const bool adapt = kp.s.adaptive_rho && kp.s.adaptive_rho_interval > 0 && it % kp.s.adaptive_rho_interval == 0;
-      if (!(check || adapt) && it < kp.s.max_iter) continue;
-      // publish the iterate for the (LDS) residual / polish / rho code
-      if (hc) {
-        x[l] = xc;
-        z[l] = zc;
-        y[l] = yc;
-        dy[l] = dyc;
-      }
-      if (hr) {
-        z[ig] = zg;
-        y[ig] = yg;
-        dy[ig] = dyg;
-        if (ha) {
-          x[ia] = xa;
-          z[ia] = za;
-          y[ia] = ya;
-          dy[ia] = dya;
-        }
-      }
-      wsync();
-      if (!(check || adapt)) continue;  // last iteration: published for the output
-      PH_STAMP(tc0);
-      const int act = admm_check<QD>(kpl, S, it, check, adapt, &status);
-      PH_ACC_SINCE(tchk, tc0);
-      if (act == 2) break;
-      load_regs();  // S^-1 / rho may have changed, the iterate may be polished
-      d_r = dv[rr_];
-      c_r = cf[rr_];
-      rc = rv[lc_];
-      ra = rv[ia];
-      rg = rv[ig];
-      irc = 1.0 / rc;
-      ira = 1.0 / ra;
-      irg = 1.0 / rg;
-      xc = x[lc_];
-      zc = z[lc_];
-      yc = y[lc_];
-      xa = x[ia];
-      za = z[ia];
-      ya = y[ia];
-      zg = z[ig];
-      yg = y[ig];
-    }
-    PHG(26);
-    PH_ADD(27, tchk);        // termination checks out of the loop's slot
-    PH_ADD(26, 0ull - tchk);
+    it = admm_loop_schur<QD>(kpl, S, &status);
   } else if constexpr (QD::reg) {
     constexpr int NX = QD::nx, NG = QD::ng;
     double Gc[NG], Kr[NX], GKr[NX];
