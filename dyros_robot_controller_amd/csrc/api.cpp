@@ -1003,7 +1003,7 @@ int drc_debug_lane_stage(drc_model* m, int enable) {
 int drc_debug_phase_cycles(unsigned long long* out, int reset) {
   for (int i = 0; i < 64; ++i) out[i] = 0;
   if (drc_amd::phase_cycles_task(out, reset) || drc_amd::phase_cycles_qp(out, reset) ||
-      drc_amd::phase_cycles_qpid(out, reset))
+      drc_amd::phase_cycles_qpid(out, reset) || drc_amd::phase_cycles_fused(out, reset))
     return DRC_ERR_HIP;
   return DRC_OK;
 }
