@@ -16,8 +16,12 @@
 
 namespace drc_amd {
 
+// Occupancy target of the fused kernel (waves per SIMD)
+#ifndef DRC_FUSED_WAVES
+#define DRC_FUSED_WAVES 2
+#endif
 template <class QD>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 8)))
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRC_FUSED_WAVES, 8)))
 fused_kernel(const DevModel* __restrict__ M0, const KParams kt, const KParams kq, const IO io) {
   extern __shared__ __attribute__((aligned(16))) double S[];
   __shared__ KParams kpl;  // LDS copy of the QP parameters for the out-of-line ADMM blocks

@@ -24,7 +24,14 @@ constexpr double kRhoMin = 1e-6, kRhoMax = 1e6, kRhoTol = 1e-4, kRhoEqRatio = 1e
 constexpr double kDivTol = 1e-30;
 
 // ------------------------------------------------------------ wave helpers
-__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+// opaque per call: lane-derived values (offsets, masks, per-lane pointers) are
+// recomputed where used instead of being hoisted out of the persistent
+// instance loops and spilled to scratch
+__device__ __forceinline__ int lane_id() {
+  int l = threadIdx.x & 63;
+  asm volatile("" : "+v"(l));
+  return l;
+}
 __device__ __forceinline__ void wsync() { __syncthreads(); }
 
 // Wave reductions: DPP within each row of 16 lanes (quad swaps, half-row
@@ -104,7 +111,11 @@ template <int GS>
 struct Grp {
   static_assert(GS == 64 || GS == 32, "lane groups of 32 or 64");
   static constexpr int size = GS;
-  static __device__ __forceinline__ int lane() { return threadIdx.x & (GS - 1); }
+  static __device__ __forceinline__ int lane() {  // opaque per call, as lane_id()
+    int l = threadIdx.x & (GS - 1);
+    asm volatile("" : "+v"(l));
+    return l;
+  }
   static __device__ __forceinline__ bool upper() { return GS == 32 && (threadIdx.x & 32); }
   static __device__ __forceinline__ unsigned long long ballot(bool p) {
     const unsigned long long m = __ballot(p);

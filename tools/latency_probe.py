@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--robot", default="fr3")
     ap.add_argument("--n", type=int, default=256)
     ap.add_argument("--solver", default="exact")
+    ap.add_argument("--batches", default="512,1024,2048,4096,8192")
     args = ap.parse_args()
     import torch
     import bench
@@ -62,12 +63,14 @@ def main():
     res["b1_total_us"] = q(a[:, 0] + a[:, 1])
     res["b1_worst"] = [[int(i), float(a[i, 0]), float(a[i, 1]), int(a[i, 2])]
                        for i in np.argsort(-(a[:, 0] + a[:, 1]))[:8]]
-    for nb in (512, 1024, 2048, 4096, 8192):
+    for nb in [int(v) for v in args.batches.split(",")]:
         sub = [t[:, :nb].contiguous() for t in (dq, dqd, dxt, dxdt)]
         it = torch.zeros(nb, dtype=torch.int32, device=dev)
         w, tk, tq = times(lambda: ctrl.QPIK_step_batch(*sub, link, iters=it), 10)
         res["batch_%d" % nb] = {"call_ms": w, "task_ms": tk, "qp_ms": tq, "solves_per_s": nb / (w * 1e-3),
                                 "iters_max": int(it.max().item())}
+        if nb <= args.n:  # the slowest of these instances alone on the GPU
+            res["batch_%d" % nb]["max_isolated_ms"] = float((a[:nb, 0] + a[:nb, 1]).max()) * 1e-3
     print(json.dumps(res))
 
 
