@@ -8,7 +8,10 @@ CSRC=dyros_robot_controller_amd/csrc
 OBJ=build/obj${DRC_VARIANT:+_$DRC_VARIANT}
 OUT=${DRC_OUT:-dyros_robot_controller_amd/libdrc_amd.so}
 mkdir -p "$OBJ"
-FLAGS="--offload-arch=gfx950 -O3 -fPIC -std=c++17 -Wall -Wno-unused-function $DRC_EXTRA_FLAGS"
+# -disable-machine-licm: the persistent instance loops would otherwise get the
+# FP64 constants of the math library and the stages hoisted into registers at
+# kernel entry, spilled to scratch and reloaded (from beyond L2) per instance
+FLAGS="--offload-arch=gfx950 -O3 -fPIC -std=c++17 -Wall -Wno-unused-function -mllvm -disable-machine-licm $DRC_EXTRA_FLAGS"
 pids=()
 for src in task_kernel.hip qp_kernel.hip fused_kernel.hip qpid_kernel.hip dynamics.hip api.cpp model.cpp; do
   $HIPCC $FLAGS -c $CSRC/$src -o "$OBJ/${src%.*}.o" &
