@@ -12,8 +12,12 @@ namespace drc_amd {
 
 // QP kernel: assembles and solves the QP of each instance from the task
 // record written by task_kernel.
+// Occupancy target (waves per SIMD): 3 (168 VGPRs) since the ADMM loop keeps
+// one register set per lane role (core / auxiliary variable) and fits without
+// spills in its iterations; the spills at this budget sit in the per-instance
+// prologue and around the every-25-iterations check
 #ifndef DRC_QP_WAVES
-#define DRC_QP_WAVES 2
+#define DRC_QP_WAVES 3
 #endif
 template <class QD>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRC_QP_WAVES, 8)))

@@ -1547,27 +1547,33 @@ __device__ __noinline__ int admm_loop_schur(const KParams& kpl, double* S, int* 
   const int a_ = hr ? aux[rr_] : -1;           // auxiliary variable of row r (or -1)
   const bool ha = a_ >= 0;
   const int ia = ha ? a_ : 0, ig = NX + rr_;   // its bound row, the G row
-  // core lane: its bound row; row lane: the G row and the aux bound row
-  const double ab_c = ab[lc_], q_c = qq[lc_], lo_c = lo[lc_], up_c = up[lc_];
-  const double g_r = ha ? G[rr_ * NX + ia] : 0.0, ab_a = ab[ia], q_a = qq[ia];
-  const double lo_a = lo[ia], up_a = up[ia], lo_g = lo[ig], up_g = up[ig];
+  // The lane's variable v (with its bound row): the core variable on a core
+  // lane, the auxiliary variable on a row lane that has one.  A lane is never
+  // both, so the two share one register set (same update formulas; fewer
+  // registers live across the loop and one code path instead of two)
+  const bool hv = hc || ha;
+  const int iv = hc ? lc_ : ia;
+  const double ab_v = ab[iv], q_v = qq[iv], lo_v = lo[iv], up_v = up[iv];
+  const double g_r = ha ? G[rr_ * NX + ia] : 0.0, lo_g = lo[ig], up_g = up[ig];
   double d_r = dv[rr_], c_r = cf[rr_];
-  double rc = rv[lc_], ra = rv[ia], rg = rv[ig];
-  double irc = 1.0 / rc, ira = 1.0 / ra, irg = 1.0 / rg;  // y / rho as a product in the loop
-  double xc = 0, zc = 0, yc = 0, dyc = 0, xa = 0, za = 0, ya = 0, dya = 0, zg = 0, yg = 0, dyg = 0;
+  double r_v = rv[iv], rg = rv[ig];
+  double ir_v = 1.0 / r_v, irg = 1.0 / rg;  // y / rho as a product in the loop
+  double xv = 0, zv = 0, yv = 0, dyv = 0, zg = 0, yg = 0, dyg = 0;
   for (it = 1; it <= max_iter; ++it) {
-    double u = 0, ta = 0, loc = 0;
+    // core: r'_c's own term; aux: r_a before the G row's share
+    const double tv = hv ? sig * xv - q_v + ab_v * (r_v * zv - yv) : 0.0;
+    double u = 0, ta = 0;
     if (hr) {
       const double wg = rg * zg - yg;
       if (ha) {
-        const double r_a = sig * xa - q_a + ab_a * (ra * za - ya) + g_r * wg;
+        const double r_a = tv + g_r * wg;
         ta = r_a * d_r;  // d_r holds 1 / d_a
         u = wg - rg * g_r * ta;
       } else {
         u = wg;
       }
     }
-    if (hc) loc = sig * xc - q_c + ab_c * (rc * zc - yc);
+    const double loc = hc ? tv : 0.0;
     double r0 = 0, r1 = 0;
     static_for<NG>([&](auto I) {
       constexpr int i = decltype(I)::value;
@@ -1584,55 +1590,39 @@ __device__ __noinline__ int admm_loop_schur(const KParams& kpl, double* S, int* 
       else s0 += R[c] * rpc;
     });
     const double sv = s0 + s1;  // core: x~_c; row: v_r = G_r,c x~_c
-    if (hc) {
-      const double zr = al * ab_c * sv + (1 - al) * zc;
-      double zn = zr + yc * irc;
-      zn = fmin(fmax(zn, lo_c), up_c);
-      dyc = rc * (zr - zn);
-      yc += dyc;
-      zc = zn;
-      xc = al * sv + (1 - al) * xc;
+    const double xta = ha ? ta - c_r * sv : 0.0;  // aux: x~_a
+    if (hv) {  // the variable's bound row: z~ = ab x~, relaxation, projection, dual update
+      const double xin = hc ? sv : xta;
+      const double zr = al * ab_v * xin + (1 - al) * zv;
+      double zn = zr + yv * ir_v;
+      zn = fmin(fmax(zn, lo_v), up_v);
+      dyv = r_v * (zr - zn);
+      yv += dyv;
+      zv = zn;
+      xv = al * xin + (1 - al) * xv;
     }
-    if (hr) {
-      const double xta = ha ? ta - c_r * sv : 0.0;
-      {  // G row
-        const double zr = al * (sv + g_r * xta) + (1 - al) * zg;
-        double zn = zr + yg * irg;
-        zn = fmin(fmax(zn, lo_g), up_g);
-        dyg = rg * (zr - zn);
-        yg += dyg;
-        zg = zn;
-      }
-      if (ha) {  // bound row of the aux variable
-        const double zr = al * ab_a * xta + (1 - al) * za;
-        double zn = zr + ya * ira;
-        zn = fmin(fmax(zn, lo_a), up_a);
-        dya = ra * (zr - zn);
-        ya += dya;
-        za = zn;
-        xa = al * xta + (1 - al) * xa;
-      }
+    if (hr) {  // G row
+      const double zr = al * (sv + g_r * xta) + (1 - al) * zg;
+      double zn = zr + yg * irg;
+      zn = fmin(fmax(zn, lo_g), up_g);
+      dyg = rg * (zr - zn);
+      yg += dyg;
+      zg = zn;
     }
     const bool check = check_every > 0 && it % check_every == 0;
     const bool adapt = adapt_every > 0 && it % adapt_every == 0;
     if (!(check || adapt) && it < max_iter) continue;
     // publish the iterate for the (LDS) residual / polish / rho code
-    if (hc) {
-      x[l] = xc;
-      z[l] = zc;
-      y[l] = yc;
-      dy[l] = dyc;
+    if (hv) {
+      x[iv] = xv;
+      z[iv] = zv;
+      y[iv] = yv;
+      dy[iv] = dyv;
     }
     if (hr) {
       z[ig] = zg;
       y[ig] = yg;
       dy[ig] = dyg;
-      if (ha) {
-        x[ia] = xa;
-        z[ia] = za;
-        y[ia] = ya;
-        dy[ia] = dya;
-      }
     }
     wsync();
     if (!(check || adapt)) continue;  // last iteration: published for the output
@@ -1643,18 +1633,13 @@ __device__ __noinline__ int admm_loop_schur(const KParams& kpl, double* S, int* 
     load_regs();  // S^-1 / rho may have changed, the iterate may be polished
     d_r = dv[rr_];
     c_r = cf[rr_];
-    rc = rv[lc_];
-    ra = rv[ia];
+    r_v = rv[iv];
     rg = rv[ig];
-    irc = 1.0 / rc;
-    ira = 1.0 / ra;
+    ir_v = 1.0 / r_v;
     irg = 1.0 / rg;
-    xc = x[lc_];
-    zc = z[lc_];
-    yc = y[lc_];
-    xa = x[ia];
-    za = z[ia];
-    ya = y[ia];
+    xv = x[iv];
+    zv = z[iv];
+    yv = y[iv];
     zg = z[ig];
     yg = y[ig];
   }
