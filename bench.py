@@ -42,7 +42,7 @@ from dyros_robot_controller_amd import dist as ddist  # noqa: E402  (no torch / 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 FP64_VECTOR_PEAK_TFS = 78.6    # AMD spec, FP64 vector
 CLOCK_GHZ = 2.4                # MI355X peak engine clock (MI355X_MICROARCH.md)
-WAVE_SLOTS = 256 * 4 * 2       # CUs x SIMDs x waves per SIMD at the kernels' 256-VGPR budget
+WAVE_SLOTS = 256 * 4 * 2       # CUs x SIMDs x waves per SIMD of the task kernel (256 VGPRs, ~19 KB LDS; QP kernel: 3)
 DEFAULT_BATCH = {"fr3": 65536, "ur5e": 65536, "husky_fr3": 16384, "xls_fr3": 65536, "caster_fr3": 65536}
 METRIC = "QP-IK solves/s (FR3 7-DoF, batch 65k) + achieved HBM GB/s vs peak"
 
@@ -424,8 +424,9 @@ def extras(torch, args, rd, mod, robot, link, q, qd, xt, xdt, dq, dqd, dxt, dxdt
         "instance_latency_us": 1e6 * lat, "call_us": 1e3 * tw.value / max(nc.value, 1), "wave_slots": WAVE_SLOTS,
         "solves_per_s": roof, "frac": line["value"] / roof,
         "note": "mean over the batch's first 32 instances, each alone on the GPU (B = 1 calls, kernel durations by "
-                "HIP events): a wave-per-instance design with WAVE_SLOTS instances in flight (two 256-VGPR waves per "
-                "SIMD) cannot beat WAVE_SLOTS / latency if instances ran at their isolated latency"}
+                "HIP events): a wave-per-instance design with WAVE_SLOTS instances in flight (two task-kernel waves per "
+                "SIMD; the QP kernel runs three since D20, so this roof is approximate) cannot beat WAVE_SLOTS / "
+                "latency if instances ran at their isolated latency"}
 
 
 if __name__ == "__main__":
