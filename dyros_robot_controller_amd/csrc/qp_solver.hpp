@@ -1390,7 +1390,7 @@ __device__ __forceinline__ int qp_scale(const KParams& kp, double* S) {
 // Ruiz factors move by v_readlane.  Same operations in the same order as
 // qp_scale (bit-identical results); P, G, q, D, E written back at the end.
 template <class QD>
-__device__ __noinline__ int qp_scale_regs(const KParams& kp, double* S) {
+__device__ __forceinline__ int qp_scale_regs(const KParams& kp, double* S) {
   using GL = Grp<QD::gs>;
   constexpr int NX = QD::nx, NG = QD::ng, NP = QD::np, M = NX + NG;
   const int l = GL::lane();
@@ -1428,18 +1428,22 @@ __device__ __noinline__ int qp_scale_regs(const KParams& kp, double* S) {
 #pragma unroll
     for (int j = 0; j < NX; ++j) sg = fmax(sg, fabs(Grow[j]));
     const double EtG = 1.0 / sqrt(clampf(sg));
-    double DtA[NX], EtGA[NG];
-    static_for<NX>([&](auto C) { DtA[decltype(C)::value] = GL::template bcastc<decltype(C)::value>(Dt); });
-    static_for<NG>([&](auto I) { EtGA[decltype(I)::value] = GL::template bcastc<decltype(I)::value>(EtG); });
-    if (hp)
-#pragma unroll
-      for (int c = 0; c < NP; ++c) Prow[c] *= Dt * DtA[c];
-    if (hx)
-#pragma unroll
-      for (int i = 0; i < NG; ++i) Gcol[i] *= EtGA[i] * Dt;
-    if (hg)
-#pragma unroll
-      for (int j = 0; j < NX; ++j) Grow[j] *= EtG * DtA[j];
+    // the broadcast factors are used as they arrive (not gathered into
+    // per-lane arrays: 39 doubles more would not fit the QP kernel's 168-VGPR
+    // budget and spilled); same products in the same order
+    static_for<NX>([&](auto C) {
+      constexpr int c = decltype(C)::value;
+      const double dc = GL::template bcastc<c>(Dt);
+      if constexpr (c < NP) {
+        if (hp) Prow[c] *= Dt * dc;
+      }
+      if (hg) Grow[c] *= EtG * dc;
+    });
+    static_for<NG>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      const double ei = GL::template bcastc<i>(EtG);
+      if (hx) Gcol[i] *= ei * Dt;
+    });
     if (hx) {
       abl *= Et * Dt;
       ql *= Dt;
