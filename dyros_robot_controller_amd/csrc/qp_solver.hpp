@@ -1494,73 +1494,106 @@ __device__ __forceinline__ int qp_scale_regs(const KParams& kp, double* S) {
   return DRC_STATUS_MAX_ITER;
 }
 
+// Addresses and lane-role indices of the Schur ADMM loop, derived from an
+// opaque copy of the parameter pointer and lane index: built once for the
+// loop's setup and again where the (every check_termination iterations)
+// publish and reload need them, so none of it stays live through the
+// iterations, where at the QP kernel's 168-VGPR budget it was spilled before
+// the loop and reloaded at every check (D20)
+template <class QD>
+struct SchurLanes {
+  static constexpr int NX = QD::nx, NG = QD::ng, NP = QD::np;
+  double *qq, *ab, *lo, *up, *x, *z, *y, *dy;
+  const double *rv, *Si, *GS, *dv, *cf, *G;
+  int l, rr, lc, ia, ig, iv;
+  bool hc, hr, ha, hv;
+  __device__ __forceinline__ SchurLanes(const KParams& kpl, double* S0) {
+    const KParams* kq = &kpl;
+    double* S = S0;
+    asm volatile("" : "+s"(kq), "+s"(S));
+    const KParams& kp = *kq;
+    l = Grp<QD::gs>::lane();
+    qq = S + kp.oQ; ab = S + kp.oAB; lo = S + kp.oL; up = S + kp.oU;
+    x = S + kp.oX; z = S + kp.oZ; y = S + kp.oY; dy = S + kp.oDY;
+    rv = S + kp.oRho;
+    Si = S + kp.oU0;
+    GS = Si + NP * NP;
+    dv = GS + NG * NP;
+    cf = dv + NG;
+    G = S + kp.oG;
+    const int* aux = reinterpret_cast<const int*>(cf + 2 * NG);
+    hc = l < NP;
+    hr = l >= NP && l < NP + NG;
+    rr = hr ? l - NP : 0;
+    lc = hc ? l : 0;
+    const int a_ = hr ? aux[rr] : -1;  // auxiliary variable of row r (or -1)
+    ha = a_ >= 0;
+    ia = ha ? a_ : 0;
+    ig = NX + rr;  // the G row
+    hv = hc || ha;
+    iv = hc ? lc : ia;
+  }
+  // lane l: row l of S^-1 then column l of G_c (core lanes); row r of G_c S^-1 (row lanes)
+  __device__ __forceinline__ void load(double (&R)[NP + NG]) const {
+    if (hc) {
+#pragma unroll
+      for (int c = 0; c < NP; ++c) R[c] = Si[lc * NP + c];
+#pragma unroll
+      for (int i = 0; i < NG; ++i) R[NP + i] = G[i * NX + lc];
+    } else {
+#pragma unroll
+      for (int c = 0; c < NP; ++c) R[c] = GS[rr * NP + c];
+#pragma unroll
+      for (int i = 0; i < NG; ++i) R[NP + i] = 0.0;
+    }
+  }
+};
+
 // The Schur-complement register ADMM loop (QD::schur shapes), out of line so
 // its register file holds only the loop's state: inlined into the kernel, the
 // values live across it (assembly, scaling, polish) pushed it into VGPR and
 // SGPR spills inside the iteration.  Reads its parameters from the LDS copy
 // kpl.  Returns the iteration count as qp_admm's loop leaves it.
+// Lane roles: l < NP core variable l (and its bound row); NP + r < NP + NG:
+// G row r together with its auxiliary variable a(r) and that variable's
+// bound row.  R[] holds, on core lanes, row l of S^-1 then column l of
+// G_c; on row lanes, row r of G_c S^-1.  Per iteration:
+//   rows: t_a = r_a / d_a, u_r = w_r - rho_r g_r t_a       (w = rho z - y)
+//   core: r'_c = sigma x_c - q_c + ab_c w_b + sum_r G_rc u_r   (NG broadcasts)
+//   core: x~_c = S^-1 r';  rows: v_r = G_r,c x~_c = (G_c S^-1)_r r'   (NP broadcasts)
+//   rows: x~_a = t_a - coef_r v_r,  (G x~)_r = v_r + g_r x~_a
 template <class QD>
 __device__ __noinline__ int admm_loop_schur(const KParams& kpl, double* S, int* status_out) {
   using GL = Grp<QD::gs>;
-  const int l = GL::lane();
   const KParams& kp = kpl;
-  double *qq = S + kp.oQ, *ab = S + kp.oAB, *lo = S + kp.oL, *up = S + kp.oU;
-  double *x = S + kp.oX, *z = S + kp.oZ, *y = S + kp.oY, *dy = S + kp.oDY;
-  const double* rv = S + kp.oRho;
   const double sig = kp.s.sigma, al = kp.s.alpha;
   const int max_iter = kp.s.max_iter, check_every = kp.s.check_termination;
   const int adapt_every = kp.s.adaptive_rho && kp.s.adaptive_rho_interval > 0 ? kp.s.adaptive_rho_interval : 0;
   int status = *status_out;
   int it;
   PHG_DECL
-  // Lane roles: l < NP core variable l (and its bound row); NP + r < NP + NG:
-  // G row r together with its auxiliary variable a(r) and that variable's
-  // bound row.  R[] holds, on core lanes, row l of S^-1 then column l of
-  // G_c; on row lanes, row r of G_c S^-1.  Per iteration:
-  //   rows: t_a = r_a / d_a, u_r = w_r - rho_r g_r t_a       (w = rho z - y)
-  //   core: r'_c = sigma x_c - q_c + ab_c w_b + sum_r G_rc u_r   (NG broadcasts)
-  //   core: x~_c = S^-1 r';  rows: v_r = G_r,c x~_c = (G_c S^-1)_r r'   (NP broadcasts)
-  //   rows: x~_a = t_a - coef_r v_r,  (G x~)_r = v_r + g_r x~_a
   constexpr int NX = QD::nx, NG = QD::ng, NP = QD::np;
+  (void)NX;
   static_assert(NP + NG <= QD::gs, "one lane per core variable and per G row");
-  const double* Si = S + kp.oU0;
-  const double* GS = Si + NP * NP;
-  const double* dv = GS + NG * NP;
-  const double* cf = dv + NG;
-  const int* aux = reinterpret_cast<const int*>(cf + 2 * NG);
-  const double* G = S + kp.oG;
   double R[NP + NG];
-  const bool hc = l < NP, hr = l >= NP && l < NP + NG;
-  const int rr_ = hr ? l - NP : 0, lc_ = hc ? l : 0;
-  auto load_regs = [&]() {
-    if (hc) {
-#pragma unroll
-      for (int c = 0; c < NP; ++c) R[c] = Si[lc_ * NP + c];
-#pragma unroll
-      for (int i = 0; i < NG; ++i) R[NP + i] = G[i * NX + lc_];
-    } else {
-#pragma unroll
-      for (int c = 0; c < NP; ++c) R[c] = GS[rr_ * NP + c];
-#pragma unroll
-      for (int i = 0; i < NG; ++i) R[NP + i] = 0.0;
-    }
-  };
-  load_regs();
-  PHG(25);
-  PH_ACC(tchk);
-  const int a_ = hr ? aux[rr_] : -1;           // auxiliary variable of row r (or -1)
-  const bool ha = a_ >= 0;
-  const int ia = ha ? a_ : 0, ig = NX + rr_;   // its bound row, the G row
   // The lane's variable v (with its bound row): the core variable on a core
   // lane, the auxiliary variable on a row lane that has one.  A lane is never
   // both, so the two share one register set (same update formulas; fewer
   // registers live across the loop and one code path instead of two)
-  const bool hv = hc || ha;
-  const int iv = hc ? lc_ : ia;
-  const double ab_v = ab[iv], q_v = qq[iv], lo_v = lo[iv], up_v = up[iv];
-  const double g_r = ha ? G[rr_ * NX + ia] : 0.0, lo_g = lo[ig], up_g = up[ig];
-  double d_r = dv[rr_], c_r = cf[rr_];
-  double r_v = rv[iv], rg = rv[ig];
+  bool hc, hr, ha, hv;
+  double ab_v, q_v, lo_v, up_v, g_r, lo_g, up_g, d_r, c_r, r_v, rg;
+  {
+    const SchurLanes<QD> L(kpl, S);
+    L.load(R);
+    hc = L.hc; hr = L.hr; ha = L.ha; hv = L.hv;
+    ab_v = L.ab[L.iv]; q_v = L.qq[L.iv]; lo_v = L.lo[L.iv]; up_v = L.up[L.iv];
+    g_r = ha ? L.G[L.rr * NX + L.ia] : 0.0;
+    lo_g = L.lo[L.ig]; up_g = L.up[L.ig];
+    d_r = L.dv[L.rr]; c_r = L.cf[L.rr];
+    r_v = L.rv[L.iv]; rg = L.rv[L.ig];
+  }
+  PHG(25);
+  PH_ACC(tchk);
   double ir_v = 1.0 / r_v, irg = 1.0 / rg;  // y / rho as a product in the loop
   double xv = 0, zv = 0, yv = 0, dyv = 0, zg = 0, yg = 0, dyg = 0;
   for (it = 1; it <= max_iter; ++it) {
@@ -1616,17 +1649,19 @@ __device__ __noinline__ int admm_loop_schur(const KParams& kpl, double* S, int* 
     const bool check = check_every > 0 && it % check_every == 0;
     const bool adapt = adapt_every > 0 && it % adapt_every == 0;
     if (!(check || adapt) && it < max_iter) continue;
-    // publish the iterate for the (LDS) residual / polish / rho code
-    if (hv) {
-      x[iv] = xv;
-      z[iv] = zv;
-      y[iv] = yv;
-      dy[iv] = dyv;
-    }
-    if (hr) {
-      z[ig] = zg;
-      y[ig] = yg;
-      dy[ig] = dyg;
+    {  // publish the iterate for the (LDS) residual / polish / rho code
+      const SchurLanes<QD> L(kpl, S);
+      if (hv) {
+        L.x[L.iv] = xv;
+        L.z[L.iv] = zv;
+        L.y[L.iv] = yv;
+        L.dy[L.iv] = dyv;
+      }
+      if (hr) {
+        L.z[L.ig] = zg;
+        L.y[L.ig] = yg;
+        L.dy[L.ig] = dyg;
+      }
     }
     wsync();
     if (!(check || adapt)) continue;  // last iteration: published for the output
@@ -1634,18 +1669,26 @@ __device__ __noinline__ int admm_loop_schur(const KParams& kpl, double* S, int* 
     const int act = admm_check<QD>(kpl, S, it, check, adapt, &status);
     PH_ACC_SINCE(tchk, tc0);
     if (act == 2) break;
-    load_regs();  // S^-1 / rho may have changed, the iterate may be polished
-    d_r = dv[rr_];
-    c_r = cf[rr_];
-    r_v = rv[iv];
-    rg = rv[ig];
-    ir_v = 1.0 / r_v;
-    irg = 1.0 / rg;
-    xv = x[iv];
-    zv = z[iv];
-    yv = y[iv];
-    zg = z[ig];
-    yg = y[ig];
+    {  // S^-1 / rho may have changed, the iterate may be polished
+      const SchurLanes<QD> L(kpl, S);
+      L.load(R);
+      // every loop constant re-read too, so none is live across the call
+      hc = L.hc; hr = L.hr; ha = L.ha; hv = L.hv;
+      ab_v = L.ab[L.iv]; q_v = L.qq[L.iv]; lo_v = L.lo[L.iv]; up_v = L.up[L.iv];
+      g_r = ha ? L.G[L.rr * NX + L.ia] : 0.0;
+      lo_g = L.lo[L.ig]; up_g = L.up[L.ig];
+      d_r = L.dv[L.rr];
+      c_r = L.cf[L.rr];
+      r_v = L.rv[L.iv];
+      rg = L.rv[L.ig];
+      ir_v = 1.0 / r_v;
+      irg = 1.0 / rg;
+      xv = L.x[L.iv];
+      zv = L.z[L.iv];
+      yv = L.y[L.iv];
+      zg = L.z[L.ig];
+      yg = L.y[L.ig];
+    }
   }
   PHG(26);
   PH_ADD(27, tchk);        // termination checks out of the loop's slot
