@@ -143,8 +143,11 @@ __device__ __forceinline__ void qpid_assemble(const DevModel* M, const KParams& 
 
 // QD: Dims<nx, ng, np, false> for the bundled robots' QPID shapes (loops
 // unroll, loads pipeline), Dims<0, 0, 0> otherwise.
+#ifndef DRC_QPID_WAVES
+#define DRC_QPID_WAVES 1
+#endif
 template <class QD>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 8)))
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRC_QPID_WAVES, 8)))
 qpid_kernel(const DevModel* __restrict__ M0, const KParams kp, const IO io) {
   extern __shared__ __attribute__((aligned(16))) double S[];
   __shared__ KParams kpl;
