@@ -5,4 +5,4 @@ for rep in 1 2; do for r in fr3 ur5e xls_fr3 husky_fr3; do for c in 2 3; do
   python3 -c "import json; d=json.load(open('gpurun_out/c_tmp.json')); print(json.dumps({'robot':'$r','chunks':$c,'value':d['value']}))" >> $out
 done; done; done
 cat $out
-bash tools/cache_pass.sh fr3
+
