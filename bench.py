@@ -61,8 +61,11 @@ def algorithmic_flops(robot, solver, q, qd, xt, xdt, n=256):
     sample of the same batch with the same settings and the kernels' pruned
     narrow phase (oracle min_distance_pruned -- same argmin as all pairs).
     + - * / sqrt count 1 each; sin / cos / atan2 / acos are reported apart.
-    The QP linear algebra is the dense reduced-KKT restatement (what the QP
-    kernel runs), so structural zeros of A are counted."""
+    ``flops_per_solve`` counts only the operations whose operands are all
+    nonzero: the oracle's QP linear algebra is dense (P^T P + A^T rho A at
+    n^2 m, dense 39 x 23 products per ADMM iteration), and its work on
+    structural zeros -- which OSQP's sparse KKT never does -- drops out.  The
+    dense count is reported beside it (``dense_flops_per_solve``)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     _, om, spec = O.load(robot)
@@ -74,10 +77,12 @@ def algorithmic_flops(robot, solver, q, qd, xt, xdt, n=256):
         try:
             O.flop_counts(reset=True)
             O.qpik_batch(om, par, pick(q), pick(qd), pick(xt), pick(xdt), nthreads=1)
-            fl, tr = O.flop_counts(reset=True)
+            fl, tr, nz = O.flop_counts(reset=True, nonzero=True)
         finally:
             O.set_pruned_narrow_phase(False)
-    return {"flops_per_solve": fl / len(idx), "transcendentals_per_solve": tr / len(idx),
+    return {"flops_per_solve": nz / len(idx), "dense_flops_per_solve": fl / len(idx),
+            "transcendentals_per_solve": tr / len(idx),
+            "rule": "operations with all operands nonzero (structural zeros of the dense restatement excluded)",
             "sample": "%d instances, every %d-th of the batch" % (len(idx), max(1, q.shape[1] // n)),
             "source": "oracle/count_build.cpp (counting build of oracle/drc_oracle.c, pruned narrow phase)"}
 
@@ -142,12 +147,14 @@ def cpu_baseline(robot, q, qd, xt, xdt, target_s=4.0, warmups=3, runs=5):
                       "%d timed runs after %d warm-ups" % (nc, n1, cores, runs, warmups)}
 
 
-def load_profile(name, robot, B):
-    """A committed profiles/ summary for this workload and batch, or None."""
+def load_profile(name, robot, B, build_id):
+    """A committed profiles/ counter summary for this workload and batch,
+    measured on THIS library build (its ``build_id`` equals drc_build_id()),
+    or None: a summary of another build is never attributed to this one."""
     try:
         with open(os.path.join(ROOT, "profiles", name)) as fh:
             d = json.load(fh)
-        if d.get("robot") == robot and int(d.get("batch")) == B:
+        if d.get("robot") == robot and int(d.get("batch")) == B and d.get("build_id") == build_id:
             return d
     except Exception:
         pass
@@ -208,6 +215,68 @@ def latency_b1(rd, robot, q, qd, xt, xdt, solver, calls=400, warmup=20):
             "cycle_budget_us": 1000.0}
 
 
+def BUNDLED_KIND(robot):
+    from dyros_robot_controller_amd import BUNDLED
+    return BUNDLED[robot]["kind"]
+
+
+def whole_job(ranks, tier_keys, backend):
+    """Whole-job fields of the bench line from the gathered per-rank rows
+    [rank, device, pci bus, wall, iters p99, iters max, non-solved,
+    instances, tier counts...]: iteration p99 / max are the max over ranks,
+    counts are sums; with more than one rank, each rank's row and the
+    transport."""
+    out = {"admm_iters_p99_max": [float(ranks[:, 4].max()), int(ranks[:, 5].max())],
+           "stress_tiers": {k: int(ranks[:, 8 + i].sum()) for i, k in enumerate(tier_keys)}}
+    if len(ranks) > 1:
+        out["ranks"] = [{"rank": int(r[0]), "device": int(r[1]), "pci_bus_id": int(r[2]), "wall_s": float(r[3]),
+                         "instances": int(r[7]), "non_solved": int(r[6]),
+                         "admm_iters_p99_max": [float(r[4]), int(r[5])]} for r in ranks]
+        out["backend"] = backend
+    return out
+
+
+def latency_cycle(robot, q, qd, solver, cycles=400, warmup=20):
+    """The reference's whole per-cycle call chain at B = 1
+    (examples/C++/src/fr3_controller.cpp:66-68,123-134 at 1 kHz,
+    examples/README.md:55): updateState -> getPose -> getVelocity ->
+    QPIKCubic -> moveJointTorqueStep(q + qdot* dt, qdot*), through the
+    pybind11 module with the reference's binding names (its C++ facade: the
+    getters share one drc_state_host round trip per state, the torque step
+    reads the cached M and g, QPIKCubic is one drc_qpik_host call).  Host wall
+    time per cycle: p50 / p99 / max; each cycle takes the next instance's state."""
+    sys.path.insert(0, os.path.join(ROOT, "dyros_robot_controller_amd", "python"))
+    import dyros_robot_controller_cpp_wrapper as drc
+    from dyros_robot_controller_amd import BUNDLED, robot_path
+    link, dt = BUNDLED[robot]["link"], 0.001
+    rd = drc.ManipulatorRobotData(robot_path(robot), robot_path(robot, "srdf"), "")
+    rc = drc.ManipulatorRobotController(dt, rd)
+    if solver != "exact":
+        rc.setExact(False)
+    ts, bad = [], 0
+    n = q.shape[1]
+    for k in range(warmup + cycles):
+        qk, qdk = np.ascontiguousarray(q[:, k % n]), np.ascontiguousarray(qd[:, k % n])
+        t0 = time.perf_counter()
+        rd.updateState(qk, qdk)
+        x = rd.getPose(link)
+        xdot = rd.getVelocity(link)
+        xt = x.copy()
+        xt[:3, 3] += (0.0, 0.1, 0.1)                      # fr3_controller.cpp:123-131
+        qdot_star = rc.QPIKCubic(xt, np.zeros(6), x, xdot, 0.3, 0.0, 3.0, link)
+        tau = rc.moveJointTorqueStep(qk + qdot_star * dt, qdot_star)
+        t1 = time.perf_counter()
+        if k >= warmup:
+            ts.append(t1 - t0)
+            bad += int(not np.all(np.isfinite(tau)))
+    ts = np.array(ts) * 1e6
+    return {"call": "updateState, getPose, getVelocity, QPIKCubic, moveJointTorqueStep (B = 1, pybind11 module "
+                    "dyros_robot_controller_cpp_wrapper over the C++ facade)",
+            "p50_us": float(np.percentile(ts, 50)), "p99_us": float(np.percentile(ts, 99)),
+            "max_us": float(ts.max()), "cycles": cycles, "nonfinite_tau": bad, "cycle_budget_us": 1000.0,
+            "round_trips_per_cycle": 2}
+
+
 def dry_run(args):
     """Launcher / sharding / reduction rehearsal without a GPU (tests): every
     rank reports its shard through the same collectives the bench uses."""
@@ -219,9 +288,17 @@ def dry_run(args):
     B = args.batch or DEFAULT_BATCH[args.robot]
     offset, cnt = ddist.shard_global(rank, world, args.global_batch) if args.global_batch else ddist.shard(rank, B)
     wall, n_cnt, off_mean = ddist.reduce_stats(0.001 * (rank + 1), cnt, offset, world)
+    # the same per-rank rows and whole-job reduction as the GPU path, with
+    # rank-dependent stand-in values: iters p99 = rank + 1, max = 10 (rank + 1),
+    # non-solved = rank, tier counts (rank, 2 rank)
+    tier_keys = ["collision", "singular"]
+    ranks = ddist.gather_stats([rank, rank, -1, 0.001 * (rank + 1), rank + 1.0, 10.0 * (rank + 1), float(rank),
+                                float(cnt), float(rank), 2.0 * rank], world)
     if rank == 0:
-        print(json.dumps({"dry_run": True, "n_gpus": world, "ranks_reporting": world, "instances": int(n_cnt),
-                          "max_wall": wall, "mean_offset": off_mean}), flush=True)
+        line = {"dry_run": True, "n_gpus": world, "ranks_reporting": world, "instances": int(n_cnt),
+                "max_wall": wall, "mean_offset": off_mean}
+        line.update(whole_job(ranks, tier_keys, backend))
+        print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
@@ -309,6 +386,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
+    wall_local = wall
     step_event_ms = ev0.elapsed_time(ev1) / args.steps   # HIP events on the launch stream
     tw, tk, tq, nc = C.c_double(), C.c_double(), C.c_double(), C.c_int()
     _capi.check(_capi.lib().drc_debug_kernel_times(handle, C.byref(tw), C.byref(tk), C.byref(tq), C.byref(nc)))
@@ -319,8 +397,18 @@ def main():
     kernel_ms, task_ms, qp_ms = tw.value / ncall, tk.value / ncall, tq.value / ncall
     wall, n_bad, it_mean = ddist.reduce_stats(wall, float((status != 1).sum().item()),
                                               float(iters.double().mean().item()), world, red_dev)
+    # per-rank statistics, gathered whole-job: iteration p99 / max (max over
+    # ranks), stress-tier counts (sums), each rank's device and its timed wall
+    it_np = iters.cpu().numpy()
+    tier_keys = sorted(tiers)
+    props = torch.cuda.get_device_properties(dev)
+    per_rank = [rank, dev.index, getattr(props, "pci_bus_id", -1), wall_local,
+                float(np.percentile(it_np, 99)), float(it_np.max()), float((status != 1).sum().item()),
+                float(B)] + [float(tiers[k]) for k in tier_keys]
+    ranks = ddist.gather_stats(per_rank, world, red_dev)
 
     if rank == 0:
+        build = _capi.build_id()
         dof, act = rd.model.dof, rd.model.actuated_dof
         total = total_per_step * args.steps
         value = total / wall
@@ -328,11 +416,14 @@ def main():
         bps = algorithmic_bytes(dof, act)
         per_launch_bytes = bps * B
         achieved = per_launch_bytes / (kernel_ms * 1e-3) / 1e9
-        traffic = load_profile("pmc_traffic_%s.json" % robot, robot, B) or load_profile("pmc_traffic.json", robot, B)
+        # counter summaries are used only when measured on this very build
+        traffic = load_profile("pmc_traffic_%s.json" % robot, robot, B, build)
         alg = algorithmic_flops(robot, args.solver, q, qd, xt, xdt)
         fl = alg["flops_per_solve"] * B / (kernel_ms * 1e-3) / 1e12
         roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS, "traffic": traffic.get("hbm_bytes_per_step") if traffic else None,
+                "traffic_source": ("profiles/pmc_traffic_%s.json (build %s)" % (robot, build)) if traffic else
+                                  "no PMC summary of this build (%s) for this robot and batch" % build,
                 "kernel": "drc_qpik_batch call (task_kernel + qp_kernel per sub-batch, %d concurrent sub-batches)"
                           % args.chunks,
                 "bytes_per_solve": bps, "bytes_per_launch": per_launch_bytes,
@@ -340,7 +431,7 @@ def main():
                 "step_event_ms": step_event_ms,
                 "fp64_algorithmic": dict(alg, achieved_tflops=fl, peak_tflops=FP64_VECTOR_PEAK_TFS,
                                          frac=fl / FP64_VECTOR_PEAK_TFS)}
-        valu = load_profile("valu_counters_%s.json" % robot, robot, B)
+        valu = load_profile("valu_counters_%s.json" % robot, robot, B, build)
         if valu:   # counter-based FP64 work per call (tools/valu_summary.py over rocprofv3 --pmc passes)
             f = valu["fp64_flops_per_step"]
             eff = valu.get("lane_efficiency") or 0.0
@@ -350,9 +441,11 @@ def main():
                                  "issued_frac": issued / FP64_VECTOR_PEAK_TFS,
                                  "executed_frac": issued * eff / FP64_VECTOR_PEAK_TFS,
                                  "fp64_flops_issued_per_step": f, "lane_efficiency": eff,
+                                 "executed_flops_per_solve": f * eff / B,
+                                 "algorithmic_over_executed": alg["flops_per_solve"] / max(f * eff / B, 1e-30),
                                  "note": "issued counts 64 lanes per FP64 instruction; executed = issued x lane "
                                          "efficiency (active lanes); neither is algorithmic work",
-                                 "source": "profiles/valu_counters_%s.json" % robot}
+                                 "source": "profiles/valu_counters_%s.json (build %s)" % (robot, build)}
         line = {
             "metric": METRIC, "value": value, "unit": "solves/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": scaling,
@@ -366,10 +459,11 @@ def main():
                        "task_stage": ["wave-per-instance", "lane-per-instance + side-stream hand-backs",
                                       "lane-per-instance + serial hand-backs"][args.task_stage]},
             "roofline": roof,
+            "build_id": build,
+            # whole-job counters over every rank's instances
             "non_solved": int(n_bad), "admm_iters_mean": it_mean,
-            "admm_iters_p99_max": [float(np.percentile(iters.cpu().numpy(), 99)), int(iters.max().item())],
-            "stress_tiers": tiers,
         }
+        line.update(whole_job(ranks, tier_keys, backend))
         if world == 1 and not args.no_extras:
             extras(torch, args, rd, mod, robot, link, q, qd, xt, xdt, dq, dqd, dxt, dxdt, line)
         if world == 1 and not args.no_cpu_baseline:
@@ -399,6 +493,8 @@ def extras(torch, args, rd, mod, robot, link, q, qd, xt, xdt, dq, dqd, dxt, dxdt
     s = timed_steps(torch, lambda: res.update(r=ctrl.QPIK_step_batch(*sub, link, iters=it_s)), max(args.steps, 20), 3)
     line["batch_%d" % nb] = dict(value=nb / s, unit="solves/s", ms_per_step=1e3 * s, **iter_stats(it_s, res["r"][1]))
     line["latency_b1"] = latency_b1(rd, robot, q, qd, xt, xdt, args.solver)
+    if BUNDLED_KIND(robot) == "manipulator":
+        line["latency_cycle"] = latency_cycle(robot, q, qd, args.solver)
     # latency roof: one instance alone on the chip (B = 1 device time) bounds a
     # wave-per-instance design at WAVE_SLOTS / latency solves/s
     import ctypes as C

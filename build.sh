@@ -12,9 +12,15 @@ mkdir -p "$OBJ"
 # FP64 constants of the math library and the stages hoisted into registers at
 # kernel entry, spilled to scratch and reloaded (from beyond L2) per instance
 FLAGS="--offload-arch=gfx950 -O3 -fPIC -std=c++17 -Wall -Wno-unused-function -mllvm -disable-machine-licm $DRC_EXTRA_FLAGS"
+# build id (drc_build_id()): hash of the library's sources and flags, so a
+# profiles/ counter summary can be matched to the build it was measured on
+# (bench.py ignores summaries of another build)
+BUILD_ID=$(cat $CSRC/*.hip $CSRC/*.hpp $CSRC/*.cpp include/drc_amd.h build.sh | { cat; echo "$FLAGS"; } | sha256sum | cut -c1-16)
 pids=()
 for src in task_kernel.hip qp_kernel.hip fused_kernel.hip qpid_kernel.hip dynamics.hip api.cpp model.cpp; do
-  $HIPCC $FLAGS -c $CSRC/$src -o "$OBJ/${src%.*}.o" &
+  XF=""
+  [ "$src" = api.cpp ] && XF="-DDRC_BUILD_ID=\"$BUILD_ID\""
+  $HIPCC $FLAGS $XF -c $CSRC/$src -o "$OBJ/${src%.*}.o" &
   pids+=($!)
 done
 rc=0

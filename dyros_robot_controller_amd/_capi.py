@@ -42,8 +42,15 @@ EXPORTED_SYMBOLS = (
     "drc_dynamics_batch", "drc_dynamics_host", "drc_joint_torque_step_batch", "drc_joint_torque_step_host",
     "drc_default_qpid_params", "drc_qpid_batch", "drc_qpid_stages_batch", "drc_qpid_host",
     "drc_qpid_stages_host", "drc_clik_batch", "drc_osf_batch", "drc_closed_form_host",
-    "drc_error_string", "drc_last_error",
+    "drc_error_string", "drc_last_error", "drc_build_id", "drc_qpik_host_timed", "drc_kinematics_batch",
+    "drc_state_host",
 )
+
+
+class TimeDuration(C.Structure):
+    """drc_time_duration = QP::TimeDuration (QP_base.h:19-43), seconds."""
+    _fields_ = [(n, C.c_double) for n in ("set_qp", "set_cost", "set_bound", "set_ineq", "set_eq", "set_constraint",
+                                          "set_solver", "solve_qp")]
 
 
 class SolverSettings(C.Structure):
@@ -112,6 +119,8 @@ def _load():
     lib.drc_error_string.argtypes = [C.c_int]
     lib.drc_last_error.restype = C.c_char_p
     lib.drc_last_error.argtypes = []
+    lib.drc_build_id.restype = C.c_char_p
+    lib.drc_build_id.argtypes = []
     lib.drc_model_create_manipulator.argtypes = [C.c_char_p, C.c_char_p, C.c_char_p, C.c_int, C.POINTER(vp)]
     lib.drc_model_create_mobile_manipulator.argtypes = [
         C.POINTER(KinematicParam), C.POINTER(JointIndex), C.POINTER(ActuatorIndex),
@@ -139,6 +148,10 @@ def _load():
                                          dp, dp, dp, dp, ip, dp]
     lib.drc_dynamics_batch.argtypes = [vp, C.c_int, C.c_int64, vp, vp, vp, vp, vp, vp, vp, vp]
     lib.drc_dynamics_host.argtypes = [vp, C.c_int, C.c_int64, dp, dp, dp, dp, dp, dp, dp]
+    lib.drc_qpik_host_timed.argtypes = [vp, C.POINTER(QPIKParams), C.c_int64, dp, dp, dp, dp, dp, dp, dp, ip, ip,
+                                        C.POINTER(TimeDuration)]
+    lib.drc_kinematics_batch.argtypes = [vp, C.c_int, C.c_int64, vp, vp, vp, vp, vp, vp]
+    lib.drc_state_host.argtypes = [vp, C.c_int, C.c_int64, dp, dp, dp, dp, dp, dp, dp, dp, dp, dp]
     lib.drc_joint_torque_step_batch.argtypes = [vp, C.c_int64, vp, vp, vp, vp, vp, C.c_double, dp, dp, vp, vp]
     lib.drc_joint_torque_step_host.argtypes = [vp, C.c_int64, dp, dp, dp, dp, dp, C.c_double, dp, dp, dp]
     lib.drc_default_qpid_params.argtypes = [vp, C.c_int, C.POINTER(QPIKParams)]
@@ -152,7 +165,7 @@ def _load():
     lib.drc_osf_batch.argtypes = [vp, C.POINTER(QPIKParams), C.c_int64, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     lib.drc_closed_form_host.argtypes = [vp, C.POINTER(QPIKParams), C.c_int, C.c_int64, dp, dp, dp, dp, dp, dp, dp, dp]
     for name in EXPORTED_SYMBOLS:
-        if name not in ("drc_model_destroy", "drc_error_string", "drc_last_error"):
+        if name not in ("drc_model_destroy", "drc_error_string", "drc_last_error", "drc_build_id"):
             getattr(lib, name).restype = C.c_int
     return lib
 
@@ -168,3 +181,8 @@ def check(rc):
     if rc != DRC_OK:
         raise DrcError(rc, _lib.drc_last_error().decode())
     return rc
+
+
+def build_id():
+    """drc_build_id(): hash of the loaded library's sources and flags (build.sh)."""
+    return lib().drc_build_id().decode()

@@ -5,6 +5,7 @@
 // in task_kernel.hip, qp_kernel.hip, qpid_kernel.hip and dynamics.hip.
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cmath>
 #include <cstdlib>
 #include <cstdio>
@@ -29,11 +30,13 @@ namespace drc_amd {
 // so they may share it; calls on two streams get disjoint contexts (the
 // C-ABI's "reentrant per stream", include/drc_amd.h).  At most kMaxStreamCtx
 // contexts are kept: a new stream beyond that evicts the least recently used
-// one (after a device synchronisation), and drc_model_release_stream frees a
-// stream's context at once, so a caller cycling through streams holds a
-// bounded amount of device memory.
+// one (once the last call that used it has finished: `done`, an event recorded
+// on the caller's stream after each call's launches), and
+// drc_model_release_stream frees a stream's context at once, so a caller
+// cycling through streams holds a bounded amount of device memory.
 struct StreamCtx {
   hipStream_t stream = nullptr;
+  hipEvent_t done = nullptr;  // recorded on `stream` after every call's launches
   uint64_t last_use = 0;
   void* pool = nullptr;  // task records / QPID dynamics / OSF M^-1, g
   int64_t pool_bytes = 0;
@@ -91,6 +94,11 @@ struct drc_model_impl {
   std::mutex host_mu;
   void* stage = nullptr;
   int64_t stage_bytes = 0;
+  // pinned host mirror of the staging buffer: the synchronous entries pack
+  // their inputs into it and copy them over in one transfer, and bring the
+  // outputs back in one (drc_qpik_host, drc_state_host: B = 1 control cycles)
+  double* pinned = nullptr;
+  int64_t pinned_bytes = 0;
   hipStream_t hstream = nullptr;
   std::mutex mu;         // the context list, timing events, concurrency
   std::mutex launch_mu;  // one call's launch sequence is enqueued as a unit, so
@@ -110,6 +118,10 @@ static int set_err(int code, const std::string& msg) {
   } while (0)
 
 static void free_ctx(StreamCtx* c) {
+  // the event outlives a destroyed stream: waiting on it orders the frees
+  // after this context's last use without draining any other stream
+  if (c->done) (void)hipEventSynchronize(c->done), (void)hipEventDestroy(c->done);
+  c->done = nullptr;
   if (c->d_queue) (void)hipFree(c->d_queue);
   if (c->pool) (void)hipFree(c->pool);
   if (c->dyn_list) (void)hipFree(c->dyn_list);
@@ -132,8 +144,8 @@ static int64_t env_int(const char* name, int64_t def, int64_t lo) {
 // The scratch context of `st` (created on first use; the caller holds
 // m->launch_mu and m->mu, so no launch still being enqueued uses an evicted
 // context).  Beyond kMaxStreamCtx streams the least recently used context is
-// freed after the device has drained (its stream may already be destroyed,
-// so the device, not the stream, is synchronised).
+// freed once its `done` event has completed (its stream may already be
+// destroyed; the event stays valid, and no other stream is waited for).
 static int stream_ctx(drc_model_impl* m, hipStream_t st, StreamCtx** out) {
   for (auto& c : m->ctxs)
     if (c->stream == st) {
@@ -145,13 +157,13 @@ static int stream_ctx(drc_model_impl* m, hipStream_t st, StreamCtx** out) {
     size_t lru = 0;
     for (size_t i = 1; i < m->ctxs.size(); ++i)
       if (m->ctxs[i]->last_use < m->ctxs[lru]->last_use) lru = i;
-    HIP_TRY(hipDeviceSynchronize());
     free_ctx(m->ctxs[lru].get());
     m->ctxs.erase(m->ctxs.begin() + static_cast<std::ptrdiff_t>(lru));
   }
   std::unique_ptr<StreamCtx> c(new StreamCtx());
   c->stream = st;
   c->last_use = ++m->ctx_tick;
+  HIP_TRY(hipEventCreateWithFlags(&c->done, hipEventDisableTiming));
   HIP_TRY(hipMalloc(&c->d_queue, StreamCtx::kQueueInts * sizeof(int)));
   *out = c.get();
   m->ctxs.push_back(std::move(c));
@@ -456,7 +468,7 @@ static int plan_layout(const DevModel& M, KParams* k, bool task_only) {
     k->kMq = takeu(k->na * k->na);
     k->kGq = takeu(k->na);
   }
-  if (k->cf) {  // W, W2 (6 x nv), M^-1, nu, g, task vectors, then the serial COD work (+ its nv x 6 result)
+  if (k->cf && k->cf != 3) {  // W, W2 (6 x nv), M^-1, nu, g, task vectors, then the serial COD work (+ its nv x 6 result)
     const int ws = 6 * nv + 36 + 6 * nv + 18 + 2 * nv + 6 * nv;
     k->kCf = takeu(2 * 6 * nv + nv * nv + 3 * nv + 48 + (ws > 160 ? ws : 160));
   }
@@ -580,7 +592,7 @@ static int make_kparams(const drc_model_impl* mm, const drc_qpik_params* p, int 
 static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int stages, int64_t B, const double* q,
                   const double* qdot, const double* xt, const double* xdt, const double* xi, const double* xdi,
                   double* out, int32_t* status, int32_t* iters, double* pose, double* jac, double* man,
-                  double* dist, int32_t* pair, double* xdd, void* stream) {
+                  double* dist, int32_t* pair, double* xdd, void* stream, uint64_t* stamps = nullptr) {
   drc_model_impl* m = const_cast<drc_model_impl*>(cm);
   if (!m || !params) return set_err(DRC_ERR_INVALID_ARGUMENT, "null model/params");
   std::lock_guard<std::mutex> launch_lock(m->launch_mu);
@@ -701,6 +713,7 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
     const int64_t gq = Bc < cap_q ? Bc : cap_q, gt = Bc < cap_t ? Bc : cap_t;
     IO io{Bc, b0, B, q, qdot, xt, xdt, xi, xdi, out, status, iters, pose, jac, man, dist, xdd, pair,
           rec ? rec + b0 * stride : nullptr, stride};
+    io.stamps = stages ? nullptr : stamps;
     int* qc = cx->d_queue + c * StreamCtx::kSlotInts;  // c < 16 (drc_set_concurrency)
     HIP_TRY(hipMemsetAsync(qc, 0, 17 * sizeof(int), cs));
     io.queue = qc;
@@ -781,6 +794,7 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
     std::lock_guard<std::mutex> g(m->mu);
     m->events.push_back(tev);
   }
+  HIP_TRY(hipEventRecord(cx->done, st));
   return DRC_OK;
 }
 
@@ -857,16 +871,49 @@ static int launch_qpid(const drc_model_impl* cm, const drc_qpik_params* params, 
     const size_t lds = static_cast<size_t>(kq_c.lds_doubles) * sizeof(double);
     HIP_TRY(static_cast<hipError_t>(launch_qpid_kernel(static_cast<unsigned>(grid), lds, st, m->d_model, kq_c, io)));
   }
+  HIP_TRY(hipEventRecord(cx->done, st));
   return DRC_OK;
 }
 
 // Closed-form controllers: [dynamics (OSF: M^-1, g)] -> task_kernel<2>.
 static int launch_closed_form(const drc_model_impl* cm, const drc_qpik_params* params, int cf, int64_t B,
                               const double* q, const double* qdot, const double* xt, const double* xdt,
-                              const double* xi, const double* xdi, const double* nullv, double* out, void* stream) {
+                              const double* xi, const double* xdi, const double* nullv, double* out, void* stream,
+                              double* pose = nullptr, double* jac = nullptr, double* xdot = nullptr) {
   drc_model_impl* m = const_cast<drc_model_impl*>(cm);
   if (!m || !params) return set_err(DRC_ERR_INVALID_ARGUMENT, "null model/params");
   std::lock_guard<std::mutex> launch_lock(m->launch_mu);
+  if (cf == 3) {  // kinematics only (drc_kinematics_batch): any model kind, no task targets
+    if (B < 0) return set_err(DRC_ERR_INVALID_ARGUMENT, "negative batch");
+    if (B == 0) return DRC_OK;
+    if (B > 0x7ffffff0) return set_err(DRC_ERR_INVALID_ARGUMENT, "batch too large");
+    if (!q || (xdot && !qdot)) return set_err(DRC_ERR_INVALID_ARGUMENT, "q (and qdot for xdot) required");
+    KParams kt;
+    drc_qpik_params pp = *params;
+    pp.mode = DRC_MODE_QPIK;
+    int rc = make_kparams(m, &pp, 1, &kt, 2, 3);
+    if (rc) return rc;
+    HIP_TRY(hipSetDevice(m->device));
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    StreamCtx* cx = nullptr;
+    {
+      std::lock_guard<std::mutex> g(m->mu);
+      if (int r = stream_ctx(m, st, &cx)) return r;
+    }
+    const int64_t grid = B < 8192 ? B : 8192;
+    kt.xcd_map = B >= 16384 ? 1 : 0;
+    // qdot may be NULL without xdot: the stage reads it, so zeros stand in
+    IO io{B, 0, B, q, qdot ? qdot : q, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, pose, jac,
+          nullptr, nullptr, xdot, nullptr, nullptr, 0};
+    // fixed assignment when every wave has one instance: no counter reset to enqueue
+    io.queue = B > grid ? cx->d_queue + StreamCtx::kQueueSlotCf * StreamCtx::kSlotInts : nullptr;
+    if (io.queue) HIP_TRY(hipMemsetAsync(io.queue, 0, 8 * sizeof(int), st));
+    HIP_TRY(static_cast<hipError_t>(launch_task_kernel(2, static_cast<unsigned>(grid),
+                                                       static_cast<size_t>(kt.lds_doubles) * sizeof(double), st,
+                                                       m->d_model, kt, io)));
+    HIP_TRY(hipEventRecord(cx->done, st));
+    return DRC_OK;
+  }
   if (m->hm.dev.kind != 0) return set_err(DRC_ERR_INVALID_ARGUMENT, "CLIK / OSF are Manipulator::RobotController entries");
   if (B < 0) return set_err(DRC_ERR_INVALID_ARGUMENT, "negative batch");
   if (B == 0) return DRC_OK;
@@ -918,6 +965,7 @@ static int launch_closed_form(const drc_model_impl* cm, const drc_qpik_params* p
   HIP_TRY(static_cast<hipError_t>(launch_task_kernel(2, static_cast<unsigned>(grid),
                                                      static_cast<size_t>(kt.lds_doubles) * sizeof(double), st,
                                                      m->d_model, kt, io)));
+  HIP_TRY(hipEventRecord(cx->done, st));
   return DRC_OK;
 }
 
@@ -942,6 +990,11 @@ const char* drc_error_string(int code) {
   }
 }
 const char* drc_last_error(void) { return drc_amd::g_last_error.c_str(); }
+
+#ifndef DRC_BUILD_ID
+#define DRC_BUILD_ID "unknown"
+#endif
+const char* drc_build_id(void) { return DRC_BUILD_ID; }
 
 int drc_debug_kernel_timing(drc_model* m, int enable) {
   if (!m) return drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "null model");
@@ -1114,6 +1167,7 @@ void drc_model_destroy(drc_model* m) {
   if (m->d_model) (void)hipFree(m->d_model);
   if (m->hstream) (void)hipStreamSynchronize(m->hstream), (void)hipStreamDestroy(m->hstream);
   if (m->stage) (void)hipFree(m->stage);
+  if (m->pinned) (void)hipHostFree(m->pinned);
   for (auto& ev : m->events)
     for (hipEvent_t e : ev) (void)hipEventDestroy(e);
   delete m;
@@ -1324,24 +1378,18 @@ int drc_qpid_stages_host(drc_model* m, const drc_qpik_params* p, int64_t B, cons
   return DRC_OK;
 }
 
+}  // extern "C"
+
 // ---- host-buffer entry points (synchronous; staged through device memory) --
-namespace {
+namespace drc_amd {
 struct HostIO {
   const double* src[6];  // q, qdot, xt, xdt, xi, xdi
   int64_t rows[6];
 };
-}  // namespace
 
-static int host_call(drc_model* m, const drc_qpik_params* p, int stages, int64_t B, const HostIO& in,
-                     double** outs, const int64_t* out_rows, int nouts, int32_t** iouts, int niouts) {
-  if (!m || !p) return drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "null model/params");
-  if (B <= 0) return B == 0 ? DRC_OK : drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "negative batch");
-  std::lock_guard<std::mutex> g(m->host_mu);
-  if (hipSetDevice(m->device) != hipSuccess) return drc_amd::set_err(DRC_ERR_HIP, "hipSetDevice");
-  int64_t words = 0;
-  for (int i = 0; i < 6; ++i) words += in.src[i] ? in.rows[i] * B : 0;
-  for (int i = 0; i < nouts; ++i) words += outs[i] ? out_rows[i] * B : 0;
-  words += niouts * ((B + 1) / 2);
+// Device staging buffer and its pinned host mirror, both >= `words` doubles
+// (the caller holds m->host_mu).
+static int ensure_staging(drc_model* m, int64_t words) {
   const int64_t bytes = words * 8;
   if (m->stage_bytes < bytes) {
     if (m->stage) (void)hipFree(m->stage);
@@ -1350,46 +1398,106 @@ static int host_call(drc_model* m, const drc_qpik_params* p, int stages, int64_t
     if (hipMalloc(&m->stage, bytes) != hipSuccess) return drc_amd::set_err(DRC_ERR_HIP, "hipMalloc (staging)");
     m->stage_bytes = bytes;
   }
+  if (m->pinned_bytes < bytes) {
+    if (m->pinned) (void)hipHostFree(m->pinned);
+    m->pinned = nullptr;
+    m->pinned_bytes = 0;
+    if (hipHostMalloc(reinterpret_cast<void**>(&m->pinned), bytes, hipHostMallocDefault) != hipSuccess)
+      return drc_amd::set_err(DRC_ERR_HIP, "hipHostMalloc (staging)");
+    m->pinned_bytes = bytes;
+  }
   if (!m->hstream && hipStreamCreateWithFlags(&m->hstream, hipStreamNonBlocking) != hipSuccess)
     return drc_amd::set_err(DRC_ERR_HIP, "hipStreamCreate");
-  double* d = reinterpret_cast<double*>(m->stage);
-  const double* din[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
-  for (int i = 0; i < 6; ++i)
-    if (in.src[i]) {
-      if (hipMemcpyAsync(d, in.src[i], in.rows[i] * B * 8, hipMemcpyHostToDevice, m->hstream) != hipSuccess)
-        return drc_amd::set_err(DRC_ERR_HIP, "hipMemcpyAsync H2D");
-      din[i] = d;
-      d += in.rows[i] * B;
-    }
-  double* dout[8] = {nullptr};
-  for (int i = 0; i < nouts; ++i)
-    if (outs[i]) {
-      dout[i] = d;
-      d += out_rows[i] * B;
-    }
-  int32_t* diout[2] = {nullptr, nullptr};
-  for (int i = 0; i < niouts; ++i)
-    if (iouts[i]) {
-      diout[i] = reinterpret_cast<int32_t*>(d);
-      d += (B + 1) / 2;
-    }
-  int rc;
-  if (!stages)
-    rc = drc_amd::launch(m, p, 0, B, din[0], din[1], din[2], din[3], din[4], din[5], dout[0], diout[0], diout[1],
-                         nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, m->hstream);
-  else
-    rc = drc_amd::launch(m, p, 1, B, din[0], din[1], din[2], din[3], din[4], din[5], nullptr, nullptr, nullptr,
-                         dout[0], dout[1], dout[2], dout[3], diout[0], dout[4], m->hstream);
-  if (rc) return rc;
-  for (int i = 0; i < nouts; ++i)
-    if (outs[i] && hipMemcpyAsync(outs[i], dout[i], out_rows[i] * B * 8, hipMemcpyDeviceToHost, m->hstream) != hipSuccess)
-      return drc_amd::set_err(DRC_ERR_HIP, "hipMemcpyAsync D2H");
-  for (int i = 0; i < niouts; ++i)
-    if (iouts[i] && hipMemcpyAsync(iouts[i], diout[i], B * 4, hipMemcpyDeviceToHost, m->hstream) != hipSuccess)
-      return drc_amd::set_err(DRC_ERR_HIP, "hipMemcpyAsync D2H");
-  if (hipStreamSynchronize(m->hstream) != hipSuccess) return drc_amd::set_err(DRC_ERR_HIP, "hipStreamSynchronize");
   return DRC_OK;
 }
+
+// A synchronous host-buffer call in one round trip: the inputs are packed
+// into the pinned mirror and sent in one transfer, `run` enqueues the
+// launches on m->hstream with device pointers into the staging buffer, and
+// the outputs (laid out contiguously after the inputs) come back in one
+// transfer.  in/out: host arrays and their sizes in 8-byte words (NULL arrays
+// are skipped; their device pointer is NULL too).
+struct HostArr {
+  const void* host;
+  int64_t words;
+};
+struct HostOut {
+  void* host;
+  int64_t words;      // staging space (whole 8-byte words)
+  int64_t bytes = -1;  // bytes copied back (default: words * 8)
+};
+template <class Run>
+static int round_trip(drc_model* m, const HostArr* in, int nin, const HostOut* out, int nout, Run run) {
+  int64_t wi = 0, wo = 0;
+  for (int i = 0; i < nin; ++i) wi += in[i].host ? in[i].words : 0;
+  for (int i = 0; i < nout; ++i) wo += out[i].host ? out[i].words : 0;
+  if (int rc = ensure_staging(m, wi + wo)) return rc;
+  double* dev = reinterpret_cast<double*>(m->stage);
+  const void* din[16] = {nullptr};
+  void* dout[16] = {nullptr};
+  int64_t o = 0;
+  for (int i = 0; i < nin; ++i)
+    if (in[i].host) {
+      std::memcpy(m->pinned + o, in[i].host, in[i].words * 8);
+      din[i] = dev + o;
+      o += in[i].words;
+    }
+  for (int i = 0; i < nout; ++i)
+    if (out[i].host) {
+      dout[i] = dev + o;
+      o += out[i].words;
+    }
+  if (wi && hipMemcpyAsync(dev, m->pinned, wi * 8, hipMemcpyHostToDevice, m->hstream) != hipSuccess)
+    return drc_amd::set_err(DRC_ERR_HIP, "hipMemcpyAsync H2D");
+  if (int rc = run(din, dout)) return rc;
+  if (wo && hipMemcpyAsync(m->pinned + wi, dev + wi, wo * 8, hipMemcpyDeviceToHost, m->hstream) != hipSuccess)
+    return drc_amd::set_err(DRC_ERR_HIP, "hipMemcpyAsync D2H");
+  if (hipStreamSynchronize(m->hstream) != hipSuccess) return drc_amd::set_err(DRC_ERR_HIP, "hipStreamSynchronize");
+  o = wi;
+  for (int i = 0; i < nout; ++i)
+    if (out[i].host) {
+      std::memcpy(out[i].host, m->pinned + o, out[i].bytes >= 0 ? out[i].bytes : out[i].words * 8);
+      o += out[i].words;
+    }
+  return DRC_OK;
+}
+
+static int host_call(drc_model* m, const drc_qpik_params* p, int stages, int64_t B, const HostIO& in,
+                     double** outs, const int64_t* out_rows, int nouts, int32_t** iouts, int niouts,
+                     uint64_t* stamps = nullptr /* host [kStamps][B]: the kernels' stage stamps */) {
+  if (!m || !p) return drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "null model/params");
+  if (B <= 0) return B == 0 ? DRC_OK : drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "negative batch");
+  std::lock_guard<std::mutex> g(m->host_mu);
+  if (hipSetDevice(m->device) != hipSuccess) return drc_amd::set_err(DRC_ERR_HIP, "hipSetDevice");
+  HostArr ha[6];
+  for (int i = 0; i < 6; ++i) ha[i] = {in.src[i], in.rows[i] * B};
+  // outputs: the double arrays, the int32 arrays (one word per two), the stamps
+  HostOut ho[8 + 2 + 1];
+  int no = 0;
+  for (int i = 0; i < nouts; ++i) ho[no++] = {outs[i], out_rows[i] * B};
+  for (int i = 0; i < niouts; ++i) ho[no++] = {iouts[i], (B + 1) / 2, 4 * B};
+  ho[no++] = {stamps, stamps ? drc_amd::kStamps * B : 0};
+  auto run = [&](const void** din, void** dout) -> int {
+    const double* d[6];
+    for (int i = 0; i < 6; ++i) d[i] = static_cast<const double*>(din[i]);
+    double* od[8] = {nullptr};
+    for (int i = 0; i < nouts; ++i) od[i] = static_cast<double*>(dout[i]);
+    int32_t* oi[2] = {nullptr, nullptr};
+    for (int i = 0; i < niouts; ++i) oi[i] = static_cast<int32_t*>(dout[nouts + i]);
+    uint64_t* ds = static_cast<uint64_t*>(dout[nouts + niouts]);
+    if (!stages)
+      return drc_amd::launch(m, p, 0, B, d[0], d[1], d[2], d[3], d[4], d[5], od[0], oi[0], oi[1], nullptr, nullptr,
+                             nullptr, nullptr, nullptr, nullptr, m->hstream, ds);
+    return drc_amd::launch(m, p, 1, B, d[0], d[1], d[2], d[3], d[4], d[5], nullptr, nullptr, nullptr, od[0], od[1],
+                           od[2], od[3], oi[0], od[4], m->hstream);
+  };
+  return round_trip(m, ha, 6, ho, no, run);
+}
+}  // namespace drc_amd
+
+extern "C" {
+using drc_amd::HostIO;
+using drc_amd::host_call;
 
 int drc_qpik_host(drc_model* m, const drc_qpik_params* p, int64_t B, const double* q, const double* qdot,
                   const double* xt, const double* xdt, const double* xi, const double* xdi, double* out,
@@ -1404,6 +1512,45 @@ int drc_qpik_host(drc_model* m, const drc_qpik_params* p, int64_t B, const doubl
   return host_call(m, p, 0, B, in, outs, rows, 1, iouts, 2);
 }
 
+int drc_qpik_host_timed(drc_model* m, const drc_qpik_params* p, int64_t B, const double* q, const double* qdot,
+                        const double* xt, const double* xdt, const double* xi, const double* xdi, double* out,
+                        int32_t* status, int32_t* iters, drc_time_duration* ts) {
+  if (!m) return drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "null model");
+  if (!out || !status || !ts) return drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "qdot_out, status and time_status are required");
+  std::memset(ts, 0, sizeof(*ts));
+  if (B <= 0) return B == 0 ? DRC_OK : drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "negative batch");
+  const int64_t n = m->hm.dev.nv, a = m->hm.dev.kind == 1 ? m->hm.dev.n_arm + m->hm.dev.n_wheel : n;
+  HostIO in{{q, qdot, xt, xdt, xi, xdi}, {n, n, 12, 6, 12, 6}};
+  double* outs[1] = {out};
+  const int64_t rows[1] = {a};
+  int32_t* iouts[2] = {status, iters};
+  std::vector<uint64_t> st(static_cast<size_t>(drc_amd::kStamps * B));
+  const auto t0 = std::chrono::steady_clock::now();
+  const int rc = host_call(m, p, 0, B, in, outs, rows, 1, iouts, 2, st.data());
+  const double wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  if (rc) return rc;
+  // stamps are s_memrealtime ticks (100 MHz); per-instance stage durations, averaged
+  const double tick = 1e-8;
+  double task = 0, asmb = 0, solve = 0, store = 0, span = 0;
+  for (int64_t b = 0; b < B; ++b) {
+    auto at = [&](int k) { return static_cast<double>(st[static_cast<size_t>(k * B + b)]); };
+    task += (at(drc_amd::ST_TASK1) - at(drc_amd::ST_TASK0)) * tick;
+    asmb += (at(drc_amd::ST_ASM) - at(drc_amd::ST_QP0)) * tick;
+    solve += (at(drc_amd::ST_SOLVED) - at(drc_amd::ST_ASM)) * tick;
+    store += (at(drc_amd::ST_OUT) - at(drc_amd::ST_SOLVED)) * tick;
+    span += (at(drc_amd::ST_OUT) - at(drc_amd::ST_TASK0)) * tick;
+  }
+  const double inv = 1.0 / static_cast<double>(B);
+  ts->set_ineq = task * inv;         // FK, J, manipulability + gradient, min distance + gradient
+  ts->set_constraint = asmb * inv;   // P, q, bounds, CBF rows stacked (QP_base.h:202-227)
+  ts->set_qp = ts->set_ineq + ts->set_constraint;
+  ts->set_solver = solve * inv;      // Ruiz scaling, factorisation, ADMM, certified polish
+  // output store plus what the call spends outside the instance (launch,
+  // transfers, synchronisation): getSolution's place in the reference
+  ts->solve_qp = store * inv + (wall - span * inv > 0 ? wall - span * inv : 0.0);
+  return DRC_OK;
+}
+
 int drc_qpik_stages_host(drc_model* m, const drc_qpik_params* p, int64_t B, const double* q, const double* qdot,
                          const double* xt, const double* xdt, const double* xi, const double* xdi, double* pose,
                          double* jac, double* man, double* dist, int32_t* pair, double* xdd) {
@@ -1416,6 +1563,44 @@ int drc_qpik_stages_host(drc_model* m, const drc_qpik_params* p, int64_t B, cons
   return host_call(m, p, 1, B, in, outs, rows, 5, iouts, 1);
 }
 
+
+// ---- per-cycle kinematics and state ----------------------
+int drc_kinematics_batch(const drc_model* m, int frame_id, int64_t B, const double* q, const double* qdot,
+                         double* pose, double* jac, double* xdot, void* stream) {
+  if (!m) return drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "null model");
+  drc_qpik_params p;
+  if (int rc = drc_default_qpik_params(m, 1, &p)) return rc;
+  p.frame_id = frame_id;
+  return drc_amd::launch_closed_form(m, &p, 3, B, q, qdot, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                                     stream, pose, jac, xdot);
+}
+
+int drc_state_host(drc_model* m, int frame_id, int64_t B, const double* q, const double* qdot, double* pose,
+                   double* jac, double* xdot, double* M, double* M_inv, double* g, double* nle, double* c) {
+  using drc_amd::set_err;
+  if (!m) return set_err(DRC_ERR_INVALID_ARGUMENT, "null model");
+  if (B <= 0) return B == 0 ? DRC_OK : set_err(DRC_ERR_INVALID_ARGUMENT, "negative batch");
+  if (!q) return set_err(DRC_ERR_INVALID_ARGUMENT, "q is required");
+  if ((xdot || nle || c) && !qdot) return set_err(DRC_ERR_INVALID_ARGUMENT, "qdot is required for xdot / nle / c");
+  const int64_t n = m->hm.dev.nv;
+  std::lock_guard<std::mutex> lk(m->host_mu);
+  HIP_TRY(hipSetDevice(m->device));
+  const drc_amd::HostArr in[2] = {{q, n * B}, {qdot, n * B}};
+  const drc_amd::HostOut out[8] = {{pose, 12 * B}, {jac, 6 * n * B}, {xdot, 6 * B}, {M, n * n * B},
+                                   {M_inv, n * n * B}, {g, n * B}, {nle, n * B}, {c, n * B}};
+  auto run = [&](const void** din, void** dout) -> int {
+    const double* dq = static_cast<const double*>(din[0]);
+    const double* dqd = static_cast<const double*>(din[1]);
+    double* o[8];
+    for (int i = 0; i < 8; ++i) o[i] = static_cast<double*>(dout[i]);
+    if (pose || jac || xdot)
+      if (int rc = drc_kinematics_batch(m, frame_id, B, dq, dqd, o[0], o[1], o[2], m->hstream)) return rc;
+    if (M || M_inv || g || nle || c)
+      if (int rc = drc_dynamics_batch(m, 0, B, dq, dqd, o[3], o[4], o[5], o[6], o[7], m->hstream)) return rc;
+    return DRC_OK;
+  };
+  return drc_amd::round_trip(m, in, 2, out, 8, run);
+}
 
 // ---- closed-form controllers ------------------------------
 int drc_clik_batch(const drc_model* m, const drc_qpik_params* p, int64_t B, const double* q, const double* qdot,
@@ -1529,9 +1714,9 @@ int drc_dynamics_batch(drc_model* m, int actuated, int64_t B, const double* q, c
   HIP_TRY(hipSetDevice(m->device));
   std::lock_guard<std::mutex> launch_lock(m->launch_mu);
   int* list = nullptr;
+  drc_amd::StreamCtx* cx = nullptr;
   if (M_inv) {
     std::lock_guard<std::mutex> lk(m->mu);
-    drc_amd::StreamCtx* cx = nullptr;
     if (int r = drc_amd::stream_ctx(m, reinterpret_cast<hipStream_t>(stream), &cx)) return r;
     if (cx->dyn_list_cap < B + 1) {
       if (cx->dyn_list) HIP_TRY(hipFree(cx->dyn_list));
@@ -1546,6 +1731,7 @@ int drc_dynamics_batch(drc_model* m, int actuated, int64_t B, const double* q, c
                                           list, reinterpret_cast<hipStream_t>(stream));
   if (rc == 1) return drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "batch too large");
   if (rc) return drc_amd::set_err(DRC_ERR_HIP, std::string("dynamics launch: ") + hipGetErrorString(hipGetLastError()));
+  if (cx) HIP_TRY(hipEventRecord(cx->done, reinterpret_cast<hipStream_t>(stream)));
   return DRC_OK;
 }
 

@@ -8,8 +8,9 @@
 // the record's HBM round trip and the kernel boundary: a call's makespan is
 // the slowest wave's sum over its instances of (task + QP) instead of the
 // slowest task plus the slowest QP, which is what bounds small batches.
-// Results are bit-identical to the two-kernel pipeline (same code, same
-// record values; tests/test_gpu_fused.py).
+// Same device functions on the same record values as the two-kernel
+// pipeline; the contract with it (tests/test_gpu_fused.py) is in
+// drc_set_fusion's comment (include/drc_amd.h).
 #include "task_stage.hpp"
 #include "qp_solver.hpp"
 #include "launch.hpp"
@@ -41,8 +42,10 @@ fused_kernel(const DevModel* __restrict__ M0, const KParams kt, const KParams kq
   for (int64_t j = seq.first(); j < seq.n; j = seq.next(j)) {
     const int64_t b = seq.at(j);
     if (b >= B) continue;
+    stage_stamp(io, ST_TASK0, io.b0 + b);
     task_instance<0>(M0, kt, iol, S, b);
     wsync();
+    stage_stamp(io, ST_TASK1, io.b0 + b);
     qp_instance<QD>(M0, kq, kpl, iol, S, b);
   }
 }

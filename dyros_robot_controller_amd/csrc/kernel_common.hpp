@@ -359,7 +359,23 @@ struct IO {
   int* hard_n;
   uint8_t* hard_flag;  // [B] 1 = instance on the hard list (QP pass over the others skips it)
   int hard_mode;       // task_kernel / qp_kernel: 1 = run the hard list; qp_kernel: 2 = skip flagged
+  // per-instance stage stamps [kStamps][B] (s_memrealtime, 100 MHz), or NULL:
+  // task start / end, QP start / assembled / solved / stored
+  // (drc_qpik_host_timed -> QP::TimeDuration, include/drc_amd.h)
+  uint64_t* stamps;
 };
+constexpr int kStamps = 6;
+enum { ST_TASK0 = 0, ST_TASK1 = 1, ST_QP0 = 2, ST_ASM = 3, ST_SOLVED = 4, ST_OUT = 5 };
+// Stage stamp k of instance gb (wave-uniform branch; no stamp executes in a
+// call without io.stamps).  The wait keeps the clock read from returning out
+// of order with the LDS reads that follow (cdna_hip_programming.md).
+__device__ __forceinline__ void stage_stamp(const IO& io, int k, int64_t gb) {
+  if (io.stamps) {
+    const uint64_t t = __builtin_amdgcn_s_memrealtime();
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    if (__lane_id() == 0) io.stamps[k * io.ld + gb] = t;
+  }
+}
 
 // J_mobile of this instance (row stride kMaxWheels) staged in LDS (kSv): the
 // model table for the configuration-independent drives; a caster base's

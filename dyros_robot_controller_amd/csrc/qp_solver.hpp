@@ -1942,7 +1942,9 @@ __device__ __forceinline__ void qp_instance(const DevModel* __restrict__ M0, con
   const int64_t gb = io.b0 + b, LD = io.ld;  // position in the caller's [field][B] arrays
   const DevModel* M = M0;
   asm volatile("" : "+s"(M));
+  stage_stamp(io, ST_QP0, gb);
   qp_assemble<QD>(M, kp, S, io, b);
+  stage_stamp(io, ST_ASM, gb);
   PH(0);
   const bool lp_inf = M->kind == 1 && kp.s.exact && moma_lp_infeasible<QD>(M, kp, S);
   int status, iters = 0;
@@ -1954,6 +1956,7 @@ __device__ __forceinline__ void qp_instance(const DevModel* __restrict__ M0, con
     else status = qp_admm<QD>(kp, kpl, S, &iters);
   }
   PH(3);
+  stage_stamp(io, ST_SOLVED, gb);
   // ---------------- outputs (zero on failure, QP_IK.cpp:56-61) ------------
   const double *D = S + kp.oD, *x = S + kp.oX;
   if (l < kp.na) io.out[(int64_t)l * LD + gb] = status == DRC_STATUS_SOLVED ? D[l] * x[l] : 0.0;
@@ -1962,6 +1965,7 @@ __device__ __forceinline__ void qp_instance(const DevModel* __restrict__ M0, con
     if (io.iters) io.iters[gb] = iters;
   }
   wsync();
+  stage_stamp(io, ST_OUT, gb);
   PH(5);
   PH_FLUSH(16);
 }

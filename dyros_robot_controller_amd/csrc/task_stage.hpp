@@ -409,7 +409,9 @@ __device__ __forceinline__ void task_instance(const DevModel* __restrict__ M0, c
   // 18-29 x_init, 30-35 xdot_init): issued here so their latency overlaps the
   // FK; the task-velocity stage reads them by v_readlane
   double tgt = 0.0;
-  if (l < 12) {
+  if (PROBLEM == 2 && kp.cf == 3) {
+    // kinematics only (drc_kinematics_batch): no task targets
+  } else if (l < 12) {
     if (kp.mode != DRC_MODE_QPIK) tgt = io.xt[l * LD + gb];
   } else if (l < 18) {
     tgt = io.xdt[(l - 12) * LD + gb];
@@ -562,6 +564,14 @@ __device__ __forceinline__ void task_instance(const DevModel* __restrict__ M0, c
   }
   PH(1);
   if constexpr (PROBLEM == 2) {  // closed-form controllers: no CBF stages
+    if (kp.cf == 3) {  // kinematics only: getPose / getJacobian / getVelocity (robot_data.cpp:378-422)
+      if (io.st_pose && l < 12) io.st_pose[l * LD + gb] = l < 9 ? Te[(l % 3) * 3 + l / 3] : Te[l];
+      if (io.st_jac)
+        for (int e = l; e < 6 * nv; e += 64) io.st_jac[(int64_t)e * LD + gb] = J[e];
+      if (io.st_xdd && l < 6) io.st_xdd[l * LD + gb] = jq;  // J qdot, row r on lane r
+      wsync();
+      return;
+    }
     closed_form_stage(M, kp, S, io, gb, LD);
     PH_FLUSH(0);
     return;

@@ -25,37 +25,56 @@ def free_port():
     return port
 
 
-def spawn_ranks(n, argv, extra_env=None, poll_s=0.2):
+def spawn_ranks(n, argv, extra_env=None, poll_s=0.2, timeout_s=None):
     """Launch ``n`` ranks of ``argv`` (one process per GPU, as torchrun would:
     RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT set)
     and wait for them.  The caller must not have touched the GPU: the ranks are
     fresh child processes (fork + exec of a new interpreter), never an exec of
     the caller.  When one rank fails, the others are terminated (by their own
-    PIDs) so none is left waiting in a collective.  Returns the first non-zero
-    exit status, or 0."""
+    PIDs) so none is left waiting in a collective; so are all of them when
+    ``timeout_s`` elapses (return value 124, as timeout(1)) or when the parent
+    is interrupted (the children never outlive this call).  The rendezvous
+    port is chosen free just before the launch; should another process take
+    it in between, the ranks fail to bind and the call returns their error.
+    Returns the first non-zero exit status, or 0."""
     port = free_port()
     procs = []
-    for r in range(n):
-        env = dict(os.environ)
-        env.update(extra_env or {})
-        env.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        procs.append(subprocess.Popen(argv, env=env))
     rc = 0
-    live = list(procs)
-    while live:
-        for p in list(live):
-            code = p.poll()
-            if code is None:
-                continue
-            live.remove(p)
-            if code != 0 and rc == 0:
-                rc = code
+    t_end = None if timeout_s is None else time.monotonic() + timeout_s
+    try:
+        for r in range(n):
+            env = dict(os.environ)
+            env.update(extra_env or {})
+            env.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+            procs.append(subprocess.Popen(argv, env=env))
+        live = list(procs)
+        while live:
+            for p in list(live):
+                code = p.poll()
+                if code is None:
+                    continue
+                live.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code
+                    for o in live:
+                        o.terminate()
+            if live and t_end is not None and time.monotonic() > t_end:
+                rc = rc or 124
                 for o in live:
-                    o.terminate()
-        time.sleep(poll_s)
-    for p in procs:
-        p.wait()
+                    o.kill()
+                break
+            time.sleep(poll_s)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=10)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
     return rc
 
 
@@ -134,3 +153,19 @@ def reduce_stats(wall_s, n_bad, iters_mean, world, device="cpu"):
         dist.all_reduce(sm, op=dist.ReduceOp.SUM)
         return mx.item(), sm[0].item(), sm[1].item() / world
     return t[0].item(), t[1].item(), t[2].item()
+
+
+def gather_stats(values, world, device="cpu"):
+    """Every rank's vector of floats (same length on every rank), gathered:
+    a [world][k] numpy array in rank order on every rank (one all-gather of
+    world x k doubles; the bench's per-rank device ids, iteration
+    percentiles and tier counts)."""
+    import numpy as np
+    import torch
+    t = torch.tensor([float(v) for v in values], dtype=torch.float64, device=device)
+    if world == 1:
+        return t.cpu().numpy()[None, :]
+    import torch.distributed as dist
+    parts = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(parts, t)
+    return np.stack([p.cpu().numpy() for p in parts])

@@ -214,6 +214,54 @@ int drc_qpik_stages_host(drc_model* model, const drc_qpik_params* params, int64_
                          const double* xdot_init, double* pose, double* jac, double* man,
                          double* dist, int32_t* pair, double* xdot_des);
 
+/* QP::TimeDuration (include/dyros_robot_controller/QP_base.h:19-43): seconds
+ * per stage of one solve, as QPBase::solveQP fills it (:100-174). */
+typedef struct drc_time_duration {
+    double set_qp;          /* set_cost + set_bound + set_ineq + set_eq + set_constraint */
+    double set_cost, set_bound, set_ineq, set_eq, set_constraint;
+    double set_solver;      /* OSQP setup + solve (QP_base.h:143-170) */
+    double solve_qp;        /* getSolution (:172-174) */
+} drc_time_duration;
+
+/* drc_qpik_host with QP::TimeDuration filled from per-instance stage stamps
+ * the kernels write (s_memrealtime, averaged over the B instances):
+ *   set_ineq       the task stage: FK, J, manipulability and its gradient, min
+ *                  self-distance and its gradient (what setCost / setIneqConstraint
+ *                  query, QP_IK.cpp:69-131, done in one pass);
+ *   set_constraint assembly of P, q, bounds and the CBF rows (QP_base.h:202-227);
+ *   set_cost, set_bound, set_eq  0 (assembled in the passes above);
+ *   set_qp         set_ineq + set_constraint;
+ *   set_solver     Ruiz scaling, factorisation, ADMM and the certified polish;
+ *   solve_qp       the output store plus the call's launch / transfer /
+ *                  synchronisation time outside the instance.
+ * Reference behaviour on failure (QP_IK.cpp:56-61, time_status.setZero()) is
+ * the caller's: the C++ facade's QPIK::getOptJointVel zeroes it. */
+int drc_qpik_host_timed(drc_model* model, const drc_qpik_params* params, int64_t B,
+                        const double* q, const double* qdot, const double* x_target,
+                        const double* xdot_target, const double* x_init, const double* xdot_init,
+                        double* qdot_out, int32_t* status, int32_t* iters, drc_time_duration* time_status);
+
+/* ---- per-cycle kinematics and robot state -----------
+ * drc_kinematics_batch: getPose / getJacobian / getVelocity of one frame for B
+ * robots (Manipulator::RobotData, src/manipulator/robot_data.cpp:378-422; the
+ * pose at the current q) without the manipulability and
+ * self-collision stages the QPIK path adds: pose [12][B], jac [6*dof][B]
+ * row-major, xdot [6][B] = J qdot.  Any output may be NULL; qdot may be NULL
+ * when xdot is.  frame_id from drc_model_find_frame (-1: the last joint).
+ * Asynchronous on `stream`. */
+int drc_kinematics_batch(const drc_model* model, int frame_id, int64_t B, const double* q,
+                         const double* qdot, double* pose, double* jac, double* xdot, void* stream);
+/* One control cycle's robot state for host arrays in ONE round trip: the
+ * frame's pose / J / J qdot (drc_kinematics_batch) and updateDynamics' M,
+ * M_inv, g, nle, c ([n*n][B], [n][B] as drc_dynamics_batch, actuated = 0) --
+ * what RobotData::updateState caches and the cycle's getPose / getVelocity /
+ * getJacobian / moveJointTorqueStep read (robot_data.cpp:91-124,378-422,
+ * robot_controller.cpp:115-125).  The inputs go over in one transfer and the
+ * outputs come back in one; any output may be NULL.  Synchronous. */
+int drc_state_host(drc_model* model, int frame_id, int64_t B, const double* q, const double* qdot,
+                   double* pose, double* jac, double* xdot, double* M, double* M_inv, double* g,
+                   double* nle, double* c);
+
 /* Diagnostics (no reference counterpart): when enabled, drc_qpik_batch
  * records HIP events on its stream around the task and QP kernels;
  * drc_debug_kernel_times waits for them and returns the summed durations
@@ -260,6 +308,11 @@ int drc_model_release_stream(drc_model* model, void* stream);
 int drc_debug_lane_stage(drc_model* model, int enable);
 
 const char* drc_error_string(int code);
+/* Identity of this library build: a hash of its sources and compile flags
+ * (build.sh).  Profiles measured on a build carry its id, so a counter
+ * summary is only ever attributed to the build it came from.  (Reference: no
+ * counterpart.) */
+const char* drc_build_id(void);
 /* Thread-local detail of the last failing call (parse position, HIP error). */
 const char* drc_last_error(void);
 

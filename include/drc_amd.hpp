@@ -26,9 +26,11 @@
 
 #include <algorithm>
 #include <array>
+#include <chrono>
 #include <cmath>
 #include <cstdint>
 #include <iostream>
+#include <map>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -79,6 +81,17 @@ struct ManipulabilityResult {  // type_define.h:152-162
     std::fill(grad_dot.begin(), grad_dot.end(), 0.0);
   }
 };
+
+namespace QP {
+// QP::TimeDuration (include/dyros_robot_controller/QP_base.h:19-43), seconds;
+// filled by the QP objects below from the kernels' stage stamps
+// (drc_qpik_host_timed, include/drc_amd.h)
+struct TimeDuration {
+  double set_qp = 0, set_cost = 0, set_bound = 0, set_ineq = 0, set_eq = 0, set_constraint = 0, set_solver = 0,
+         solve_qp = 0;
+  void setZero() { *this = TimeDuration(); }
+};
+}  // namespace QP
 
 // Owns a drc_model* and the host copy of the robot state.
 class ModelBase {
@@ -143,6 +156,36 @@ class ModelBase {
                             d.g.data(), d.nle.data(), d.c.data()));
     return d;
   }
+  // The control cycle's getters at the stored state: the frame's pose, J and
+  // J qdot (getPose / getJacobian / getVelocity, robot_data.cpp:378-422) and,
+  // on the first call after updateState, updateDynamics' M, M^-1, g, nle, c
+  // (:109-124) -- one drc_state_host round trip per (state, link); the
+  // cycle's further getters and moveJointTorqueStep read the cache.
+  struct Kin {
+    std::array<double, 12> pose;
+    Vec jac, xdot;
+  };
+  const Kin& stateKinematics(const std::string& link) const {
+    auto it = kin_.find(link);
+    if (it != kin_.end()) return it->second;
+    const int fid = frameId(link);
+    Kin k;
+    k.jac.assign(6 * dof_, 0.0);
+    k.xdot.assign(6, 0.0);
+    const bool dyn = !dyn_ok_;
+    if (dyn) {
+      dyn_.M.assign(dof_ * dof_, 0.0);
+      dyn_.Minv.assign(dof_ * dof_, 0.0);
+      dyn_.g.assign(dof_, 0.0);
+      dyn_.nle.assign(dof_, 0.0);
+      dyn_.c.assign(dof_, 0.0);
+    }
+    check(drc_state_host(model_, fid, 1, q_.data(), qdot_.data(), k.pose.data(), k.jac.data(), k.xdot.data(),
+                         dyn ? dyn_.M.data() : nullptr, dyn ? dyn_.Minv.data() : nullptr, dyn ? dyn_.g.data() : nullptr,
+                         dyn ? dyn_.nle.data() : nullptr, dyn ? dyn_.c.data() : nullptr));
+    if (dyn) dyn_ok_ = true;
+    return kin_.emplace(link, std::move(k)).first->second;
+  }
   // updateDynamics' cached quantities at the stored state (robot_data.cpp:109-124)
   const Dyn& stateDynamics(bool actuated = false) const {
     Dyn& d = actuated ? dyn_act_ : dyn_;
@@ -189,6 +232,7 @@ class ModelBase {
     q_ = q;
     qdot_ = qdot;
     dyn_ok_ = dyn_act_ok_ = false;
+    kin_.clear();
   }
   drc_model* model_ = nullptr;
   int dof_ = 0, act_ = 0, mani_ = 0, mobi_ = 0;
@@ -196,6 +240,7 @@ class ModelBase {
   Vec q_, qdot_;
   mutable Dyn dyn_, dyn_act_;
   mutable bool dyn_ok_ = false, dyn_act_ok_ = false;
+  mutable std::map<std::string, Kin> kin_;  // stateKinematics per link, cleared by updateState
 };
 
 inline MinDistResult minDist(const Vec& dist, const Vec& graddot, bool with_grad, bool with_graddot) {
@@ -289,13 +334,11 @@ class RobotData : public ModelBase {
   Vec computeJacobian(const Vec& q, const std::string& link) const {  // 6 x dof, row-major
     return stages(q, Vec(dof_, 0.0), link).jac;
   }
-  Pose getPose(const std::string& link) const { return pose44(stages(q_, qdot_, link).pose.data()); }
-  Vec getJacobian(const std::string& link) const { return stages(q_, qdot_, link).jac; }
+  // the cycle's getters: one round trip per state and link (stateKinematics)
+  Pose getPose(const std::string& link) const { return pose44(stateKinematics(link).pose.data()); }
+  Vec getJacobian(const std::string& link) const { return stateKinematics(link).jac; }
   Vec getVelocity(const std::string& link) const {  // J qdot (robot_data.cpp:419-422)
-    Vec J = getJacobian(link), v(6, 0.0);
-    for (int r = 0; r < 6; ++r)
-      for (int c = 0; c < dof_; ++c) v[r] += J[r * dof_ + c] * qdot_[c];
-    return v;
+    return stateKinematics(link).xdot;
   }
   ManipulabilityResult getManipulability(bool with_grad, bool with_graddot, const std::string& link) const {
     Stages s = stages(q_, qdot_, link);
@@ -953,6 +996,165 @@ class RobotController : public ControllerBase {
   Vec Kp_mani_joint_, Kv_mani_joint_;
 };
 
+}  // namespace MobileManipulator
+
+// ---- the QP layer (include/dyros_robot_controller/{manipulator,mobile_manipulator}/QP_{IK,ID}.h)
+// QP objects over the robot data's stored state, for callers that drive the
+// QP directly instead of through the controller.  The velocity QP solves
+// through drc_qpik_host_timed (the same kernels as the controllers' QPIK) and
+// fills QP::TimeDuration from the kernels' stage stamps.
+namespace detail {
+// QPIK::setDesiredTaskVel / getOptJointVel (QP_IK.cpp:47-67; MoMa QP_IK.cpp:37-57)
+class QPIKObject {
+ public:
+  void setDesiredTaskVel(const Vec& xdot_desired, const std::string& link_name) {
+    if (xdot_desired.size() != 6) throw std::runtime_error("xdot_desired must be of size 6.");
+    xdot_desired_ = xdot_desired;
+    link_name_ = link_name;
+  }
+  // false (opt_qdot zero, time_status zero) unless the QP is Solved
+  bool getOptJointVel(Vec& opt_qdot, QP::TimeDuration& time_status) const {
+    const int A = model_->getActuatorDof();
+    opt_qdot.assign(A, 0.0);
+    if (xdot_desired_.size() != 6) throw std::runtime_error("setDesiredTaskVel has not been called.");
+    drc_qpik_params p = params_;
+    p.mode = DRC_MODE_QPIK;  // the QP's task velocity is xdot_desired itself
+    p.frame_id = model_->frameId(link_name_);
+    drc_time_duration t;
+    int32_t status = 0, iters = 0;
+    check(drc_qpik_host_timed(model_->handle(), &p, 1, model_->getJointPosition().data(),
+                              model_->getJointVelocity().data(), nullptr, xdot_desired_.data(), nullptr, nullptr,
+                              opt_qdot.data(), &status, &iters, &t));
+    iters_ = iters;
+    status_ = status;
+    if (status != DRC_STATUS_SOLVED) {
+      opt_qdot.assign(A, 0.0);
+      time_status.setZero();
+      return false;
+    }
+    time_status.set_qp = t.set_qp;
+    time_status.set_cost = t.set_cost;
+    time_status.set_bound = t.set_bound;
+    time_status.set_ineq = t.set_ineq;
+    time_status.set_eq = t.set_eq;
+    time_status.set_constraint = t.set_constraint;
+    time_status.set_solver = t.set_solver;
+    time_status.solve_qp = t.solve_qp;
+    return true;
+  }
+  // extensions: solver settings ("exact" certified optimum by default, or the
+  // reference's OSQP settings) and the last solve's status / ADMM iterations
+  void setExact(bool exact) { params_.solver = model_->defaultParams(exact).solver; }
+  int lastStatus() const { return status_; }
+  int lastIterations() const { return iters_; }
+
+ protected:
+  explicit QPIKObject(const ModelBase* model) : model_(model), params_(model->defaultParams(true)) {}
+  const ModelBase* model_;
+  drc_qpik_params params_;
+  Vec xdot_desired_;
+  std::string link_name_;
+  mutable int status_ = 0, iters_ = 0;
+};
+// QPID::setDesiredTaskAcc / getOptJoint (QP_ID.cpp:66-90; MoMa QP_ID.cpp:49-73)
+class QPIDObject {
+ public:
+  void setDesiredTaskAcc(const Vec& xddot_desired, const std::string& link_name) {
+    if (xddot_desired.size() != 6) throw std::runtime_error("xddot_desired must be of size 6.");
+    xddot_desired_ = xddot_desired;
+    link_name_ = link_name;
+  }
+  // false (both outputs zero, time_status zero) unless the QP is Solved;
+  // time_status.set_solver holds the call's wall time (the QPID kernels carry
+  // no stage stamps)
+  bool getOptJoint(Vec& opt_qddot, Vec& opt_torque, QP::TimeDuration& time_status) const {
+    const int A = model_->getActuatorDof();
+    opt_qddot.assign(A, 0.0);
+    opt_torque.assign(A, 0.0);
+    if (xddot_desired_.size() != 6) throw std::runtime_error("setDesiredTaskAcc has not been called.");
+    drc_qpik_params p = params_;
+    p.mode = DRC_MODE_QPID;
+    p.frame_id = model_->frameId(link_name_);
+    int32_t status = 0, iters = 0;
+    const auto t0 = std::chrono::steady_clock::now();
+    check(drc_qpid_host(model_->handle(), &p, 1, model_->getJointPosition().data(), model_->getJointVelocity().data(),
+                        nullptr, xddot_desired_.data(), nullptr, nullptr, opt_qddot.data(), opt_torque.data(), &status,
+                        &iters));
+    const double wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    status_ = status;
+    time_status.setZero();
+    if (status != DRC_STATUS_SOLVED) {  // the kernel's failure output is the controller's (tau = g): zero here
+      opt_qddot.assign(A, 0.0);
+      opt_torque.assign(A, 0.0);
+      return false;
+    }
+    time_status.set_solver = wall;
+    return true;
+  }
+  void setExact(bool exact) {
+    drc_qpik_params d;
+    check(drc_default_qpid_params(model_->handle(), exact ? 1 : 0, &d));
+    params_.solver = d.solver;
+  }
+  int lastStatus() const { return status_; }
+
+ protected:
+  explicit QPIDObject(const ModelBase* model) : model_(model) {
+    check(drc_default_qpid_params(model_->handle(), 1, &params_));
+  }
+  const ModelBase* model_;
+  drc_qpik_params params_;
+  Vec xddot_desired_;
+  std::string link_name_;
+  mutable int status_ = 0;
+};
+}  // namespace detail
+
+namespace Manipulator {
+// Manipulator::QPIK (manipulator/QP_IK.h:16-100): x = [qdot | slacks]; the
+// optimal joint velocity (dof)
+class QPIK : public detail::QPIKObject {
+ public:
+  explicit QPIK(std::shared_ptr<RobotData> robot_data)
+      : detail::QPIKObject(robot_data.get()), robot_data_(std::move(robot_data)) {}
+
+ private:
+  std::shared_ptr<RobotData> robot_data_;
+};
+// Manipulator::QPID (manipulator/QP_ID.h): optimal qddot and torque (dof each)
+class QPID : public detail::QPIDObject {
+ public:
+  explicit QPID(std::shared_ptr<RobotData> robot_data)
+      : detail::QPIDObject(robot_data.get()), robot_data_(std::move(robot_data)) {}
+
+ private:
+  std::shared_ptr<RobotData> robot_data_;
+};
+}  // namespace Manipulator
+
+namespace MobileManipulator {
+// MobileManipulator::QPIK (mobile_manipulator/QP_IK.h:16-93): x = eta, the
+// actuated velocities in ActuatorIndex order
+class QPIK : public detail::QPIKObject {
+ public:
+  explicit QPIK(std::shared_ptr<RobotData> robot_data)
+      : detail::QPIKObject(static_cast<const Manipulator::RobotData*>(robot_data.get())),
+        robot_data_(std::move(robot_data)) {}
+
+ private:
+  std::shared_ptr<RobotData> robot_data_;
+};
+// MobileManipulator::QPID (mobile_manipulator/QP_ID.h): eta_dot and the
+// actuated torques
+class QPID : public detail::QPIDObject {
+ public:
+  explicit QPID(std::shared_ptr<RobotData> robot_data)
+      : detail::QPIDObject(static_cast<const Manipulator::RobotData*>(robot_data.get())),
+        robot_data_(std::move(robot_data)) {}
+
+ private:
+  std::shared_ptr<RobotData> robot_data_;
+};
 }  // namespace MobileManipulator
 }  // namespace drc_amd
 

@@ -16,6 +16,11 @@
 //   mobile_manipulator/robot_data.h:26,77     ctor, updateState(6 x VectorXd)     same
 //   mobile_manipulator/robot_controller.h:30,130-173
 //                           void QPIK*(..., VectorXd& qdot_mobile, VectorXd& qdot_mani)  same
+//   QP_base.h:19-43        QP::TimeDuration                                    same
+//   manipulator/QP_IK.h:25-38, mobile_manipulator/QP_IK.h:25-38
+//                           QPIK(shared_ptr<RobotData>), setDesiredTaskVel, getOptJointVel  same
+//   manipulator/QP_ID.h:25-39, mobile_manipulator/QP_ID.h:25-39
+//                           QPID(shared_ptr<RobotData>), setDesiredTaskAcc, getOptJoint     same
 //
 // A reference example such as examples/C++/src/fr3_controller.cpp switches by
 // including this header instead of the reference's and linking libdrc_amd.so;
@@ -63,6 +68,10 @@ inline MatrixXd rowmajor(const drc_amd::Vec& v, int rows, int cols) {
   return M;
 }
 }  // namespace eigen_detail
+
+namespace QP {
+using TimeDuration = drc_amd::QP::TimeDuration;
+}
 
 namespace Manipulator {
 
@@ -175,6 +184,44 @@ class RobotController {
   drc_amd::Manipulator::RobotController impl_;
 };
 
+// QPIK / QPID objects (manipulator/QP_IK.h:16-100, QP_ID.h)
+class QPIK {
+ public:
+  explicit QPIK(std::shared_ptr<RobotData> robot_data) : robot_data_(std::move(robot_data)), impl_(robot_data_->impl()) {}
+  void setDesiredTaskVel(const VectorXd& xdot_desired, const std::string& link_name) {
+    impl_.setDesiredTaskVel(eigen_detail::vec(xdot_desired), link_name);
+  }
+  bool getOptJointVel(VectorXd& opt_qdot, QP::TimeDuration& time_status) {
+    drc_amd::Vec v;
+    const bool ok = impl_.getOptJointVel(v, time_status);
+    opt_qdot = eigen_detail::evec(v);
+    return ok;
+  }
+  drc_amd::Manipulator::QPIK& impl() { return impl_; }
+
+ private:
+  std::shared_ptr<RobotData> robot_data_;
+  drc_amd::Manipulator::QPIK impl_;
+};
+class QPID {
+ public:
+  explicit QPID(std::shared_ptr<RobotData> robot_data) : robot_data_(std::move(robot_data)), impl_(robot_data_->impl()) {}
+  void setDesiredTaskAcc(const VectorXd& xddot_desired, const std::string& link_name) {
+    impl_.setDesiredTaskAcc(eigen_detail::vec(xddot_desired), link_name);
+  }
+  bool getOptJoint(VectorXd& opt_qddot, VectorXd& opt_torque, QP::TimeDuration& time_status) {
+    drc_amd::Vec a, t;
+    const bool ok = impl_.getOptJoint(a, t, time_status);
+    opt_qddot = eigen_detail::evec(a);
+    opt_torque = eigen_detail::evec(t);
+    return ok;
+  }
+
+ private:
+  std::shared_ptr<RobotData> robot_data_;
+  drc_amd::Manipulator::QPID impl_;
+};
+
 }  // namespace Manipulator
 
 namespace Mobile {
@@ -248,6 +295,43 @@ class RobotController {
  protected:
   std::shared_ptr<RobotData> robot_data_;
   drc_amd::MobileManipulator::RobotController impl_;
+};
+
+// QPIK / QPID objects (mobile_manipulator/QP_IK.h:16-93, QP_ID.h): eta in ActuatorIndex order
+class QPIK {
+ public:
+  explicit QPIK(std::shared_ptr<RobotData> robot_data) : robot_data_(std::move(robot_data)), impl_(robot_data_->mm()) {}
+  void setDesiredTaskVel(const VectorXd& xdot_desired, const std::string& link_name) {
+    impl_.setDesiredTaskVel(eigen_detail::vec(xdot_desired), link_name);
+  }
+  bool getOptJointVel(VectorXd& opt_qdot, QP::TimeDuration& time_status) {
+    drc_amd::Vec v;
+    const bool ok = impl_.getOptJointVel(v, time_status);
+    opt_qdot = eigen_detail::evec(v);
+    return ok;
+  }
+
+ private:
+  std::shared_ptr<RobotData> robot_data_;
+  drc_amd::MobileManipulator::QPIK impl_;
+};
+class QPID {
+ public:
+  explicit QPID(std::shared_ptr<RobotData> robot_data) : robot_data_(std::move(robot_data)), impl_(robot_data_->mm()) {}
+  void setDesiredTaskAcc(const VectorXd& xddot_desired, const std::string& link_name) {
+    impl_.setDesiredTaskAcc(eigen_detail::vec(xddot_desired), link_name);
+  }
+  bool getOptJoint(VectorXd& opt_etadot, VectorXd& opt_torque, QP::TimeDuration& time_status) {
+    drc_amd::Vec a, t;
+    const bool ok = impl_.getOptJoint(a, t, time_status);
+    opt_etadot = eigen_detail::evec(a);
+    opt_torque = eigen_detail::evec(t);
+    return ok;
+  }
+
+ private:
+  std::shared_ptr<RobotData> robot_data_;
+  drc_amd::MobileManipulator::QPID impl_;
 };
 
 }  // namespace MobileManipulator

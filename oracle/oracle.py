@@ -145,12 +145,16 @@ class counting_build:
         return False
 
 
-def flop_counts(reset=True):
+def flop_counts(reset=True, nonzero=False):
     """(flops, transcendentals) counted in this process since the last reset
-    (counting build only)."""
-    f, t = C.c_ulonglong(), C.c_ulonglong()
+    (counting build only); with nonzero=True, (flops, transcendentals,
+    nonzero-operand flops): the operations whose operands are all nonzero,
+    i.e. without the dense restatement's work on structural zeros
+    (flopcount.hpp)."""
+    f, t, z = C.c_ulonglong(), C.c_ulonglong(), C.c_ulonglong()
+    lib().oracle_flop_counts_nz(C.byref(z), C.c_int(0))
     lib().oracle_flop_counts(C.byref(f), C.byref(t), C.c_int(1 if reset else 0))
-    return f.value, t.value
+    return (f.value, t.value, z.value) if nonzero else (f.value, t.value)
 
 
 def set_pruned_narrow_phase(on):

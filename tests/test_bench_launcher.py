@@ -35,17 +35,26 @@ def test_gpus_2_launches_two_ranks_weak():
     assert d["instances"] == 2 * 65536                # weak: 65 536 per rank
     assert d["max_wall"] == 0.002                     # max over ranks of 0.001 * (rank + 1)
     assert d["mean_offset"] == 65536 / 2              # rank offsets 0 and 65 536
+    # whole-job fields (bench.whole_job): iteration p99 / max are maxima over
+    # ranks, tier counts sums, one row per rank, and the transport
+    assert d["admm_iters_p99_max"] == [2.0, 20]
+    assert d["stress_tiers"] == {"collision": 1, "singular": 2}
+    assert [r["rank"] for r in d["ranks"]] == [0, 1] and [r["instances"] for r in d["ranks"]] == [65536, 65536]
+    assert [r["non_solved"] for r in d["ranks"]] == [0, 1] and d["backend"] == "gloo"
 
 
 def test_gpus_3_strong_scaling_global_batch():
     d = _line(_run(["--gpus", "3", "--robot", "xls_fr3", "--global-batch", "23", "--dry-run"]))
     assert d["n_gpus"] == 3 and d["instances"] == 23  # [0, 7) [7, 15) [15, 23)
     assert abs(d["mean_offset"] - (0 + 7 + 15) / 3) < 1e-12
+    assert d["admm_iters_p99_max"] == [3.0, 30] and d["stress_tiers"] == {"collision": 3, "singular": 6}
+    assert [r["instances"] for r in d["ranks"]] == [7, 8, 8]
 
 
 def test_single_gpu_runs_in_process():
     d = _line(_run(["--dry-run"]))
     assert d["n_gpus"] == 1 and d["instances"] == 65536
+    assert "ranks" not in d and d["admm_iters_p99_max"] == [1.0, 10]
 
 
 def test_world_size_must_match_gpus():
@@ -77,3 +86,5 @@ def test_algorithmic_flop_count():
         O.qpik_batch(om, par, *[np.ascontiguousarray(v[:, idx]) for v in (q, qd, xt, xdt)])
         full, _ = O.flop_counts(reset=True)
     assert a["flops_per_solve"] < full / len(idx)
+    # the nonzero-operand count excludes the dense restatement's structural zeros
+    assert a["flops_per_solve"] < 0.5 * a["dense_flops_per_solve"]

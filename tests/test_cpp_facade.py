@@ -108,10 +108,25 @@ int main(int argc, char** argv) {
                                                          drc::eigen_detail::vec(xdot_), 0.5, 0.0, 1.0, "fr3_link8");
   double err = 0;
   for (int i = 0; i < dof_; ++i) err = std::fmax(err, std::fabs(qdot_desired_(i) - ref[i]));
-  std::printf("%d %d %ld %ld %.3e\n", (int)qdot_desired_.size(), (int)tau_desired_.size(), (long)J.rows(),
-              (long)J.cols(), err);
+  // the QP layer driven directly (manipulator/QP_IK.h:31-38, QP_base.h:19-43):
+  // the same optimum as the controller's QPIK, stage times filled
+  drc::Manipulator::QPIK qp(robot_data_);
+  Eigen::VectorXd xd = Eigen::VectorXd::Zero(6);
+  xd(0) = 0.05;
+  qp.setDesiredTaskVel(xd, "fr3_link8");
+  Eigen::VectorXd qd_qp;
+  drc::QP::TimeDuration ts;
+  const bool ok = qp.getOptJointVel(qd_qp, ts);
+  Eigen::VectorXd qd_rc = robot_controller_->QPIK(xd, "fr3_link8");
+  double err2 = 0;
+  for (int i = 0; i < dof_; ++i) err2 = std::fmax(err2, std::fabs(qd_qp(i) - qd_rc(i)));
+  const bool times = ts.set_ineq > 0 && ts.set_constraint > 0 && ts.set_solver > 0 && ts.solve_qp > 0 &&
+                     std::fabs(ts.set_qp - ts.set_ineq - ts.set_constraint) < 1e-15 && ts.set_ineq < 0.1;
+  std::printf("%d %d %ld %ld %.3e %d %.3e %.2e %.2e %.2e %.2e\n", (int)qdot_desired_.size(), (int)tau_desired_.size(),
+              (long)J.rows(), (long)J.cols(), err, (int)ok, err2, ts.set_ineq, ts.set_constraint, ts.set_solver,
+              ts.solve_qp);
   return (qdot_desired_.size() == dof_ && tau_desired_.size() == dof_ && J.rows() == 6 && J.cols() == dof_ &&
-          err == 0.0) ? 0 : 1;
+          err == 0.0 && ok && err2 == 0.0 && times) ? 0 : 1;
 }
 '''
 

@@ -94,7 +94,9 @@ def main():
                    "dispatches": [nf.get(k, 0), nw.get(k, 0)], "avg_duration_ns": avg.get(k)}
     per_dispatch = sum(v["fetch_bytes"] + v["write_bytes"] for v in kern.values())
     # each dispatch pair covers one sub-batch (batch / chunks instances); a step is one call
-    out = {"robot": robot, "batch": batch, "chunks": chunks, "tag": tag, "kernels": kern,
+    with open(os.path.join(src, "bench.json")) as fh:
+        build = json.loads(fh.read().strip().splitlines()[-1]).get("build_id")
+    out = {"robot": robot, "batch": batch, "chunks": chunks, "tag": tag, "build_id": build, "kernels": kern,
            "hbm_bytes_per_step": chunks * per_dispatch,
            "hbm_bytes_per_instance": chunks * per_dispatch / batch,
            "corrections": "FETCH_SIZE KiB x1024 x2 (gfx950 half-count), WRITE_SIZE KiB x1024",

@@ -7,6 +7,8 @@ ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 TAG=$1; shift
 OUT=$ROOT/gpurun_out/valu_$TAG
 mkdir -p $OUT
+# the library build these counters belong to (drc_build_id; no GPU call)
+python3 -c "import sys; sys.path.insert(0, '$ROOT'); from dyros_robot_controller_amd import _capi; print(_capi.build_id())" > $OUT/build_id
 cd /tmp
 export TMPDIR=/tmp
 A="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_FLOPS_FP64 SQ_INSTS_VALU_FLOPS_FP64_TRANS"

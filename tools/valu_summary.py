@@ -58,7 +58,9 @@ def main():
     step_hw = chunks * sum(kern[k]["fp64_flops_hw_per_dispatch"] or 0 for k in qp)
     tc = sum(kern[k]["per_dispatch"].get("SQ_THREAD_CYCLES_VALU", 0) for k in qp)
     ac = sum(kern[k]["per_dispatch"].get("SQ_ACTIVE_INST_VALU", 0) for k in qp)
-    out = {"robot": robot, "batch": batch, "chunks": chunks, "tag": tag, "kernels": kern,
+    with open(os.path.join(src, "build_id")) as fh:
+        build = fh.read().strip()
+    out = {"robot": robot, "batch": batch, "chunks": chunks, "tag": tag, "build_id": build, "kernels": kern,
            "fp64_flops_per_step": step, "fp64_flops_hw_per_step": step_hw,
            "fp64_flops_per_solve": step / batch, "lane_efficiency": tc / max(64 * ac, 1),
            "note": "FLOP = 64 x (2 FMA + ADD + MUL) FP64 instructions per dispatch, summed over the task and QP "
