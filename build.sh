@@ -11,7 +11,13 @@ mkdir -p "$OBJ"
 # -disable-machine-licm: the persistent instance loops would otherwise get the
 # FP64 constants of the math library and the stages hoisted into registers at
 # kernel entry, spilled to scratch and reloaded (from beyond L2) per instance
-FLAGS="--offload-arch=gfx950 -O3 -fPIC -std=c++17 -Wall -Wno-unused-function -mllvm -disable-machine-licm $DRC_EXTRA_FLAGS"
+# -ffp-contract=on: a*b+c is fused only within one source expression, decided
+# before inlining, so a device function rounds the same in every kernel it is
+# inlined into -- the fused kernel and the two-kernel pipeline (and hence any
+# batch size and sub-batch split) return bit-identical results
+# (tests/test_gpu_fused.py, tests/test_gpu_dist.py).  Measured equal speed
+# to the default (fast) contraction (profiles/r04c_ab_fpon.jsonl).
+FLAGS="--offload-arch=gfx950 -O3 -fPIC -std=c++17 -Wall -Wno-unused-function -ffp-contract=on -mllvm -disable-machine-licm $DRC_EXTRA_FLAGS"
 # build id (drc_build_id()): hash of the library's sources and flags, so a
 # profiles/ counter summary can be matched to the build it was measured on
 # (bench.py ignores summaries of another build)

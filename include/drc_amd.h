@@ -284,7 +284,9 @@ int drc_set_concurrency(drc_model* model, int chunks);
  * waves take an instance through the task stage and the QP before the next,
  * the task record kept in LDS; 0 always runs the task-kernel -> QP-kernel
  * pipeline (drc_set_concurrency sub-batches), as larger batches do.  Results
- * agree to rounding (the compiler forms FMAs per kernel). */
+ * are bit-identical either way (the library is built with -ffp-contract=on:
+ * every multiply-add rounds the same in both kernels), so an instance's
+ * result depends neither on the batch size nor on this switch. */
 int drc_set_fusion(drc_model* model, int enable);
 
 /* Frees the per-stream scratch (task-record pool, work-queue counters) the

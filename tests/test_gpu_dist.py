@@ -15,13 +15,17 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("robot,per_rank,mode", [("fr3", 384, "weak"), ("xls_fr3", 257, "strong")])
+@pytest.mark.parametrize("robot,per_rank,mode", [("fr3", 384, "weak"), ("xls_fr3", 257, "strong"),
+                                                 ("fr3", 4500, "weak")])
 def test_two_ranks_match_single_process(tmp_path, robot, per_rank, mode):
+    """(fr3, 4500): each rank's shard runs the fused kernel (B <= 8 192), the
+    single-process run of the whole 9 000 the sub-batch pipeline; the
+    bit-identity contract holds across that threshold."""
     sys.path.insert(0, ROOT)
     from dyros_robot_controller_amd import dist as ddist
     rc = ddist.spawn_ranks(2, [sys.executable, "-u", os.path.join(ROOT, "tests", "_dist_gpu_worker.py"),
                                str(tmp_path), robot, str(per_rank), mode],
-                           extra_env={"DRC_DIST_BACKEND": "gloo"})
+                           extra_env={"DRC_DIST_BACKEND": "gloo"}, timeout_s=100)
     assert rc == 0
     with open(tmp_path / "dist_result.json") as fh:
         r = json.load(fh)

@@ -1,10 +1,12 @@
 """The fused task + QP kernel (fused_kernel.hip, the default for the compiled
-QP shapes) against the two-kernel pipeline (drc_set_fusion(model, 0)): the
-same code on the same task-record values.  The compiler forms FMAs per
-kernel, so a few results differ in the last bits (measured <= 2e-16); the
-contract is status identical and q-dot* within 1e-12 -- for QPIK, QPIKStep
-and QPIKCubic, stress-tier inputs, several batch sizes (one wave, partial
-and full grids)."""
+QP shapes and B <= 8 192) against the two-kernel pipeline
+(drc_set_fusion(model, 0)): the same device functions on the same
+task-record values, built with -ffp-contract=on (build.sh) so that every
+multiply-add rounds the same in both kernels.  The contract is bit-identical
+q-dot*, status and ADMM iteration counts -- for QPIK, QPIKStep and QPIKCubic,
+stress-tier inputs, several batch sizes (one wave, partial and full grids).
+An instance's result therefore depends neither on the batch size nor on the
+fusion threshold (tests/test_gpu_dist.py crosses it)."""
 import ctypes as C
 
 import numpy as np
@@ -43,6 +45,6 @@ def test_fused_matches_two_kernel_pipeline(cuda, robot, B):
     for mode in ("step", "qpik", "cubic") if B == 300 else ("step",):
         (o1, s1, i1), (o0, s0, i0) = (_run(ctrl, rd, f, mode, q, qd, xt, xdt, robot) for f in (1, 0))
         np.testing.assert_array_equal(s1, s0)
-        np.testing.assert_allclose(o1, o0, rtol=0, atol=1e-12)
-        assert np.mean(i1 != i0) <= 0.01, (mode, np.nonzero(i1 != i0))
+        np.testing.assert_array_equal(o1, o0)
+        np.testing.assert_array_equal(i1, i0)
     _capi.check(_capi.lib().drc_set_fusion(rd.model.handle, C.c_int(1)))

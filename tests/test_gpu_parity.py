@@ -1,27 +1,27 @@
 """GPU parity: the HIP kernel (through the C-ABI) vs the oracle restatement.
 
-Tolerances (FP64 throughout):
+Tolerances (FP64 throughout; the code is tests/_common.py):
   pose / Jacobian        1e-12 abs        (same formulas, different op order)
   manipulability         1e-10 rel; grad 1e-8 abs
-  min distance           1e-9 abs separated; penetrating 1e-9 unless EPA hits
-                         its vertex cap on a deep curved contact, then 1e-6
-                         (hpp-fcl's default EPA tolerance); grad 1e-5 abs when
-                         separated (GJK witness
-                         points converge as sqrt of the 1e-12 support gap),
-                         1e-3 when penetrating (EPA face-barycentre witnesses on
-                         curved surfaces); larger only where the
-                         min distance is non-smooth (gradient ill-defined)
-  QP-IK qdot* (exact)    (tests/_common.py:assert_qpik_parity)
+  min distance           1e-9 abs separated, 1e-6 penetrating (EPA stops at
+                         hpp-fcl's default 1e-6 face gap; the winner's
+                         witnesses are then refined to the exact critical
+                         point on both sides);
+                         grad 1e-6 abs, or the oracle's min distance is
+                         non-smooth at q (one-sided derivatives differ: the
+                         reference's gradient is ill-defined)
+                         (narrow_phase_close)
+  argmin pair            the oracle's, or a pair at the same distance
+  QP-IK qdot* (exact)    assert_qpik_parity:
                          on the device's distance stage: EVERY instance within
                          1e-6 abs and task residual |J dq|_inf <= 1e-6
                          (north_star bound 1e-4), status identical;
-                         end to end: status identical, median 1e-9, and the
-                         instances beyond 1e-4 at most the measured count in
-                         EXPECTED_OFF, each explained by a distance stage
-                         within the narrow-phase tolerance above (penetrating
-                         witness gradients up to 2e-2: EPA at hpp-fcl's
-                         64-vertex cap on cylinder pairs).  Inputs include the
-                         SURVEY §8d stress tiers (ids "stress").
+                         end to end (the oracle's own narrow phase): status
+                         identical, median |dq| <= 1e-9, and EVERY instance
+                         within 1e-4 in q-dot and in the task residual
+                         (EXPECTED_OFF = 0 for every robot and seed).
+                         Inputs include the SURVEY §8d stress tiers (ids
+                         "stress").
 """
 import numpy as np
 import pytest
