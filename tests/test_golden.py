@@ -24,3 +24,24 @@ def test_oracle_reproduces_golden(path):
 
 def test_golden_present():
     assert len(GOLD) == 6
+
+
+@pytest.mark.parametrize("path", GOLD, ids=[os.path.basename(p) for p in GOLD])
+def test_golden_distance_stage_certified(path):
+    """Every fixture instance whose argmin pair ran GJK / EPA: the refined
+    witnesses attain both supports (the D17 certificate, tools/gen_golden.py
+    certify_distance), so the fixtures' distance stage -- which the QP rows and
+    the KKT certificate of the fixtures are built from -- is exact, not only
+    the oracle agreeing with itself."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    from gen_golden import certify_distance
+    g = np.load(path)
+    robot = os.path.basename(path).split("_qpik")[0]
+    pm, om, spec = O.load(robot)
+    certified = 0
+    for b in range(g["q"].shape[1]):
+        d, _, _ = O.min_distance(om, g["q"][:, b])
+        assert abs(d - g["dist"][0, b]) <= 1e-12
+        certified += certify_distance(pm, om, g["q"][:, b])
+    assert certified >= 5   # 8-25 of the 96 instances per fixture have a GJK / EPA winner

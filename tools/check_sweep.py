@@ -15,13 +15,14 @@ robot = sys.argv[1] if len(sys.argv) > 1 else "fr3"
 link = {"fr3": "fr3_link8", "ur5e": "tool0"}[robot]
 B = 65536
 rd = make_manipulator(robot, dev)
-q, qd, xt, xdt = step_inputs(rd, robot, 12345, B, dev)
+q, qd, xt, xdt = step_inputs(rd, robot, 12345, B, dev, stress=True)   # bench.py's workload
 args = [_batch.as_device(a, dev) for a in (q, qd, xt, xdt)]
 st = torch.cuda.current_stream(dev)
 ref = None
 knobs = sys.argv[2] if len(sys.argv) > 2 else "check"
-grid = ([(25, 25, 10), (20, 20, 10), (15, 15, 10), (10, 10, 10), (15, 25, 10), (10, 25, 10), (5, 25, 10)]
-        if knobs == "check" else [(25, 25, 10), (25, 25, 5), (25, 25, 3), (25, 25, 1), (25, 25, 0)])
+grid = {"check": [(25, 25, 10), (15, 25, 10), (10, 25, 10), (8, 25, 10), (5, 25, 10), (3, 25, 10), (1, 25, 10)],
+        "long": [(25, 25, 10), (50, 25, 10), (75, 25, 10), (50, 50, 10), (100, 100, 10)],
+        "scaling": [(25, 25, 10), (25, 25, 5), (25, 25, 3), (25, 25, 1), (25, 25, 0)]}[knobs]
 for ct, ar, sc in grid:
     p = manipulator.QPIKParamsBuilder(rd.model, exact=True).params(link, _capi.MODE_QPIK_STEP)
     p.solver.check_termination = ct
@@ -41,5 +42,5 @@ for ct, ar, sc in grid:
     if ref is None:
         ref = o
     print(json.dumps(dict(check=ct, adapt=ar, scaling=sc, ms=e0.elapsed_time(e1) / 10, iters_mean=float(it.float().mean()),
-                          iters_max=int(it.max()), solved=float((status == 0).float().mean()),
+                          iters_max=int(it.max()), solved=float((status == 1).float().mean()),
                           maxdiff_vs_25=float((o - ref).abs().max()))), flush=True)

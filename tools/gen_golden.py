@@ -31,6 +31,30 @@ def pose12(T):
     return v
 
 
+def certify_distance(pm, om, q):
+    """The narrow-phase certificate of DESIGN.md D17 for one instance whose
+    argmin pair ran GJK / EPA (tests/test_oracle_witness.py): with
+    n = (pB - pA) / d the refined witness pA attains A's support in n and pB
+    attains B's support in -n (1e-12), so a separated distance is exact and a
+    penetration depth is an attained support overlap.  Witnesses the
+    refinement keeps (parallel flat features) are exempt.  Returns 1 when the
+    instance was certified, 0 when it needed none."""
+    d, _, pair = O.min_distance(om, q)
+    d0, pA0, pB0, how = O.pair_distance_raw(om, q, pair)
+    if how == 0:
+        return 0
+    dd, pA, pB = O.pair_distance(om, q, pair)
+    if np.array_equal(pA, pA0) and np.array_equal(pB, pB0):
+        return 0
+    a, c = pm.pairs[pair]
+    Tg = R.geom_poses(pm, R.fk(pm, q))
+    n = (pB - pA) / dd
+    assert abs(np.linalg.norm(pB - pA) - abs(dd)) <= 1e-12
+    assert abs(n @ pA - n @ R.support(pm.geoms[a], Tg[a], n)) <= 1e-12
+    assert abs(-n @ pB + n @ R.support(pm.geoms[c], Tg[c], -n)) <= 1e-12
+    return 1
+
+
 def gen(robot, seed, B):
     pm, om, spec = O.load(robot)
     q, qd = workload.joint_states(pm.lower, pm.upper, pm.vel, seed, B)
@@ -54,6 +78,8 @@ def gen(robot, seed, B):
         x, y, s2 = R.solve_qp_exact(P, qv, A, l, u)
         assert st == 1 and s2 == 1
         assert np.max(np.abs(x[:pm.nv] - o)) < 1e-7, (robot, seed, b, np.max(np.abs(x[:pm.nv] - o)))
+        # the distance stage the QP was built on rests on its own certificate
+        certify_distance(pm, om, q[:, b])
     path = os.path.join(ROOT, "tests", "golden", "%s_qpik_step_seed%d.npz" % (robot, seed))
     np.savez_compressed(path, q=q, qdot=qd, x_target=xt, xdot_target=xdt, poses=poses, qdot_opt=out,
                         status=status, man=man, dist=dist, pair=pair, xdot_des=xdd)
