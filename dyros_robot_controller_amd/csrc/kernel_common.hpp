@@ -335,6 +335,19 @@ struct InstSeqG {
   }
 };
 
+// The model pointer, opaque to the optimizer (re-derived per instance so that
+// model-constant loads are not hoisted out of the persistent instance loops
+// into spilled registers, D19) but still known to point to constant memory:
+// the opaque copy is taken in the constant address space and only then cast
+// back, so uniform model reads stay scalar loads (s_load) instead of turning
+// into per-lane flat loads.
+typedef __attribute__((address_space(4))) const DevModel const_devmodel;
+__device__ __forceinline__ const DevModel* opaque_model(const DevModel* M0) {
+  const_devmodel* Mc = (const_devmodel*)M0;
+  asm volatile("" : "+s"(Mc));
+  return (const DevModel*)Mc;
+}
+
 struct IO {
   int64_t B;       // instances of this launch
   int64_t b0, ld;  // global offset of instance 0, row stride of the [field][B] arrays

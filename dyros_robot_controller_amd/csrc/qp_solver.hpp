@@ -1428,29 +1428,36 @@ __device__ __forceinline__ int qp_scale_regs(const KParams& kp, double* S) {
 #pragma unroll
     for (int j = 0; j < NX; ++j) sg = fmax(sg, fabs(Grow[j]));
     const double EtG = 1.0 / sqrt(clampf(sg));
-    // the broadcast factors are used as they arrive (not gathered into
-    // per-lane arrays: 39 doubles more would not fit the QP kernel's 168-VGPR
-    // budget and spilled); same products in the same order
-    static_for<NX>([&](auto C) {
-      constexpr int c = decltype(C)::value;
-      const double dc = GL::template bcastc<c>(Dt);
-      if constexpr (c < NP) {
-        if (hp) Prow[c] *= Dt * dc;
+    // every factor of this pass exactly 1 (the fixed-point pass, usually the
+    // second): the products below would multiply by 1.0, an identity, so
+    // they are skipped -- bit for bit the same matrices, without the pass's
+    // 23 broadcasts
+    const bool unit = GL::all((!hx || (Dt == 1.0 && Et == 1.0)) && (!hg || EtG == 1.0));
+    if (!unit) {
+      // the broadcast factors are used as they arrive (not gathered into
+      // per-lane arrays: 39 doubles more would not fit the QP kernel's 168-VGPR
+      // budget and spilled); same products in the same order
+      static_for<NX>([&](auto C) {
+        constexpr int c = decltype(C)::value;
+        const double dc = GL::template bcastc<c>(Dt);
+        if constexpr (c < NP) {
+          if (hp) Prow[c] *= Dt * dc;
+        }
+        if (hg) Grow[c] *= EtG * dc;
+      });
+      static_for<NG>([&](auto I) {
+        constexpr int i = decltype(I)::value;
+        const double ei = GL::template bcastc<i>(EtG);
+        if (hx) Gcol[i] *= ei * Dt;
+      });
+      if (hx) {
+        abl *= Et * Dt;
+        ql *= Dt;
+        Dl *= Dt;
+        El *= Et;
       }
-      if (hg) Grow[c] *= EtG * dc;
-    });
-    static_for<NG>([&](auto I) {
-      constexpr int i = decltype(I)::value;
-      const double ei = GL::template bcastc<i>(EtG);
-      if (hx) Gcol[i] *= ei * Dt;
-    });
-    if (hx) {
-      abl *= Et * Dt;
-      ql *= Dt;
-      Dl *= Dt;
-      El *= Et;
+      if (hg) EGl *= EtG;
     }
-    if (hg) EGl *= EtG;
     // cost scaling: mean column norm of P vs |q|_inf
     double cn = 0, qn = 0;
     if (hp)
@@ -1469,7 +1476,7 @@ __device__ __forceinline__ int qp_scale_regs(const KParams& kp, double* S) {
     cs *= ct;
     // fixed point: every factor of this pass was exactly 1, so the remaining
     // passes would repeat it bit for bit (oracle: same exit)
-    if (ct == 1.0 && GL::all((!hx || (Dt == 1.0 && Et == 1.0)) && (!hg || EtG == 1.0))) break;
+    if (ct == 1.0 && unit) break;
   }
   if (hp)
 #pragma unroll
@@ -1500,18 +1507,26 @@ __device__ __forceinline__ int qp_scale_regs(const KParams& kp, double* S) {
 // publish and reload need them, so none of it stays live through the
 // iterations, where at the QP kernel's 168-VGPR budget it was spilled before
 // the loop and reloaded at every check (D20)
+// LDS (address space 3) views: the opaque copies below must keep their
+// address space, or every access through them becomes a flat access (vector
+// memory path and its waits) instead of a ds_read / ds_write
+typedef __attribute__((address_space(3))) double lds_double;
+typedef __attribute__((address_space(3))) const double lds_cdouble;
+typedef __attribute__((address_space(3))) const int lds_cint;
+typedef __attribute__((address_space(3))) const KParams lds_ckparams;
 template <class QD>
 struct SchurLanes {
   static constexpr int NX = QD::nx, NG = QD::ng, NP = QD::np;
-  double *qq, *ab, *lo, *up, *x, *z, *y, *dy;
-  const double *rv, *Si, *GS, *dv, *cf, *G;
+  lds_double *qq, *ab, *lo, *up, *x, *z, *y, *dy;
+  lds_cdouble *rv, *Si, *GS, *dv, *cf, *G;
   int l, rr, lc, ia, ig, iv;
   bool hc, hr, ha, hv;
   __device__ __forceinline__ SchurLanes(const KParams& kpl, double* S0) {
-    const KParams* kq = &kpl;
-    double* S = S0;
+    // kpl and S0 point into this wave's LDS (the kernel's __shared__ copy and plan)
+    lds_ckparams* kq = (lds_ckparams*)&kpl;
+    lds_double* S = (lds_double*)S0;
     asm volatile("" : "+s"(kq), "+s"(S));
-    const KParams& kp = *kq;
+    lds_ckparams& kp = *kq;
     l = Grp<QD::gs>::lane();
     qq = S + kp.oQ; ab = S + kp.oAB; lo = S + kp.oL; up = S + kp.oU;
     x = S + kp.oX; z = S + kp.oZ; y = S + kp.oY; dy = S + kp.oDY;
@@ -1521,7 +1536,7 @@ struct SchurLanes {
     dv = GS + NG * NP;
     cf = dv + NG;
     G = S + kp.oG;
-    const int* aux = reinterpret_cast<const int*>(cf + 2 * NG);
+    lds_cint* aux = (lds_cint*)(cf + 2 * NG);
     hc = l < NP;
     hr = l >= NP && l < NP + NG;
     rr = hr ? l - NP : 0;
@@ -1562,8 +1577,13 @@ struct SchurLanes {
 //   core: r'_c = sigma x_c - q_c + ab_c w_b + sum_r G_rc u_r   (NG broadcasts)
 //   core: x~_c = S^-1 r';  rows: v_r = G_r,c x~_c = (G_c S^-1)_r r'   (NP broadcasts)
 //   rows: x~_a = t_a - coef_r v_r,  (G x~)_r = v_r + g_r x~_a
+#ifdef DRC_INLINE_ADMM_LOOP  // experiment: the loop in the QP kernel's own frame
+#define DRC_ADMM_LOOP_ATTR __forceinline__
+#else
+#define DRC_ADMM_LOOP_ATTR __noinline__
+#endif
 template <class QD>
-__device__ __noinline__ int admm_loop_schur(const KParams& kpl, double* S, int* status_out) {
+__device__ DRC_ADMM_LOOP_ATTR int admm_loop_schur(const KParams& kpl, double* S, int* status_out) {
   using GL = Grp<QD::gs>;
   const KParams& kp = kpl;
   const double sig = kp.s.sigma, al = kp.s.alpha;
@@ -1940,8 +1960,7 @@ __device__ __forceinline__ void qp_instance(const DevModel* __restrict__ M0, con
   const int l = GL::lane();
   PH_DECL
   const int64_t gb = io.b0 + b, LD = io.ld;  // position in the caller's [field][B] arrays
-  const DevModel* M = M0;
-  asm volatile("" : "+s"(M));
+  const DevModel* M = opaque_model(M0);
   stage_stamp(io, ST_QP0, gb);
   qp_assemble<QD>(M, kp, S, io, b);
   stage_stamp(io, ST_ASM, gb);

@@ -164,8 +164,7 @@ qpid_kernel(const DevModel* __restrict__ M0, const KParams kp, const IO io) {
     const int64_t b = seq.at(j);
     if (b >= B) continue;
     const int64_t gb = io.b0 + b, LD = io.ld;
-    const DevModel* M = M0;
-    asm volatile("" : "+s"(M));
+    const DevModel* M = opaque_model(M0);
     qpid_assemble(M, kp, S, io, b);
     int status, iters = 0;
     status = qp_scale<QD>(kp, S);

@@ -396,8 +396,7 @@ __device__ __forceinline__ void task_instance(const DevModel* __restrict__ M0, c
           unsigned long long epa_calls = 0, epa_steps = 0, epa_maxsteps = 0, epa_t[3] = {0, 0, 0};)
   // re-derive the model pointer each instance: keeps LICM from hoisting
   // model-constant loads out of the instance loop into spilled registers
-  const DevModel* M = M0;
-  asm volatile("" : "+s"(M));
+  const DevModel* M = opaque_model(M0);
   // ---------------- state in ----------------
   double* qv = S + kp.kq;
   double* qd = S + kp.kqd;
