@@ -236,15 +236,18 @@ DRC_HD __forceinline__ void st3(double* p, V3 v) {
   p[2] = v.z;
 }
 // T = [R row-major | p]
-DRC_HD __forceinline__ V3 rot(const double* T, V3 v) {
+template <class PT>
+DRC_HD __forceinline__ V3 rot(PT T, V3 v) {
   return v3(T[0] * v.x + T[1] * v.y + T[2] * v.z, T[3] * v.x + T[4] * v.y + T[5] * v.z,
             T[6] * v.x + T[7] * v.y + T[8] * v.z);
 }
-DRC_HD __forceinline__ V3 rotT(const double* T, V3 v) {
+template <class PT>
+DRC_HD __forceinline__ V3 rotT(PT T, V3 v) {
   return v3(T[0] * v.x + T[3] * v.y + T[6] * v.z, T[1] * v.x + T[4] * v.y + T[7] * v.z,
             T[2] * v.x + T[5] * v.y + T[8] * v.z);
 }
-DRC_HD __forceinline__ V3 xform(const double* T, V3 v) { return rot(T, v) + v3(T[9], T[10], T[11]); }
+template <class PT>
+DRC_HD __forceinline__ V3 xform(PT T, V3 v) { return rot(T, v) + v3(T[9], T[10], T[11]); }
 // c = a * b (12-vector transforms)
 DRC_HD __forceinline__ void tmul(const double* a, const double* b, double* c) {
   double r[12];
@@ -259,13 +262,28 @@ DRC_HD __forceinline__ void tmul(const double* a, const double* b, double* c) {
 }
 
 // ------------------------------------------------------------ narrow phase
-struct Shape {
+// A primitive and its pose.  The pose pointer's type is a parameter: the
+// wave task stage's poses live in LDS and its shapes carry an LDS-typed
+// pointer (ShapeL), so every support evaluation of GJK / EPA / the witness
+// refinement reads them with ds_read; a generic pointer (Shape: host code,
+// the lane stage's private poses, the tests) would make each of those reads
+// a flat access
+template <class PT>
+struct ShapeT {
   int type;
-  const double* T;   // pose in LDS
+  PT T;              // pose (3x3 row-major rotation, then the origin)
   double p0, p1, p2; // parameters
 };
+using Shape = ShapeT<const double*>;
+#ifdef __HIP_DEVICE_COMPILE__
+typedef __attribute__((address_space(3))) const double lds_pose;
+#else
+typedef const double lds_pose;
+#endif
+using ShapeL = ShapeT<lds_pose*>;
 
-DRC_HD __forceinline__ V3 support(const Shape& s, V3 d) {
+template <class SH>
+DRC_HD __forceinline__ V3 support(const SH& s, V3 d) {
   if (s.type == kSphere) return v3(s.T[9], s.T[10], s.T[11]);
   V3 dl = rotT(s.T, d), loc;
   if (s.type == kCylinder) {
@@ -284,7 +302,8 @@ DRC_HD __forceinline__ V3 support(const Shape& s, V3 d) {
 struct SV {
   V3 w, a, b;
 };
-DRC_HD __forceinline__ SV sup_md(const Shape& A, const Shape& B, V3 d) {
+template <class SH>
+DRC_HD __forceinline__ SV sup_md(const SH& A, const SH& B, V3 d) {
   SV o;
   o.a = support(A, d);
   o.b = support(B, -1.0 * d);
@@ -489,8 +508,8 @@ struct GjkState {
 // cut: the caller only needs the distance if it is <= cut.  Every support
 // point gives the lower bound v.w / |v| of the (signed) distance; once it
 // exceeds cut the pair cannot matter and the run stops with pruned = 1.
-template <bool ANY = false>
-DRC_HD __forceinline__ void gjk_run(const Shape& A, const Shape& B, GjkState& g, double cut = 1e300) {
+template <bool ANY = false, class SH = Shape>
+DRC_HD __forceinline__ void gjk_run(const SH& A, const SH& B, GjkState& g, double cut = 1e300) {
   SV2(&S)[4] = g.S;
 #pragma unroll
   for (int i = 0; i < 4; ++i) S[i].w = S[i].a = v3(0, 0, 0);
@@ -558,7 +577,8 @@ struct GjkDist {
   double dist;
   V3 pA, pB;
 };
-DRC_HD inline __noinline__ GjkDist gjk(const Shape A, const Shape B, double cut = 1e300) {
+template <class SH>
+DRC_HD inline __noinline__ GjkDist gjk(const SH A, const SH B, double cut = 1e300) {
   GjkState g;
   gjk_run(A, B, g, cut);
   GjkDist o;
@@ -662,7 +682,8 @@ DRC_HD __forceinline__ void epa_bind(EpaPoly* E, int f0, int e0, int f1, int e1)
 }
 // rerun GJK and build the initial tetrahedron from its final simplex
 // (lane-serial)
-DRC_HD __forceinline__ void epa_init(const Shape A, const Shape B, EpaPoly* E) {
+template <class SH>
+DRC_HD __forceinline__ void epa_init(const SH A, const SH B, EpaPoly* E) {
   GjkState g;
   gjk_run(A, B, g);
   E->nv = 0;
@@ -972,7 +993,8 @@ __device__ __forceinline__ void epa_grow_wave(EpaPoly* E, const SV& w, int best)
 // signed distance (-depth) on every lane; lane ln leaves the witnesses in
 // E->out.  Same steps and result as epa_serial.  st (timing builds): steps,
 // cycles in face scan, support + tests, growth.
-__device__ __forceinline__ double epa_run_wave(const Shape& A, const Shape& B, EpaPoly* E, int ln,
+template <class SH>
+__device__ __forceinline__ double epa_run_wave(const SH& A, const SH& B, EpaPoly* E, int ln,
                                                unsigned long long* st = nullptr) {
   const int l = threadIdx.x & 63;
   if (l == ln) epa_init(A, B, E);
@@ -1022,7 +1044,8 @@ __device__ __forceinline__ double epa_run_wave(const Shape& A, const Shape& B, E
   return __shfl(dres, ln, 64);
 }
 // one expansion step (lane-serial form, host harness)
-DRC_HD inline void epa_step(const Shape& A, const Shape& B, EpaPoly* E, int best) {
+template <class SH>
+DRC_HD inline void epa_step(const SH& A, const SH& B, EpaPoly* E, int best) {
   const SV w = sup_md(A, B, ld3(E->fn[best]));
   bool stop = epa_gap_stop(E, best, w);
   for (int i = 0; !stop && i < E->nv; ++i) stop = epa_is_dup(E, i, w);
@@ -1044,7 +1067,8 @@ DRC_HD inline int epa_best_serial(const EpaPoly* E) {
   return best;
 }
 // lane-serial driver (host harness and single-lane use)
-DRC_HD inline double epa_serial(const Shape& A, const Shape& B, EpaPoly* E) {
+template <class SH>
+DRC_HD inline double epa_serial(const SH& A, const SH& B, EpaPoly* E) {
   epa_init(A, B, E);
   for (int it = 0; it < 255 && !E->stop; ++it) epa_step(A, B, E, epa_best_serial(E));
   const int bb = epa_best_serial(E);
@@ -1052,7 +1076,8 @@ DRC_HD inline double epa_serial(const Shape& A, const Shape& B, EpaPoly* E) {
 }
 
 // signed distance + closest surface point of a solid cylinder / box
-DRC_HD __forceinline__ double point_cylinder(V3 c, const Shape& s, V3* qw) {
+template <class SH>
+DRC_HD __forceinline__ double point_cylinder(V3 c, const SH& s, V3* qw) {
   V3 loc = rotT(s.T, c - v3(s.T[9], s.T[10], s.T[11])), q = loc;
   double r = s.p0, h = s.p1, rho = sqrt(loc.x * loc.x + loc.y * loc.y), sd;
   if (!(rho <= r && fabs(loc.z) <= h)) {
@@ -1085,7 +1110,8 @@ DRC_HD __forceinline__ double point_cylinder(V3 c, const Shape& s, V3* qw) {
   *qw = xform(s.T, q);
   return sd;
 }
-DRC_HD __forceinline__ double point_box(V3 c, const Shape& s, V3* qw) {
+template <class SH>
+DRC_HD __forceinline__ double point_box(V3 c, const SH& s, V3* qw) {
   V3 loc = rotT(s.T, c - v3(s.T[9], s.T[10], s.T[11])), q = loc;
   double hx[3] = {s.p0, s.p1, s.p2}, l[3] = {loc.x, loc.y, loc.z}, qq[3] = {loc.x, loc.y, loc.z}, sd;
   bool inside = fabs(l[0]) <= hx[0] && fabs(l[1]) <= hx[1] && fabs(l[2]) <= hx[2];
@@ -1113,7 +1139,8 @@ DRC_HD __forceinline__ double point_box(V3 c, const Shape& s, V3* qw) {
 
 // Closed-form pairs (sphere-X).  Returns the hpp-fcl convention
 // pB - pA = d * n with n the A->B direction.
-DRC_HD __forceinline__ double sphere_pair(const Shape& A, const Shape& B, V3* pA, V3* pB) {
+template <class SH>
+DRC_HD __forceinline__ double sphere_pair(const SH& A, const SH& B, V3* pA, V3* pB) {
   if (A.type == kSphere && B.type == kSphere) {
     V3 cA = v3(A.T[9], A.T[10], A.T[11]), cB = v3(B.T[9], B.T[10], B.T[11]);
     V3 v = cB - cA;
@@ -1124,8 +1151,8 @@ DRC_HD __forceinline__ double sphere_pair(const Shape& A, const Shape& B, V3* pA
     return L - A.p0 - B.p0;
   }
   bool flip = B.type == kSphere;
-  const Shape& s = flip ? B : A;
-  const Shape& o = flip ? A : B;
+  const SH& s = flip ? B : A;
+  const SH& o = flip ? A : B;
   V3 c = v3(s.T[9], s.T[10], s.T[11]), q;
   double sd = o.type == kCylinder ? point_cylinder(c, o, &q) : point_box(c, o, &q);
   V3 u = q - c;
@@ -1186,9 +1213,11 @@ constexpr double kRwTau = 1e-4, kRwPivot = 1e-9, kRwStep = 1e-12, kRwCone = 1e-9
 
 DRC_HD __forceinline__ double v3c(V3 v, int i) { return i == 0 ? v.x : (i == 1 ? v.y : v.z); }
 DRC_HD __forceinline__ V3 v3e(int i) { return v3(i == 0, i == 1, i == 2); }
-DRC_HD __forceinline__ double shp(const Shape& s, int i) { return i == 0 ? s.p0 : (i == 1 ? s.p1 : s.p2); }
+template <class SH>
+DRC_HD __forceinline__ double shp(const SH& s, int i) { return i == 0 ? s.p0 : (i == 1 ? s.p1 : s.p2); }
 
-DRC_HD inline void rw_classify(const Shape& s, V3 x, Feat* f) {
+template <class SH>
+DRC_HD inline void rw_classify(const SH& s, V3 x, Feat* f) {
   f->fx = f->fy = f->fz = 0;
   f->s = x.z > 0 ? 1.0 : -1.0;
   if (s.type == kCylinder) {
@@ -1238,7 +1267,8 @@ DRC_HD inline FParam rw_params(const Feat& f, V3 x) {
 }
 // world point, unit-speed tangents t0, t1 (zero where the feature has fewer
 // parameters) and the curvature vector c0 of the first (angle: arc length)
-DRC_HD inline V3 rw_eval(const Shape& s, const Feat& f, const FParam& u, V3* t0, V3* t1, V3* c0) {
+template <class SH>
+DRC_HD inline V3 rw_eval(const SH& s, const Feat& f, const FParam& u, V3* t0, V3* t1, V3* c0) {
   V3 x, a = v3(0, 0, 0), b = v3(0, 0, 0), c = v3(0, 0, 0);
   if (f.kind == kFtSide || f.kind == kFtRim) {
     const double r = s.p0;
@@ -1269,7 +1299,8 @@ DRC_HD inline V3 rw_eval(const Shape& s, const Feat& f, const FParam& u, V3* t0,
   *c0 = rot(s.T, c);
   return xform(s.T, x);
 }
-DRC_HD __forceinline__ void rw_step(const Shape& s, const Feat& f, FParam* u, double d0, double d1) {
+template <class SH>
+DRC_HD __forceinline__ void rw_step(const SH& s, const Feat& f, FParam* u, double d0, double d1) {
   if (f.kind == kFtSide || f.kind == kFtRim) {  // rotate the radial vector by the arc d0 (retraction)
     const double w = d0 / s.p0, ca = u->a - w * u->b, sa = u->b + w * u->a, n = 1.0 / sqrt(ca * ca + sa * sa);
     u->a = ca * n;
@@ -1282,7 +1313,8 @@ DRC_HD __forceinline__ void rw_step(const Shape& s, const Feat& f, FParam* u, do
 }
 // Newton on grad |X_A - X_B|^2 = 0 (unknowns A0 A1 B0 B1; absent ones get
 // identity rows); false when degenerate or not converged.
-DRC_HD inline bool rw_newton(const Shape& A, const Feat& fA, FParam* uA, const Shape& B, const Feat& fB, FParam* uB,
+template <class SH>
+DRC_HD inline bool rw_newton(const SH& A, const Feat& fA, FParam* uA, const SH& B, const Feat& fB, FParam* uB,
                              V3* XA, V3* XB) {
   const int mA = fA.nparam(), mB = fB.nparam();
   const bool act[4] = {mA > 0, mA > 1, mB > 0, mB > 1};
@@ -1351,7 +1383,8 @@ DRC_HD inline bool rw_newton(const Shape& A, const Feat& fA, FParam* uA, const S
   return false;
 }
 // outside the feature's domain: move to the bounding feature (true)
-DRC_HD inline bool rw_domain(const Shape& s, Feat* f, const FParam& u) {
+template <class SH>
+DRC_HD inline bool rw_domain(const SH& s, Feat* f, const FParam& u) {
   if (f->kind == kFtSide && fabs(u.c) > s.p1) {
     f->kind = kFtRim;
     f->s = u.c > 0 ? 1 : -1;
@@ -1377,7 +1410,8 @@ DRC_HD inline bool rw_domain(const Shape& s, Feat* f, const FParam& u) {
 }
 // the outward normal nrm in the normal cone of f at u: -1 impossible, 1
 // feature moves to a neighbour, 0 holds
-DRC_HD inline int rw_cone(const Shape& s, Feat* f, const FParam& u, V3 nrm) {
+template <class SH>
+DRC_HD inline int rw_cone(const SH& s, Feat* f, const FParam& u, V3 nrm) {
   const V3 ax = v3(s.T[2], s.T[5], s.T[8]);
   if (f->kind == kFtBox) {
     const int nfix = (f->fx != 0) + (f->fy != 0) + (f->fz != 0);
@@ -1408,7 +1442,8 @@ DRC_HD inline int rw_cone(const Shape& s, Feat* f, const FParam& u, V3 nrm) {
   return 0;
 }
 // sharpens (d, pA, pB) in place; false: the estimates stay
-DRC_HD inline __noinline__ bool refine_witness(const Shape A, const Shape B, double* d, V3* pA, V3* pB) {
+template <class SH>
+DRC_HD inline __noinline__ bool refine_witness(const SH A, const SH B, double* d, V3* pA, V3* pB) {
   Feat fA, fB;
   const V3 cA = v3(A.T[9], A.T[10], A.T[11]), cB = v3(B.T[9], B.T[10], B.T[11]);
   const V3 xA = rotT(A.T, *pA - cA), xB = rotT(B.T, *pB - cB);
@@ -1447,7 +1482,8 @@ DRC_HD inline __noinline__ bool refine_witness(const Shape A, const Shape B, dou
 // Lower bound on the distance of two geometries via their swept cores:
 // cylinder -> axis segment (radius r), box -> centre point (bounding radius),
 // sphere -> centre.  Exact closed form for segment/segment.
-DRC_HD __forceinline__ void core_segment(const Shape& s, double bound, V3* a, V3* b, double* rad) {
+template <class SH>
+DRC_HD __forceinline__ void core_segment(const SH& s, double bound, V3* a, V3* b, double* rad) {
   V3 c = v3(s.T[9], s.T[10], s.T[11]);
   if (s.type == kCylinder) {
     V3 ax = v3(s.T[2], s.T[5], s.T[8]);
@@ -1465,7 +1501,8 @@ DRC_HD __forceinline__ void core_segment(const Shape& s, double bound, V3* a, V3
 // bound is attained -- the exact distance GJK converges to.  Separated,
 // non-parallel pairs only; every other cylinder pair goes to GJK/EPA.
 // Oracle twin: cyl_cyl_side in oracle/drc_oracle.c (same operation order).
-DRC_HD __forceinline__ bool cyl_cyl_side(const Shape& A, const Shape& B, double* d, V3* pA, V3* pB) {
+template <class SH>
+DRC_HD __forceinline__ bool cyl_cyl_side(const SH& A, const SH& B, double* d, V3* pA, V3* pB) {
   const V3 ua = v3(A.T[2], A.T[5], A.T[8]), ub = v3(B.T[2], B.T[5], B.T[8]);
   const V3 p1 = v3(A.T[9], A.T[10], A.T[11]) - A.p1 * ua, p2 = v3(B.T[9], B.T[10], B.T[11]) - B.p1 * ub;
   const V3 d1 = (2.0 * A.p1) * ua, d2 = (2.0 * B.p1) * ub, r = p1 - p2;
@@ -1528,7 +1565,8 @@ DRC_HD __forceinline__ double seg_seg_dist(V3 p1, V3 q1, V3 p2, V3 q2, V3* c1o =
 // along the core closest-point direction n,  min_B n.x - max_A n.x  (the
 // geometry lies inside its core's swept volume, so this is never below the
 // core bound).
-DRC_HD __forceinline__ double pair_lower_bound(const Shape& A, const Shape& B, double boundA, double boundB) {
+template <class SH>
+DRC_HD __forceinline__ double pair_lower_bound(const SH& A, const SH& B, double boundA, double boundB) {
   V3 a0, a1, b0, b1, c1, c2;
   double ra, rb;
   core_segment(A, boundA, &a0, &a1, &ra);

@@ -691,8 +691,8 @@ __device__ __forceinline__ void task_instance(const DevModel* __restrict__ M0, c
   // runs one or two pair types instead of all of them
   for (int sl = l; sl < M->npairs; sl += 64) {
     const int p = M->pair_order[sl], ga = M->slot_a[sl], gb = M->slot_b[sl];
-    Shape A{M->gtype[ga], Tg + 12 * ga, M->gparam[ga][0], M->gparam[ga][1], M->gparam[ga][2]};
-    Shape Bs{M->gtype[gb], Tg + 12 * gb, M->gparam[gb][0], M->gparam[gb][1], M->gparam[gb][2]};
+    ShapeL A{M->gtype[ga], (lds_pose*)(Tg + 12 * ga), M->gparam[ga][0], M->gparam[ga][1], M->gparam[ga][2]};
+    ShapeL Bs{M->gtype[gb], (lds_pose*)(Tg + 12 * gb), M->gparam[gb][0], M->gparam[gb][1], M->gparam[gb][2]};
     V3 pA, pB;
     double d;
     const bool closed = (A.type == kSphere || Bs.type == kSphere)
@@ -732,8 +732,8 @@ __device__ __forceinline__ void task_instance(const DevModel* __restrict__ M0, c
     for (int c = l; c < ncand; c += 64) {
       const int p = cand[c];
       const int ga = M->pair_a[p], gb = M->pair_b[p];
-      Shape A{M->gtype[ga], Tg + 12 * ga, M->gparam[ga][0], M->gparam[ga][1], M->gparam[ga][2]};
-      Shape Bs{M->gtype[gb], Tg + 12 * gb, M->gparam[gb][0], M->gparam[gb][1], M->gparam[gb][2]};
+      ShapeL A{M->gtype[ga], (lds_pose*)(Tg + 12 * ga), M->gparam[ga][0], M->gparam[ga][1], M->gparam[ga][2]};
+      ShapeL Bs{M->gtype[gb], (lds_pose*)(Tg + 12 * gb), M->gparam[gb][0], M->gparam[gb][1], M->gparam[gb][2]};
       // early exit once GJK's lower bound shows the pair cannot reach ub
       const GjkDist g = gjk(A, Bs, ub + 1e-9);
       if (g.pruned) {
@@ -774,8 +774,8 @@ __device__ __forceinline__ void task_instance(const DevModel* __restrict__ M0, c
       wave_argmin(cpd, cp);
       if (cp == 0x7fffffff || cpd > gbd || (cpd == gbd && cp > gbi)) break;
       const int p = cp, ln = p & 63, ga = M->pair_a[p], gb = M->pair_b[p];
-      const Shape A{M->gtype[ga], Tg + 12 * ga, M->gparam[ga][0], M->gparam[ga][1], M->gparam[ga][2]};
-      const Shape Bs{M->gtype[gb], Tg + 12 * gb, M->gparam[gb][0], M->gparam[gb][1], M->gparam[gb][2]};
+      const ShapeL A{M->gtype[ga], (lds_pose*)(Tg + 12 * ga), M->gparam[ga][0], M->gparam[ga][1], M->gparam[ga][2]};
+      const ShapeL Bs{M->gtype[gb], (lds_pose*)(Tg + 12 * gb), M->gparam[gb][0], M->gparam[gb][1], M->gparam[gb][2]};
       PH_ONLY(epa_calls++; unsigned long long est[4] = {0, 0, 0, 0};)
       const double dall = epa_run_wave(A, Bs, ews, ln PH_ONLY(, est));
       PH_ONLY(epa_steps += est[0]; if (est[0] > epa_maxsteps) epa_maxsteps = est[0];
@@ -808,8 +808,8 @@ __device__ __forceinline__ void task_instance(const DevModel* __restrict__ M0, c
   // the witnesses, so QPID refines here.
   auto refine_winner = [&]() {
     const int ga = M->pair_a[besti], gb = M->pair_b[besti];
-    const Shape A{M->gtype[ga], Tg + 12 * ga, M->gparam[ga][0], M->gparam[ga][1], M->gparam[ga][2]};
-    const Shape Bs{M->gtype[gb], Tg + 12 * gb, M->gparam[gb][0], M->gparam[gb][1], M->gparam[gb][2]};
+    const ShapeL A{M->gtype[ga], (lds_pose*)(Tg + 12 * ga), M->gparam[ga][0], M->gparam[ga][1], M->gparam[ga][2]};
+    const ShapeL Bs{M->gtype[gb], (lds_pose*)(Tg + 12 * gb), M->gparam[gb][0], M->gparam[gb][1], M->gparam[gb][2]};
     double dref = S[kp.oSc + SC_DIST];
     V3 rA = ld3(red), rB = ld3(red + 3);
 #ifdef DRC_NO_REFINE  // diagnostic build: the raw GJK / EPA witnesses
