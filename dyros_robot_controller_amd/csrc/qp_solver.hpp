@@ -1602,6 +1602,9 @@ __device__ DRC_ADMM_LOOP_ATTR int admm_loop_schur(const KParams& kpl, double* S,
   // registers live across the loop and one code path instead of two)
   bool hc, hr, ha, hv;
   double ab_v, q_v, lo_v, up_v, g_r, lo_g, up_g, d_r, c_r, r_v, rg;
+#ifdef DRC_ADMM_LDS_BCAST
+  int rr_l = 0, lc_l = 0;
+#endif
   {
     const SchurLanes<QD> L(kpl, S);
     L.load(R);
@@ -1611,6 +1614,10 @@ __device__ DRC_ADMM_LOOP_ATTR int admm_loop_schur(const KParams& kpl, double* S,
     lo_g = L.lo[L.ig]; up_g = L.up[L.ig];
     d_r = L.dv[L.rr]; c_r = L.cf[L.rr];
     r_v = L.rv[L.iv]; rg = L.rv[L.ig];
+#ifdef DRC_ADMM_LDS_BCAST
+    rr_l = L.rr;
+    lc_l = L.lc;
+#endif
   }
   PHG(25);
   PH_ACC(tchk);
@@ -1632,6 +1639,27 @@ __device__ DRC_ADMM_LOOP_ATTR int admm_loop_schur(const KParams& kpl, double* S,
     }
     const double loc = hc ? tv : 0.0;
     double r0 = 0, r1 = 0;
+#ifdef DRC_ADMM_LDS_BCAST  // experiment: the two passes' vectors broadcast through LDS
+    lds_double* wb = (lds_double*)(S + kpl.oT1);
+    if (hr) wb[rr_l] = u;
+    asm volatile("" ::: "memory");
+    static_for<NG>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      const double ui = wb[i];
+      if constexpr (i & 1) r1 += R[NP + i] * ui;
+      else r0 += R[NP + i] * ui;
+    });
+    const double rp = loc + (r0 + r1);
+    if (hc) wb[NG + lc_l] = rp;
+    asm volatile("" ::: "memory");
+    double s0 = 0, s1 = 0;
+    static_for<NP>([&](auto C) {
+      constexpr int c = decltype(C)::value;
+      const double rpc = wb[NG + c];
+      if constexpr (c & 1) s1 += R[c] * rpc;
+      else s0 += R[c] * rpc;
+    });
+#else
     static_for<NG>([&](auto I) {
       constexpr int i = decltype(I)::value;
       const double ui = GL::template bcastc<NP + i>(u);
@@ -1646,6 +1674,7 @@ __device__ DRC_ADMM_LOOP_ATTR int admm_loop_schur(const KParams& kpl, double* S,
       if constexpr (c & 1) s1 += R[c] * rpc;
       else s0 += R[c] * rpc;
     });
+#endif
     const double sv = s0 + s1;  // core: x~_c; row: v_r = G_r,c x~_c
     const double xta = ha ? ta - c_r * sv : 0.0;  // aux: x~_a
     if (hv) {  // the variable's bound row: z~ = ab x~, relaxation, projection, dual update
