@@ -52,6 +52,7 @@ struct KParams {
   drc_solver_settings s;
   // persistent QP region
   int oP, oG, oQ, oAB, oL, oU, oD, oE, oRho, oX, oZ, oY, oDY, oXT, oZT, oT1, oT2, oRed, oSc;
+  int oBc;  // 32 doubles: vectors broadcast through LDS (ADMM passes, polish KKT sweeps)
   // union region (kinematics | K^-1 | polish)
   int oU0;
   int oHi;  // whole-body polish: cached rows of (P + delta I)^-1 (persistent, nx * nx), -1 if unused
@@ -341,6 +342,13 @@ struct InstSeqG {
 // the opaque copy is taken in the constant address space and only then cast
 // back, so uniform model reads stay scalar loads (s_load) instead of turning
 // into per-lane flat loads.
+// LDS (address space 3) views: an opaque copy of an LDS address must keep its
+// address space, or every access through it becomes a flat access (vector
+// memory path and its waits) instead of a ds_read / ds_write
+typedef __attribute__((address_space(3))) double lds_double;
+typedef __attribute__((address_space(3))) const double lds_cdouble;
+typedef __attribute__((address_space(3))) const int lds_cint;
+typedef __attribute__((address_space(3))) const KParams lds_ckparams;
 typedef __attribute__((address_space(4))) const DevModel const_devmodel;
 __device__ __forceinline__ const DevModel* opaque_model(const DevModel* M0) {
   const_devmodel* Mc = (const_devmodel*)M0;

@@ -234,6 +234,10 @@ __device__ __noinline__ void schur_setup(const KParams& kp, double* S) {
   double Sr[NP];
 #pragma unroll
   for (int c = 0; c < NP; ++c) Sr[c] = Si[lr * NP + c];
+  // the pivot row reaches the lanes through LDS on 64-lane waves (the pivot
+  // lane writes it, every lane reads the same addresses: no VALU broadcasts)
+  lds_double* bc = (lds_double*)(S + kp.oBc);
+  constexpr bool kLds = QD::gs == 64;
   static_for<NP>([&](auto K) {
     constexpr int k = decltype(K)::value;
     if (l == k) {
@@ -241,14 +245,22 @@ __device__ __noinline__ void schur_setup(const KParams& kp, double* S) {
       Sr[k] = 1.0;
 #pragma unroll
       for (int j = 0; j < NP; ++j) Sr[j] *= pv;
+      if constexpr (kLds) {
+#pragma unroll
+        for (int j = 0; j < NP; ++j) bc[j] = Sr[j];
+      }
     }
+    if constexpr (kLds) asm volatile("" ::: "memory");
     const double f = Sr[k];
     if (l != k) Sr[k] = 0.0;
     static_for<NP>([&](auto J) {
       constexpr int j = decltype(J)::value;
-      const double rkj = GL::template bcastc<k>(Sr[j]);
+      double rkj;
+      if constexpr (kLds) rkj = bc[j];
+      else rkj = GL::template bcastc<k>(Sr[j]);
       if (l != k) Sr[j] -= f * rkj;
     });
+    if constexpr (kLds) asm volatile("" ::: "memory");
   });
   if (l < NP) {
 #pragma unroll
@@ -558,7 +570,13 @@ __device__ __forceinline__ bool eqp_regs(const KParams& kp, double* S, int actb,
       Ki[j] = v + (j == l ? (hf ? kp.s.delta : (hr ? -kp.s.delta : 0.0)) : 0.0);
     }
   }
-  // Gauss-Jordan inverse of the regularised KKT
+  // Gauss-Jordan inverse of the regularised KKT.  The pivot row and the
+  // vectors of the products below reach every lane through LDS (the pivot
+  // lane / the owners write, every lane reads the same addresses): no VALU
+  // broadcast instructions, same values, same products (64-lane waves; a
+  // lane group of 32 keeps the register broadcasts)
+  lds_double* bc = (lds_double*)(S + kp.oBc);
+  constexpr bool kLds = QD::gs == 64;
 #pragma unroll
   for (int k = 0; k < NK; ++k) {
     if (k >= N) break;
@@ -569,25 +587,43 @@ __device__ __forceinline__ bool eqp_regs(const KParams& kp, double* S, int actb,
       Ki[k] = 1.0;
 #pragma unroll
       for (int j = 0; j < NK; ++j) Ki[j] *= p;
+      if constexpr (kLds) {
+#pragma unroll
+        for (int j = 0; j < NK; ++j) {
+          if (j >= N) break;
+          bc[j] = Ki[j];
+        }
+      }
     }
+    if constexpr (kLds) asm volatile("" ::: "memory");
     const double f = Ki[k];
     if (l != k) Ki[k] = 0.0;
 #pragma unroll
     for (int j = 0; j < NK; ++j) {
       if (j >= N) break;
-      const double rkj = GL::bcast(Ki[j], k);
+      double rkj;
+      if constexpr (kLds) rkj = bc[j];
+      else rkj = GL::bcast(Ki[j], k);
       if (l != k) Ki[j] -= f * rkj;
     }
+    if constexpr (kLds) asm volatile("" ::: "memory");
   }
   auto apply = [&](const double (&A)[NK], double v) {  // row l of A times the vector held by lanes 0..N-1
+    if constexpr (kLds) {
+      if (l < N) bc[l] = v;
+      asm volatile("" ::: "memory");
+    }
     double s0 = 0, s1 = 0;
 #pragma unroll
     for (int j = 0; j < NK; ++j) {
       if (j >= N) break;
-      const double vj = GL::bcast(v, j);
+      double vj;
+      if constexpr (kLds) vj = bc[j];
+      else vj = GL::bcast(v, j);
       if (j & 1) s1 += A[j] * vj;
       else s0 += A[j] * vj;
     }
+    if constexpr (kLds) asm volatile("" ::: "memory");
     return s0 + s1;
   };
   double sol = apply(Ki, rhs);
@@ -1507,13 +1543,7 @@ __device__ __forceinline__ int qp_scale_regs(const KParams& kp, double* S) {
 // publish and reload need them, so none of it stays live through the
 // iterations, where at the QP kernel's 168-VGPR budget it was spilled before
 // the loop and reloaded at every check (D20)
-// LDS (address space 3) views: the opaque copies below must keep their
-// address space, or every access through them becomes a flat access (vector
-// memory path and its waits) instead of a ds_read / ds_write
-typedef __attribute__((address_space(3))) double lds_double;
-typedef __attribute__((address_space(3))) const double lds_cdouble;
-typedef __attribute__((address_space(3))) const int lds_cint;
-typedef __attribute__((address_space(3))) const KParams lds_ckparams;
+// SchurLanes' opaque copies keep the LDS address space (lds_double, kernel_common.hpp)
 template <class QD>
 struct SchurLanes {
   static constexpr int NX = QD::nx, NG = QD::ng, NP = QD::np;
@@ -1602,7 +1632,7 @@ __device__ DRC_ADMM_LOOP_ATTR int admm_loop_schur(const KParams& kpl, double* S,
   // registers live across the loop and one code path instead of two)
   bool hc, hr, ha, hv;
   double ab_v, q_v, lo_v, up_v, g_r, lo_g, up_g, d_r, c_r, r_v, rg;
-#ifdef DRC_ADMM_LDS_BCAST
+#ifndef DRC_ADMM_READLANE_BCAST
   int rr_l = 0, lc_l = 0;
 #endif
   {
@@ -1614,7 +1644,7 @@ __device__ DRC_ADMM_LOOP_ATTR int admm_loop_schur(const KParams& kpl, double* S,
     lo_g = L.lo[L.ig]; up_g = L.up[L.ig];
     d_r = L.dv[L.rr]; c_r = L.cf[L.rr];
     r_v = L.rv[L.iv]; rg = L.rv[L.ig];
-#ifdef DRC_ADMM_LDS_BCAST
+#ifndef DRC_ADMM_READLANE_BCAST
     rr_l = L.rr;
     lc_l = L.lc;
 #endif
@@ -1639,8 +1669,8 @@ __device__ DRC_ADMM_LOOP_ATTR int admm_loop_schur(const KParams& kpl, double* S,
     }
     const double loc = hc ? tv : 0.0;
     double r0 = 0, r1 = 0;
-#ifdef DRC_ADMM_LDS_BCAST  // experiment: the two passes' vectors broadcast through LDS
-    lds_double* wb = (lds_double*)(S + kpl.oT1);
+#ifndef DRC_ADMM_READLANE_BCAST  // the two passes' vectors broadcast through LDS (r04: +1-3 %)
+    lds_double* wb = (lds_double*)(S + kpl.oBc);
     if (hr) wb[rr_l] = u;
     asm volatile("" ::: "memory");
     static_for<NG>([&](auto I) {
