@@ -350,6 +350,14 @@ typedef __attribute__((address_space(3))) const double lds_cdouble;
 typedef __attribute__((address_space(3))) const int lds_cint;
 typedef __attribute__((address_space(3))) const KParams lds_ckparams;
 typedef __attribute__((address_space(4))) const DevModel const_devmodel;
+// opaque copy of a wave-uniform LDS address, held in an SGPR (readfirstlane
+// first: inside an out-of-line function the argument arrives in a VGPR)
+template <class T>
+__device__ __forceinline__ T* opaque_lds(T* p) {
+  uint32_t v = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(reinterpret_cast<uintptr_t>(p)));
+  asm volatile("" : "+s"(v));
+  return reinterpret_cast<T*>(static_cast<uintptr_t>(v));
+}
 __device__ __forceinline__ const DevModel* opaque_model(const DevModel* M0) {
   const_devmodel* Mc = (const_devmodel*)M0;
   asm volatile("" : "+s"(Mc));

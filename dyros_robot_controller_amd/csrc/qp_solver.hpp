@@ -1553,9 +1553,8 @@ struct SchurLanes {
   bool hc, hr, ha, hv;
   __device__ __forceinline__ SchurLanes(const KParams& kpl, double* S0) {
     // kpl and S0 point into this wave's LDS (the kernel's __shared__ copy and plan)
-    lds_ckparams* kq = (lds_ckparams*)&kpl;
-    lds_double* S = (lds_double*)S0;
-    asm volatile("" : "+s"(kq), "+s"(S));
+    lds_ckparams* kq = opaque_lds((lds_ckparams*)&kpl);
+    lds_double* S = opaque_lds((lds_double*)S0);
     lds_ckparams& kp = *kq;
     l = Grp<QD::gs>::lane();
     qq = S + kp.oQ; ab = S + kp.oAB; lo = S + kp.oL; up = S + kp.oU;
@@ -1650,7 +1649,6 @@ __device__ DRC_ADMM_LOOP_ATTR int admm_loop_schur(const KParams& kpl, double* S,
 #endif
   }
   PHG(25);
-  PH_ACC(tchk);
   double ir_v = 1.0 / r_v, irg = 1.0 / rg;  // y / rho as a product in the loop
   double xv = 0, zv = 0, yv = 0, dyv = 0, zg = 0, yg = 0, dyg = 0;
   for (it = 1; it <= max_iter; ++it) {
@@ -1746,7 +1744,7 @@ __device__ DRC_ADMM_LOOP_ATTR int admm_loop_schur(const KParams& kpl, double* S,
     if (!(check || adapt)) continue;  // last iteration: published for the output
     PH_STAMP(tc0);
     const int act = admm_check<QD>(kpl, S, it, check, adapt, &status);
-    PH_ACC_SINCE(tchk, tc0);
+    PH_ONLY(const unsigned long long dchk = __builtin_amdgcn_s_memtime() - tc0; PH_ADD(27, dchk); PH_ADD(26, 0ull - dchk));  // checks out of the loop's slot
     if (act == 2) break;
     {  // S^-1 / rho may have changed, the iterate may be polished
       const SchurLanes<QD> L(kpl, S);
@@ -1770,8 +1768,6 @@ __device__ DRC_ADMM_LOOP_ATTR int admm_loop_schur(const KParams& kpl, double* S,
     }
   }
   PHG(26);
-  PH_ADD(27, tchk);        // termination checks out of the loop's slot
-  PH_ADD(26, 0ull - tchk);
   *status_out = status;
   return it;
 }
@@ -1813,7 +1809,6 @@ __device__ __forceinline__ int qp_admm(const KParams& kp, const KParams& kpl, do
     prep_admm_mats<QD>(kpl, S);
     load_admm_regs<QD>(kp, S, Gc, Kr, GKr);
     PHG(25);
-    PH_ACC(tchk);
     const bool hb = l < NX, hg = l < NG;
     const int lb_ = hb ? l : 0, lg_ = hg ? NX + l : 0;
     const double ab_l = ab[lb_], q_l = qq[lb_], lo_b = lo[lb_], up_b = up[lb_], lo_g = lo[lg_], up_g = up[lg_];
@@ -1878,7 +1873,7 @@ __device__ __forceinline__ int qp_admm(const KParams& kp, const KParams& kpl, do
       if (!(check || adapt)) continue;  // last iteration: published for the output
       PH_STAMP(tc0);
       const int act = admm_check<QD>(kpl, S, it, check, adapt, &status);
-      PH_ACC_SINCE(tchk, tc0);
+      PH_ONLY(const unsigned long long dchk = __builtin_amdgcn_s_memtime() - tc0; PH_ADD(27, dchk); PH_ADD(26, 0ull - dchk));  // checks out of the loop's slot
       if (act == 2) break;
       // Always re-read the register state from LDS (published above, or
       // updated by the check): nothing large stays live across the call, so
@@ -1893,8 +1888,6 @@ __device__ __forceinline__ int qp_admm(const KParams& kp, const KParams& kpl, do
       yg = y[lg_];
     }
     PHG(26);
-    PH_ADD(27, tchk);        // termination checks out of the loop's slot
-    PH_ADD(26, 0ull - tchk);
   } else {
     for (it = 1; it <= kp.s.max_iter; ++it) {
       for (int row = l; row < m; row += GL::size) w[row] = rv[row] * z[row] - y[row];
