@@ -997,6 +997,20 @@ const char* drc_last_error(void) { return drc_amd::g_last_error.c_str(); }
 #endif
 const char* drc_build_id(void) { return DRC_BUILD_ID; }
 
+int drc_debug_lds_plan(drc_model* m, const drc_qpik_params* params, int problem, int* task_bytes, int* qp_bytes,
+                       int* fused_bytes) {
+  if (!m || !params || !task_bytes || !qp_bytes || !fused_bytes) return drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "null argument");
+  if (problem != 0 && problem != 1) return drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "problem must be 0 (QPIK) or 1 (QPID)");
+  drc_amd::KParams kt, kq;
+  if (int rc = drc_amd::make_kparams(m, params, 1, &kt, problem)) return rc;
+  if (int rc = drc_amd::make_kparams(m, params, 0, &kq, problem)) return rc;
+  *task_bytes = kt.lds_doubles * 8;
+  *qp_bytes = kq.lds_doubles * 8;
+  // the fused kernel (QPIK only): the larger plan plus the task record
+  *fused_bytes = problem == 0 ? ((kt.lds_doubles > kq.lds_doubles ? kt.lds_doubles : kq.lds_doubles) + ((kt.rLen + 1) & ~1)) * 8 : 0;
+  return DRC_OK;
+}
+
 int drc_debug_kernel_timing(drc_model* m, int enable) {
   if (!m) return drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "null model");
   m->timing = enable != 0;

@@ -267,6 +267,11 @@ int drc_state_host(drc_model* model, int frame_id, int64_t B, const double* q, c
  * drc_debug_kernel_times waits for them and returns the summed durations
  * (ms) and the number of timed calls since the last query. */
 int drc_debug_kernel_timing(drc_model* model, int enable);
+/* Per-wave LDS of this model's kernels (bytes): task kernel, QP kernel and the
+ * fused kernel (0 for QPID), problem 0 = QPIK, 1 = QPID.  Diagnostic (DESIGN.md
+ * "Occupancy"); no reference counterpart. */
+int drc_debug_lds_plan(drc_model* model, const drc_qpik_params* params, int problem, int* task_bytes, int* qp_bytes,
+                       int* fused_bytes);
 /* wall_ms: summed caller-stream time of the timed calls (fork to join);
  * task_ms / qp_ms: summed durations of the task / QP kernels of every
  * sub-batch (they overlap in time when a call runs several sub-batches). */
