@@ -167,6 +167,8 @@ def _load():
     lib.drc_osf_batch.argtypes = [vp, C.POINTER(QPIKParams), C.c_int64, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     lib.drc_closed_form_host.argtypes = [vp, C.POINTER(QPIKParams), C.c_int, C.c_int64, dp, dp, dp, dp, dp, dp, dp, dp]
     for name in EXPORTED_SYMBOLS:
+        if name == "drc_debug_lds_plan" and not hasattr(lib, name):
+            continue
         if name not in ("drc_model_destroy", "drc_error_string", "drc_last_error", "drc_build_id"):
             getattr(lib, name).restype = C.c_int
     return lib
