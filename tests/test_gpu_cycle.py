@@ -146,7 +146,8 @@ def test_cycle_through_module_matches_oracle(cuda):
 def test_lds_plan(cuda, robot):
     """Per-wave LDS of the three QPIK kernels (drc_debug_lds_plan): the QP
     kernel's plan fits three waves per SIMD (12 per CU in 160 KB), the task
-    kernel's two, and the fused plan holds the larger of the two plus the record."""
+    kernel's at least one (its VGPRs allow two; DESIGN.md "Occupancy"), and the
+    fused plan holds the larger of the two plus the record."""
     moma = robot in ("husky_fr3", "xls_fr3", "caster_fr3")
     rd = make_moma(robot, cuda) if moma else make_manipulator(robot, cuda)
     p = manipulator.QPIKParamsBuilder(rd.model, exact=True).params(LINK[robot], _capi.MODE_QPIK_STEP)
@@ -154,5 +155,5 @@ def test_lds_plan(cuda, robot):
     _capi.check(_capi.lib().drc_debug_lds_plan(rd.model.handle, C.byref(p), 0, C.byref(t), C.byref(q), C.byref(f)))
     print(robot, "task", t.value, "qp", q.value, "fused", f.value)
     assert 0 < q.value <= 160 * 1024 // 12
-    assert 0 < t.value <= 160 * 1024 // 8
+    assert 0 < t.value <= 160 * 1024 // 4
     assert f.value > max(t.value, q.value)
