@@ -19,8 +19,14 @@ namespace drc_amd {
 #endif
 // PROBLEM 0: QPIK stage data; 1: also the QPID extras (a separate
 // instantiation, so the QPIK kernel carries no call frame for them); 2: CLIK / OSF
-template <int PROBLEM>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRC_TASK_WAVES, 8)))
+// WAVES: the register budget's occupancy target; the QPIK stage also has a
+// three-wave build (168 VGPRs, more spills) for models whose LDS plan lets a
+// CU hold more than the 8 waves the two-wave build can: UR5e (15.7 KB per
+// wave, 10 waves per CU) +3.6 %, while FR3 / the whole-body robots (19.6 /
+// 20.6-22.6 KB: 8 or 7 waves per CU either way) lose 1.6-3 % to the spills
+// (profiles/r04j_ab_lds.jsonl)
+template <int PROBLEM, int WAVES = DRC_TASK_WAVES>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
 task_kernel(const DevModel* __restrict__ M0, const KParams kp, const IO io) {
   extern __shared__ __attribute__((aligned(16))) double S[];
   const int64_t B = io.B;
@@ -41,7 +47,11 @@ task_kernel(const DevModel* __restrict__ M0, const KParams kp, const IO io) {
 
 int launch_task_kernel(int problem, unsigned grid, size_t lds, hipStream_t st, const DevModel* m, const KParams& kp,
                        const IO& io) {
-  if (problem == 0)
+  // LDS-limited residency of the two-wave build is 8 waves per CU (160 KB / 20 KB);
+  // a plan of <= 16 KB lets the three-wave build hold 10 or more
+  if (problem == 0 && lds <= 16 * 1024)
+    hipLaunchKernelGGL((task_kernel<0, 3>), dim3(grid), dim3(64), lds, st, m, kp, io);
+  else if (problem == 0)
     hipLaunchKernelGGL(task_kernel<0>, dim3(grid), dim3(64), lds, st, m, kp, io);
   else if (problem == 1)
     hipLaunchKernelGGL(task_kernel<1>, dim3(grid), dim3(64), lds, st, m, kp, io);
