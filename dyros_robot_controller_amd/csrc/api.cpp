@@ -448,7 +448,7 @@ static int plan_layout(const DevModel& M, KParams* k, bool task_only) {
   k->kq = takeu(nv);
   k->kqd = takeu(nv);
   k->kPd = takeu(M.npairs);
-  k->kPf = takeu(M.npairs);
+  k->kPf = takeu((M.npairs + 7) / 8);  // one byte per pair
   k->kxdd = takeu(6);
   k->kmg = takeu(k->narm);
   k->kdg = takeu(nv);

@@ -618,13 +618,16 @@ DRC_HD inline __noinline__ GjkDist gjk(const SH A, const SH B, double cut = 1e30
 // epa_max_face_num 128, epa_max_iterations 255), mirrored by the oracle
 constexpr int kEpaMaxV = 64, kEpaMaxF = 128;
 static_assert(kEpaMaxF == 128, "face bit masks are two 64-bit words");
+static_assert(kEpaMaxF <= 256 && kEpaMaxV <= 127, "EpaPoly's 8-bit face and horizon fields");
 struct EpaPoly {
   double vw[kEpaMaxV][3], va[kEpaMaxV][3];
   double fn[kEpaMaxF][3], fd[kEpaMaxF];
   double out[6];
-  int32_t adj[kEpaMaxF][3];  // neighbour across edge e: face | (its edge << 16)
-  int32_t hl[kEpaMaxV];      // a step's horizon edges: face | (edge << 16)
-  int32_t vout[kEpaMaxV], vin[kEpaMaxV];  // horizon edge leaving / entering each vertex
+  // narrow index types (faces < 128, edges < 3, horizon positions < 64): the
+  // polytope is most of the task kernel's per-wave LDS
+  int16_t adj[kEpaMaxF][3];  // neighbour across edge e: face | (its edge << 8)
+  int16_t hl[kEpaMaxV];      // a step's horizon edges: face | (edge << 8)
+  int8_t vout[kEpaMaxV], vin[kEpaMaxV];  // horizon edge leaving / entering each vertex (-1: none)
   int16_t fv[kEpaMaxF][3];
   int16_t freel[kEpaMaxF];  // recycled slots, last freed first
   int8_t alive[kEpaMaxF];
@@ -677,8 +680,8 @@ DRC_HD __forceinline__ int epa_newface(EpaPoly* E, int a, int b, int c) {
   return ok ? f : -1;
 }
 DRC_HD __forceinline__ void epa_bind(EpaPoly* E, int f0, int e0, int f1, int e1) {
-  E->adj[f0][e0] = f1 | (e1 << 16);
-  E->adj[f1][e1] = f0 | (e0 << 16);
+  E->adj[f0][e0] = f1 | (e1 << 8);
+  E->adj[f1][e1] = f0 | (e0 << 8);
 }
 // rerun GJK and build the initial tetrahedron from its final simplex
 // (lane-serial)
@@ -752,7 +755,7 @@ DRC_HD inline void epa_grow_canon(EpaPoly* E, const SV w, int best) {
     for (int f = 0; f < nf; ++f) {
       if (inC[f] || !E->alive[f] || !epa_sees(E, f, w.w)) continue;
       for (int e = 0; e < 3; ++e)
-        if (inC[E->adj[f][e] & 0xffff]) {
+        if (inC[E->adj[f][e] & 0xff]) {
           inC[f] = true;
           grown = true;
           break;
@@ -765,7 +768,7 @@ DRC_HD inline void epa_grow_canon(EpaPoly* E, const SV w, int best) {
   for (int c = 0; c < nf && ok; ++c) {
     if (!inC[c]) continue;
     for (int e = 0; e < 3 && ok; ++e) {
-      if (inC[E->adj[c][e] & 0xffff]) continue;
+      if (inC[E->adj[c][e] & 0xff]) continue;
       const int a = E->fv[c][e], b = E->fv[c][epa_next_edge(e)];
       if (H >= kEpaMaxV || E->vout[a] >= 0 || E->vin[b] >= 0) {
         ok = false;
@@ -813,9 +816,9 @@ DRC_HD inline void epa_grow_canon(EpaPoly* E, const SV w, int best) {
     E->fv[f][2] = wi;
     const int g = E->adj[c][e];
     E->adj[f][0] = g;
-    E->adj[g & 0xffff][g >> 16] = f;
-    E->adj[f][1] = slot[(k + 1) % H] | (2 << 16);
-    E->adj[f][2] = slot[(k + H - 1) % H] | (1 << 16);
+    E->adj[g & 0xff][g >> 8] = f;
+    E->adj[f][1] = slot[(k + 1) % H] | (2 << 8);
+    E->adj[f][2] = slot[(k + H - 1) % H] | (1 << 8);
   }
   const int nfree0 = E->nfree > H ? E->nfree - H : 0;
   if (H > E->nfree) E->nf = nf + (H - E->nfree);
@@ -873,9 +876,9 @@ __device__ __forceinline__ void epa_grow_wave(EpaPoly* E, const SV& w, int best)
   uint64_t clo = best < 64 ? 1ull << best : 0ull, chi = best < 64 ? 0ull : 1ull << (best - 64);
   for (;;) {  // component of best among the visible faces, one ring per round
     const bool j0 = s0 && !in(clo, chi, f0) &&
-                    (in(clo, chi, n0[0] & 0xffff) || in(clo, chi, n0[1] & 0xffff) || in(clo, chi, n0[2] & 0xffff));
+                    (in(clo, chi, n0[0] & 0xff) || in(clo, chi, n0[1] & 0xff) || in(clo, chi, n0[2] & 0xff));
     const bool j1 = s1 && !in(clo, chi, f1) &&
-                    (in(clo, chi, n1[0] & 0xffff) || in(clo, chi, n1[1] & 0xffff) || in(clo, chi, n1[2] & 0xffff));
+                    (in(clo, chi, n1[0] & 0xff) || in(clo, chi, n1[1] & 0xff) || in(clo, chi, n1[2] & 0xff));
     const uint64_t nlo = clo | __ballot(j0), nhi = chi | __ballot(j1);
     if (nlo == clo && nhi == chi) break;
     clo = nlo;
@@ -886,8 +889,8 @@ __device__ __forceinline__ void epa_grow_wave(EpaPoly* E, const SV& w, int best)
   bool hz[6];
 #pragma unroll
   for (int e = 0; e < 3; ++e) {
-    hz[e] = c0 && !in(clo, chi, n0[e] & 0xffff);
-    hz[3 + e] = c1 && !in(clo, chi, n1[e] & 0xffff);
+    hz[e] = c0 && !in(clo, chi, n0[e] & 0xff);
+    hz[3 + e] = c1 && !in(clo, chi, n1[e] & 0xff);
   }
   const uint64_t below = (1ull << l) - 1;
   int H = 0;
@@ -905,7 +908,7 @@ __device__ __forceinline__ void epa_grow_wave(EpaPoly* E, const SV& w, int best)
     for (int j = 0; j < 6; ++j)
       if (hz[j]) {
         const int c = j < 3 ? f0 : f1, e = j % 3;
-        E->hl[pos[j]] = c | (e << 16);
+        E->hl[pos[j]] = c | (e << 8);
         E->vout[E->fv[c][e]] = pos[j];
         E->vin[E->fv[c][epa_next_edge(e)]] = pos[j];
       }
@@ -915,8 +918,8 @@ __device__ __forceinline__ void epa_grow_wave(EpaPoly* E, const SV& w, int best)
   int hc = 0, he_ = 0, a = 0, b = 0, nx = 0, pv = 0;
   if (own) {
     const int hv = E->hl[l];
-    hc = hv & 0xffff;
-    he_ = hv >> 16;
+    hc = hv & 0xff;
+    he_ = hv >> 8;
     a = E->fv[hc][he_];
     b = E->fv[hc][epa_next_edge(he_)];
     nx = E->vout[b];
@@ -965,9 +968,9 @@ __device__ __forceinline__ void epa_grow_wave(EpaPoly* E, const SV& w, int best)
     E->fv[slot][1] = b;
     E->fv[slot][2] = wi;
     E->adj[slot][0] = g;
-    E->adj[g & 0xffff][g >> 16] = slot;
-    E->adj[slot][1] = snx | (2 << 16);
-    E->adj[slot][2] = spv | (1 << 16);
+    E->adj[g & 0xff][g >> 8] = slot;
+    E->adj[slot][1] = snx | (2 << 8);
+    E->adj[slot][2] = spv | (1 << 8);
     E->alive[slot] = 1;
   }
   if (in(rlo, rhi, f0)) {

@@ -681,7 +681,7 @@ __device__ __forceinline__ void task_instance(const DevModel* __restrict__ M0, c
   // witness points in registers (ties -> lowest pair index, the oracle's
   // first-strict-min rule), so the winner's witnesses never get recomputed.
   double* pd = S + kp.kPd;
-  double* pf = S + kp.kPf;
+  int8_t* pf = reinterpret_cast<int8_t*>(S + kp.kPf);  // 0 open, 1 done, 2 penetrating (EPA)
   double bestd = 1.7976931348623157e308;
   int besti = 0x7fffffff;
   int bhow = 0;  // how the running best was found: 0 closed form, 1 GJK, 2 EPA
@@ -699,7 +699,7 @@ __device__ __forceinline__ void task_instance(const DevModel* __restrict__ M0, c
                             ? (d = sphere_pair(A, Bs, &pA, &pB), true)
                             : (A.type == kCylinder && Bs.type == kCylinder && cyl_cyl_side(A, Bs, &d, &pA, &pB));
     if (closed) {
-      pf[p] = 1.0;
+      pf[p] = 1;
       ub = fmin(ub, d);
       if (d < bestd || (d == bestd && p < besti)) {  // ties -> lowest pair index
         bestd = d;
@@ -710,7 +710,7 @@ __device__ __forceinline__ void task_instance(const DevModel* __restrict__ M0, c
       }
     } else {  // swept-core / separating-axis lower bound
       pd[p] = pair_lower_bound(A, Bs, M->gbound[ga], M->gbound[gb]);
-      pf[p] = 0.0;
+      pf[p] = 0;
     }
   }
   ub = -wave_max(-ub);
@@ -723,7 +723,7 @@ __device__ __forceinline__ void task_instance(const DevModel* __restrict__ M0, c
     int ncand = 0;
     for (int p0 = 0; p0 < M->npairs; p0 += 64) {
       const int p = p0 + l;
-      const bool c = p < M->npairs && pf[p] == 0.0 && pd[p] - 1e-9 <= ub;
+      const bool c = p < M->npairs && pf[p] == 0 && pd[p] - 1e-9 <= ub;
       const unsigned long long m = __ballot(c);
       if (c) cand[ncand + __popcll(m & ((1ull << l) - 1))] = p;
       ncand += __popcll(m);
@@ -737,11 +737,11 @@ __device__ __forceinline__ void task_instance(const DevModel* __restrict__ M0, c
       // early exit once GJK's lower bound shows the pair cannot reach ub
       const GjkDist g = gjk(A, Bs, ub + 1e-9);
       if (g.pruned) {
-        pf[p] = 1.0;
+        pf[p] = 1;
       } else if (g.intersect) {
-        pf[p] = 2.0;  // penetrating: EPA below
+        pf[p] = 2;  // penetrating: EPA below
       } else {
-        pf[p] = 1.0;
+        pf[p] = 1;
         if (g.dist < bestd || (g.dist == bestd && p < besti)) {
           bestd = g.dist;
           besti = p;
@@ -767,7 +767,7 @@ __device__ __forceinline__ void task_instance(const DevModel* __restrict__ M0, c
       double cpd = 1.7976931348623157e308;
       int cp = 0x7fffffff;
       for (int p = l; p < M->npairs; p += 64)
-        if (pf[p] == 2.0 && pd[p] < cpd) {
+        if (pf[p] == 2 && pd[p] < cpd) {
           cpd = pd[p];
           cp = p;
         }
@@ -791,7 +791,7 @@ __device__ __forceinline__ void task_instance(const DevModel* __restrict__ M0, c
         gbd = dall;
         gbi = p;
       }
-      if (l == ln) pf[p] = 1.0;
+      if (l == ln) pf[p] = 1;
       wsync();
     }
   }
