@@ -10,6 +10,8 @@
 #include "task_stage.hpp"
 #include "launch.hpp"
 
+#include <cstdlib>
+
 namespace drc_amd {
 
 // Occupancy target of the task kernel (waves per SIMD): the lane-serial
@@ -49,7 +51,13 @@ int launch_task_kernel(int problem, unsigned grid, size_t lds, hipStream_t st, c
                        const IO& io) {
   // LDS-limited residency of the two-wave build is 8 waves per CU (160 KB / 20 KB);
   // a plan of <= 16 KB lets the three-wave build hold 10 or more
-  if (problem == 0 && lds <= 16 * 1024)
+  // (DRC_TASK_W3=0 / 1 forces the choice: A/B experiments)
+  static const int w3_env = [] {
+    const char* e = std::getenv("DRC_TASK_W3");
+    return e ? std::atoi(e) : -1;
+  }();
+  const bool w3 = w3_env >= 0 ? w3_env != 0 : lds <= 16 * 1024;
+  if (problem == 0 && w3)
     hipLaunchKernelGGL((task_kernel<0, 3>), dim3(grid), dim3(64), lds, st, m, kp, io);
   else if (problem == 0)
     hipLaunchKernelGGL(task_kernel<0>, dim3(grid), dim3(64), lds, st, m, kp, io);
