@@ -25,6 +25,7 @@ template <class QD>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRC_FUSED_WAVES, 8)))
 fused_kernel(const DevModel* __restrict__ M0, const KParams kt, const KParams kq, const IO io) {
   extern __shared__ __attribute__((aligned(16))) double S[];
+  PH_KSCOPE();
   __shared__ KParams kpl;  // LDS copy of the QP parameters for the out-of-line ADMM blocks
   {
     static_assert(sizeof(KParams) % 8 == 0, "KParams copied as 8-byte words");

@@ -9,14 +9,38 @@
 #ifdef DRC_PHASE_TIMING
 namespace drc_amd {
 static __device__ unsigned long long g_phase_cycles[64];
+// per-wave accumulators in LDS (lane 0 adds; the kernel adds them to the
+// device array once, at its end): a global atomic per phase and call from
+// every wave queued at the L2 and inflated the very cycles being measured
+static __shared__ unsigned long long g_ph_lds[64];
 }
+#define PH_KINIT()                         \
+  do {                                     \
+    g_ph_lds[__lane_id()] = 0ull;          \
+    __builtin_amdgcn_wave_barrier();       \
+  } while (0)
+#define PH_KFLUSH()                                                   \
+  do {                                                                \
+    __builtin_amdgcn_wave_barrier();                                  \
+    const unsigned long long v_ = g_ph_lds[__lane_id()];              \
+    if (v_) atomicAdd(&g_phase_cycles[__lane_id()], v_);              \
+  } while (0)
+// PH_KSCOPE(): zero the wave's slots at kernel entry, add them to the device
+// array at kernel exit
+namespace drc_amd {
+struct PhKernelScope {
+  __device__ PhKernelScope() { PH_KINIT(); }
+  __device__ ~PhKernelScope() { PH_KFLUSH(); }
+};
+}
+#define PH_KSCOPE() drc_amd::PhKernelScope ph_kscope_
 // whole statements that exist only in the timing build
 #define PH_ONLY(...) __VA_ARGS__
 // a named stamp, and its elapsed cycles added to a slot by lane 0
 #define PH_STAMP(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
 #define PH_ADD(slot, val)                                                                        \
   do {                                                                                           \
-    if (__lane_id() == 0) atomicAdd(&g_phase_cycles[(slot)], (unsigned long long)(val));         \
+    if (__lane_id() == 0) g_ph_lds[(slot)] += (unsigned long long)(val);                        \
   } while (0)
 #define PH_SINCE(slot, v) PH_ADD(slot, __builtin_amdgcn_s_memtime() - (v))
 // a private accumulator and an addition of the cycles since a stamp
@@ -34,14 +58,14 @@ static __device__ unsigned long long g_phase_cycles[64];
 #define PH_FLUSH(base)                                                                     \
   do {                                                                                     \
     if (__lane_id() == 0)                                                                  \
-      for (int k_ = 0; k_ < 16; ++k_) atomicAdd(&g_phase_cycles[(base) + k_], ph_acc[k_]); \
+      for (int k_ = 0; k_ < 16; ++k_) g_ph_lds[(base) + k_] += ph_acc[k_];                 \
   } while (0)
 // direct accumulation (functions without the kernel's stamp locals)
 #define PHG_DECL unsigned long long phg_t = __builtin_amdgcn_s_memtime();
 #define PHG(slot)                                                                 \
   do {                                                                            \
     unsigned long long t_ = __builtin_amdgcn_s_memtime();                         \
-    if (__lane_id() == 0) atomicAdd(&g_phase_cycles[(slot)], t_ - phg_t);         \
+    if (__lane_id() == 0) g_ph_lds[(slot)] += t_ - phg_t;                        \
     phg_t = t_;                                                                   \
   } while (0)
 #define PHG_RESET() \
@@ -53,7 +77,7 @@ static __device__ unsigned long long g_phase_cycles[64];
 #define CK_T(slot)                                                      \
   do {                                                                  \
     const unsigned long long t_ = __builtin_amdgcn_s_memtime();         \
-    if (__lane_id() == 0) atomicAdd(&g_phase_cycles[(slot)], t_ - ck_t); \
+    if (__lane_id() == 0) g_ph_lds[(slot)] += t_ - ck_t;                \
     ck_t = t_;                                                          \
   } while (0)
 #define CK_N(slot) PH_ADD(slot, 1)
@@ -71,6 +95,9 @@ static __device__ unsigned long long g_phase_cycles[64];
   }
 #else
 #define PH_ONLY(...)
+#define PH_KINIT() do {} while (0)
+#define PH_KFLUSH() do {} while (0)
+#define PH_KSCOPE() do {} while (0)
 #define PH_STAMP(v) do {} while (0)
 #define PH_ADD(slot, val) do {} while (0)
 #define PH_SINCE(slot, v) do {} while (0)

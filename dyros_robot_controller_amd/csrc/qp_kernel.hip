@@ -23,6 +23,7 @@ template <class QD>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRC_QP_WAVES, 8)))
 qp_kernel(const DevModel* __restrict__ M0, const KParams kp, const IO io) {
   extern __shared__ __attribute__((aligned(16))) double S[];
+  PH_KSCOPE();
   // LDS copy of the parameters for the out-of-line (rare) ADMM blocks: a
   // reference to the kernel argument itself would be copied to scratch
   __shared__ KParams kpl;

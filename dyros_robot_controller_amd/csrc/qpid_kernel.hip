@@ -150,6 +150,7 @@ template <class QD>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DRC_QPID_WAVES, 8)))
 qpid_kernel(const DevModel* __restrict__ M0, const KParams kp, const IO io) {
   extern __shared__ __attribute__((aligned(16))) double S[];
+  PH_KSCOPE();
   __shared__ KParams kpl;
   const int l = lane_id();
   {

@@ -31,6 +31,7 @@ template <int PROBLEM, int WAVES = DRC_TASK_WAVES>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
 task_kernel(const DevModel* __restrict__ M0, const KParams kp, const IO io) {
   extern __shared__ __attribute__((aligned(16))) double S[];
+  PH_KSCOPE();
   const int64_t B = io.B;
   // hard mode: the instances the lane-per-instance stage left (grid stride)
   const bool hard_mode = io.hard_mode != 0;
