@@ -381,7 +381,7 @@ static int plan_layout(const DevModel& M, KParams* k, bool task_only) {
   k->oT2 = take(m > nx ? m : nx);
   k->oRed = take(64);
   k->oSc = take(32);
-  k->oBc = take(ng + np > 32 ? ng + np : 32);  // ADMM passes: NG rows then NP cores; EQP: <= kEqpRegCap
+  k->oBc = take(nx + ng > 32 ? nx + ng : 32);  // Ruiz factors (nx + ng), ADMM passes (ng + np), EQP (<= kEqpRegCap)
   }
   k->oHi = -1;
   if (!task_only && k->problem == 0 && M.kind == 1 && qp_compiled(nx, ng, np)) k->oHi = take(nx * nx);

@@ -52,7 +52,7 @@ struct KParams {
   drc_solver_settings s;
   // persistent QP region
   int oP, oG, oQ, oAB, oL, oU, oD, oE, oRho, oX, oZ, oY, oDY, oXT, oZT, oT1, oT2, oRed, oSc;
-  int oBc;  // max(32, ng + np) doubles: vectors broadcast through LDS (ADMM passes, polish KKT sweeps)
+  int oBc;  // max(32, nx + ng) doubles: vectors broadcast through LDS (ADMM passes, polish KKT sweeps)
   // union region (kinematics | K^-1 | polish)
   int oU0;
   int oHi;  // whole-body polish: cached rows of (P + delta I)^-1 (persistent, nx * nx), -1 if unused

@@ -1421,6 +1421,21 @@ __device__ __forceinline__ int qp_scale(const KParams& kp, double* S) {
   return status;
 }
 
+// max |a_i| as a balanced tree: fmax of non-NaN values is exact and
+// order-free, so this is bit for bit the serial chain's result at a depth of
+// log2 N instead of N dependent fmax (the Ruiz passes' critical path)
+template <int N>
+__device__ __forceinline__ double absmax_tree(const double (&a)[N]) {
+  double t[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) t[i] = fabs(a[i]);
+#pragma unroll
+  for (int w = 1; w < N; w *= 2)
+#pragma unroll
+    for (int i = 0; i + w < N; i += 2 * w) t[i] = fmax(t[i], t[i + w]);
+  return t[0];
+}
+
 // Register form of qp_scale for compile-time shapes: lane l holds row l of P
 // (= column l: P is symmetric bit for bit), column l and row l of G; the
 // Ruiz factors move by v_readlane.  Same operations in the same order as
@@ -1452,17 +1467,12 @@ __device__ __forceinline__ int qp_scale_regs(const KParams& kp, double* S) {
   double abl = ab[lx], ql = qq[lx], Dl = 1.0, El = 1.0, EGl = 1.0, cs = 1.0;
   auto clampf = [](double v) { return v < kMinScaling ? 1.0 : (v > kMaxScaling ? kMaxScaling : v); };
   for (int it = 0; it < kp.s.scaling; ++it) {
-    double s = fabs(abl);
-    if (hp)
-#pragma unroll
-      for (int i = 0; i < NP; ++i) s = fmax(s, fabs(Prow[i]));
-#pragma unroll
-    for (int i = 0; i < NG; ++i) s = fmax(s, fabs(Gcol[i]));
+    // (the inputs are finite -- checked above -- so every fmax below is exact)
+    const double sgc = absmax_tree(Gcol);
+    const double s = fmax(fabs(abl), hp ? fmax(absmax_tree(Prow), sgc) : sgc);
     const double Dt = 1.0 / sqrt(clampf(s));
     const double Et = 1.0 / sqrt(clampf(fabs(abl)));
-    double sg = 0;
-#pragma unroll
-    for (int j = 0; j < NX; ++j) sg = fmax(sg, fabs(Grow[j]));
+    const double sg = absmax_tree(Grow);
     const double EtG = 1.0 / sqrt(clampf(sg));
     // every factor of this pass exactly 1 (the fixed-point pass, usually the
     // second): the products below would multiply by 1.0, an identity, so
@@ -1473,9 +1483,21 @@ __device__ __forceinline__ int qp_scale_regs(const KParams& kp, double* S) {
       // the broadcast factors are used as they arrive (not gathered into
       // per-lane arrays: 39 doubles more would not fit the QP kernel's 168-VGPR
       // budget and spilled); same products in the same order
+      // (64-lane waves: the factors reach the lanes through LDS -- each lane
+      // writes its own, every lane reads them all -- instead of NX + NG VALU
+      // broadcasts)
+      constexpr bool kLds = QD::gs == 64;
+      lds_double* wb = (lds_double*)(S + kp.oBc);  // NX + NG doubles (plan_layout)
+      if constexpr (kLds) {
+        if (hx) wb[l] = Dt;
+        if (hg) wb[NX + l] = EtG;
+        asm volatile("" ::: "memory");
+      }
       static_for<NX>([&](auto C) {
         constexpr int c = decltype(C)::value;
-        const double dc = GL::template bcastc<c>(Dt);
+        double dc;
+        if constexpr (kLds) dc = wb[c];
+        else dc = GL::template bcastc<c>(Dt);
         if constexpr (c < NP) {
           if (hp) Prow[c] *= Dt * dc;
         }
@@ -1483,9 +1505,12 @@ __device__ __forceinline__ int qp_scale_regs(const KParams& kp, double* S) {
       });
       static_for<NG>([&](auto I) {
         constexpr int i = decltype(I)::value;
-        const double ei = GL::template bcastc<i>(EtG);
+        double ei;
+        if constexpr (kLds) ei = wb[NX + i];
+        else ei = GL::template bcastc<i>(EtG);
         if (hx) Gcol[i] *= ei * Dt;
       });
+      if constexpr (kLds) asm volatile("" ::: "memory");
       if (hx) {
         abl *= Et * Dt;
         ql *= Dt;
@@ -1496,9 +1521,7 @@ __device__ __forceinline__ int qp_scale_regs(const KParams& kp, double* S) {
     }
     // cost scaling: mean column norm of P vs |q|_inf
     double cn = 0, qn = 0;
-    if (hp)
-#pragma unroll
-      for (int i = 0; i < NP; ++i) cn = fmax(cn, fabs(Prow[i]));
+    if (hp) cn = absmax_tree(Prow);
     if (hx) qn = fabs(ql);
     cn = GL::sum(cn) / NX;
     qn = GL::max(qn);
