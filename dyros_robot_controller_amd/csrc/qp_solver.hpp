@@ -1467,6 +1467,7 @@ __device__ __forceinline__ int qp_scale_regs(const KParams& kp, double* S) {
   double abl = ab[lx], ql = qq[lx], Dl = 1.0, El = 1.0, EGl = 1.0, cs = 1.0;
   auto clampf = [](double v) { return v < kMinScaling ? 1.0 : (v > kMaxScaling ? kMaxScaling : v); };
   for (int it = 0; it < kp.s.scaling; ++it) {
+    PH_ADD(49, 1);  // Ruiz passes
     // (the inputs are finite -- checked above -- so every fmax below is exact)
     const double sgc = absmax_tree(Gcol);
     const double s = fmax(fabs(abl), hp ? fmax(absmax_tree(Prow), sgc) : sgc);

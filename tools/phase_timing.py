@@ -40,3 +40,4 @@ print("admm_check: residuals %.0f cyc/inst (%d calls), polish %.0f cyc/inst (%d 
 print("eqp: %d calls, %.0f cycles/call, mean KKT size %.1f; polish residuals %.0f cycles/call" % (v[41], v[40] / max(v[41], 1), v[42] / max(v[41], 1), v[43] / max(v[41], 1)))
 print("qp record load (inside load+assemble): %.0f cyc/inst" % (v[44] / B))
 print("polish steps: infeasible->add/drop %d, wrong dual sign->drop %d, ratio-test blocks %d, KKT residual failures %d" % (v[45], v[46], v[47], v[48]))
+print("Ruiz passes: %.2f per instance" % (v[49] / B))
