@@ -41,6 +41,8 @@ from dyros_robot_controller_amd import dist as ddist  # noqa: E402  (no torch / 
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 FP64_VECTOR_PEAK_TFS = 78.6    # AMD spec, FP64 vector
+SIMDS = 256 * 4                # CUs x SIMDs (MI355X_MICROARCH.md)
+CLOCK_HZ = 2.4e9               # max engine clock (MI355X_MICROARCH.md chip table)
 CLOCK_GHZ = 2.4                # MI355X peak engine clock (MI355X_MICROARCH.md)
 WAVE_SLOTS = 256 * 4 * 2       # CUs x SIMDs x waves per SIMD of the task kernel (256 VGPRs, ~19 KB LDS; QP kernel: 3)
 DEFAULT_BATCH = {"fr3": 65536, "ur5e": 65536, "husky_fr3": 16384, "xls_fr3": 65536, "caster_fr3": 65536}
@@ -446,6 +448,17 @@ def main():
                                  "note": "issued counts 64 lanes per FP64 instruction; executed = issued x lane "
                                          "efficiency (active lanes); neither is algorithmic work",
                                  "source": "profiles/valu_counters_%s.json (build %s)" % (robot, build)}
+            cyc = valu.get("valu_issue_cycles_per_solve")
+            if cyc:   # a hardware roof: every SIMD issuing VALU work back to back at the maximum clock
+                iroof = SIMDS * CLOCK_HZ / cyc
+                roof["valu_issue_roof"] = {
+                    "issue_cycles_per_solve": cyc, "valu_insts_per_solve": valu["valu_insts_per_solve"],
+                    "solves_per_s": iroof, "frac": value / iroof,
+                    "note": "1 024 SIMDs x 2.4 GHz over the VALU issue cycles per solve counted on this build "
+                            "(SQ_INSTS_VALU and its FP64 classes, task + QP kernels: 4 cycles per wave64 FP64 "
+                            "instruction, 2 per other VALU instruction); SALU, LDS and memory instructions issue "
+                            "beside it and are not charged",
+                    "source": "profiles/valu_counters_%s.json (build %s)" % (robot, build)}
         line = {
             "metric": METRIC, "value": value, "unit": "solves/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": scaling,
@@ -519,10 +532,10 @@ def extras(torch, args, rd, mod, robot, link, q, qd, xt, xdt, dq, dqd, dxt, dxdt
     line["roofline"]["latency_roof"] = {
         "instance_latency_us": 1e6 * lat, "call_us": 1e3 * tw.value / max(nc.value, 1), "wave_slots": WAVE_SLOTS,
         "solves_per_s": roof, "frac": line["value"] / roof,
-        "note": "mean over the batch's first 32 instances, each alone on the GPU (B = 1 calls, kernel durations by "
-                "HIP events): a wave-per-instance design with WAVE_SLOTS instances in flight (two task-kernel waves per "
-                "SIMD; the QP kernel runs three since D20, so this roof is approximate) cannot beat WAVE_SLOTS / "
-                "latency if instances ran at their isolated latency"}
+        "note": "design-relative, not a hardware limit (the hardware roof is valu_issue_roof): mean over the "
+                "batch's first 32 instances, each alone on the GPU (B = 1 calls, kernel durations by HIP events); "
+                "WAVE_SLOTS instances in flight (two task-kernel waves per SIMD; the QP kernel runs three, so this "
+                "roof is approximate) at their isolated latency would give WAVE_SLOTS / latency"}
 
 
 if __name__ == "__main__":

@@ -58,11 +58,21 @@ def main():
     step_hw = chunks * sum(kern[k]["fp64_flops_hw_per_dispatch"] or 0 for k in qp)
     tc = sum(kern[k]["per_dispatch"].get("SQ_THREAD_CYCLES_VALU", 0) for k in qp)
     ac = sum(kern[k]["per_dispatch"].get("SQ_ACTIVE_INST_VALU", 0) for k in qp)
+    # VALU issue cycles on the SIMD: a wave64 FP64 instruction (16 FP64 lanes per
+    # cycle: the 78.6 TFLOP/s vector peak = 1 024 SIMDs x 2.4 GHz x 16 FMA) takes
+    # 4 cycles, any other VALU instruction 2 (32 lanes per cycle, MI355X_MICROARCH.md)
+    def f64(a):
+        return sum(a.get(c, 0) for c in ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64",
+                                          "SQ_INSTS_VALU_TRANS_F64"))
+    issue = chunks * sum(4 * f64(kern[k]["per_dispatch"]) + 2 * (kern[k]["per_dispatch"].get("SQ_INSTS_VALU", 0)
+                                                                   - f64(kern[k]["per_dispatch"])) for k in qp)
+    valu_insts = chunks * sum(kern[k]["per_dispatch"].get("SQ_INSTS_VALU", 0) for k in qp)
     with open(os.path.join(src, "build_id")) as fh:
         build = fh.read().strip()
     out = {"robot": robot, "batch": batch, "chunks": chunks, "tag": tag, "build_id": build, "kernels": kern,
            "fp64_flops_per_step": step, "fp64_flops_hw_per_step": step_hw,
            "fp64_flops_per_solve": step / batch, "lane_efficiency": tc / max(64 * ac, 1),
+           "valu_insts_per_solve": valu_insts / batch, "valu_issue_cycles_per_solve": issue / batch,
            "note": "FLOP = 64 x (2 FMA + ADD + MUL) FP64 instructions per dispatch, summed over the task and QP "
                    "kernels of one call (chunks dispatches each); lane efficiency = thread-cycles / (64 x active "
                    "VALU quad-cycles) over both kernels"}
