@@ -23,10 +23,8 @@ namespace drc_amd {
 // instantiation, so the QPIK kernel carries no call frame for them); 2: CLIK / OSF
 // WAVES: the register budget's occupancy target; the QPIK stage also has a
 // three-wave build (168 VGPRs, more spills) for models whose LDS plan lets a
-// CU hold more than the 8 waves the two-wave build can: UR5e (15.7 KB per
-// wave, 10 waves per CU) +3.6 %, while FR3 / the whole-body robots (19.6 /
-// 20.6-22.6 KB: 8 or 7 waves per CU either way) lose 1.6-3 % to the spills
-// (profiles/r04j_ab_lds.jsonl)
+// CU hold more than the 8 waves the two-wave build can (FR3, UR5e); where the
+// plan allows only 8 it loses 1.6-3 % to the spills (profiles/r04j_ab_lds.jsonl)
 template <int PROBLEM, int WAVES = DRC_TASK_WAVES>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
 task_kernel(const DevModel* __restrict__ M0, const KParams kp, const IO io) {
@@ -50,14 +48,15 @@ task_kernel(const DevModel* __restrict__ M0, const KParams kp, const IO io) {
 
 int launch_task_kernel(int problem, unsigned grid, size_t lds, hipStream_t st, const DevModel* m, const KParams& kp,
                        const IO& io) {
-  // LDS-limited residency of the two-wave build is 8 waves per CU (160 KB / 20 KB);
-  // a plan of <= 16 KB lets the three-wave build hold 10 or more
+  // the two-wave build holds 8 waves per CU; the three-wave build pays where the
+  // plan lets a CU hold 9 or more (<= 160 KB / 9: FR3 17.1 KB +0.9 %, UR5e 14.0 KB
+  // +11 % with the narrowed plan, profiles/r04l_envab_w3.jsonl, r04k_ab_w3_ldsnarrow.jsonl)
   // (DRC_TASK_W3=0 / 1 forces the choice: A/B experiments)
   static const int w3_env = [] {
     const char* e = std::getenv("DRC_TASK_W3");
     return e ? std::atoi(e) : -1;
   }();
-  const bool w3 = w3_env >= 0 ? w3_env != 0 : lds <= 16 * 1024;
+  const bool w3 = w3_env >= 0 ? w3_env != 0 : lds * 9 <= 160 * 1024;
   if (problem == 0 && w3)
     hipLaunchKernelGGL((task_kernel<0, 3>), dim3(grid), dim3(64), lds, st, m, kp, io);
   else if (problem == 0)
