@@ -12,9 +12,12 @@ namespace drc_amd {
 // ------------------------------------------------------------------------
 // OSQP residuals (lane-parallel): fills SC_* slots.  x, z, y in LDS (scaled)
 // ------------------------------------------------------------------------
-template <class QD, bool UNSCALED = true>
+// PRE: the caller already holds this lane's A x entry (bound row: ab x, G row:
+// G x, formed by the same expressions in the same order -- the polish's
+// candidate), so the products are not formed twice
+template <class QD, bool UNSCALED = true, bool PRE = false>
 __device__ __forceinline__ void residuals(const KParams& kp, double* S, const double* x, const double* z, const double* y,
-                          double eps_abs, double eps_rel) {
+                          double eps_abs, double eps_rel, double axb_pre = 0.0, double axg_pre = 0.0) {
   using GL = Grp<QD::gs>;
   // UNSCALED = false (the polish's certification) skips the unscaled norms
   // that only adaptive rho reads (SC_PRIS .. SC_NQ keep the ADMM values)
@@ -24,7 +27,7 @@ __device__ __forceinline__ void residuals(const KParams& kp, double* S, const do
   double dr = 0, drs = 0, nPx = 0, nAty = 0, nq = 0, nPxs = 0, nAtys = 0, nqs = 0;
   if (l < nx) {  // bound row l and variable l
     const int lx = l < nx ? l : 0;
-    double ax = ab[lx] * x[lx], r = ax - z[lx];
+    double ax = PRE ? axb_pre : ab[lx] * x[lx], r = ax - z[lx];
     prs = fabs(r);
     pr = fabs(r / E[lx]);
     nAx = fabs(ax / E[lx]);
@@ -53,8 +56,12 @@ __device__ __forceinline__ void residuals(const KParams& kp, double* S, const do
   if (l < ng) {
     const int lg = l < ng ? l : 0;
     double ax = 0;
+    if constexpr (PRE) {
+      ax = axg_pre;
+    } else {
 #pragma unroll
-    for (int j = 0; j < nx; ++j) ax += G[lg * nx + j] * x[j];
+      for (int j = 0; j < nx; ++j) ax += G[lg * nx + j] * x[j];
+    }
     int row = nx + lg;
     double r = ax - z[row];
     prs = fmax(prs, fabs(r));
@@ -1081,7 +1088,7 @@ __device__ __forceinline__ bool polish(const KParams& kp, double* S, bool strict
     }
     wsync();
     PH_STAMP(rs_t0);
-    residuals<QD, false>(kp, S, xx, zz, yy, kp.s.eps_exact, kp.s.eps_exact);
+    residuals<QD, false, true>(kp, S, xx, zz, yy, kp.s.eps_exact, kp.s.eps_exact, axb, axg);
     PH_SINCE(43, rs_t0);
     const double pr1 = sc[SC_PRI], dr1 = sc[SC_DUA], epsp = sc[SC_EPSP], epsd = sc[SC_EPSD], c = sc[SC_C];
     bool ok = (pr1 < pr0 && dr1 < dr0) || (pr1 < pr0 && dr0 < 1e-10) || (dr1 < dr0 && pr0 < 1e-10);

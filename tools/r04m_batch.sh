@@ -3,3 +3,6 @@ mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gputest_r04m.log 2>&1
 rc=$?; tail -3 gpurun_out/gputest_r04m.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 600 bash tools/ab_bench.sh r04m_ruiz "libdrc_amd_base.so libdrc_amd.so" "fr3 xls_fr3 ur5e husky_fr3" 3 || exit 1
+DRC_AMD_LIB=libdrc_amd_base.so timeout -k 10 300 python3 tools/lib_bits.py base > gpurun_out/r04m_bits.log 2>&1 || exit 1
+timeout -k 10 300 python3 tools/lib_bits.py new >> gpurun_out/r04m_bits.log 2>&1 || exit 1
+python3 tools/lib_bits.py --compare base new >> gpurun_out/r04m_bits.log 2>&1; tail -5 gpurun_out/r04m_bits.log
