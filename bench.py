@@ -163,6 +163,22 @@ def load_profile(name, robot, B, build_id):
     return None
 
 
+def valu_issue_roof(valu, value, world=1):
+    """A hardware roof from a same-build VALU counter summary: every SIMD of
+    the job's GPUs issuing VALU work back to back at the maximum clock, over
+    the counted issue cycles per solve (None without the count)."""
+    cyc = valu.get("valu_issue_cycles_per_solve")
+    if not cyc:
+        return None
+    roof = world * SIMDS * CLOCK_HZ / cyc
+    return {"issue_cycles_per_solve": cyc, "valu_insts_per_solve": valu.get("valu_insts_per_solve"),
+            "solves_per_s": roof, "frac": value / roof, "n_gpus": world,
+            "note": "n_gpus x 1 024 SIMDs x 2.4 GHz over the VALU issue cycles per solve counted on this build "
+                    "(SQ_INSTS_VALU and its FP64 classes, task + QP kernels: 4 cycles per wave64 FP64 instruction, "
+                    "2 per other VALU instruction); SALU, LDS and memory instructions issue beside it and are not "
+                    "charged"}
+
+
 def timed_steps(torch, step, steps, warmup):
     """Warm-up, then ``steps`` calls bracketed by synchronisation: seconds per
     call (host wall clock over the whole run)."""
@@ -448,17 +464,9 @@ def main():
                                  "note": "issued counts 64 lanes per FP64 instruction; executed = issued x lane "
                                          "efficiency (active lanes); neither is algorithmic work",
                                  "source": "profiles/valu_counters_%s.json (build %s)" % (robot, build)}
-            cyc = valu.get("valu_issue_cycles_per_solve")
-            if cyc:   # a hardware roof: every SIMD issuing VALU work back to back at the maximum clock
-                iroof = SIMDS * CLOCK_HZ / cyc
-                roof["valu_issue_roof"] = {
-                    "issue_cycles_per_solve": cyc, "valu_insts_per_solve": valu["valu_insts_per_solve"],
-                    "solves_per_s": iroof, "frac": value / iroof,
-                    "note": "1 024 SIMDs x 2.4 GHz over the VALU issue cycles per solve counted on this build "
-                            "(SQ_INSTS_VALU and its FP64 classes, task + QP kernels: 4 cycles per wave64 FP64 "
-                            "instruction, 2 per other VALU instruction); SALU, LDS and memory instructions issue "
-                            "beside it and are not charged",
-                    "source": "profiles/valu_counters_%s.json (build %s)" % (robot, build)}
+            ir = valu_issue_roof(valu, value, world)
+            if ir:
+                roof["valu_issue_roof"] = dict(ir, source="profiles/valu_counters_%s.json (build %s)" % (robot, build))
         line = {
             "metric": METRIC, "value": value, "unit": "solves/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": scaling,

@@ -88,3 +88,15 @@ def test_algorithmic_flop_count():
     assert a["flops_per_solve"] < full / len(idx)
     # the nonzero-operand count excludes the dense restatement's structural zeros
     assert a["flops_per_solve"] < 0.5 * a["dense_flops_per_solve"]
+
+
+def test_valu_issue_roof():
+    """roofline.valu_issue_roof: SIMDs x clock over the counted issue cycles,
+    scaled by the job's GPUs, and absent without a count."""
+    import bench
+    r = bench.valu_issue_roof({"valu_issue_cycles_per_solve": 41084.0, "valu_insts_per_solve": 15194.0}, 22.32e6)
+    assert abs(r["solves_per_s"] - 1024 * 2.4e9 / 41084.0) < 1.0
+    assert abs(r["frac"] - 22.32e6 / r["solves_per_s"]) < 1e-12
+    r8 = bench.valu_issue_roof({"valu_issue_cycles_per_solve": 41084.0}, 8 * 22.32e6, 8)
+    assert abs(r8["frac"] - r["frac"]) < 1e-12
+    assert bench.valu_issue_roof({}, 1.0) is None
