@@ -32,7 +32,21 @@ __device__ __forceinline__ int lane_id() {
   asm volatile("" : "+v"(l));
   return l;
 }
+// Lane exchange point of the one-wave workgroups (task / QP / fused / QPID
+// kernels), whose lanes talk through LDS only.  A wave's LDS instructions
+// execute in issue order, so a compiler barrier is enough: no vmcnt / lgkmcnt
+// drain, no s_barrier (__syncthreads waited for every outstanding global and
+// scratch access at each exchange).  Measured bit-identical on all five robots'
+// bench batches, FR3 +1 % (profiles/r04q_*).  -DDRC_BLOCK_SYNC restores it.
+#ifndef DRC_BLOCK_SYNC
+__device__ __forceinline__ void wsync() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
+#else
 __device__ __forceinline__ void wsync() { __syncthreads(); }
+#endif
 
 // Wave reductions: DPP within each row of 16 lanes (quad swaps, half-row
 // and row mirrors: every lane of a row ends with the row's value), then the
