@@ -37,7 +37,7 @@ __device__ __forceinline__ int lane_id() {
 // execute in issue order, so a compiler barrier is enough: no vmcnt / lgkmcnt
 // drain, no s_barrier (__syncthreads waited for every outstanding global and
 // scratch access at each exchange).  Measured bit-identical on all five robots'
-// bench batches, FR3 +1 % (profiles/r04q_*).  -DDRC_BLOCK_SYNC restores it.
+// bench batches, FR3 +1 % (profiles/r04q_ab_wavesync.jsonl, r04q_bits.log).  -DDRC_BLOCK_SYNC restores it.
 #ifndef DRC_BLOCK_SYNC
 __device__ __forceinline__ void wsync() {
   asm volatile("" ::: "memory");
