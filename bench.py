@@ -334,7 +334,7 @@ def main():
                     help="exact: certified optimum (parity contract); osqp_default: the reference's OSQP settings")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip reference_settings / batch_4096 / latency_b1")
-    ap.add_argument("--chunks", type=int, default=3, help="concurrent sub-batches per call")
+    ap.add_argument("--chunks", type=int, default=4, help="concurrent sub-batches per call")
     ap.add_argument("--task-stage", type=int, default=0, choices=(0, 1, 2),
                     help="0 wave-per-instance task kernel (default), 1 lane stage + side-stream hand-backs, "
                          "2 lane stage + serial hand-backs (drc_debug_lane_stage)")

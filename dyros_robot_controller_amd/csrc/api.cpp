@@ -80,13 +80,15 @@ struct drc_model_impl {
   int lane_stage = 0;  // drc_debug_lane_stage: 0 off, 1 lane stage + side-stream hard path, 2 + serial hard path, 3 auto
   // timed calls: {caller-stream start, caller-stream end, per chunk: task start, task end, qp end}
   std::vector<std::vector<hipEvent_t>> events;
-  // concurrent sub-batches: the batch is cut into `chunks` contiguous ranges
-  // run on internal streams forked from / joined to the caller's stream, so
-  // one range's task kernel overlaps another's QP kernel and the straggler
-  // tails of the kernels interleave.  3 measured best on MI355X (FR3, B = 65 536:
-  // 1 / 2 / 3 / 4 chunks = 7.3 / 8.5 / 8.9 / 7.3 M solves/s; 3 lanes plus the
-  // caller's stream fit the 4 hardware queues a process gets by default)
-  int chunks = 3;
+  // concurrent sub-batches: the batch is cut into `chunks` contiguous ranges,
+  // the last on the caller's stream and the others on internal streams forked
+  // from / joined to it, so one range's task kernel overlaps another's QP
+  // kernel and the straggler tails of the kernels interleave.  4 streams fit
+  // the 4 hardware queues a process gets by default; measured on MI355X
+  // (r04u, B = 65 536): 4 sub-batches FR3 23.6 M / UR5e 20.3 M / XLS-FR3 17.9 M
+  // against 22.6 / 19.1 / 17.7 M at 3 (then on 3 internal streams + the
+  // caller's); 6 sub-batches, with 8 hardware queues or 4, were slower
+  int chunks = 4;
   // fused task + QP kernel for the compiled QPIK shapes and small batches
   // (fused_kernel.hip; drc_set_fusion): one launch per call, the record in LDS
   int fused = 1;
@@ -698,8 +700,11 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
   if (S > 1) HIP_TRY(hipEventRecord(m->ln.fork, st));
   for (int c = 0; c < S; ++c) {
     const int64_t b0 = B * c / S, b1 = B * (c + 1) / S, Bc = b1 - b0;
-    hipStream_t cs = S > 1 ? m->ln.lanes[c] : st;
-    if (S > 1) HIP_TRY(hipStreamWaitEvent(cs, m->ln.fork, 0));
+    // the last sub-batch runs on the caller's stream itself: S sub-batches take
+    // S streams, so S = 4 still fits HIP's default 4 hardware queues per process
+    const bool own = S > 1 && c < S - 1;
+    hipStream_t cs = own ? m->ln.lanes[c] : st;
+    if (own) HIP_TRY(hipStreamWaitEvent(cs, m->ln.fork, 0));
     KParams kt_c = kt, kq_c = kq;
     kt_c.xcd_map = kq_c.xcd_map = Bc >= 16384 ? 1 : 0;
     // persistent grids (work queues hand out the instances): 2048 waves per
@@ -786,10 +791,9 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
       io.hard_mode = 0;
     }
     if (timed) HIP_TRY(hipEventRecord(e2, cs));
-    if (S > 1) HIP_TRY(hipEventRecord(m->ln.joins[c], cs));
+    if (own) HIP_TRY(hipEventRecord(m->ln.joins[c], cs));
   }
-  if (S > 1)
-    for (int c = 0; c < S; ++c) HIP_TRY(hipStreamWaitEvent(st, m->ln.joins[c], 0));
+  for (int c = 0; c < S - 1; ++c) HIP_TRY(hipStreamWaitEvent(st, m->ln.joins[c], 0));
   if (timed) {
     HIP_TRY(hipEventRecord(e_end, st));
     std::lock_guard<std::mutex> g(m->mu);

@@ -1,6 +1,6 @@
 """Every BASELINE.json configuration's own bench path at its own batch size
 (bench.py's workload: SURVEY §8d with the three stress tiers, seed 12345), so
-the code the bench times -- three concurrent sub-batches, the XCD-aware
+the code the bench times -- four concurrent sub-batches, the XCD-aware
 instance order for sub-batches of >= 16 Ki, the compile-time QP shapes
 Dims<23,16,7> / <20,14,6> / <9,16,9> / <11,16,11>, the fused kernel at
 B <= 8 192 -- is the code the oracle checks:
@@ -15,8 +15,9 @@ B <= 8 192 -- is the code the oracle checks:
   Caster-FR3                               caster_fr3   65 536   0
 
 Properties checked on every instance:
-  * sub-batch invariance: the call split into 1 or 3 concurrent sub-batches
-    (drc_set_concurrency) returns bit-identical q-dot, status and iterations;
+  * sub-batch invariance: the call split into 1, 3 or 4 (the default) concurrent
+    sub-batches (drc_set_concurrency) returns bit-identical q-dot, status and
+    iterations;
     at B = 4 096 the fused kernel against the two-kernel pipeline
     (drc_set_fusion), bit for bit;
   * feasibility: every output finite; non-solved instances exactly zero
@@ -62,7 +63,7 @@ def _run(cfg, cuda):
     h = rd.model.handle
     runs = {}
     # (label, concurrency, fusion): the bench's default call last
-    variants = [("one", 1, 1), ("three", 3, 1)] if B > 8192 else [("pipeline", 3, 0), ("fused", 3, 1)]
+    variants = [("one", 1, 1), ("three", 3, 1), ("four", 4, 1)] if B > 8192 else [("pipeline", 4, 0), ("fused", 4, 1)]
     for label, chunks, fused in variants:
         _capi.check(_capi.lib().drc_set_concurrency(h, chunks))
         _capi.check(_capi.lib().drc_set_fusion(h, C.c_int(fused)))
@@ -70,7 +71,7 @@ def _run(cfg, cuda):
         out, status = ctrl.QPIK_step_batch(*args, LINK[robot], iters=iters)
         torch.cuda.synchronize()
         runs[label] = (out.cpu().numpy(), status.cpu().numpy(), iters.cpu().numpy())
-    _capi.check(_capi.lib().drc_set_concurrency(h, 3))
+    _capi.check(_capi.lib().drc_set_concurrency(h, 4))
     _capi.check(_capi.lib().drc_set_fusion(h, C.c_int(1)))
     res = (rd, moma, (q, qd, xt, xdt), runs, variants[-1][0])
     _cache[cfg] = res
@@ -80,9 +81,10 @@ def _run(cfg, cuda):
 @pytest.mark.parametrize("cfg", CONFIGS, ids=IDS)
 def test_fullsize_invariance(cuda, cfg):
     _, _, _, runs, _ = _run(cfg, cuda)
-    a, b = list(runs.values())
-    for x, y in zip(a, b):
-        assert np.array_equal(x, y), np.count_nonzero(np.any(np.atleast_2d(x != y), axis=0))
+    a, *rest = list(runs.values())
+    for b in rest:
+        for x, y in zip(a, b):
+            assert np.array_equal(x, y), np.count_nonzero(np.any(np.atleast_2d(x != y), axis=0))
 
 
 @pytest.mark.parametrize("cfg", CONFIGS, ids=IDS)
@@ -118,8 +120,9 @@ def test_fullsize_sample_matches_oracle(cuda, cfg):
     rd, moma, (q, qd, xt, xdt), runs, default = _run(cfg, cuda)
     out, status, _ = runs[default]
     B = q.shape[1]
-    third = B // 3
-    edges = [0, 1, third - 1, third, 2 * third - 1, 2 * third, B - 2, B - 1]
+    # every sub-batch boundary of the 3- and 4-way splits (api.cpp: [B c / S, B (c + 1) / S))
+    cuts = sorted({B * c // S for S in (3, 4) for c in range(1, S)})
+    edges = [0, 1, B - 2, B - 1] + [e for c in cuts for e in (c - 1, c)]
     idx = np.unique(np.concatenate([np.linspace(0, B - 1, 1000).astype(int), edges]))
     sub = lambda a: np.ascontiguousarray(a[:, idx])
     assert_qpik_parity(cfg[0], rd.model, sub(q), sub(qd), sub(xt), sub(xdt), sub(out), status[idx], EXPECTED_OFF)

@@ -4,8 +4,8 @@
 # rocprofv3 kernel-trace stats, the FETCH_SIZE / WRITE_SIZE passes and the
 # FP64 VALU passes) into gpurun_out/prof_<tag>_<robot>/ and valu_<tag>_<robot>/;
 # then the FR3 B = 4 096 line.  Summarise afterwards on the build host with
-#   python tools/pmc_summary.py <tag>_<robot> <robot> <B> 3
-#   python tools/valu_summary.py <tag>_<robot> <robot> <B> 3
+#   python tools/pmc_summary.py <tag>_<robot> <robot> <B> 4
+#   python tools/valu_summary.py <tag>_<robot> <robot> <B> 4
 #   usage: bash tools/final_round.sh <tag> [robot ...]
 set -o pipefail
 ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}

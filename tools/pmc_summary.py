@@ -77,7 +77,7 @@ def main():
     tag = sys.argv[1]
     robot = sys.argv[2] if len(sys.argv) > 2 else "fr3"
     batch = int(sys.argv[3]) if len(sys.argv) > 3 else 65536
-    chunks = int(sys.argv[4]) if len(sys.argv) > 4 else 3   # sub-batches per drc_qpik_batch call (bench default)
+    chunks = int(sys.argv[4]) if len(sys.argv) > 4 else 4   # sub-batches per drc_qpik_batch call (bench default)
     src = os.path.join(ROOT, "gpurun_out", "prof_" + tag)
     dst = os.path.join(ROOT, "profiles")
     os.makedirs(dst, exist_ok=True)

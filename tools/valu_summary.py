@@ -32,7 +32,7 @@ def short(name):
 
 def main():
     tag, robot, batch = sys.argv[1], sys.argv[2], int(sys.argv[3])
-    chunks = int(sys.argv[4]) if len(sys.argv) > 4 else 3
+    chunks = int(sys.argv[4]) if len(sys.argv) > 4 else 4
     src = os.path.join(ROOT, "gpurun_out", "valu_" + tag)
     vals = defaultdict(lambda: defaultdict(list))
     for f in glob.glob(os.path.join(src, "**", "*counter_collection.csv"), recursive=True):
