@@ -278,9 +278,10 @@ int drc_debug_lds_plan(drc_model* model, const drc_qpik_params* params, int prob
 int drc_debug_kernel_times(drc_model* model, double* wall_ms, double* task_ms, double* qp_ms, int* calls);
 
 /* Concurrency of drc_qpik_batch: the batch is split into up to `chunks`
- * contiguous sub-batches (each >= 16384 instances) that run on internal
- * streams forked from and joined back to the caller's stream (default 3).
- * Results do not depend on it. */
+ * contiguous sub-batches (each >= 4096 instances, >= 16384 when there are 4)
+ * that run concurrently: the last on the caller's stream, the others on
+ * internal streams forked from and joined back to it (default 4: 4 streams,
+ * HIP's default hardware queues per process).  Results do not depend on it. */
 int drc_set_concurrency(drc_model* model, int chunks);
 
 /* Fused task + QP kernel for the QP shapes the library compiles (the bundled
