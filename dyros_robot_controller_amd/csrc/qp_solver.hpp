@@ -1568,6 +1568,119 @@ __device__ __forceinline__ int qp_scale_regs(const KParams& kp, double* S) {
   return DRC_STATUS_MAX_ITER;
 }
 
+// Ruiz passes with one role per lane (64-lane waves, NX + NG <= 64): lane c < NX
+// holds column c of [P; G] (P's part only for c < NP), lane NX + r holds row r
+// of G, so a lane forms one absolute maximum, one factor F (D~ on column lanes,
+// E~ on row lanes) and one set of products instead of all three.  Same
+// operands, same products in the same order as qp_scale_regs (bit-identical);
+// the column copy of G is dropped at the end, as there.
+template <class QD>
+__device__ __forceinline__ int qp_scale_roles(const KParams& kp, double* S) {
+  using GL = Grp<64>;
+  constexpr int NX = QD::nx, NG = QD::ng, NP = QD::np, M = NX + NG;
+  constexpr int KV = NP + NG > NX ? NP + NG : NX;
+  static_assert(M <= 64, "one lane per column and per G row");
+  const int l = GL::lane();
+  double *P = S + kp.oP, *G = S + kp.oG, *qq = S + kp.oQ, *ab = S + kp.oAB, *lo = S + kp.oL, *up = S + kp.oU;
+  double *D = S + kp.oD, *E = S + kp.oE, *sc = S + kp.oSc;
+  {
+    bool finite = true;
+    for (int e = l; e < NP * NP; e += GL::size) finite &= isfinite(P[e]);
+    for (int e = l; e < NG * NX; e += GL::size) finite &= isfinite(G[e]);
+    if (l < NX) finite &= isfinite(qq[l]);
+    for (int row = l; row < M; row += GL::size) finite &= !isnan(lo[row]) && !isnan(up[row]);
+    if (!GL::all(finite)) return DRC_STATUS_NONFINITE;
+  }
+  const bool col = l < NX, row = l >= NX && l < M, hp = l < NP;
+  const int lc = col ? l : 0, lp = hp ? l : 0, r = row ? l - NX : 0;
+  double V[KV];
+#pragma unroll
+  for (int k = 0; k < KV; ++k) {
+    double vc = 0.0, vr = 0.0;
+    if (k < NP) vc = hp ? P[lp * NP + k] : 0.0;
+    else if (k - NP < NG) vc = G[(k - NP) * NX + lc];
+    if (k < NX) vr = G[r * NX + k];
+    V[k] = col ? vc : (row ? vr : 0.0);
+  }
+  double abl = ab[lc], ql = qq[lc], Dl = 1.0, El = 1.0, EGl = 1.0, cs = 1.0;
+  auto clampf = [](double v) { return v < kMinScaling ? 1.0 : (v > kMaxScaling ? kMaxScaling : v); };
+  lds_double* wb = (lds_double*)(S + kp.oBc);  // NX + NG doubles (plan_layout)
+  for (int it = 0; it < kp.s.scaling; ++it) {
+    PH_ADD(49, 1);  // Ruiz passes
+    const double mx = absmax_tree(V);
+    const double F = 1.0 / sqrt(clampf(col ? fmax(fabs(abl), mx) : mx));  // D~ (column) / E~ (row)
+    const double Et = 1.0 / sqrt(clampf(fabs(abl)));                       // bound-row E~ (column lanes)
+    const bool unit = GL::all((!col || (F == 1.0 && Et == 1.0)) && (!row || F == 1.0));
+    if (!unit) {
+      if (l < M) wb[l] = F;  // wb[c] = D~_c, wb[NX + r] = E~_r
+      asm volatile("" ::: "memory");
+      static_for<KV>([&](auto K) {
+        constexpr int k = decltype(K)::value;
+        if constexpr (k < NP) {  // column: P entry (D~_l D~_k); row: G entry (E~_r D~_k)
+          V[k] *= F * wb[k];
+        } else {
+          double m = 1.0;
+          if constexpr (k - NP < NG) m = wb[NX + k - NP] * F;  // column: G entry (E~_i D~_l)
+          if constexpr (k < NX) {
+            const double mr = F * wb[k];  // row: G entry (E~_r D~_k)
+            m = col ? m : mr;
+          }
+          V[k] *= m;
+        }
+      });
+      asm volatile("" ::: "memory");
+      if (col) {
+        abl *= Et * F;
+        ql *= F;
+        Dl *= F;
+        El *= Et;
+      }
+      if (row) EGl *= F;
+    }
+    // cost scaling: mean column norm of P vs |q|_inf
+    double cn = 0, qn = 0;
+    if (hp) {
+      double t[NP];
+#pragma unroll
+      for (int c = 0; c < NP; ++c) t[c] = V[c];
+      cn = absmax_tree(t);
+    }
+    if (col) qn = fabs(ql);
+    cn = GL::sum(cn) / NX;
+    qn = GL::max(qn);
+    qn = clampf(qn);
+    double ct = clampf(fmax(cn, qn));
+    ct = 1.0 / ct;
+    if (hp)
+#pragma unroll
+      for (int c = 0; c < NP; ++c) V[c] *= ct;
+    if (col) ql *= ct;
+    cs *= ct;
+    if (ct == 1.0 && unit) break;
+  }
+  if (hp)
+#pragma unroll
+    for (int c = 0; c < NP; ++c) P[l * NP + c] = V[c];
+  if (row)
+#pragma unroll
+    for (int j = 0; j < NX; ++j) G[r * NX + j] = V[j];
+  if (col) {
+    ab[l] = abl;
+    qq[l] = ql;
+    D[l] = Dl;
+    E[l] = El;
+  }
+  if (row) E[NX + r] = EGl;
+  if (l == 0) sc[SC_C] = cs;
+  wsync();
+  for (int rw = l; rw < M; rw += GL::size) {
+    lo[rw] = fmax(lo[rw], -kInf) * E[rw];
+    up[rw] = fmin(up[rw], kInf) * E[rw];
+  }
+  wsync();
+  return DRC_STATUS_MAX_ITER;
+}
+
 // Addresses and lane-role indices of the Schur ADMM loop, derived from an
 // opaque copy of the parameter pointer and lane index: built once for the
 // loop's setup and again where the (every check_termination iterations)
@@ -2050,7 +2163,8 @@ __device__ __forceinline__ void qp_instance(const DevModel* __restrict__ M0, con
   PH(0);
   const bool lp_inf = M->kind == 1 && kp.s.exact && moma_lp_infeasible<QD>(M, kp, S);
   int status, iters = 0;
-  if constexpr (QD::reg) status = qp_scale_regs<QD>(kpl, S);
+  if constexpr (QD::reg && QD::gs == 64 && QD::nx + QD::ng <= 64) status = qp_scale_roles<QD>(kpl, S);
+  else if constexpr (QD::reg) status = qp_scale_regs<QD>(kpl, S);
   else status = qp_scale<QD>(kp, S);
   PH(1);
   if (status != DRC_STATUS_NONFINITE) {
