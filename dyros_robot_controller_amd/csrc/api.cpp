@@ -132,6 +132,22 @@ static void free_ctx(StreamCtx* c) {
   c->dyn_list = nullptr;
 }
 
+// Records a stream context's `done` event on every exit of a launch path
+// once the context is in use, so eviction (free_ctx) never frees scratch that
+// kernels of this call still use.  A call that fails after enqueueing part of
+// its work may have left kernels on the internal fork streams that `done` on
+// the caller's stream does not follow: that path drains the device first.
+struct DoneGuard {
+  StreamCtx* const& cx;
+  hipStream_t st;
+  bool ok = false;
+  ~DoneGuard() {
+    if (!cx || !cx->done) return;
+    if (!ok) (void)hipDeviceSynchronize();
+    (void)hipEventRecord(cx->done, st);
+  }
+};
+
 // A tuning knob from the environment: its integer value when set and
 // parsable, clamped to >= lo; otherwise the default.
 static int64_t env_int(const char* name, int64_t def, int64_t lo) {
@@ -623,6 +639,7 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
   int* hard = nullptr;           // lane-stage hard list, B ints
   uint8_t* hard_flag = nullptr;  // and its per-instance flags
   StreamCtx* cx = nullptr;
+  DoneGuard done_guard{cx, st};
   // lane-per-instance task stage (lane_task.hpp) for the compiled joint counts
   const DevModel& dm = m->hm.dev;
   // (3, auto: stage-only calls, where nothing overlaps the task stage.  The
@@ -801,7 +818,7 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
     std::lock_guard<std::mutex> g(m->mu);
     m->events.push_back(tev);
   }
-  HIP_TRY(hipEventRecord(cx->done, st));
+  done_guard.ok = true;
   return DRC_OK;
 }
 
@@ -840,6 +857,7 @@ static int launch_qpid(const drc_model_impl* cm, const drc_qpik_params* params, 
   const int64_t dyn_words = stages ? 0 : (int64_t(na) * na + na + (d.kind == 1 ? nv : 0)) * B;
   double *rec = nullptr, *dM = nullptr, *dG = nullptr, *dGf = nullptr;
   StreamCtx* cx = nullptr;
+  DoneGuard done_guard{cx, st};
   {
     std::lock_guard<std::mutex> g(m->mu);
     if (int r = stream_ctx(m, st, &cx)) return r;
@@ -878,7 +896,7 @@ static int launch_qpid(const drc_model_impl* cm, const drc_qpik_params* params, 
     const size_t lds = static_cast<size_t>(kq_c.lds_doubles) * sizeof(double);
     HIP_TRY(static_cast<hipError_t>(launch_qpid_kernel(static_cast<unsigned>(grid), lds, st, m->d_model, kq_c, io)));
   }
-  HIP_TRY(hipEventRecord(cx->done, st));
+  done_guard.ok = true;
   return DRC_OK;
 }
 
@@ -903,13 +921,17 @@ static int launch_closed_form(const drc_model_impl* cm, const drc_qpik_params* p
     HIP_TRY(hipSetDevice(m->device));
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     StreamCtx* cx = nullptr;
+    DoneGuard done_guard{cx, st};
     {
       std::lock_guard<std::mutex> g(m->mu);
       if (int r = stream_ctx(m, st, &cx)) return r;
     }
     const int64_t grid = B < 8192 ? B : 8192;
     kt.xcd_map = B >= 16384 ? 1 : 0;
-    // qdot may be NULL without xdot: the stage reads it, so zeros stand in
+    // qdot may be NULL when xdot is not requested.  The stage still loads a
+    // qdot vector (its J qdot product is then discarded, never stored), so q
+    // stands in as a readable buffer of the same shape; with xdot requested
+    // the caller's qdot is required (checked above)
     IO io{B, 0, B, q, qdot ? qdot : q, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, pose, jac,
           nullptr, nullptr, xdot, nullptr, nullptr, 0};
     // fixed assignment when every wave has one instance: no counter reset to enqueue
@@ -918,7 +940,7 @@ static int launch_closed_form(const drc_model_impl* cm, const drc_qpik_params* p
     HIP_TRY(static_cast<hipError_t>(launch_task_kernel(2, static_cast<unsigned>(grid),
                                                        static_cast<size_t>(kt.lds_doubles) * sizeof(double), st,
                                                        m->d_model, kt, io)));
-    HIP_TRY(hipEventRecord(cx->done, st));
+    done_guard.ok = true;
     return DRC_OK;
   }
   if (m->hm.dev.kind != 0) return set_err(DRC_ERR_INVALID_ARGUMENT, "CLIK / OSF are Manipulator::RobotController entries");
@@ -940,6 +962,7 @@ static int launch_closed_form(const drc_model_impl* cm, const drc_qpik_params* p
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   double *dMi = nullptr, *dG = nullptr;
   StreamCtx* cx = nullptr;
+  DoneGuard done_guard{cx, st};
   {
     std::lock_guard<std::mutex> g(m->mu);
     if (int r = stream_ctx(m, st, &cx)) return r;
@@ -972,7 +995,7 @@ static int launch_closed_form(const drc_model_impl* cm, const drc_qpik_params* p
   HIP_TRY(static_cast<hipError_t>(launch_task_kernel(2, static_cast<unsigned>(grid),
                                                      static_cast<size_t>(kt.lds_doubles) * sizeof(double), st,
                                                      m->d_model, kt, io)));
-  HIP_TRY(hipEventRecord(cx->done, st));
+  done_guard.ok = true;
   return DRC_OK;
 }
 
@@ -1506,6 +1529,8 @@ static int host_call(drc_model* m, const drc_qpik_params* p, int stages, int64_t
     int32_t* oi[2] = {nullptr, nullptr};
     for (int i = 0; i < niouts; ++i) oi[i] = static_cast<int32_t*>(dout[nouts + i]);
     uint64_t* ds = static_cast<uint64_t*>(dout[nouts + niouts]);
+    if (ds && hipMemsetAsync(ds, 0, sizeof(uint64_t) * drc_amd::kStamps * B, m->hstream) != hipSuccess)
+      return drc_amd::set_err(DRC_ERR_HIP, "hipMemsetAsync(stamps)");
     if (!stages)
       return drc_amd::launch(m, p, 0, B, d[0], d[1], d[2], d[3], d[4], d[5], od[0], oi[0], oi[1], nullptr, nullptr,
                              nullptr, nullptr, nullptr, nullptr, m->hstream, ds);
@@ -1551,17 +1576,30 @@ int drc_qpik_host_timed(drc_model* m, const drc_qpik_params* p, int64_t B, const
   const double wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   if (rc) return rc;
   // stamps are s_memrealtime ticks (100 MHz); per-instance stage durations, averaged
+  // (the region was cleared before the launch: an instance whose stamps are
+  // missing -- a debug task stage that does not stamp -- or out of order is
+  // left out of the averages)
   const double tick = 1e-8;
   double task = 0, asmb = 0, solve = 0, store = 0, span = 0;
+  int64_t valid = 0;
   for (int64_t b = 0; b < B; ++b) {
-    auto at = [&](int k) { return static_cast<double>(st[static_cast<size_t>(k * B + b)]); };
-    task += (at(drc_amd::ST_TASK1) - at(drc_amd::ST_TASK0)) * tick;
-    asmb += (at(drc_amd::ST_ASM) - at(drc_amd::ST_QP0)) * tick;
-    solve += (at(drc_amd::ST_SOLVED) - at(drc_amd::ST_ASM)) * tick;
-    store += (at(drc_amd::ST_OUT) - at(drc_amd::ST_SOLVED)) * tick;
-    span += (at(drc_amd::ST_OUT) - at(drc_amd::ST_TASK0)) * tick;
+    auto at = [&](int k) { return st[static_cast<size_t>(k * B + b)]; };
+    bool ok = at(0) != 0;
+    for (int k = 1; k < drc_amd::kStamps && ok; ++k) ok = at(k) >= at(k - 1);
+    if (!ok) continue;
+    auto dt = [&](int k1, int k0) { return static_cast<double>(at(k1) - at(k0)) * tick; };
+    task += dt(drc_amd::ST_TASK1, drc_amd::ST_TASK0);
+    asmb += dt(drc_amd::ST_ASM, drc_amd::ST_QP0);
+    solve += dt(drc_amd::ST_SOLVED, drc_amd::ST_ASM);
+    store += dt(drc_amd::ST_OUT, drc_amd::ST_SOLVED);
+    span += dt(drc_amd::ST_OUT, drc_amd::ST_TASK0);
+    ++valid;
   }
-  const double inv = 1.0 / static_cast<double>(B);
+  if (valid == 0) {  // no stamps (a debug stage): the whole call counts as getSolution's place
+    ts->solve_qp = wall;
+    return DRC_OK;
+  }
+  const double inv = 1.0 / static_cast<double>(valid);
   ts->set_ineq = task * inv;         // FK, J, manipulability + gradient, min distance + gradient
   ts->set_constraint = asmb * inv;   // P, q, bounds, CBF rows stacked (QP_base.h:202-227)
   ts->set_qp = ts->set_ineq + ts->set_constraint;
@@ -1736,6 +1774,7 @@ int drc_dynamics_batch(drc_model* m, int actuated, int64_t B, const double* q, c
   std::lock_guard<std::mutex> launch_lock(m->launch_mu);
   int* list = nullptr;
   drc_amd::StreamCtx* cx = nullptr;
+  drc_amd::DoneGuard done_guard{cx, reinterpret_cast<hipStream_t>(stream)};
   if (M_inv) {
     std::lock_guard<std::mutex> lk(m->mu);
     if (int r = drc_amd::stream_ctx(m, reinterpret_cast<hipStream_t>(stream), &cx)) return r;
@@ -1752,7 +1791,7 @@ int drc_dynamics_batch(drc_model* m, int actuated, int64_t B, const double* q, c
                                           list, reinterpret_cast<hipStream_t>(stream));
   if (rc == 1) return drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "batch too large");
   if (rc) return drc_amd::set_err(DRC_ERR_HIP, std::string("dynamics launch: ") + hipGetErrorString(hipGetLastError()));
-  if (cx) HIP_TRY(hipEventRecord(cx->done, reinterpret_cast<hipStream_t>(stream)));
+  done_guard.ok = true;
   return DRC_OK;
 }
 

@@ -398,11 +398,15 @@ enum { ST_TASK0 = 0, ST_TASK1 = 1, ST_QP0 = 2, ST_ASM = 3, ST_SOLVED = 4, ST_OUT
 // Stage stamp k of instance gb (wave-uniform branch; no stamp executes in a
 // call without io.stamps).  The wait keeps the clock read from returning out
 // of order with the LDS reads that follow (cdna_hip_programming.md).
+// Written by the leader of the instance's lane group (every instance of a
+// two-instance QP wave gets its stamps); the host clears the region before the
+// launch and skips instances whose stamps are missing or out of order.
+template <int GS = 64>
 __device__ __forceinline__ void stage_stamp(const IO& io, int k, int64_t gb) {
   if (io.stamps) {
     const uint64_t t = __builtin_amdgcn_s_memrealtime();
     __builtin_amdgcn_s_waitcnt(0xC07F);
-    if (__lane_id() == 0) io.stamps[k * io.ld + gb] = t;
+    if ((__lane_id() & (GS - 1)) == 0) io.stamps[k * io.ld + gb] = t;
   }
 }
 

@@ -33,16 +33,19 @@ __device__ __forceinline__ int lane_id() {
   return l;
 }
 // Lane exchange point of the one-wave workgroups (task / QP / fused / QPID
-// kernels), whose lanes talk through LDS only.  A wave's LDS instructions
-// execute in issue order, so a compiler barrier is enough: no vmcnt / lgkmcnt
-// drain, no s_barrier (__syncthreads waited for every outstanding global and
-// scratch access at each exchange).  Measured bit-identical on all five robots'
-// bench batches, FR3 +1 % (profiles/r04q_ab_wavesync.jsonl, r04q_bits.log).  -DDRC_BLOCK_SYNC restores it.
+// kernels), whose lanes talk through LDS only.  A wavefront-scope release /
+// acquire fence pair around the wave barrier: the compiler's memory model then
+// emits whatever waits one lane's store -> another lane's load needs for the
+// address space each access compiles to (ds_* or, through a generic pointer,
+// flat_*), instead of this code relying on the issue order of LDS instructions.
+// No vmcnt / lgkmcnt drain of unrelated accesses and no s_barrier
+// (__syncthreads waited for every outstanding global and scratch access at each
+// exchange).  -DDRC_BLOCK_SYNC restores __syncthreads.
 #ifndef DRC_BLOCK_SYNC
 __device__ __forceinline__ void wsync() {
-  asm volatile("" ::: "memory");
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
-  asm volatile("" ::: "memory");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 #else
 __device__ __forceinline__ void wsync() { __syncthreads(); }

@@ -1729,32 +1729,177 @@ static int qp_eqp(const QPW* w, const OracleSettings* s, const int* flag, double
 #define POLISH_MAX_TOTAL 12   /* then at convergence only the tight ADMM fallback */
 #define POLISH_FEAS_ATTEMPTS 4
 #define POLISH_AS_ITERS 24
+
+/* a working-set row with no weight on the free variables depends on the
+ * fixed bounds alone and makes the reduced KKT singular; when the fixed
+ * values already satisfy it strictly it is not active: drop it (the
+ * kernel's polish applies the same rule) */
+static void polish_drop_fixed_rows(const QPW* w, int* flag) {
+    int n = w->n, m = w->m;
+    for (int i = n; i < m; ++i) {
+        if (!flag[i]) continue;
+        double sf = 0, sa = 0, act = 0;
+        for (int j = 0; j < n; ++j) {
+            double g = w->A[i * n + j];
+            sa = fmax(sa, fabs(g));
+            if (!flag[j]) sf = fmax(sf, fabs(g));
+            else act += g * (flag[j] > 0 ? w->u[j] : w->l[j]) / w->A[j * n + j];
+        }
+        double b = flag[i] < 0 ? w->l[i] : w->u[i], slack = flag[i] < 0 ? act - b : b - act;
+        if (sf <= 1e-12 * sa && slack > 1e-12 * (fabs(act) + fabs(b))) flag[i] = 0;
+    }
+}
+
+/* ---- polish census (diagnostic, tools/polish_census.py) ------------------
+ * Counts the certified polish's steps and scores alternative first guesses of
+ * the active set against the one each successful polish certifies.  Off by
+ * default; no decision of the solver depends on it. */
+#define PC_RULES 16
+enum { PC_CALLS, PC_OK, PC_EQP, PC_ADD, PC_DROP, PC_RATIO, PC_OK1, PC_HIST0 = 8, PC_MATCH0 = PC_HIST0 + 8,
+       PC_FN0 = PC_MATCH0 + PC_RULES, PC_FP0 = PC_FN0 + PC_RULES, PC_N = PC_FP0 + PC_RULES };
+static long long g_pc[PC_N];
+static long long g_pc_row[3][ORC_MAXC];  /* rule 0: false neg / false pos / final active, per row */
+void oracle_polish_census_rows(long long* out, int reset) {
+    if (out) memcpy(out, g_pc_row, sizeof(g_pc_row));
+    if (reset) memset(g_pc_row, 0, sizeof(g_pc_row));
+}
+static int g_pc_on = 0, g_pc_guess = -1;
+void oracle_polish_guess(int rule) { g_pc_guess = rule; }
+static double g_pc_tol[PC_RULES];
+void oracle_polish_census(int on, const double* tol, long long* out, int reset) {
+    if (out) for (int i = 0; i < PC_N; ++i) out[i] = __atomic_load_n(&g_pc[i], __ATOMIC_RELAXED);
+    if (reset) for (int i = 0; i < PC_N; ++i) __atomic_store_n(&g_pc[i], 0, __ATOMIC_RELAXED);
+    if (tol) memcpy(g_pc_tol, tol, sizeof(g_pc_tol));
+    g_pc_on = on;
+}
+static void pc_add(int k, long long v) { __atomic_fetch_add(&g_pc[k], v, __ATOMIC_RELAXED); }
+/* candidate first guesses from the ADMM iterate (scaled problem) */
+static void pc_guess(const QPW* w, int rule, int* f) {
+    int n = w->n, m = w->m;
+    double t = g_pc_tol[rule];
+    double gr[ORC_MAXX];  /* Lagrangian gradient without the bound multipliers */
+    for (int j = 0; j < n; ++j) {
+        double s = w->q[j];
+        for (int k = 0; k < n; ++k) s += w->P[j * n + k] * w->x[k];
+        for (int i = n; i < m; ++i) s += w->A[i * n + j] * w->y[i];
+        gr[j] = s;
+    }
+    /* projected Gauss-Seidel (11-13: 1, 2, 4 sweeps) / Jacobi (14: 3 sweeps,
+     * step t) on the bound rows of variables with P_ii > 0, G-row duals fixed */
+    double xgs[ORC_MAXX];
+    memcpy(xgs, w->x, n * sizeof(double));
+    if (rule >= 11) {
+        int sweeps = rule == 11 ? 1 : rule == 12 ? 2 : rule == 13 ? 4 : 3;
+        for (int sw = 0; sw < sweeps; ++sw) {
+            double xo[ORC_MAXX];
+            memcpy(xo, xgs, n * sizeof(double));
+            for (int j = 0; j < n; ++j) {
+                if (!(w->P[j * n + j] > 0)) continue;
+                double s = w->q[j];
+                const double* xs = rule == 14 ? xo : xgs;
+                for (int k = 0; k < n; ++k) s += w->P[j * n + k] * xs[k];
+                for (int i = n; i < m; ++i) s += w->A[i * n + j] * w->y[i];
+                double a = w->A[j * n + j], v = xs[j] - (rule == 14 ? t : 1.0) * s / w->P[j * n + j];
+                v = fmin(fmax(v, w->l[j] / a), w->u[j] / a);
+                xgs[j] = v;
+            }
+        }
+    }
+    for (int i = 0; i < m; ++i) {
+        double ax = 0;
+        for (int j = 0; j < n; ++j) ax += w->A[i * n + j] * w->x[j];
+        const double l = w->l[i], u = w->u[i], z = w->z[i], y = w->y[i];
+        int g = 0;
+        switch (rule) {
+        case 0: g = (z - l < -y) ? -1 : ((u - z < y) ? 1 : 0); break;                  /* OSQP */
+        case 1: g = (ax - l < -y) ? -1 : ((u - ax < y) ? 1 : 0); break;                /* OSQP on A x */
+        case 2: g = (y < -t) ? -1 : (y > t ? 1 : 0); break;                            /* dual sign */
+        case 3: g = (ax - l < t) ? -1 : (u - ax < t ? 1 : 0); break;                   /* primal near */
+        case 4: g = (z - l < -y || ax - l < -t) ? -1 : ((u - z < y || u - ax < -t) ? 1 : 0); break; /* OSQP + violated */
+        case 5: g = (z - l < -y + t) ? -1 : ((u - z < y + t) ? 1 : 0); break;          /* OSQP, widened */
+        case 6: g = (ax - l < -y + t) ? -1 : ((u - ax < y + t) ? 1 : 0); break;
+        case 7: g = ((ax - l < t && y < 0) || ax - l < -t) ? -1 : (((u - ax < t && y > 0) || u - ax < -t) ? 1 : 0); break;
+        case 11: case 12: case 13: case 14:
+            if (i < n && w->P[i * n + i] > 0) {
+                const double a = w->A[i * n + i];
+                g = (a * xgs[i] <= l) ? -1 : (a * xgs[i] >= u ? 1 : 0);
+            } else g = (z - l < -y) ? -1 : ((u - z < y) ? 1 : 0);
+            break;
+        case 8: case 9: case 10:
+            if (i < n && w->P[i * n + i] > 0) {
+                const double a = w->A[i * n + i], xt = w->x[i] - t * gr[i] / w->P[i * n + i];
+                g = (a * xt <= l) ? -1 : (a * xt >= u ? 1 : 0);
+                if (rule == 9 && !g) g = (z - l < -y) ? -1 : ((u - z < y) ? 1 : 0);
+            } else g = (z - l < -y) ? -1 : ((u - z < y) ? 1 : 0);
+            break;
+        default: g = 0;
+        }
+        if (l < -INFTY * MIN_SCALING && g < 0) g = 0;
+        if (u > INFTY * MIN_SCALING && g > 0) g = 0;
+        f[i] = g;
+    }
+    polish_drop_fixed_rows(w, f);
+}
+
+/* First active-set guess of the parity-mode polish (QPIK, polish_guess = 1):
+ * the bound rows of the variables with cost curvature (P_jj > 0: the q-dot)
+ * take the sides at which POLISH_JACOBI_SWEEPS projected Jacobi sweeps on
+ * their box, with the G-row duals of the ADMM iterate held fixed, clamp
+ * them; every other row keeps OSQP's rule.  At the first check the ADMM
+ * iterate has usually not reached the velocity bounds the optimum saturates,
+ * so OSQP's rule misses about two rows per FR3 instance (12 % right first
+ * time, 2.7 EQP solves per polish); this guess 77 %, 1.55
+ * (tools/polish_census.py).  Only the path to the certified optimum changes,
+ * not the optimum.  Same rule and summation order as the kernel's polish(). */
+#define POLISH_JACOBI_SWEEPS 3
+static void polish_guess_jacobi(const QPW* w, int* flag) {
+    int n = w->n, m = w->m;
+    double c[ORC_MAXX], xv[ORC_MAXX], xo[ORC_MAXX];
+    int side[ORC_MAXX];
+    for (int j = 0; j < n; ++j) {
+        double s = w->q[j];
+        for (int i = n; i < m; ++i) s += w->A[i * n + j] * w->y[i];
+        c[j] = s;
+        xv[j] = w->x[j];
+        side[j] = 0;
+    }
+    for (int sw = 0; sw < POLISH_JACOBI_SWEEPS; ++sw) {
+        memcpy(xo, xv, n * sizeof(double));
+        for (int j = 0; j < n; ++j) {
+            const double pjj = w->P[j * n + j];
+            if (!(pjj > 0)) continue;
+            double g = c[j];
+            for (int k = 0; k < n; ++k) g += w->P[j * n + k] * xo[k];
+            const double a = w->A[j * n + j], v = xo[j] - g / pjj, av = a * v;
+            side[j] = av <= w->l[j] ? -1 : (av >= w->u[j] ? 1 : 0);
+            xv[j] = side[j] < 0 ? w->l[j] / a : (side[j] > 0 ? w->u[j] / a : v);
+        }
+    }
+    for (int j = 0; j < n; ++j)
+        if (w->P[j * n + j] > 0) flag[j] = side[j];
+}
+
 static int qp_polish(QPW* w, const OracleSettings* s, int strict) {
     int n = w->n, m = w->m;
     int flag[ORC_MAXC];  /* -1 lower-active, +1 upper-active, 0 inactive */
     for (int i = 0; i < m; ++i)
         flag[i] = (w->z[i] - w->l[i] < -w->y[i]) ? -1 : ((w->u[i] - w->z[i] < w->y[i]) ? 1 : 0);
+    if (strict && s->polish_guess == 1) polish_guess_jacobi(w, flag);
+    if (g_pc_guess >= 0 && strict) pc_guess(w, g_pc_guess, flag);
     const double pr0 = w->r.pri_res, dr0 = w->r.dua_res;
     Res tmp;
     double xp[ORC_MAXX], yp[ORC_MAXC], zp[ORC_MAXC], ax[ORC_MAXC], xc[ORC_MAXX];
-    int have_feasible = 0;
+    int have_feasible = 0, neqp = 0;
+    static __thread int pcg[PC_RULES][ORC_MAXC];
+    const int census = g_pc_on && strict;
+    if (census) {
+        pc_add(PC_CALLS, 1);
+        for (int r = 0; r < PC_RULES; ++r) pc_guess(w, r, pcg[r]);
+    }
     for (int it = 0; it < (strict ? POLISH_FEAS_ATTEMPTS + POLISH_AS_ITERS : 1); ++it) {
-        /* a working-set row with no weight on the free variables depends on
-         * the fixed bounds alone and makes the reduced KKT singular; when the
-         * fixed values already satisfy it strictly it is not active: drop it
-         * (the kernel's polish applies the same rule) */
-        for (int i = n; i < m; ++i) {
-            if (!flag[i]) continue;
-            double sf = 0, sa = 0, act = 0;
-            for (int j = 0; j < n; ++j) {
-                double g = w->A[i * n + j];
-                sa = fmax(sa, fabs(g));
-                if (!flag[j]) sf = fmax(sf, fabs(g));
-                else act += g * (flag[j] > 0 ? w->u[j] : w->l[j]) / w->A[j * n + j];
-            }
-            double b = flag[i] < 0 ? w->l[i] : w->u[i], slack = flag[i] < 0 ? act - b : b - act;
-            if (sf <= 1e-12 * sa && slack > 1e-12 * (fabs(act) + fabs(b))) flag[i] = 0;
-        }
+        polish_drop_fixed_rows(w, flag);
+        ++neqp;
+        if (census) pc_add(PC_EQP, 1);
         if (!qp_eqp(w, s, flag, xp, yp)) return 0;
         double stepmax = 0, xnorm = 0;
         if (have_feasible) {
@@ -1776,7 +1921,7 @@ static int qp_polish(QPW* w, const OracleSettings* s, int strict) {
             }
             double alpha = amin < 0 ? 0 : amin;
             for (int j = 0; j < n; ++j) xc[j] += alpha * (xp[j] - xc[j]);
-            if (blk >= 0) { flag[blk] = side; continue; }
+            if (blk >= 0) { flag[blk] = side; if (census) pc_add(PC_RATIO, 1); continue; }
             /* full step: xc is the EQP minimiser, fall through to the checks */
         }
         for (int i = 0; i < m; ++i) {
@@ -1813,14 +1958,37 @@ static int qp_polish(QPW* w, const OracleSettings* s, int strict) {
             memcpy(w->z, zp, m * sizeof(double));
             w->r.pri_res = tmp.pri_res;
             w->r.dua_res = tmp.dua_res;
+            if (census) {
+                pc_add(PC_OK, 1);
+                if (neqp == 1) pc_add(PC_OK1, 1);
+                pc_add(PC_HIST0 + (neqp < 8 ? neqp - 1 : 7), 1);
+                for (int r = 0; r < PC_RULES; ++r) {
+                    int fn = 0, fp = 0;
+                    for (int i = 0; i < m; ++i) {
+                        if (flag[i] && pcg[r][i] != flag[i]) ++fn;
+                        else if (!flag[i] && pcg[r][i]) ++fp;
+                    }
+                    if (!fn && !fp) pc_add(PC_MATCH0 + r, 1);
+                    if (r == 0)
+                        for (int i = 0; i < m; ++i) {
+                            if (flag[i] && pcg[r][i] != flag[i]) __atomic_fetch_add(&g_pc_row[0][i], 1, __ATOMIC_RELAXED);
+                            else if (!flag[i] && pcg[r][i]) __atomic_fetch_add(&g_pc_row[1][i], 1, __ATOMIC_RELAXED);
+                            if (flag[i]) __atomic_fetch_add(&g_pc_row[2][i], 1, __ATOMIC_RELAXED);
+                        }
+                    pc_add(PC_FN0 + r, fn);
+                    pc_add(PC_FP0 + r, fp);
+                }
+            }
             return 1;
         }
         if (!strict) return 0;
         if (have_feasible) {
             if (worst < 0) return 0;   /* KKT residual failure, not an active-set issue */
             flag[worst] = 0;
+            if (census) pc_add(PC_DROP, 1);
             memcpy(xc, xp, n * sizeof(double));
         } else {
+            if (census) pc_add(PC_ADD, 1);
             if (it >= POLISH_FEAS_ATTEMPTS - 1) return 0;
             /* not yet feasible: add every violated inactive row at its
              * violated side (QPIK: the ADMM guess typically misses a
@@ -1972,6 +2140,7 @@ void oracle_default_params(int kind, OracleParams* p, int exact) {
      * takes N > 16 there (D16) */
     s->polish_cap = kind == 0 ? 16 : 0;
     s->polish_add_all = 1;
+    s->polish_guess = exact ? 1 : 0;
 }
 
 /* Farkas certificate for the whole-body QP (mobile_manipulator/QP_IK.cpp:
@@ -2187,6 +2356,7 @@ void oracle_default_qpid_params(int kind, OracleParams* p, int exact) {
     if (exact) p->solver.delta = 1e-10;
     p->solver.polish_cap = 48;              /* the kernel's QPID polish KKT (ncap)     */
     p->solver.polish_add_all = 0;           /* one row per step (kernel: problem 1)    */
+    p->solver.polish_guess = 0;             /* OSQP's first guess (kernel: problem 1)  */
 }
 
 /* Manipulator::QPID (src/manipulator/QP_ID.cpp:7-193) and MobileManipulator::

@@ -79,6 +79,9 @@ typedef struct OracleSettings {
     int polish_add_all;              /* infeasible polish point: add every
                                       * violated row (QPIK) or only the most
                                       * violated one (QPID)                 */
+    int polish_guess;                /* first active-set guess: 0 OSQP's rule,
+                                      * 1 projected Jacobi on the q-dot box
+                                      * (QPIK parity mode, polish_guess_jacobi) */
 } OracleSettings;
 
 typedef struct OracleParams {

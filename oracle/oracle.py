@@ -71,6 +71,7 @@ class OracleSettings(C.Structure):
         ("eps_fallback", C.c_double),
         ("polish_cap", C.c_int),
         ("polish_add_all", C.c_int),
+        ("polish_guess", C.c_int),
     ]
 
 

@@ -137,6 +137,8 @@ def test_cycle_through_module_matches_oracle(cuda):
                                      xi=xi12[:, None], xdi=xdot[:, None], mode=2, t=0.4, t0=0.0, T=3.0)
         if st[0] == 1:
             np.testing.assert_allclose(qdot_star, ref[:, 0], atol=1e-6)
+        else:   # QP_IK.cpp:56-61: a failed solve returns zeros on both sides
+            assert np.all(qdot_star == 0.0) and np.all(ref[:, 0] == 0.0), (qdot_star, ref[:, 0])
         d = R.dynamics(pm, q[:, b], qd[:, b])
         qdd = 400 * (qdot_star * dt) + 40 * (qdot_star - qd[:, b])
         np.testing.assert_allclose(tau, d["M"] @ qdd + d["g"], rtol=1e-10, atol=1e-8)
