@@ -44,7 +44,8 @@ FP64_VECTOR_PEAK_TFS = 78.6    # AMD spec, FP64 vector
 SIMDS = 256 * 4                # CUs x SIMDs (MI355X_MICROARCH.md)
 CLOCK_HZ = 2.4e9               # max engine clock (MI355X_MICROARCH.md chip table)
 CLOCK_GHZ = 2.4                # MI355X peak engine clock (MI355X_MICROARCH.md)
-WAVE_SLOTS = 256 * 4 * 2       # CUs x SIMDs x waves per SIMD of the task kernel (256 VGPRs, ~19 KB LDS; QP kernel: 3)
+CUS = 256                      # MI355X compute units (MI355X_MICROARCH.md)
+LDS_PER_CU = 160 * 1024        # bytes
 DEFAULT_BATCH = {"fr3": 65536, "ur5e": 65536, "husky_fr3": 16384, "xls_fr3": 65536, "caster_fr3": 65536}
 METRIC = "QP-IK solves/s (FR3 7-DoF, batch 65k) + achieved HBM GB/s vs peak"
 
@@ -219,6 +220,8 @@ def latency_b1(rd, robot, q, qd, xt, xdt, solver, calls=400, warmup=20):
     lib, h = _capi.lib(), rd.model.handle
     ts = []
     for k in range(warmup + calls):
+        if k == warmup:   # host-side phase stamps of the timed calls (drc_debug_host_timeline)
+            _capi.check(lib.drc_debug_host_timeline(h, 1, None, 0, None))
         t0 = time.perf_counter()
         rc = lib.drc_qpik_host(h, C.byref(p), C.c_int64(1), dp(q1), dp(qd1), dp(xt1), dp(xdt1), dp(xi1), dp(xdi1),
                                dp(out), ip(st), ip(it))
@@ -226,11 +229,24 @@ def latency_b1(rd, robot, q, qd, xt, xdt, solver, calls=400, warmup=20):
         _capi.check(rc)
         if k >= warmup:
             ts.append(t1 - t0)
+    tl = np.zeros((calls, 5), np.int64)
+    n = C.c_int64()
+    _capi.check(lib.drc_debug_host_timeline(h, 0, tl.ctypes.data_as(C.POINTER(C.c_int64)), calls, C.byref(n)))
     ts = np.array(ts) * 1e6
+    ph = np.diff(tl[:n.value], axis=1) / 1e3            # pack, enqueue, wait, unpack (us)
+    names = ["pack_inputs", "enqueue_copy_launch_copy", "wait_completion", "unpack_outputs"]
+    worst = int(np.argmax(ts))
+    breakdown = {"p50_us": {k: float(np.percentile(ph[:, i], 50)) for i, k in enumerate(names)},
+                 "max_us": {k: float(ph[:, i].max()) for i, k in enumerate(names)},
+                 "slowest_call_us": {k: float(ph[worst, i]) for i, k in enumerate(names)} if len(ph) == calls else None,
+                 "outside_library_slowest_us": float(ts[worst] - (tl[worst, 4] - tl[worst, 0]) / 1e3)
+                 if len(ph) == calls else None,
+                 "host_wait": "poll" if int(os.environ.get("DRC_HOST_WAIT", "1")) else "block",
+                 "calls_over_us": {str(t): int(np.sum(ts > t)) for t in (200, 300, 500)}}
     return {"call": "QPIKCubic, B = 1, drc_qpik_host (host buffers in and out, synchronous)",
             "p50_us": float(np.percentile(ts, 50)), "p99_us": float(np.percentile(ts, 99)),
             "max_us": float(ts.max()), "calls": calls, "status": int(st[0]), "admm_iters": int(it[0]),
-            "cycle_budget_us": 1000.0}
+            "cycle_budget_us": 1000.0, "phases": breakdown}
 
 
 def BUNDLED_KIND(robot):
@@ -535,15 +551,28 @@ def extras(torch, args, rd, mod, robot, link, q, qd, xt, xdt, dq, dqd, dxt, dxdt
     tw, tk, tq, nc = C.c_double(), C.c_double(), C.c_double(), C.c_int()
     _capi.check(lib.drc_debug_kernel_times(h, C.byref(tw), C.byref(tk), C.byref(tq), C.byref(nc)))
     _capi.check(lib.drc_debug_kernel_timing(h, 0))
-    lat = (tk.value + tq.value) / max(nc.value, 1) * 1e-3          # task + QP kernel(s) of one instance, seconds
-    roof = WAVE_SLOTS / lat
+    lt, lq = tk.value / max(nc.value, 1) * 1e-3, tq.value / max(nc.value, 1) * 1e-3   # task / QP latency, seconds
+    # waves per CU of each kernel as the call launches it: the register build's
+    # waves per SIMD (drc_debug_waves) x 4, capped by the LDS plan (drc_debug_lds_plan)
+    from dyros_robot_controller_amd import manipulator
+    p = manipulator.QPIKParamsBuilder(rd.model, exact=(args.solver == "exact")).params(link, _capi.MODE_QPIK_STEP)
+    wt, wq, bt, bq, bf = C.c_int(), C.c_int(), C.c_int(), C.c_int(), C.c_int()
+    _capi.check(lib.drc_debug_waves(h, C.byref(p), C.byref(wt), C.byref(wq)))
+    _capi.check(lib.drc_debug_lds_plan(h, C.byref(p), 0, C.byref(bt), C.byref(bq), C.byref(bf)))
+    cu_t = min(4 * wt.value, LDS_PER_CU // max(bt.value, 1))
+    cu_q = min(4 * wq.value, LDS_PER_CU // max(bq.value, 1))
+    # an instance holds a task-wave slot for lt and a QP-wave slot for lq:
+    # CUS / (lt / cu_t + lq / cu_q) instances per second with every slot busy
+    roof = CUS / (lt / cu_t + lq / cu_q)
     line["roofline"]["latency_roof"] = {
-        "instance_latency_us": 1e6 * lat, "call_us": 1e3 * tw.value / max(nc.value, 1), "wave_slots": WAVE_SLOTS,
+        "instance_latency_us": 1e6 * (lt + lq), "task_latency_us": 1e6 * lt, "qp_latency_us": 1e6 * lq,
+        "call_us": 1e3 * tw.value / max(nc.value, 1), "task_waves_per_cu": cu_t, "qp_waves_per_cu": cu_q,
         "solves_per_s": roof, "frac": line["value"] / roof,
-        "note": "design-relative, not a hardware limit (the hardware roof is valu_issue_roof): mean over the "
-                "batch's first 32 instances, each alone on the GPU (B = 1 calls, kernel durations by HIP events); "
-                "WAVE_SLOTS instances in flight (two task-kernel waves per SIMD; the QP kernel runs three, so this "
-                "roof is approximate) at their isolated latency would give WAVE_SLOTS / latency"}
+        "note": "design-relative, not a hardware limit (the hardware roof is valu_issue_roof): task and QP kernel "
+                "latency of one instance alone on the GPU (mean over the batch's first 32 instances, B = 1 calls, "
+                "HIP events); with the waves per CU each kernel is launched at (register build x 4 SIMDs, capped "
+                "by its LDS plan), 256 CUs complete 256 / (t_task / w_task + t_qp / w_qp) instances per second "
+                "if every wave slot stays busy at the isolated latency"}
 
 
 if __name__ == "__main__":

@@ -102,6 +102,11 @@ struct drc_model_impl {
   double* pinned = nullptr;
   int64_t pinned_bytes = 0;
   hipStream_t hstream = nullptr;
+  hipEvent_t hdone = nullptr;  // recorded after a synchronous entry's copy back
+  // drc_debug_host_timeline: per synchronous call, steady-clock ns at entry,
+  // inputs packed, H2D + launches + D2H enqueued, completion seen, exit
+  int tl_on = 0;
+  std::vector<int64_t> tl;
   std::mutex mu;         // the context list, timing events, concurrency
   std::mutex launch_mu;  // one call's launch sequence is enqueued as a unit, so
                          // two host threads sharing a stream cannot interleave
@@ -1040,6 +1045,27 @@ int drc_debug_lds_plan(drc_model* m, const drc_qpik_params* params, int problem,
   return DRC_OK;
 }
 
+int drc_debug_waves(drc_model* m, const drc_qpik_params* params, int* task_waves, int* qp_waves) {
+  if (!m || !params || !task_waves || !qp_waves) return drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "null argument");
+  drc_amd::KParams kt;
+  if (int rc = drc_amd::make_kparams(m, params, 1, &kt, 0)) return rc;
+  *task_waves = drc_amd::task_waves_per_simd(0, static_cast<size_t>(kt.lds_doubles) * 8);
+  *qp_waves = drc_amd::qp_waves_per_simd();
+  return DRC_OK;
+}
+
+int drc_debug_host_timeline(drc_model* m, int enable, int64_t* out, int64_t cap, int64_t* n) {
+  if (!m) return drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "null model");
+  std::lock_guard<std::mutex> g(m->host_mu);
+  const int64_t rows = static_cast<int64_t>(m->tl.size() / 5);
+  if (n) *n = rows;
+  if (out)
+    for (int64_t i = 0; i < rows * 5 && i < cap * 5; ++i) out[i] = m->tl[static_cast<size_t>(i)];
+  m->tl.clear();
+  m->tl_on = enable != 0;
+  return DRC_OK;
+}
+
 int drc_debug_kernel_timing(drc_model* m, int enable) {
   if (!m) return drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "null model");
   m->timing = enable != 0;
@@ -1212,6 +1238,7 @@ void drc_model_destroy(drc_model* m) {
   if (m->hstream) (void)hipStreamSynchronize(m->hstream), (void)hipStreamDestroy(m->hstream);
   if (m->stage) (void)hipFree(m->stage);
   if (m->pinned) (void)hipHostFree(m->pinned);
+  if (m->hdone) (void)hipEventDestroy(m->hdone);
   for (auto& ev : m->events)
     for (hipEvent_t e : ev) (void)hipEventDestroy(e);
   delete m;
@@ -1450,6 +1477,8 @@ static int ensure_staging(drc_model* m, int64_t words) {
       return drc_amd::set_err(DRC_ERR_HIP, "hipHostMalloc (staging)");
     m->pinned_bytes = bytes;
   }
+  if (!m->hdone && hipEventCreateWithFlags(&m->hdone, hipEventDisableTiming) != hipSuccess)
+    return drc_amd::set_err(DRC_ERR_HIP, "hipEventCreate (host entries)");
   if (!m->hstream && hipStreamCreateWithFlags(&m->hstream, hipStreamNonBlocking) != hipSuccess)
     return drc_amd::set_err(DRC_ERR_HIP, "hipStreamCreate");
   return DRC_OK;
@@ -1470,8 +1499,31 @@ struct HostOut {
   int64_t words;      // staging space (whole 8-byte words)
   int64_t bytes = -1;  // bytes copied back (default: words * 8)
 };
+static inline int64_t now_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+// How a synchronous entry waits for its copy back (DRC_HOST_WAIT): 1 (default)
+// polls the completion event, 0 blocks in hipEventSynchronize.  Polling keeps
+// the calling thread on its core for the ~100 us of one B = 1 cycle instead of
+// handing it to the scheduler and waking it up again.
+static int wait_done(drc_model* m) {
+  static const int64_t spin = env_int("DRC_HOST_WAIT", 1, 0);
+  if (hipEventRecord(m->hdone, m->hstream) != hipSuccess) return drc_amd::set_err(DRC_ERR_HIP, "hipEventRecord");
+  if (spin) {
+    for (;;) {
+      const hipError_t e = hipEventQuery(m->hdone);
+      if (e == hipSuccess) return DRC_OK;
+      if (e != hipErrorNotReady) return drc_amd::set_err(DRC_ERR_HIP, "hipEventQuery");
+    }
+  }
+  if (hipEventSynchronize(m->hdone) != hipSuccess) return drc_amd::set_err(DRC_ERR_HIP, "hipEventSynchronize");
+  return DRC_OK;
+}
+
 template <class Run>
 static int round_trip(drc_model* m, const HostArr* in, int nin, const HostOut* out, int nout, Run run) {
+  const int64_t t0 = m->tl_on ? now_ns() : 0;
   int64_t wi = 0, wo = 0;
   for (int i = 0; i < nin; ++i) wi += in[i].host ? in[i].words : 0;
   for (int i = 0; i < nout; ++i) wo += out[i].host ? out[i].words : 0;
@@ -1491,18 +1543,25 @@ static int round_trip(drc_model* m, const HostArr* in, int nin, const HostOut* o
       dout[i] = dev + o;
       o += out[i].words;
     }
+  const int64_t t1 = m->tl_on ? now_ns() : 0;
   if (wi && hipMemcpyAsync(dev, m->pinned, wi * 8, hipMemcpyHostToDevice, m->hstream) != hipSuccess)
     return drc_amd::set_err(DRC_ERR_HIP, "hipMemcpyAsync H2D");
   if (int rc = run(din, dout)) return rc;
   if (wo && hipMemcpyAsync(m->pinned + wi, dev + wi, wo * 8, hipMemcpyDeviceToHost, m->hstream) != hipSuccess)
     return drc_amd::set_err(DRC_ERR_HIP, "hipMemcpyAsync D2H");
-  if (hipStreamSynchronize(m->hstream) != hipSuccess) return drc_amd::set_err(DRC_ERR_HIP, "hipStreamSynchronize");
+  const int64_t t2 = m->tl_on ? now_ns() : 0;
+  if (int rc = wait_done(m)) return rc;
+  const int64_t t3 = m->tl_on ? now_ns() : 0;
   o = wi;
   for (int i = 0; i < nout; ++i)
     if (out[i].host) {
       std::memcpy(out[i].host, m->pinned + o, out[i].bytes >= 0 ? out[i].bytes : out[i].words * 8);
       o += out[i].words;
     }
+  if (m->tl_on) {
+    const int64_t t4 = now_ns();
+    for (int64_t v : {t0, t1, t2, t3, t4}) m->tl.push_back(v);
+  }
   return DRC_OK;
 }
 

@@ -57,6 +57,8 @@ bool qp_compiled(int nx, int ng, int np) {
          (nx == 11 && ng == 16 && np == 11);
 }
 
+int qp_waves_per_simd() { return DRC_QP_WAVES; }
+
 int launch_qp_kernel(unsigned grid, size_t lds, hipStream_t st, const DevModel* m, const KParams& kp, const IO& io) {
   const dim3 g(grid), blk(64);
   const size_t lg = lds * (64 / kQpGroup);  // one LDS plan per lane group

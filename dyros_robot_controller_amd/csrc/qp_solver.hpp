@@ -527,6 +527,7 @@ __device__ __forceinline__ bool eqp_regs(const KParams& kp, double* S, int actb,
                *up = S + kp.oU;
   int* Fidx = reinterpret_cast<int*>(S + kp.oU0);  // 64 ints
   int* Ridx = Fidx + 64;                           // 64 ints
+  PH_STAMP(er_t0);
   const unsigned long long below = (1ull << l) - 1;
   if (l < NX && actb == 0) Fidx[__popcll(freeMask & below)] = l;
   if (l < NG && actg != 0) Ridx[__popcll(rowMask & below)] = l;
@@ -577,6 +578,8 @@ __device__ __forceinline__ bool eqp_regs(const KParams& kp, double* S, int actb,
       Ki[j] = v + (j == l ? (hf ? kp.s.delta : (hr ? -kp.s.delta : 0.0)) : 0.0);
     }
   }
+  PH_SINCE(52, er_t0);
+  PH_STAMP(er_t1);
   // Gauss-Jordan inverse of the regularised KKT.  The pivot row and the
   // vectors of the products below reach every lane through LDS (the pivot
   // lane / the owners write, every lane reads the same addresses): no VALU
@@ -633,11 +636,15 @@ __device__ __forceinline__ bool eqp_regs(const KParams& kp, double* S, int actb,
     if constexpr (kLds) asm volatile("" ::: "memory");
     return s0 + s1;
   };
+  PH_SINCE(53, er_t1);
+  PH_STAMP(er_t2);
   double sol = apply(Ki, rhs);
   for (int it = 0; it < kp.s.polish_refine_iter; ++it) {
     const double res = rhs - apply(K0, sol);
     sol += apply(Ki, res);
   }
+  PH_SINCE(54, er_t2);
+  PH_STAMP(er_t3);
   if (hf) xx[fi] = sol;
   for (int row = l; row < M; row += GL::size) yy[row] = 0.0;
   wsync();
@@ -656,6 +663,7 @@ __device__ __forceinline__ bool eqp_regs(const KParams& kp, double* S, int actb,
     yy[lx] = -g / ab[lx];
   }
   wsync();
+  PH_SINCE(55, er_t3);
   return true;
 }
 
@@ -1001,6 +1009,7 @@ __device__ __forceinline__ bool polish(const KParams& kp, double* S, bool strict
   // misses about two rows per FR3 instance (12 % right first time, 2.7 EQP
   // solves per polish); with this guess 77 % and 1.55 (tools/polish_census.py).
   // Same rule and summation order as oracle/drc_oracle.c:polish_guess_jacobi.
+  PH_STAMP(pj_t0);
   if (strict && kp.problem == 0 && np < nx) {
     const double *P = S + kp.oP, *qv = S + kp.oQ;
     lds_double* bc = (lds_double*)(S + kp.oBc);
@@ -1023,6 +1032,7 @@ __device__ __forceinline__ bool polish(const KParams& kp, double* S, bool strict
     }
     if (l < np) actb = side;
   }
+  PH_SINCE(50, pj_t0);
   double* U = S + kp.oU0;
   double* xx = U + 64;       // [nx]
   double* yy = U + 128;      // [m] (<= 128)
@@ -1033,6 +1043,7 @@ __device__ __forceinline__ bool polish(const KParams& kp, double* S, bool strict
   bool have_feas = false;
   const int iters = strict ? kPolishFeasAttempts + kPolishAsIters : 1;
   for (int it = 0; it < iters; ++it) {
+    PH_STAMP(pd_t0);
     {
       // a working-set G row with no weight on the free variables depends on
       // the fixed bounds alone and makes the reduced KKT singular (its
@@ -1055,7 +1066,9 @@ __device__ __forceinline__ bool polish(const KParams& kp, double* S, bool strict
         if (sf <= 1e-12 * sa && slack > 1e-12 * (fabs(act) + fabs(b))) actg = 0;
       }
     }
+    PH_SINCE(51, pd_t0);
     if (!eqp<QD>(kp, S, actb, actg, xx, yy)) break;
+    PH_STAMP(pr_t0);
     if (have_feas) {
       double stepmax = 0, xnorm = 0;
       if (l < nx) {
@@ -1099,10 +1112,13 @@ __device__ __forceinline__ bool polish(const KParams& kp, double* S, bool strict
           const int row = enc >> 2, sd = (enc & 3) - 1;
           if (row < nx) { if (l == row) actb = sd; }
           else if (l == row - nx) actg = sd;
+          PH_SINCE(56, pr_t0);
           continue;
         }
       }
     }
+    PH_SINCE(56, pr_t0);
+    PH_STAMP(pc_t0);
     // candidate point: z = clamp(A x), residuals, certification
     double axb = 0, axg = 0;
     if (l < nx) {
@@ -1116,9 +1132,11 @@ __device__ __forceinline__ bool polish(const KParams& kp, double* S, bool strict
       zz[nx + lg] = fmin(fmax(axg, lo[nx + lg]), up[nx + lg]);
     }
     wsync();
+    PH_SINCE(57, pc_t0);
     PH_STAMP(rs_t0);
     residuals<QD, false, true>(kp, S, xx, zz, yy, kp.s.eps_exact, kp.s.eps_exact, axb, axg);
     PH_SINCE(43, rs_t0);
+    PH_STAMP(pk_t0);
     const double pr1 = sc[SC_PRI], dr1 = sc[SC_DUA], epsp = sc[SC_EPSP], epsd = sc[SC_EPSD], c = sc[SC_C];
     bool ok = (pr1 < pr0 && dr1 < dr0) || (pr1 < pr0 && dr0 < 1e-10) || (dr1 < dr0 && pr0 < 1e-10);
     double wv = 0;
@@ -1156,6 +1174,7 @@ __device__ __forceinline__ bool polish(const KParams& kp, double* S, bool strict
         z[row] = zz[row];
       }
       wsync();
+      PH_SINCE(58, pk_t0);
       return true;
     }
     if (!strict) break;
@@ -1205,6 +1224,7 @@ __device__ __forceinline__ bool polish(const KParams& kp, double* S, bool strict
         else if (l == row - nx) actg = sd;
       }
     }
+    PH_SINCE(58, pk_t0);
   }
   if (l == 0) {  // restore the ADMM residuals for the caller
     sc[SC_PRI] = pr0;

@@ -46,8 +46,7 @@ task_kernel(const DevModel* __restrict__ M0, const KParams kp, const IO io) {
 
 #include "lane_task.hpp"  // lane-per-instance stage (inside namespace drc_amd)
 
-int launch_task_kernel(int problem, unsigned grid, size_t lds, hipStream_t st, const DevModel* m, const KParams& kp,
-                       const IO& io) {
+int task_waves_per_simd(int problem, size_t lds) {
   // the two-wave build holds 8 waves per CU; the three-wave build pays where the
   // plan lets a CU hold 9 or more (<= 160 KB / 9: FR3 17.1 KB +0.9 %, UR5e 14.0 KB
   // +11 % with the narrowed plan, profiles/r04l_envab_w3.jsonl, r04k_ab_w3_ldsnarrow.jsonl)
@@ -57,6 +56,12 @@ int launch_task_kernel(int problem, unsigned grid, size_t lds, hipStream_t st, c
     return e ? std::atoi(e) : -1;
   }();
   const bool w3 = w3_env >= 0 ? w3_env != 0 : lds * 9 <= 160 * 1024;
+  return problem == 0 && w3 ? 3 : DRC_TASK_WAVES;
+}
+
+int launch_task_kernel(int problem, unsigned grid, size_t lds, hipStream_t st, const DevModel* m, const KParams& kp,
+                       const IO& io) {
+  const bool w3 = task_waves_per_simd(problem, lds) == 3 && DRC_TASK_WAVES != 3;
   if (problem == 0 && w3)
     hipLaunchKernelGGL((task_kernel<0, 3>), dim3(grid), dim3(64), lds, st, m, kp, io);
   else if (problem == 0)

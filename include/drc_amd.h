@@ -267,6 +267,14 @@ int drc_state_host(drc_model* model, int frame_id, int64_t B, const double* q, c
  * drc_debug_kernel_times waits for them and returns the summed durations
  * (ms) and the number of timed calls since the last query. */
 int drc_debug_kernel_timing(drc_model* model, int enable);
+/* Host-side timeline of the synchronous entries (drc_qpik_host and the other
+ * *_host calls): while enabled, each call appends five steady-clock ns stamps
+ * -- entry, inputs packed into the pinned buffer, copy in + launches + copy
+ * back enqueued, completion seen, exit.  Returns up to `cap` rows of the calls
+ * since the last query in out[5 * cap] (n = rows recorded), clears them and
+ * sets the enable state.  Diagnostic (bench.py latency_b1); no reference
+ * counterpart. */
+int drc_debug_host_timeline(drc_model* model, int enable, int64_t* out, int64_t cap, int64_t* n);
 /* Per-wave LDS of this model's kernels (bytes): task kernel, QP kernel and the
  * fused kernel (0 for QPID), problem 0 = QPIK, 1 = QPID.  Diagnostic (DESIGN.md
  * "Occupancy"); no reference counterpart. */
@@ -276,6 +284,10 @@ int drc_debug_lds_plan(drc_model* model, const drc_qpik_params* params, int prob
  * task_ms / qp_ms: summed durations of the task / QP kernels of every
  * sub-batch (they overlap in time when a call runs several sub-batches). */
 int drc_debug_kernel_times(drc_model* model, double* wall_ms, double* task_ms, double* qp_ms, int* calls);
+/* Register-budget occupancy (waves per SIMD) of the QPIK task-kernel build a
+ * call with these params launches (two- or three-wave build, chosen from its
+ * LDS plan) and of the QP kernel.  Diagnostic (bench.py latency roof). */
+int drc_debug_waves(drc_model* model, const drc_qpik_params* params, int* task_waves, int* qp_waves);
 
 /* Concurrency of drc_qpik_batch: the batch is split into up to `chunks`
  * contiguous sub-batches (each >= 4096 instances, >= 16384 when there are 4)

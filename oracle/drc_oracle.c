@@ -2016,6 +2016,9 @@ static int qp_polish(QPW* w, const OracleSettings* s, int strict) {
     return 0;
 }
 
+/* the last termination check's max(pri_res / eps_pri, dua_res / eps_dua) of
+ * this thread's last oracle_solve_qp (OracleDiag.res_ratio) */
+static __thread double g_res_ratio;
 int oracle_solve_qp(int n, int m, const double* P, const double* qv, const double* A,
                     const double* l, const double* u, const OracleSettings* s,
                     double* x, double* y, int* iters, int* polished) {
@@ -2042,6 +2045,7 @@ int oracle_solve_qp(int n, int m, const double* P, const double* qv, const doubl
     memset(w.z, 0, sizeof(w.z));
     memset(w.y, 0, sizeof(w.y));
     int status = ORC_MAX_ITER, it, pol = 0, pfail = 0;
+    g_res_ratio = NAN;
     double alpha = s->alpha;
     for (it = 1; it <= s->max_iter; ++it) {
         double xt[ORC_MAXX], zt[ORC_MAXC], rhs[ORC_MAXX];
@@ -2065,7 +2069,9 @@ int oracle_solve_qp(int n, int m, const double* P, const double* qv, const doubl
         int check = s->check_termination > 0 && it % s->check_termination == 0;
         int adapt = s->adaptive_rho && s->adaptive_rho_interval > 0 && it % s->adaptive_rho_interval == 0;
         if (check || adapt) qp_residuals(&w, &w.r, w.x, w.z, w.y, s->eps_abs, s->eps_rel);
-        if (check) {
+        if (check) g_res_ratio = fmax(w.r.pri_res / w.r.eps_pri, w.r.dua_res / w.r.eps_dua);
+        if (s->stop_at > 0 && it == s->stop_at) { status = ORC_SOLVED; break; }
+        if (check && s->stop_at <= 0) {
             int conv = w.r.pri_res < w.r.eps_pri && w.r.dua_res < w.r.eps_dua;
             if (getenv("ORC_DEBUG") && it <= 200)
                 fprintf(stderr, "it %d rho %.4g pri %.3e/%.3e dua %.3e/%.3e x3 %.6f\n", it, w.rho, w.r.pri_res, w.r.eps_pri,
@@ -2329,6 +2335,7 @@ static int qpik_one_impl(const OracleModel* m, const OracleParams* p, const doub
         diag->pair = pair;
         diag->iters = iters;
         diag->polished = pol;
+        diag->res_ratio = g_res_ratio;
     }
     return st;
 }
@@ -2518,6 +2525,7 @@ int oracle_qpid_one(const OracleModel* m, const OracleParams* p, const double* q
         diag->pair = pair;
         diag->iters = iters;
         diag->polished = pol;
+        diag->res_ratio = g_res_ratio;
         memcpy(diag->jdot_v, bias, sizeof(bias));
         memcpy(diag->man_graddot, mgd, n * sizeof(double));
         memcpy(diag->dist_graddot, dgd, nv * sizeof(double));

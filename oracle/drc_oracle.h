@@ -82,6 +82,9 @@ typedef struct OracleSettings {
     int polish_guess;                /* first active-set guess: 0 OSQP's rule,
                                       * 1 projected Jacobi on the q-dot box
                                       * (QPIK parity mode, polish_guess_jacobi) */
+    int stop_at;                     /* > 0: stop at that ADMM iteration and
+                                      * return its iterate as Solved (tests:
+                                      * the other side's stopping point)    */
 } OracleSettings;
 
 typedef struct OracleParams {
@@ -107,7 +110,8 @@ typedef struct OracleDiag {
     double man_graddot[ORC_MAXJ];    /* getManipulability grad_dot (arm)    */
     double dist_graddot[ORC_MAXJ];   /* getMinDistance grad_dot (full dof)  */
     double man_gd, dist_gd;          /* grad_dot . qdot_arm used in the rows */
-    double Jdot[6 * ORC_MAXJ];       /* frame Jacobian time variation        */
+    double Jdot[6 * ORC_MAXJ];
+    double res_ratio;                /* last termination check: max(pri/eps_pri, dua/eps_dua) */       /* frame Jacobian time variation        */
 } OracleDiag;
 
 enum { ORC_SOLVED = 1, ORC_MAX_ITER = -2, ORC_PRIMAL_INFEASIBLE = -3, ORC_NONFINITE = -10 };

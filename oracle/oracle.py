@@ -72,6 +72,7 @@ class OracleSettings(C.Structure):
         ("polish_cap", C.c_int),
         ("polish_add_all", C.c_int),
         ("polish_guess", C.c_int),
+        ("stop_at", C.c_int),
     ]
 
 
@@ -98,6 +99,7 @@ class OracleDiag(C.Structure):
         ("man_graddot", C.c_double * MAXJ), ("dist_graddot", C.c_double * MAXJ),
         ("man_gd", C.c_double), ("dist_gd", C.c_double),
         ("Jdot", C.c_double * (6 * MAXJ)),
+        ("res_ratio", C.c_double),
     ]
 
 

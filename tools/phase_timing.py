@@ -41,3 +41,7 @@ print("eqp: %d calls, %.0f cycles/call, mean KKT size %.1f; polish residuals %.0
 print("qp record load (inside load+assemble): %.0f cyc/inst" % (v[44] / B))
 print("polish steps: infeasible->add/drop %d, wrong dual sign->drop %d, ratio-test blocks %d, KKT residual failures %d" % (v[45], v[46], v[47], v[48]))
 print("Ruiz passes: %.2f per instance" % (v[49] / B))
+sub = [("jacobi guess", 50), ("drop rule", 51), ("eqp setup (K0, rhs)", 52), ("eqp Gauss-Jordan", 53),
+       ("eqp solve + refinement", 54), ("eqp x, y, stationarity", 55), ("ratio test", 56), ("candidate z", 57),
+       ("polish residuals", 43), ("certify + add/drop", 58)]
+print("polish sub-phases (cycles/instance): " + ", ".join("%s %.0f" % (n, v[k] / B) for n, k in sub))
