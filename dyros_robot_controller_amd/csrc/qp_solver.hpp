@@ -989,6 +989,7 @@ __device__ __forceinline__ bool eqp(const KParams& kp, double* S, int actb, int 
 // (Nocedal & Wright Alg. 16.3) from the first feasible polished point.  Same
 // decisions, in the same row order, as oracle/drc_oracle.c:qp_polish.
 constexpr int kPolishFeasAttempts = 4, kPolishAsIters = 24, kPolishJacobiSweeps = 3;
+constexpr double kPolishSlackTol = 0.3;
 template <class QD>
 __device__ __forceinline__ bool polish(const KParams& kp, double* S, bool strict) {
   using GL = Grp<QD::gs>;
@@ -1007,8 +1008,9 @@ __device__ __forceinline__ bool polish(const KParams& kp, double* S, bool strict
   // fixed -- clamp them.  At the first check the ADMM iterate has usually not
   // reached the velocity bounds the optimum saturates: OSQP's rule above then
   // misses about two rows per FR3 instance (12 % right first time, 2.7 EQP
-  // solves per polish); with this guess 77 % and 1.55 (tools/polish_census.py).
-  // Same rule and summation order as oracle/drc_oracle.c:polish_guess_jacobi.
+  // solves per polish); with this guess 77 % and 1.55, with the slack rule
+  // below 81 % and 1.45 (tools/polish_census.py).  Same rules and summation
+  // order as oracle/drc_oracle.c:polish_guess_jacobi / polish_guess_slack.
   PH_STAMP(pj_t0);
   if (strict && kp.problem == 0 && np < nx) {
     const double *P = S + kp.oP, *qv = S + kp.oQ;
@@ -1031,6 +1033,29 @@ __device__ __forceinline__ bool polish(const KParams& kp, double* S, bool strict
       xv = side < 0 ? bl / a : (side > 0 ? bu / a : v);
     }
     if (l < np) actb = side;
+    // slack lanes (no curvature, a linear cost, in exactly one G row r): the
+    // bound stays active only while its multiplier from stationarity with the
+    // ADMM dual of row r, -(q_l + g_rl y_r) / ab_l, is below
+    // -kPolishSlackTol |q_l| / ab_l (oracle: polish_guess_slack)
+    if (l >= np && l < nx) {
+      const int lx = l < nx ? l : 0;
+      double gv = 0.0, yr = 0.0;
+      int cnt = 0;
+#pragma unroll
+      for (int i = 0; i < ng; ++i) {
+        const double g = G[i * nx + lx];
+        if (g != 0.0) {
+          gv = g;
+          yr = y[nx + i];
+          ++cnt;
+        }
+      }
+      const double ql = qv[lx], a = ab[lx];
+      if (cnt == 1 && ql != 0.0) {
+        const double yb = -(ql + gv * yr) / a;
+        actb = yb < -kPolishSlackTol * fabs(ql) / a ? -1 : 0;
+      }
+    }
   }
   PH_SINCE(50, pj_t0);
   double* U = S + kp.oU0;

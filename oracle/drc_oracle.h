@@ -81,7 +81,9 @@ typedef struct OracleSettings {
                                       * violated one (QPID)                 */
     int polish_guess;                /* first active-set guess: 0 OSQP's rule,
                                       * 1 projected Jacobi on the q-dot box
-                                      * (QPIK parity mode, polish_guess_jacobi) */
+                                      * (polish_guess_jacobi), 2 that plus the
+                                      * slack rule (polish_guess_slack; QPIK
+                                      * parity mode) */
     int stop_at;                     /* > 0: stop at that ADMM iteration and
                                       * return its iterate as Solved (tests:
                                       * the other side's stopping point)    */
