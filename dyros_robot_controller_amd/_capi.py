@@ -139,8 +139,12 @@ def _load():
     lib.drc_qpik_stages_batch.argtypes = [vp, C.POINTER(QPIKParams), C.c_int64, vp, vp, vp, vp, vp, vp,
                                           vp, vp, vp, vp, vp, vp, vp]
     lib.drc_debug_kernel_timing.argtypes = [vp, C.c_int]
-    lib.drc_debug_waves.argtypes = [vp, C.c_void_p, ip, ip]
-    lib.drc_debug_host_timeline.argtypes = [vp, C.c_int, C.POINTER(C.c_int64), C.c_int64, C.POINTER(C.c_int64)]
+    # diagnostics added in r05: bound only when present, so A/B runs can load
+    # an older build (tests/test_capi_symbols.py checks the product exports them)
+    if hasattr(lib, "drc_debug_waves"):
+        lib.drc_debug_waves.argtypes = [vp, C.c_void_p, ip, ip]
+    if hasattr(lib, "drc_debug_host_timeline"):
+        lib.drc_debug_host_timeline.argtypes = [vp, C.c_int, C.POINTER(C.c_int64), C.c_int64, C.POINTER(C.c_int64)]
     if hasattr(lib, "drc_debug_lds_plan"):  # diagnostic; absent from older A/B builds (tools/ab_bench.sh)
         lib.drc_debug_lds_plan.argtypes = [vp, C.POINTER(QPIKParams), C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]
     lib.drc_debug_kernel_times.argtypes = [vp, dp, dp, dp, ip]
@@ -170,8 +174,8 @@ def _load():
     lib.drc_osf_batch.argtypes = [vp, C.POINTER(QPIKParams), C.c_int64, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     lib.drc_closed_form_host.argtypes = [vp, C.POINTER(QPIKParams), C.c_int, C.c_int64, dp, dp, dp, dp, dp, dp, dp, dp]
     for name in EXPORTED_SYMBOLS:
-        if name == "drc_debug_lds_plan" and not hasattr(lib, name):
-            continue
+        if name in ("drc_debug_lds_plan", "drc_debug_waves", "drc_debug_host_timeline") and not hasattr(lib, name):
+            continue  # diagnostics an older A/B build may lack
         if name not in ("drc_model_destroy", "drc_error_string", "drc_last_error", "drc_build_id"):
             getattr(lib, name).restype = C.c_int
     return lib

@@ -1347,6 +1347,15 @@ int drc_default_qpik_params(const drc_model* m, int exact, drc_qpik_params* p) {
   s.exact = exact ? 1 : 0;
   s.eps_exact = 1e-9;
   s.eps_fallback = 1e-7;
+  // exact mode: the ADMM iterate only seeds the certified polish's first
+  // active-set guess, so how often it is tried is a speed choice
+  // (DRC_EXACT_CHECK: A/B experiments)
+  static const int64_t exact_check = drc_amd::env_int("DRC_EXACT_CHECK", 25, 1);
+  static const int64_t exact_refine = drc_amd::env_int("DRC_EXACT_REFINE", 3, 0);
+  if (exact) {
+    s.check_termination = static_cast<int>(exact_check);
+    s.polish_refine_iter = static_cast<int>(exact_refine);
+  }
   return DRC_OK;
 }
 
@@ -1380,6 +1389,8 @@ int drc_default_qpid_params(const drc_model* m, int exact, drc_qpik_params* p) {
   // P is singular on null(J); OSQP's polish delta 1e-6 cannot certify at
   // eps_exact there, so parity mode regularises the polish with 1e-10
   if (exact) p->solver.delta = 1e-10;
+  p->solver.check_termination = 25;  // QPID keeps OSQP's check interval and
+  p->solver.polish_refine_iter = 3;   // refinement count in every mode
   return DRC_OK;
 }
 

@@ -159,3 +159,31 @@ def test_lds_plan(cuda, robot):
     assert 0 < q.value <= 160 * 1024 // 12
     assert 0 < t.value <= 160 * 1024 // 4
     assert f.value > max(t.value, q.value)
+
+
+def test_host_timeline_and_waves(cuda):
+    """drc_debug_host_timeline: one row of five ordered steady-clock stamps per
+    synchronous call while enabled; drc_debug_waves: the task build the call
+    launches (two or three waves per SIMD) and the QP kernel's three."""
+    rd = make_manipulator("fr3", cuda)
+    B = 2
+    q, qd, xt, xdt = step_inputs(rd, "fr3", 35, B, cuda)
+    p = manipulator.QPIKParamsBuilder(rd.model, exact=True).params(LINK["fr3"], _capi.MODE_QPIK_STEP)
+    n = rd.model.dof
+    o, s, it = np.zeros((n, B)), np.zeros(B, np.int32), np.zeros(B, np.int32)
+    lib, h = _capi.lib(), rd.model.handle
+    _capi.check(lib.drc_debug_host_timeline(h, 1, None, 0, None))
+    for _ in range(3):
+        _capi.check(lib.drc_qpik_host(h, C.byref(p), B, dp(q), dp(qd), dp(xt), dp(xdt), None, None, dp(o), ip(s), ip(it)))
+    tl = np.zeros((8, 5), np.int64)
+    cnt = C.c_int64()
+    _capi.check(lib.drc_debug_host_timeline(h, 0, tl.ctypes.data_as(C.POINTER(C.c_int64)), 8, C.byref(cnt)))
+    assert cnt.value == 3
+    assert np.all(np.diff(tl[:3], axis=1) >= 0) and np.all(tl[:3, 0] > 0)
+    assert np.all(tl[1:3, 0] >= tl[0:2, 4])
+    _capi.check(lib.drc_qpik_host(h, C.byref(p), B, dp(q), dp(qd), dp(xt), dp(xdt), None, None, dp(o), ip(s), ip(it)))
+    _capi.check(lib.drc_debug_host_timeline(h, 0, None, 0, C.byref(cnt)))
+    assert cnt.value == 0                                   # disabled: nothing recorded
+    wt, wq = C.c_int(), C.c_int()
+    _capi.check(lib.drc_debug_waves(h, C.byref(p), C.byref(wt), C.byref(wq)))
+    assert wt.value in (2, 3) and wq.value == 3

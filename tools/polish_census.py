@@ -73,11 +73,14 @@ def main():
     ap.add_argument("--tol", type=float, nargs="*", default=[1e-6, 1e-4, 1e-3, 1e-2])
     ap.add_argument("--guess", type=int, default=-1, help="first-guess rule of the polish (-1: OSQP's)")
     ap.add_argument("--check", type=int, default=0, help="check_termination (0: the default 25)")
+    ap.add_argument("--refine", type=int, default=-1, help="polish_refine_iter (-1: the default 3)")
     a = ap.parse_args()
     _, om, spec = O.load(a.robot)
     par = O.default_params(spec["kind"], exact=True)
     if a.check:
         par.solver.check_termination = a.check
+    if a.refine >= 0:
+        par.solver.polish_refine_iter = a.refine
     inputs = workload(om, a.robot, a.batch, a.seed)
     O.lib().oracle_polish_guess(C.c_int(a.guess))
     res = {"robot": a.robot, "batch": a.batch, "seed": a.seed, "by_tol": []}
