@@ -9,6 +9,27 @@
 
 namespace drc_amd {
 
+// The columns of G row r a product has to visit.  QPIK manipulator shapes
+// (compile-time nx = np + ng, problem 0): row r holds the np q-dot columns and
+// its own slack column np + r only (QP_IK.cpp:99-131, qp_assemble), so a row
+// product visits np + 1 entries instead of nx -- the same nonzero terms in the
+// same order as the dense sum, which adds only exact zeros (bit-identical).
+// Every other shape visits all nx columns.
+template <class QD, class F>
+__device__ __forceinline__ void g_row_cols(const KParams& kp, int r, F&& f) {
+  if constexpr (QD::nx > 0 && QD::nx == QD::np + QD::ng) {
+    if (kp.problem == 0) {
+#pragma unroll
+      for (int j = 0; j < QD::np; ++j) f(j);
+      f(QD::np + r);
+      return;
+    }
+  }
+  const int nx = DNX;
+#pragma unroll
+  for (int j = 0; j < nx; ++j) f(j);
+}
+
 // ------------------------------------------------------------------------
 // OSQP residuals (lane-parallel): fills SC_* slots.  x, z, y in LDS (scaled)
 // ------------------------------------------------------------------------
@@ -59,8 +80,7 @@ __device__ __forceinline__ void residuals(const KParams& kp, double* S, const do
     if constexpr (PRE) {
       ax = axg_pre;
     } else {
-#pragma unroll
-      for (int j = 0; j < nx; ++j) ax += G[lg * nx + j] * x[j];
+      g_row_cols<QD>(kp, lg, [&](int j) { ax += G[lg * nx + j] * x[j]; });
     }
     int row = nx + lg;
     double r = ax - z[row];
@@ -549,8 +569,7 @@ __device__ __forceinline__ bool eqp_regs(const KParams& kp, double* S, int actb,
   if (l < NG && actg != 0) {
     const int lg = l < NG ? l : 0;
     double r = actg < 0 ? lo[NX + lg] : up[NX + lg];
-#pragma unroll
-    for (int c = 0; c < NX; ++c) r -= G[lg * NX + c] * xx[c];
+    g_row_cols<QD>(kp, lg, [&](int c) { r -= G[lg * NX + c] * xx[c]; });
     rG = r;
   }
   const bool hf = l < nF, hr = l >= nF && l < N;
@@ -996,12 +1015,13 @@ __device__ __forceinline__ bool polish(const KParams& kp, double* S, bool strict
   const int l = GL::lane(), nx = DNX, ng = DNG, np = DNP, m = DM;
   const double *G = S + kp.oG, *ab = S + kp.oAB, *lo = S + kp.oL, *up = S + kp.oU, *E = S + kp.oE;
   double *x = S + kp.oX, *z = S + kp.oZ, *y = S + kp.oY;
-  int actb = 0, actg = 0;
-  if (l < nx) actb = (z[l] - lo[l] < -y[l]) ? -1 : ((up[l] - z[l] < y[l]) ? 1 : 0);
+  int ob = 0, og = 0;  // OSQP's guess
+  if (l < nx) ob = (z[l] - lo[l] < -y[l]) ? -1 : ((up[l] - z[l] < y[l]) ? 1 : 0);
   if (l < ng) {
     int r = nx + l;
-    actg = (z[r] - lo[r] < -y[r]) ? -1 : ((up[r] - z[r] < y[r]) ? 1 : 0);
+    og = (z[r] - lo[r] < -y[r]) ? -1 : ((up[r] - z[r] < y[r]) ? 1 : 0);
   }
+  int actb = ob, actg = og;
   // QPIK parity mode: the bound rows of the q-dot (the variables with cost
   // curvature, P_ll > 0) take the sides at which kPolishJacobiSweeps projected
   // Jacobi sweeps on their box -- the G-row duals of the ADMM iterate held
@@ -1019,19 +1039,20 @@ __device__ __forceinline__ bool polish(const KParams& kp, double* S, bool strict
     double xv = x[lp], c = qv[lp];
 #pragma unroll
     for (int i = 0; i < ng; ++i) c += G[i * nx + lp] * y[nx + i];
-    const double pll = P[lp * np + lp], a = ab[lp], bl = lo[lp], bu = up[lp];
+    const double ipll = 1.0 / P[lp * np + lp], a = ab[lp], bl = lo[lp], bu = up[lp];
     int side = 0;
     for (int sw = 0; sw < kPolishJacobiSweeps; ++sw) {
-      if (l < np) bc[l] = xv;
+      lds_double* xb = bc + (sw & 1) * np;  // alternate halves: no exchange point between the reads and the next writes
+      if (l < np) xb[l] = xv;
       wsync();
       double g = c;
 #pragma unroll
-      for (int k = 0; k < np; ++k) g += P[lp * np + k] * bc[k];
-      wsync();
-      const double v = xv - g / pll, av = a * v;
+      for (int k = 0; k < np; ++k) g += P[lp * np + k] * xb[k];
+      const double v = xv - g * ipll, av = a * v;
       side = av <= bl ? -1 : (av >= bu ? 1 : 0);
       xv = side < 0 ? bl / a : (side > 0 ? bu / a : v);
     }
+    wsync();
     if (l < np) actb = side;
     // slack lanes (no curvature, a linear cost, in exactly one G row r): the
     // bound stays active only while its multiplier from stationarity with the
@@ -1058,6 +1079,11 @@ __device__ __forceinline__ bool polish(const KParams& kp, double* S, bool strict
     }
   }
   PH_SINCE(50, pj_t0);
+  // when the polish from this guess fails and it differs from OSQP's, the
+  // same polish runs once more from OSQP's guess (oracle: qp_polish): a guess
+  // whose ADMM duals settle slowly can fail at every check, and a UR5e bench
+  // instance then ran 1 400 ADMM iterations instead of one extra attempt
+  const bool alt = GL::any(actb != ob || actg != og);
   double* U = S + kp.oU0;
   double* xx = U + 64;       // [nx]
   double* yy = U + 128;      // [m] (<= 128)
@@ -1065,8 +1091,14 @@ __device__ __forceinline__ bool polish(const KParams& kp, double* S, bool strict
   double* xc = S + kp.oXT;   // feasible iterate of the active-set phase
   double* sc = S + kp.oSc;
   const double pr0 = sc[SC_PRI], dr0 = sc[SC_DUA];
-  bool have_feas = false;
   const int iters = strict ? kPolishFeasAttempts + kPolishAsIters : 1;
+  for (int pass = 0; pass < 2; ++pass) {
+  if (pass == 1) {
+    if (!alt) break;
+    actb = ob;
+    actg = og;
+  }
+  bool have_feas = false;
   for (int it = 0; it < iters; ++it) {
     PH_STAMP(pd_t0);
     {
@@ -1080,13 +1112,12 @@ __device__ __forceinline__ bool polish(const KParams& kp, double* S, bool strict
       if (l < ng && actg != 0) {
         const int lg = l < ng ? l : 0, row = nx + lg;
         double sf = 0, sa = 0, act = 0;
-#pragma unroll
-        for (int j = 0; j < nx; ++j) {
+        g_row_cols<QD>(kp, lg, [&](int j) {
           const double g = G[lg * nx + j];
           sa = fmax(sa, fabs(g));
           if (!((fixed >> j) & 1ull)) sf = fmax(sf, fabs(g));
           else act += g * (((atup >> j) & 1ull) ? up[j] : lo[j]) / ab[j];
-        }
+        });
         const double b = actg < 0 ? lo[row] : up[row], slack = actg < 0 ? act - b : b - act;
         if (sf <= 1e-12 * sa && slack > 1e-12 * (fabs(act) + fabs(b))) actg = 0;
       }
@@ -1116,11 +1147,10 @@ __device__ __forceinline__ bool polish(const KParams& kp, double* S, bool strict
         if (l < ng && actg == 0) {
           const int lg = l < ng ? l : 0, row = nx + lg;
           double axc = 0, ap = 0, a = 2.0;
-#pragma unroll
-          for (int j = 0; j < nx; ++j) {
+          g_row_cols<QD>(kp, lg, [&](int j) {
             axc += G[lg * nx + j] * xc[j];
             ap += G[lg * nx + j] * (xx[j] - xc[j]);
-          }
+          });
           int sd = 0;
           if (ap < 0 && lo[row] > -kInf * kMinScaling) { a = (lo[row] - axc) / ap; sd = -1; }
           else if (ap > 0 && up[row] < kInf * kMinScaling) { a = (up[row] - axc) / ap; sd = 1; }
@@ -1152,8 +1182,7 @@ __device__ __forceinline__ bool polish(const KParams& kp, double* S, bool strict
     }
     if (l < ng) {
       const int lg = l < ng ? l : 0;
-#pragma unroll
-      for (int j = 0; j < nx; ++j) axg += G[lg * nx + j] * xx[j];
+      g_row_cols<QD>(kp, lg, [&](int j) { axg += G[lg * nx + j] * xx[j]; });
       zz[nx + lg] = fmin(fmax(axg, lo[nx + lg]), up[nx + lg]);
     }
     wsync();
@@ -1251,6 +1280,7 @@ __device__ __forceinline__ bool polish(const KParams& kp, double* S, bool strict
     }
     PH_SINCE(58, pk_t0);
   }
+  }  // pass
   if (l == 0) {  // restore the ADMM residuals for the caller
     sc[SC_PRI] = pr0;
     sc[SC_DUA] = dr0;

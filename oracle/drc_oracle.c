@@ -1774,7 +1774,7 @@ static void polish_drop_fixed_rows(const QPW* w, int* flag) {
  * the active set against the one each successful polish certifies.  Off by
  * default; no decision of the solver depends on it. */
 #define PC_RULES 16
-enum { PC_CALLS, PC_OK, PC_EQP, PC_ADD, PC_DROP, PC_RATIO, PC_OK1, PC_HIST0 = 8, PC_MATCH0 = PC_HIST0 + 8,
+enum { PC_CALLS, PC_OK, PC_EQP, PC_ADD, PC_DROP, PC_RATIO, PC_OK1, PC_RETRY, PC_HIST0 = 8, PC_MATCH0 = PC_HIST0 + 8,
        PC_FN0 = PC_MATCH0 + PC_RULES, PC_FP0 = PC_FN0 + PC_RULES, PC_N = PC_FP0 + PC_RULES };
 static long long g_pc[PC_N];
 static long long g_pc_row[3][ORC_MAXC];  /* rule 0: false neg / false pos / final active, per row */
@@ -1889,7 +1889,7 @@ static void polish_guess_jacobi(const QPW* w, int* flag) {
             if (!(pjj > 0)) continue;
             double g = c[j];
             for (int k = 0; k < n; ++k) g += w->P[j * n + k] * xo[k];
-            const double a = w->A[j * n + j], v = xo[j] - g / pjj, av = a * v;
+            const double ipjj = 1.0 / pjj, a = w->A[j * n + j], v = xo[j] - g * ipjj, av = a * v;
             side[j] = av <= w->l[j] ? -1 : (av >= w->u[j] ? 1 : 0);
             xv[j] = side[j] < 0 ? w->l[j] / a : (side[j] > 0 ? w->u[j] / a : v);
         }
@@ -1996,27 +1996,14 @@ static void polish_guess_slack(const QPW* w, int* flag) {
     }
 }
 
-static int qp_polish(QPW* w, const OracleSettings* s, int strict) {
+static __thread int pcg[PC_RULES][ORC_MAXC];
+/* the polish from one first guess of the active set (flag, modified) */
+static int qp_polish_from(QPW* w, const OracleSettings* s, int strict, int* flag, double pr0, double dr0,
+                          int census) {
     int n = w->n, m = w->m;
-    int flag[ORC_MAXC];  /* -1 lower-active, +1 upper-active, 0 inactive */
-    for (int i = 0; i < m; ++i)
-        flag[i] = (w->z[i] - w->l[i] < -w->y[i]) ? -1 : ((w->u[i] - w->z[i] < w->y[i]) ? 1 : 0);
-    if (strict && s->polish_guess >= 1) polish_guess_jacobi(w, flag);
-    if (strict && s->polish_guess >= 2) polish_guess_slack(w, flag);
-    if (g_pc_guess >= 0 && g_pc_guess < 15 && strict) pc_guess(w, g_pc_guess, flag);
-    if (g_pc_guess == 15 && strict) pc_guess_slacks(w, flag, g_pc_tol[15]);
-    if (g_pc_guess == 16 && strict) pc_guess_effbox(w, flag);
-    if (g_pc_guess == 17 && strict) { pc_guess_effbox(w, flag); pc_guess_slacks(w, flag, g_pc_tol[15]); }
-    const double pr0 = w->r.pri_res, dr0 = w->r.dua_res;
     Res tmp;
     double xp[ORC_MAXX], yp[ORC_MAXC], zp[ORC_MAXC], ax[ORC_MAXC], xc[ORC_MAXX];
     int have_feasible = 0, neqp = 0;
-    static __thread int pcg[PC_RULES][ORC_MAXC];
-    const int census = g_pc_on && strict;
-    if (census) {
-        pc_add(PC_CALLS, 1);
-        for (int r = 0; r < PC_RULES; ++r) pc_guess(w, r, pcg[r]);
-    }
     for (int it = 0; it < (strict ? POLISH_FEAS_ATTEMPTS + POLISH_AS_ITERS : 1); ++it) {
         polish_drop_fixed_rows(w, flag);
         ++neqp;
@@ -2135,6 +2122,36 @@ static int qp_polish(QPW* w, const OracleSettings* s, int strict) {
         }
     }
     return 0;
+}
+
+/* Parity mode: the polish from the QPIK guess (polish_guess >= 1); when that
+ * fails and differs from OSQP's own guess, once more from OSQP's guess, so a
+ * guess that keeps failing at every check (the ADMM duals it reads settle
+ * slowly on some instances: a UR5e bench instance ran 1 400 ADMM iterations
+ * without this) costs one extra attempt instead of the ADMM tail. */
+static int qp_polish(QPW* w, const OracleSettings* s, int strict) {
+    int m = w->m;
+    int osqp[ORC_MAXC], flag[ORC_MAXC];  /* -1 lower-active, +1 upper-active, 0 inactive */
+    for (int i = 0; i < m; ++i)
+        osqp[i] = (w->z[i] - w->l[i] < -w->y[i]) ? -1 : ((w->u[i] - w->z[i] < w->y[i]) ? 1 : 0);
+    memcpy(flag, osqp, m * sizeof(int));
+    if (strict && s->polish_guess >= 1) polish_guess_jacobi(w, flag);
+    if (strict && s->polish_guess >= 2) polish_guess_slack(w, flag);
+    if (g_pc_guess >= 0 && g_pc_guess < 15 && strict) pc_guess(w, g_pc_guess, flag);
+    if (g_pc_guess == 15 && strict) pc_guess_slacks(w, flag, g_pc_tol[15]);
+    if (g_pc_guess == 16 && strict) pc_guess_effbox(w, flag);
+    if (g_pc_guess == 17 && strict) { pc_guess_effbox(w, flag); pc_guess_slacks(w, flag, g_pc_tol[15]); }
+    const int differs = memcmp(flag, osqp, m * sizeof(int)) != 0;
+    const double pr0 = w->r.pri_res, dr0 = w->r.dua_res;
+    const int census = g_pc_on && strict;
+    if (census) {
+        pc_add(PC_CALLS, 1);
+        for (int r = 0; r < PC_RULES; ++r) pc_guess(w, r, pcg[r]);
+    }
+    if (qp_polish_from(w, s, strict, flag, pr0, dr0, census)) return 1;
+    if (!strict || !differs) return 0;
+    if (census) pc_add(PC_RETRY, 1);
+    return qp_polish_from(w, s, strict, osqp, pr0, dr0, census);
 }
 
 /* the last termination check's max(pri_res / eps_pri, dua_res / eps_dua) of

@@ -2,7 +2,7 @@
 # One GPU lease, a sequence of steps (replaces the per-iteration batch files):
 #   bash tools/lease.sh <tag> <step> [<step> ...]
 # Steps (each under its own time limit; the first failure ends the lease):
-#   test                       pytest -m gpu (gpurun_out/gputest_<tag>.log)
+#   test[:<k expr>]            pytest -m gpu [-k expr, commas become spaces] (gpurun_out/gputest_<tag>.log)
 #   smoke                      __graft_entry__.smoke()
 #   bench:<robot>[,<robot>]    one bench line per robot, no CPU baseline (tools/gpu_check.sh's summary)
 #   line[:<args>]              the default bench line (with CPU baseline), extra bench.py args after ':'
@@ -13,6 +13,7 @@
 #   phase:<robot>              DRC_PHASE_TIMING build's phase shares (tools/phase_timing.py)
 #   gpus2                      two-rank rehearsal on the one GPU (gloo), gpurun_out/gpus2_<tag>.json
 #   final[:<robot>,..]         round-end measurement (tools/final_round.sh)
+#   refcensus                  reference-settings census (tools/reference_census.py)
 set -o pipefail
 ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 cd $ROOT
@@ -38,7 +39,7 @@ for step in "$@"; do
   case $kind in
     test)
       timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
-        > gpurun_out/gputest_$TAG.log 2>&1
+        ${rest:+-k "${rest//,/ }"} > gpurun_out/gputest_$TAG.log 2>&1
       rc=$?; tail -3 gpurun_out/gputest_$TAG.log; [ $rc -eq 0 ] || exit $rc ;;
     smoke)
       timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 \
@@ -76,6 +77,10 @@ for step in "$@"; do
       grep -h '^{' gpurun_out/gpus2_$TAG.json | cut -c1-240 ;;
     final)
       timeout -k 10 3000 bash tools/final_round.sh $TAG ${rest//,/ } || exit 1 ;;
+    refcensus)
+      timeout -k 10 600 python3 -u tools/reference_census.py > gpurun_out/refcensus_$TAG.log 2>&1 \
+        || { tail -20 gpurun_out/refcensus_$TAG.log; exit 1; }
+      cut -c1-400 gpurun_out/refcensus_$TAG.log ;;
     *) echo "lease.sh: unknown step $step" >&2; exit 2 ;;
   esac
 done
