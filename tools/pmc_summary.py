@@ -87,11 +87,17 @@ def main():
     avg, ndisp = trace_durations(os.path.join(src, "kt"))
     fetch, nf = counters(os.path.join(src, "fetch"), "FETCH_SIZE")
     write, nw = counters(os.path.join(src, "write"), "WRITE_SIZE")
+    hit, _ = counters(os.path.join(src, "tcc"), "TCC_HIT_sum")
+    miss, _ = counters(os.path.join(src, "tcc"), "TCC_MISS_sum")
     kern = {}
     for k in sorted(set(fetch) | set(write)):
         kern[k] = {"FETCH_SIZE_KiB_raw": fetch.get(k), "WRITE_SIZE_KiB_raw": write.get(k),
                    "fetch_bytes": 2 * 1024 * fetch.get(k, 0.0), "write_bytes": 1024 * write.get(k, 0.0),
                    "dispatches": [nf.get(k, 0), nw.get(k, 0)], "avg_duration_ns": avg.get(k)}
+        if k in hit and k in miss and hit[k] + miss[k] > 0:
+            kern[k]["TCC_HIT"] = hit[k]
+            kern[k]["TCC_MISS"] = miss[k]
+            kern[k]["l2_hit_rate"] = hit[k] / (hit[k] + miss[k])
     per_dispatch = sum(v["fetch_bytes"] + v["write_bytes"] for v in kern.values())
     # each dispatch pair covers one sub-batch (batch / chunks instances); a step is one call
     with open(os.path.join(src, "bench.json")) as fh:

@@ -21,4 +21,7 @@ timeout -k 10 420 rocprofv3 --pmc FETCH_SIZE -f csv -d $OUT/fetch -o fetch -- py
 echo "fetch pass done"
 timeout -k 10 420 rocprofv3 --pmc WRITE_SIZE -f csv -d $OUT/write -o write -- python3 $ROOT/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-extras $ARGS > $OUT/write.log 2>&1
 echo "write pass done"
+# L2 hit / miss of the same dispatches (is the spill stream served by L2?)
+timeout -k 10 420 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -f csv -d $OUT/tcc -o tcc -- python3 $ROOT/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-extras $ARGS > $OUT/tcc.log 2>&1
+echo "tcc pass done"
 bash $ROOT/tools/valu_pass.sh $TAG $ARGS
