@@ -2276,7 +2276,7 @@ void oracle_default_params(int kind, OracleParams* p, int exact) {
     s->eps_abs = 1e-3; s->eps_rel = 1e-3; s->eps_prim_inf = 1e-4;
     s->max_iter = 4000; s->check_termination = 25; s->scaling = 10;
     s->adaptive_rho = 1; s->adaptive_rho_interval = 25; s->adaptive_rho_tolerance = 5;
-    s->polish = exact ? 1 : 0; s->polish_refine_iter = exact ? 2 : 3; s->delta = 1e-6;  /* kernel: drc_default_qpik_params */
+    s->polish = exact ? 1 : 0; s->polish_refine_iter = 3; s->delta = 1e-6;
     s->exact = exact; s->eps_exact = 1e-9; s->eps_fallback = 1e-7;
     /* the kernel's QPIK polish KKT cap (kEqpRegCap, its register EQP): a
      * larger reduced KKT fails that polish attempt and ADMM continues.  The
