@@ -9,27 +9,6 @@
 
 namespace drc_amd {
 
-// The columns of G row r a product has to visit.  QPIK manipulator shapes
-// (compile-time nx = np + ng, problem 0): row r holds the np q-dot columns and
-// its own slack column np + r only (QP_IK.cpp:99-131, qp_assemble), so a row
-// product visits np + 1 entries instead of nx -- the same nonzero terms in the
-// same order as the dense sum, which adds only exact zeros (bit-identical).
-// Every other shape visits all nx columns.
-template <class QD, class F>
-__device__ __forceinline__ void g_row_cols(const KParams& kp, int r, F&& f) {
-  if constexpr (QD::nx > 0 && QD::nx == QD::np + QD::ng) {
-    if (kp.problem == 0) {
-#pragma unroll
-      for (int j = 0; j < QD::np; ++j) f(j);
-      f(QD::np + r);
-      return;
-    }
-  }
-  const int nx = DNX;
-#pragma unroll
-  for (int j = 0; j < nx; ++j) f(j);
-}
-
 // ------------------------------------------------------------------------
 // OSQP residuals (lane-parallel): fills SC_* slots.  x, z, y in LDS (scaled)
 // ------------------------------------------------------------------------
@@ -80,7 +59,8 @@ __device__ __forceinline__ void residuals(const KParams& kp, double* S, const do
     if constexpr (PRE) {
       ax = axg_pre;
     } else {
-      g_row_cols<QD>(kp, lg, [&](int j) { ax += G[lg * nx + j] * x[j]; });
+#pragma unroll
+      for (int j = 0; j < nx; ++j) ax += G[lg * nx + j] * x[j];
     }
     int row = nx + lg;
     double r = ax - z[row];
@@ -412,8 +392,11 @@ __device__ __forceinline__ void load_admm_regs(const KParams& kp, const double* 
 // line (runs every check_termination iterations).  Works on the published
 // LDS iterate.  Returns 0 = continue, 1 = continue after reloading the
 // registers (K^-1 or rho changed, or the iterate was touched), 2 = stop.
+#ifndef DRC_POLISH_ATTR
+#define DRC_POLISH_ATTR __forceinline__
+#endif
 template <class QD>
-__device__ __forceinline__ bool polish(const KParams& kp, double* S, bool strict);
+__device__ DRC_POLISH_ATTR bool polish(const KParams& kp, double* S, bool strict);
 
 template <class QD>
 __device__ __noinline__ int admm_check(const KParams& kp, double* S, int it, int check, int adapt, int* status) {
@@ -427,52 +410,53 @@ __device__ __noinline__ int admm_check(const KParams& kp, double* S, int it, int
   // polish reads only the iterate, so the ADMM residuals -- which decide
   // convergence, the fallback and adaptive rho -- are formed only when it
   // fails (the usual case solves here and never needs them)
-  bool early_failed = false;
-  if (check && kp.s.exact && sc[SC_PFAIL] < kPolishMaxEarly) {
-    CK_T(34);
-    const bool ok_ = polish<QD>(kp, S, true);
-    CK_T(35);
-    CK_N(36);
-    if (ok_) {
-      CK_N(37);
-      *status = DRC_STATUS_SOLVED;
-      return 2;
-    }
-    if (GL::lane() == 0) sc[SC_PFAIL] += 1.0;
-    factor_any<QD>(kp, S);
-    CK_T(38);  // polish used the union region
-    early_failed = true;
-    reload = 1;
-  }
-  residuals<QD>(kp, S, x, z, y, kp.s.eps_abs, kp.s.eps_rel);
-  CK_T(32);
-  CK_N(33);
-  if (check) {
-    const bool conv = sc[SC_PRI] < sc[SC_EPSP] && sc[SC_DUA] < sc[SC_EPSD];
+  bool early_failed = false, conv = false;
+  // One polish call site (inlined once): round 0 is the early polish (exact
+  // mode, fewer than kPolishMaxEarly failed attempts), round 1 forms the ADMM
+  // residuals and, at convergence, polishes when round 0 did not try
+  for (int round = 0; round < 2; ++round) {
+    bool try_polish;
+    if (round == 0) {
+      try_polish = check && kp.s.exact && sc[SC_PFAIL] < kPolishMaxEarly;
+    } else {
+      residuals<QD>(kp, S, x, z, y, kp.s.eps_abs, kp.s.eps_rel);
+      CK_T(32);
+      CK_N(33);
+      if (!check) break;
+      conv = sc[SC_PRI] < sc[SC_EPSP] && sc[SC_DUA] < sc[SC_EPSD];
 #ifdef DRC_QP_DEBUG
-    if (GL::lane() == 0 && it <= 200)
-      printf("it %d rho %.4g pri %.3e/%.3e dua %.3e/%.3e x3 %.6f\n", it, sc[SC_RHO], sc[SC_PRI], sc[SC_EPSP],
-             sc[SC_DUA], sc[SC_EPSD], x[3] * S[kp.oD + 3]);
+      if (GL::lane() == 0 && it <= 200)
+        printf("it %d rho %.4g pri %.3e/%.3e dua %.3e/%.3e x3 %.6f\n", it, sc[SC_RHO], sc[SC_PRI], sc[SC_EPSP],
+               sc[SC_DUA], sc[SC_EPSD], x[3] * S[kp.oD + 3]);
 #endif
-    if (conv) {
+      if (!conv) break;
       if (!kp.s.exact) {
         *status = DRC_STATUS_SOLVED;
         return 2;
       }
-      if (!early_failed && sc[SC_PFAIL] < kPolishMaxTotal) {
-        CK_T(34);
-        const bool ok_ = polish<QD>(kp, S, true);
-        CK_T(35);
-        CK_N(36);
-        if (ok_) {
-          CK_N(37);
-          *status = DRC_STATUS_SOLVED;
-          return 2;
-        }
-        if (GL::lane() == 0) sc[SC_PFAIL] += 1.0;
-        factor_any<QD>(kp, S);
-        CK_T(38);
+      try_polish = !early_failed && sc[SC_PFAIL] < kPolishMaxTotal;
+    }
+    if (try_polish) {
+      CK_T(34);
+      const bool ok_ = polish<QD>(kp, S, true);
+      CK_T(35);
+      CK_N(36);
+      if (ok_) {
+        CK_N(37);
+        *status = DRC_STATUS_SOLVED;
+        return 2;
       }
+      if (GL::lane() == 0) sc[SC_PFAIL] += 1.0;
+      factor_any<QD>(kp, S);
+      CK_T(38);  // polish used the union region
+      if (round == 0) {
+        early_failed = true;
+        reload = 1;
+      }
+    }
+  }
+  if (check) {
+    if (conv) {
       residuals<QD>(kp, S, x, z, y, kp.s.eps_fallback, kp.s.eps_fallback);
       if (sc[SC_PRI] < sc[SC_EPSP] && sc[SC_DUA] < sc[SC_EPSD]) {
         *status = DRC_STATUS_SOLVED;
@@ -569,7 +553,8 @@ __device__ __forceinline__ bool eqp_regs(const KParams& kp, double* S, int actb,
   if (l < NG && actg != 0) {
     const int lg = l < NG ? l : 0;
     double r = actg < 0 ? lo[NX + lg] : up[NX + lg];
-    g_row_cols<QD>(kp, lg, [&](int c) { r -= G[lg * NX + c] * xx[c]; });
+#pragma unroll
+    for (int c = 0; c < NX; ++c) r -= G[lg * NX + c] * xx[c];
     rG = r;
   }
   const bool hf = l < nF, hr = l >= nF && l < N;
@@ -1010,7 +995,7 @@ __device__ __forceinline__ bool eqp(const KParams& kp, double* S, int actb, int 
 constexpr int kPolishFeasAttempts = 4, kPolishAsIters = 24, kPolishJacobiSweeps = 3;
 constexpr double kPolishSlackTol = 0.3;
 template <class QD>
-__device__ __forceinline__ bool polish(const KParams& kp, double* S, bool strict) {
+__device__ DRC_POLISH_ATTR bool polish(const KParams& kp, double* S, bool strict) {
   using GL = Grp<QD::gs>;
   const int l = GL::lane(), nx = DNX, ng = DNG, np = DNP, m = DM;
   const double *G = S + kp.oG, *ab = S + kp.oAB, *lo = S + kp.oL, *up = S + kp.oU, *E = S + kp.oE;
@@ -1112,12 +1097,13 @@ __device__ __forceinline__ bool polish(const KParams& kp, double* S, bool strict
       if (l < ng && actg != 0) {
         const int lg = l < ng ? l : 0, row = nx + lg;
         double sf = 0, sa = 0, act = 0;
-        g_row_cols<QD>(kp, lg, [&](int j) {
+#pragma unroll
+        for (int j = 0; j < nx; ++j) {
           const double g = G[lg * nx + j];
           sa = fmax(sa, fabs(g));
           if (!((fixed >> j) & 1ull)) sf = fmax(sf, fabs(g));
           else act += g * (((atup >> j) & 1ull) ? up[j] : lo[j]) / ab[j];
-        });
+        }
         const double b = actg < 0 ? lo[row] : up[row], slack = actg < 0 ? act - b : b - act;
         if (sf <= 1e-12 * sa && slack > 1e-12 * (fabs(act) + fabs(b))) actg = 0;
       }
@@ -1147,10 +1133,11 @@ __device__ __forceinline__ bool polish(const KParams& kp, double* S, bool strict
         if (l < ng && actg == 0) {
           const int lg = l < ng ? l : 0, row = nx + lg;
           double axc = 0, ap = 0, a = 2.0;
-          g_row_cols<QD>(kp, lg, [&](int j) {
+#pragma unroll
+          for (int j = 0; j < nx; ++j) {
             axc += G[lg * nx + j] * xc[j];
             ap += G[lg * nx + j] * (xx[j] - xc[j]);
-          });
+          }
           int sd = 0;
           if (ap < 0 && lo[row] > -kInf * kMinScaling) { a = (lo[row] - axc) / ap; sd = -1; }
           else if (ap > 0 && up[row] < kInf * kMinScaling) { a = (up[row] - axc) / ap; sd = 1; }
@@ -1182,7 +1169,8 @@ __device__ __forceinline__ bool polish(const KParams& kp, double* S, bool strict
     }
     if (l < ng) {
       const int lg = l < ng ? l : 0;
-      g_row_cols<QD>(kp, lg, [&](int j) { axg += G[lg * nx + j] * xx[j]; });
+#pragma unroll
+      for (int j = 0; j < nx; ++j) axg += G[lg * nx + j] * xx[j];
       zz[nx + lg] = fmin(fmax(axg, lo[nx + lg]), up[nx + lg]);
     }
     wsync();

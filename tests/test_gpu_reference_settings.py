@@ -71,9 +71,10 @@ def _device(ctrl, robot, args, cuda):
     return out.cpu().numpy(), status.cpu().numpy(), iters.cpu().numpy()
 
 
-def check_reference_contract(robot, args, out, status, iters):
-    """Items 1-4 of the module docstring on the given instances; returns
-    (status mismatches, instances that do not agree)."""
+def check_reference_contract(robot, args, out, status, iters, rated=None):
+    """Items 1-4 of the module docstring on the given instances (the rates of
+    item 3 over the `rated` ones: a spread sample, not the device's failures
+    appended to it); returns (status mismatches, instances that do not agree)."""
     par, om = oracle_params(robot, exact=False)
     pex, _ = oracle_params(robot, exact=True)
     ref, rstat, riters = O.qpik_batch(om, par, *args, nthreads=16)
@@ -86,9 +87,10 @@ def check_reference_contract(robot, args, out, status, iters):
     other = np.nonzero(~agree)[0]
     long_run = np.maximum(iters, riters) >= LONG_RUN
     assert np.all(long_run[other]), [(int(b), int(iters[b]), int(riters[b])) for b in other if not long_run[b]]
-    assert agree.mean() >= 0.99, agree.mean()
-    mism = int(np.sum(status != rstat))
-    assert mism <= math.ceil(2e-3 * B), (mism, B)
+    rated = np.ones(B, bool) if rated is None else rated
+    assert agree[rated].mean() >= 0.99, agree[rated].mean()
+    mism = int(np.sum((status != rstat)[rated]))
+    assert mism <= math.ceil(2e-3 * rated.sum()), (mism, int(rated.sum()))
     both = (status == 1) & (rstat == 1) & (xstat == 1)
     if both.any():
         band_o = np.abs(ref - ex).max(axis=0)[both]
@@ -118,8 +120,10 @@ def test_reference_settings_bench_batch(cuda, robot):
     args = (moma_step_inputs if robot in MOMA else step_inputs)(rd, robot, 12345, B, cuda, stress=True)
     out, status, iters = _device(ctrl, robot, args, cuda)
     failed = np.nonzero(status != 1)[0]
-    idx = np.unique(np.concatenate([np.linspace(0, B - 1, 1000).astype(int), failed]))
+    spread = np.unique(np.linspace(0, B - 1, 1000).astype(int))
+    idx = np.unique(np.concatenate([spread, failed]))
     sub = lambda a: np.ascontiguousarray(a[:, idx])
-    mism, other = check_reference_contract(robot, [sub(a) for a in args], sub(out), status[idx], iters[idx])
+    mism, other = check_reference_contract(robot, [sub(a) for a in args], sub(out), status[idx], iters[idx],
+                                           rated=np.isin(idx, spread))
     print(robot, "B", B, "device non-solved", failed.size, "sample status mismatches", mism,
           "not agreeing (long runs)", other)
