@@ -219,6 +219,9 @@ def latency_b1(rd, robot, q, qd, xt, xdt, solver, calls=400, warmup=20):
     ip = lambda a: a.ctypes.data_as(C.POINTER(C.c_int))
     lib, h = _capi.lib(), rd.model.handle
     ts = []
+    import gc
+    gc_was = gc.isenabled()
+    gc.disable()      # a 1 kHz control loop does not let the collector run inside a cycle
     for k in range(warmup + calls):
         if k == warmup:   # host-side phase stamps of the timed calls (drc_debug_host_timeline)
             _capi.check(lib.drc_debug_host_timeline(h, 1, None, 0, None))
@@ -229,6 +232,8 @@ def latency_b1(rd, robot, q, qd, xt, xdt, solver, calls=400, warmup=20):
         _capi.check(rc)
         if k >= warmup:
             ts.append(t1 - t0)
+    if gc_was:
+        gc.enable()
     tl = np.zeros((calls, 5), np.int64)
     n = C.c_int64()
     _capi.check(lib.drc_debug_host_timeline(h, 0, tl.ctypes.data_as(C.POINTER(C.c_int64)), calls, C.byref(n)))
@@ -241,6 +246,7 @@ def latency_b1(rd, robot, q, qd, xt, xdt, solver, calls=400, warmup=20):
                  "slowest_call_us": {k: float(ph[worst, i]) for i, k in enumerate(names)} if len(ph) == calls else None,
                  "outside_library_slowest_us": float(ts[worst] - (tl[worst, 4] - tl[worst, 0]) / 1e3)
                  if len(ph) == calls else None,
+                 "library_max_us": float((tl[:n.value, 4] - tl[:n.value, 0]).max() / 1e3) if n.value else None,
                  "host_wait": "poll" if int(os.environ.get("DRC_HOST_WAIT", "1")) else "block",
                  "calls_over_us": {str(t): int(np.sum(ts > t)) for t in (200, 300, 500)}}
     return {"call": "QPIKCubic, B = 1, drc_qpik_host (host buffers in and out, synchronous)",
@@ -540,6 +546,8 @@ def extras(torch, args, rd, mod, robot, link, q, qd, xt, xdt, dq, dqd, dxt, dxdt
     lib, h = _capi.lib(), rd.model.handle
     it1 = torch.zeros(1, dtype=torch.int32, device=dq.device)
     ones = [[t[:, k:k + 1].contiguous() for t in (dq, dqd, dxt, dxdt)] for k in range(32)]
+    # the two-kernel pipeline (what a full batch runs): task and QP kernel apart
+    _capi.check(lib.drc_set_fusion(h, C.c_int(0)))
     for one in ones:
         ctrl.QPIK_step_batch(*one, link, iters=it1)
     torch.cuda.synchronize()
@@ -551,6 +559,7 @@ def extras(torch, args, rd, mod, robot, link, q, qd, xt, xdt, dq, dqd, dxt, dxdt
     tw, tk, tq, nc = C.c_double(), C.c_double(), C.c_double(), C.c_int()
     _capi.check(lib.drc_debug_kernel_times(h, C.byref(tw), C.byref(tk), C.byref(tq), C.byref(nc)))
     _capi.check(lib.drc_debug_kernel_timing(h, 0))
+    _capi.check(lib.drc_set_fusion(h, C.c_int(1)))
     lt, lq = tk.value / max(nc.value, 1) * 1e-3, tq.value / max(nc.value, 1) * 1e-3   # task / QP latency, seconds
     # waves per CU of each kernel as the call launches it: the register build's
     # waves per SIMD (drc_debug_waves) x 4, capped by the LDS plan (drc_debug_lds_plan)
@@ -569,8 +578,8 @@ def extras(torch, args, rd, mod, robot, link, q, qd, xt, xdt, dq, dqd, dxt, dxdt
         "call_us": 1e3 * tw.value / max(nc.value, 1), "task_waves_per_cu": cu_t, "qp_waves_per_cu": cu_q,
         "solves_per_s": roof, "frac": line["value"] / roof,
         "note": "design-relative, not a hardware limit (the hardware roof is valu_issue_roof): task and QP kernel "
-                "latency of one instance alone on the GPU (mean over the batch's first 32 instances, B = 1 calls, "
-                "HIP events); with the waves per CU each kernel is launched at (register build x 4 SIMDs, capped "
+                "latency of one instance alone on the GPU (mean over the batch's first 32 instances, B = 1 calls "
+                "through the two-kernel pipeline, HIP events); with the waves per CU each kernel is launched at (register build x 4 SIMDs, capped "
                 "by its LDS plan), 256 CUs complete 256 / (t_task / w_task + t_qp / w_qp) instances per second "
                 "if every wave slot stays busy at the isolated latency"}
 
