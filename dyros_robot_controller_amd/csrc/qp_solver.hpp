@@ -1024,7 +1024,7 @@ __device__ DRC_POLISH_ATTR bool polish(const KParams& kp, double* S, bool strict
     double xv = x[lp], c = qv[lp];
 #pragma unroll
     for (int i = 0; i < ng; ++i) c += G[i * nx + lp] * y[nx + i];
-    const double ipll = 1.0 / P[lp * np + lp], a = ab[lp], bl = lo[lp], bu = up[lp];
+    const double ipll = 1.0 / P[lp * np + lp], a = ab[lp], bl = lo[lp], bu = up[lp], xl = bl / a, xu = bu / a;
     int side = 0;
     for (int sw = 0; sw < kPolishJacobiSweeps; ++sw) {
       lds_double* xb = bc + (sw & 1) * np;  // alternate halves: no exchange point between the reads and the next writes
@@ -1035,7 +1035,7 @@ __device__ DRC_POLISH_ATTR bool polish(const KParams& kp, double* S, bool strict
       for (int k = 0; k < np; ++k) g += P[lp * np + k] * xb[k];
       const double v = xv - g * ipll, av = a * v;
       side = av <= bl ? -1 : (av >= bu ? 1 : 0);
-      xv = side < 0 ? bl / a : (side > 0 ? bu / a : v);
+      xv = side < 0 ? xl : (side > 0 ? xu : v);
     }
     wsync();
     if (l < np) actb = side;
@@ -1093,7 +1093,11 @@ __device__ DRC_POLISH_ATTR bool polish(const KParams& kp, double* S, bool strict
       // manipulability gradient of the first/last joint).  When the fixed
       // values already satisfy it strictly it is not active: drop it (the
       // oracle's qp_polish applies the same rule)
-      const unsigned long long fixed = GL::ballot(l < nx && actb != 0), atup = GL::ballot(l < nx && actb > 0);
+      // (the fixed values b_j / ab_j, one division per variable lane, go to xx
+      // -- where the EQP puts them too -- instead of a division per term)
+      const unsigned long long fixed = GL::ballot(l < nx && actb != 0);
+      if (l < nx) xx[l] = actb == 0 ? 0.0 : (actb < 0 ? lo[l] : up[l]) / ab[l];
+      wsync();
       if (l < ng && actg != 0) {
         const int lg = l < ng ? l : 0, row = nx + lg;
         double sf = 0, sa = 0, act = 0;
@@ -1102,7 +1106,7 @@ __device__ DRC_POLISH_ATTR bool polish(const KParams& kp, double* S, bool strict
           const double g = G[lg * nx + j];
           sa = fmax(sa, fabs(g));
           if (!((fixed >> j) & 1ull)) sf = fmax(sf, fabs(g));
-          else act += g * (((atup >> j) & 1ull) ? up[j] : lo[j]) / ab[j];
+          else act += g * xx[j];
         }
         const double b = actg < 0 ? lo[row] : up[row], slack = actg < 0 ? act - b : b - act;
         if (sf <= 1e-12 * sa && slack > 1e-12 * (fabs(act) + fabs(b))) actg = 0;

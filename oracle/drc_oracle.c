@@ -1762,7 +1762,7 @@ static void polish_drop_fixed_rows(const QPW* w, int* flag) {
             double g = w->A[i * n + j];
             sa = fmax(sa, fabs(g));
             if (!flag[j]) sf = fmax(sf, fabs(g));
-            else act += g * (flag[j] > 0 ? w->u[j] : w->l[j]) / w->A[j * n + j];
+            else act += g * ((flag[j] > 0 ? w->u[j] : w->l[j]) / w->A[j * n + j]);  /* kernel: the fixed value b_j / ab_j */
         }
         double b = flag[i] < 0 ? w->l[i] : w->u[i], slack = flag[i] < 0 ? act - b : b - act;
         if (sf <= 1e-12 * sa && slack > 1e-12 * (fabs(act) + fabs(b))) flag[i] = 0;
