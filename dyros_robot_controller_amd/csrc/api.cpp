@@ -393,6 +393,8 @@ static int plan_layout(const DevModel& M, KParams* k, bool task_only) {
   k->oU = take(m);
   k->oD = take(nx);
   k->oE = take(m);
+  k->oDi = take(nx);
+  k->oEi = take(m);
   k->oRho = take(m);
   k->oX = take(nx);
   k->oZ = take(m);

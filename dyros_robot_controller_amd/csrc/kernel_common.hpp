@@ -52,6 +52,7 @@ struct KParams {
   drc_solver_settings s;
   // persistent QP region
   int oP, oG, oQ, oAB, oL, oU, oD, oE, oRho, oX, oZ, oY, oDY, oXT, oZT, oT1, oT2, oRed, oSc;
+  int oDi, oEi;  // D^-1 and E^-1 beside the scaling (OSQP scaling.c keeps Dinv / Einv)
   int oBc;  // max(32, nx + ng) doubles: vectors broadcast through LDS (ADMM passes, polish KKT sweeps)
   // union region (kinematics | K^-1 | polish)
   int oU0;
@@ -69,7 +70,7 @@ struct KParams {
 
 // scalar slots in the oSc region
 enum { SC_C = 0, SC_RHO, SC_MAN, SC_DIST, SC_PAIR, SC_PRI, SC_DUA, SC_EPSP, SC_EPSD, SC_PRIS, SC_DUAS,
-       SC_NAX, SC_NZ, SC_NPX, SC_NATY, SC_NQ, SC_NF, SC_NR, SC_WIN, SC_PFAIL, SC_HIV, SC_HOW, SC_COUNT };
+       SC_NAX, SC_NZ, SC_NPX, SC_NATY, SC_NQ, SC_NF, SC_NR, SC_WIN, SC_PFAIL, SC_HIV, SC_HOW, SC_CINV, SC_COUNT };
 // Parity mode tries the certified polish at every termination check, but only
 // until this many attempts failed on a not-yet-converged iterate; after that
 // only at convergence (bounds the cost of slow or non-converging instances —

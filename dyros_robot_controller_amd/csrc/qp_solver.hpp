@@ -22,16 +22,16 @@ __device__ __forceinline__ void residuals(const KParams& kp, double* S, const do
   // UNSCALED = false (the polish's certification) skips the unscaled norms
   // that only adaptive rho reads (SC_PRIS .. SC_NQ keep the ADMM values)
   const int l = GL::lane(), nx = DNX, ng = DNG, np = DNP;
-  const double *P = S + kp.oP, *G = S + kp.oG, *q = S + kp.oQ, *ab = S + kp.oAB, *D = S + kp.oD, *E = S + kp.oE;
+  const double *P = S + kp.oP, *G = S + kp.oG, *q = S + kp.oQ, *ab = S + kp.oAB, *Di = S + kp.oDi, *Ei = S + kp.oEi;
   double pr = 0, prs = 0, nAx = 0, nz = 0, nAxs = 0, nzs = 0;
   double dr = 0, drs = 0, nPx = 0, nAty = 0, nq = 0, nPxs = 0, nAtys = 0, nqs = 0;
   if (l < nx) {  // bound row l and variable l
     const int lx = l < nx ? l : 0;
     double ax = PRE ? axb_pre : ab[lx] * x[lx], r = ax - z[lx];
     prs = fabs(r);
-    pr = fabs(r / E[lx]);
-    nAx = fabs(ax / E[lx]);
-    nz = fabs(z[lx] / E[lx]);
+    pr = fabs(r * Ei[lx]);
+    nAx = fabs(ax * Ei[lx]);
+    nz = fabs(z[lx] * Ei[lx]);
     nAxs = fabs(ax);
     nzs = fabs(z[lx]);
     double px = 0;
@@ -45,10 +45,10 @@ __device__ __forceinline__ void residuals(const KParams& kp, double* S, const do
     for (int i = 0; i < ng; ++i) aty += G[i * nx + lx] * y[nx + i];
     double rr = px + q[lx] + aty;
     drs = fabs(rr);
-    dr = fabs(rr / D[lx]);
-    nPx = fabs(px / D[lx]);
-    nAty = fabs(aty / D[lx]);
-    nq = fabs(q[lx] / D[lx]);
+    dr = fabs(rr * Di[lx]);
+    nPx = fabs(px * Di[lx]);
+    nAty = fabs(aty * Di[lx]);
+    nq = fabs(q[lx] * Di[lx]);
     nPxs = fabs(px);
     nAtys = fabs(aty);
     nqs = fabs(q[lx]);
@@ -65,9 +65,9 @@ __device__ __forceinline__ void residuals(const KParams& kp, double* S, const do
     int row = nx + lg;
     double r = ax - z[row];
     prs = fmax(prs, fabs(r));
-    pr = fmax(pr, fabs(r / E[row]));
-    nAx = fmax(nAx, fabs(ax / E[row]));
-    nz = fmax(nz, fabs(z[row] / E[row]));
+    pr = fmax(pr, fabs(r * Ei[row]));
+    nAx = fmax(nAx, fabs(ax * Ei[row]));
+    nz = fmax(nz, fabs(z[row] * Ei[row]));
     nAxs = fmax(nAxs, fabs(ax));
     nzs = fmax(nzs, fabs(z[row]));
   }
@@ -87,11 +87,11 @@ __device__ __forceinline__ void residuals(const KParams& kp, double* S, const do
     nAtys = GL::max(nAtys);
     nqs = GL::max(nqs);
   }
-  double c = S[kp.oSc + SC_C];
+  const double ci = S[kp.oSc + SC_CINV];
   if (l == 0) {
     double* sc = S + kp.oSc;
     sc[SC_PRI] = pr;
-    sc[SC_DUA] = dr / c;
+    sc[SC_DUA] = dr * ci;
     if constexpr (UNSCALED) {
       sc[SC_PRIS] = prs;
       sc[SC_DUAS] = drs;
@@ -102,8 +102,24 @@ __device__ __forceinline__ void residuals(const KParams& kp, double* S, const do
       sc[SC_NQ] = nqs;
     }
     sc[SC_EPSP] = eps_abs + eps_rel * fmax(nAx, nz);
-    sc[SC_EPSD] = eps_abs + eps_rel * fmax(fmax(nPx, nAty), nq) / c;
+    sc[SC_EPSD] = eps_abs + eps_rel * fmax(fmax(nPx, nAty), nq) * ci;
   }
+  wsync();
+}
+
+// OSQP keeps D^-1, E^-1 and c^-1 beside the Ruiz scaling (scaling.c) and its
+// residuals and tolerances multiply by them (vec_scaled_norm_inf): one division
+// per entry once per instance, none per residual evaluation.  The oracle's
+// qp_scale / qp_residuals do the same.
+template <class QD>
+__device__ __forceinline__ void scaling_inverses(const KParams& kp, double* S) {
+  using GL = Grp<QD::gs>;
+  const int l = GL::lane(), nx = DNX, m = DM;
+  const double *D = S + kp.oD, *E = S + kp.oE;
+  double *Di = S + kp.oDi, *Ei = S + kp.oEi;
+  for (int i = l; i < nx; i += GL::size) Di[i] = 1.0 / D[i];
+  for (int i = l; i < m; i += GL::size) Ei[i] = 1.0 / E[i];
+  if (l == 0) S[kp.oSc + SC_CINV] = 1.0 / S[kp.oSc + SC_C];
   wsync();
 }
 
@@ -334,7 +350,7 @@ __device__ __forceinline__ bool primal_infeasible(const KParams& kp, double* S, 
   if (l < nx) {
     double s = ab[l] * dy[l];
     for (int i = 0; i < ng; ++i) s += G[i * nx + l] * dy[nx + i];
-    viol = fabs(s / D[l]);
+    viol = fabs(s * S[kp.oDi + l]);
   }
   viol = GL::max(viol);
   return viol < eps * nrm;
@@ -1183,7 +1199,8 @@ __device__ DRC_POLISH_ATTR bool polish(const KParams& kp, double* S, bool strict
     residuals<QD, false, true>(kp, S, xx, zz, yy, kp.s.eps_exact, kp.s.eps_exact, axb, axg);
     PH_SINCE(43, rs_t0);
     PH_STAMP(pk_t0);
-    const double pr1 = sc[SC_PRI], dr1 = sc[SC_DUA], epsp = sc[SC_EPSP], epsd = sc[SC_EPSD], c = sc[SC_C];
+    const double pr1 = sc[SC_PRI], dr1 = sc[SC_DUA], epsp = sc[SC_EPSP], epsd = sc[SC_EPSD], ci = sc[SC_CINV];
+    const double* Ei = S + kp.oEi;
     bool ok = (pr1 < pr0 && dr1 < dr0) || (pr1 < pr0 && dr0 < 1e-10) || (dr1 < dr0 && pr0 < 1e-10);
     double wv = 0;
     int worst = 0x7fffffff;
@@ -1191,11 +1208,11 @@ __device__ DRC_POLISH_ATTR bool polish(const KParams& kp, double* S, bool strict
     if (strict) {
       ok = feasible && dr1 <= epsd;
       if (l < nx && actb != 0 && lo[l] != up[l]) {
-        double yi = E[l] * yy[l] / c, viol = actb < 0 ? yi - epsd : -yi - epsd;
+        double yi = E[l] * yy[l] * ci, viol = actb < 0 ? yi - epsd : -yi - epsd;
         if (viol > wv) { wv = viol; worst = l; }
       }
       if (l < ng && actg != 0 && lo[nx + l] != up[nx + l]) {
-        double yi = E[nx + l] * yy[nx + l] / c, viol = actg < 0 ? yi - epsd : -yi - epsd;
+        double yi = E[nx + l] * yy[nx + l] * ci, viol = actg < 0 ? yi - epsd : -yi - epsd;
         if (viol > wv) { wv = viol; worst = nx + l; }
       }
       GL::argmax(wv, worst);
@@ -1243,14 +1260,14 @@ __device__ DRC_POLISH_ATTR bool polish(const KParams& kp, double* S, bool strict
       int sb = 0, sg = 0, add = 0x7fffffff;
       double av = 0;
       if (l < nx && actb == 0) {
-        const double vlo = (lo[l] - axb) / E[l] - epsp, vhi = (axb - up[l]) / E[l] - epsp;
+        const double vlo = (lo[l] - axb) * Ei[l] - epsp, vhi = (axb - up[l]) * Ei[l] - epsp;
         if (vlo > 0 || vhi > 0) sb = vhi > vlo ? 1 : -1;
         if (vlo > av) { av = vlo; add = l * 4 + 0; }
         if (vhi > av) { av = vhi; add = l * 4 + 2; }
       }
       if (l < ng && actg == 0) {
         const int row = nx + l;
-        const double vlo = (lo[row] - axg) / E[row] - epsp, vhi = (axg - up[row]) / E[row] - epsp;
+        const double vlo = (lo[row] - axg) * Ei[row] - epsp, vhi = (axg - up[row]) * Ei[row] - epsp;
         if (vlo > 0 || vhi > 0) sg = vhi > vlo ? 1 : -1;
         if (vlo > av) { av = vlo; add = row * 4 + 0; }
         if (vhi > av) { av = vhi; add = row * 4 + 2; }
@@ -2262,6 +2279,7 @@ __device__ __forceinline__ void qp_instance(const DevModel* __restrict__ M0, con
   if constexpr (QD::reg && QD::gs == 64 && QD::nx + QD::ng <= 64) status = qp_scale_roles<QD>(kpl, S);
   else if constexpr (QD::reg) status = qp_scale_regs<QD>(kpl, S);
   else status = qp_scale<QD>(kp, S);
+  scaling_inverses<QD>(kp, S);
   PH(1);
   if (status != DRC_STATUS_NONFINITE) {
     if (lp_inf) status = DRC_STATUS_PRIMAL_INFEASIBLE;

@@ -169,6 +169,7 @@ qpid_kernel(const DevModel* __restrict__ M0, const KParams kp, const IO io) {
     qpid_assemble(M, kp, S, io, b);
     int status, iters = 0;
     status = qp_scale<QD>(kp, S);
+    scaling_inverses<QD>(kp, S);
     if (status != DRC_STATUS_NONFINITE) status = qp_admm<QD>(kp, kpl, S, &iters);
     // outputs: QP_ID.cpp:74-83 getOptJoint; failure -> qdd = 0, tau = gravity
     // (robot_controller.cpp:333-336; MoMa :208-213 slices the joint-order

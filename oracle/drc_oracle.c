@@ -1539,6 +1539,7 @@ typedef struct QPW {
     int n, m;
     double P[ORC_MAXX * ORC_MAXX], q[ORC_MAXX], A[ORC_MAXC * ORC_MAXX], l[ORC_MAXC], u[ORC_MAXC];
     double D[ORC_MAXX], E[ORC_MAXC], c;
+    double Dinv[ORC_MAXX], Einv[ORC_MAXC], cinv;  /* OSQP scaling.c keeps them; residuals multiply */
     double rho_vec[ORC_MAXC], rho;
     int ctype[ORC_MAXC];  /* -1 loose, 0 ineq, 1 eq */
     double L[ORC_MAXX * ORC_MAXX];
@@ -1607,6 +1608,9 @@ static void qp_scale(QPW* w, int iters) {
         w->l[i] *= w->E[i];
         w->u[i] *= w->E[i];
     }
+    for (int j = 0; j < n; ++j) w->Dinv[j] = 1.0 / w->D[j];
+    for (int i = 0; i < m; ++i) w->Einv[i] = 1.0 / w->E[i];
+    w->cinv = 1.0 / w->c;
 }
 
 /* residuals at the current iterate (scaled and unscaled) */
@@ -1619,9 +1623,9 @@ static void qp_residuals(const QPW* w, Res* o, const double* x, const double* z,
     for (int i = 0; i < m; ++i) {
         double r = Ax[i] - z[i];
         prs = fmax(prs, fabs(r));
-        pr = fmax(pr, fabs(r / w->E[i]));
-        nAx = fmax(nAx, fabs(Ax[i] / w->E[i]));
-        nz = fmax(nz, fabs(z[i] / w->E[i]));
+        pr = fmax(pr, fabs(r * w->Einv[i]));
+        nAx = fmax(nAx, fabs(Ax[i] * w->Einv[i]));
+        nz = fmax(nz, fabs(z[i] * w->Einv[i]));
         nAxs = fmax(nAxs, fabs(Ax[i]));
         nzs = fmax(nzs, fabs(z[i]));
     }
@@ -1629,21 +1633,21 @@ static void qp_residuals(const QPW* w, Res* o, const double* x, const double* z,
     for (int i = 0; i < n; ++i) {
         double r = Px[i] + w->q[i] + Aty[i];
         drs = fmax(drs, fabs(r));
-        dr = fmax(dr, fabs(r / w->D[i]));
-        nPx = fmax(nPx, fabs(Px[i] / w->D[i]));
-        nAty = fmax(nAty, fabs(Aty[i] / w->D[i]));
-        nq = fmax(nq, fabs(w->q[i] / w->D[i]));
+        dr = fmax(dr, fabs(r * w->Dinv[i]));
+        nPx = fmax(nPx, fabs(Px[i] * w->Dinv[i]));
+        nAty = fmax(nAty, fabs(Aty[i] * w->Dinv[i]));
+        nq = fmax(nq, fabs(w->q[i] * w->Dinv[i]));
         nPxs = fmax(nPxs, fabs(Px[i]));
         nAtys = fmax(nAtys, fabs(Aty[i]));
         nqs = fmax(nqs, fabs(w->q[i]));
     }
     o->pri_res = pr;
-    o->dua_res = dr / w->c;
+    o->dua_res = dr * w->cinv;
     o->pri_res_s = prs;
     o->dua_res_s = drs;
     o->nAx_s = nAxs; o->nz_s = nzs; o->nPx_s = nPxs; o->nAty_s = nAtys; o->nq_s = nqs;
     o->eps_pri = eps_abs + eps_rel * fmax(nAx, nz);
-    o->eps_dua = eps_abs + eps_rel * fmax(fmax(nPx, nAty), nq) / w->c;
+    o->eps_dua = eps_abs + eps_rel * fmax(fmax(nPx, nAty), nq) * w->cinv;
 }
 
 static int qp_primal_infeasible(QPW* w, double eps) {
@@ -1667,7 +1671,7 @@ static int qp_primal_infeasible(QPW* w, double eps) {
     for (int j = 0; j < n; ++j) {
         double s = 0;
         for (int i = 0; i < m; ++i) s += w->A[i * n + j] * dy[i];
-        if (fabs(s / w->D[j]) >= eps * nrm) return 0;
+        if (fabs(s * w->Dinv[j]) >= eps * nrm) return 0;
     }
     return 1;
 }
@@ -2047,7 +2051,7 @@ static int qp_polish_from(QPW* w, const OracleSettings* s, int strict, int* flag
             ok = feasible && tmp.dua_res <= tmp.eps_dua;
             for (int i = 0; i < m; ++i) {
                 if (!flag[i] || w->l[i] == w->u[i]) continue;
-                double yi = w->E[i] * yp[i] / w->c;
+                double yi = w->E[i] * yp[i] * w->cinv;
                 double viol = flag[i] < 0 ? yi - tmp.eps_dua : -yi - tmp.eps_dua;
                 if (viol > wv) { wv = viol; worst = i; }
             }
@@ -2106,7 +2110,7 @@ static int qp_polish_from(QPW* w, const OracleSettings* s, int strict, int* flag
             for (int i = 0; i < m; ++i) {
                 add[i] = 0;
                 if (flag[i]) continue;
-                double lo = (w->l[i] - ax[i]) / w->E[i] - tmp.eps_pri, hi = (ax[i] - w->u[i]) / w->E[i] - tmp.eps_pri;
+                double lo = (w->l[i] - ax[i]) * w->Einv[i] - tmp.eps_pri, hi = (ax[i] - w->u[i]) * w->Einv[i] - tmp.eps_pri;
                 if (lo > 0 || hi > 0) { add[i] = hi > lo ? 1 : -1; ++nadd; }
                 if (lo > av) { av = lo; best = i; bf = -1; }
                 if (hi > av) { av = hi; best = i; bf = 1; }
