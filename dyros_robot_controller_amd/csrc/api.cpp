@@ -1350,9 +1350,12 @@ int drc_default_qpik_params(const drc_model* m, int exact, drc_qpik_params* p) {
   s.eps_exact = 1e-9;
   s.eps_fallback = 1e-7;
   // exact mode: the ADMM iterate only seeds the certified polish's first
-  // active-set guess, so how often it is tried is a speed choice
-  // (DRC_EXACT_CHECK: A/B experiments)
-  static const int64_t exact_check = drc_amd::env_int("DRC_EXACT_CHECK", 25, 1);
+  // active-set guess, so how often it is tried is a speed choice.  With the
+  // projected-Jacobi guess the first polish pays off at iteration 20: +1-2.5 %
+  // on all five robots against 25 (profiles/r05h_envab_check20.jsonl; 15 helps
+  // UR5e and costs FR3, profiles/r05g_envab_check.jsonl).  The oracle's exact
+  // mode uses the same interval.  DRC_EXACT_CHECK overrides (A/B experiments)
+  static const int64_t exact_check = drc_amd::env_int("DRC_EXACT_CHECK", 20, 1);
   // OSQP's 3 refinement steps.  2 certify the same attempts at eps_exact
   // (tools/polish_census.py --refine; 1 fails half) and measured UR5e +1.1 %,
   // FR3 +0.1 % (profiles/r05b_envab.jsonl), but leave ~2e-9 in q-dot on some

@@ -2289,6 +2289,8 @@ void oracle_default_params(int kind, OracleParams* p, int exact) {
     s->polish_cap = kind == 0 ? 16 : 0;
     s->polish_add_all = 1;
     s->polish_guess = exact ? 2 : 0;
+    /* parity mode: the first polish at iteration 20 (kernel: drc_default_qpik_params) */
+    if (exact) s->check_termination = 20;
 }
 
 /* Farkas certificate for the whole-body QP (mobile_manipulator/QP_IK.cpp:
@@ -2507,6 +2509,7 @@ void oracle_default_qpid_params(int kind, OracleParams* p, int exact) {
     p->solver.polish_add_all = 0;           /* one row per step (kernel: problem 1)    */
     p->solver.polish_guess = 0;             /* OSQP's first guess (kernel: problem 1)  */
     p->solver.polish_refine_iter = 3;       /* OSQP's refinement count (kernel: QPID)  */
+    p->solver.check_termination = 25;       /* OSQP's check interval (kernel: QPID)    */
 }
 
 /* Manipulator::QPID (src/manipulator/QP_ID.cpp:7-193) and MobileManipulator::
