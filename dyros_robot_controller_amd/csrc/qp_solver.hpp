@@ -1036,10 +1036,25 @@ __device__ DRC_POLISH_ATTR bool polish(const KParams& kp, double* S, bool strict
   if (strict && kp.problem == 0 && np < nx) {
     const double *P = S + kp.oP, *qv = S + kp.oQ;
     lds_double* bc = (lds_double*)(S + kp.oBc);
-    const int lp = l < np ? l : 0;
-    double xv = x[lp], c = qv[lp];
+    const int lp = l < np ? l : 0, lx = l < nx ? l : 0;
+    // one pass over this lane's G column: the q-dot lanes' Jacobi constant
+    // c = q_l + sum_i g_il y_i (two partial sums) and the slack lanes' single
+    // row (gv, yr, cnt; used below)
+    double c0 = qv[lx], c1 = 0.0, gv = 0.0, yr = 0.0;
+    int cnt = 0;
 #pragma unroll
-    for (int i = 0; i < ng; ++i) c += G[i * nx + lp] * y[nx + i];
+    for (int i = 0; i < ng; ++i) {
+      const double g = G[i * nx + lx], yi = y[nx + i];
+      if (i & 1) c1 += g * yi;
+      else c0 += g * yi;
+      if (g != 0.0) {
+        gv = g;
+        yr = yi;
+        ++cnt;
+      }
+    }
+    const double c = c0 + c1;
+    double xv = x[lp];
     const double ipll = 1.0 / P[lp * np + lp], a = ab[lp], bl = lo[lp], bu = up[lp], xl = bl / a, xu = bu / a;
     int side = 0;
     for (int sw = 0; sw < kPolishJacobiSweeps; ++sw) {
@@ -1060,18 +1075,6 @@ __device__ DRC_POLISH_ATTR bool polish(const KParams& kp, double* S, bool strict
     // ADMM dual of row r, -(q_l + g_rl y_r) / ab_l, is below
     // -kPolishSlackTol |q_l| / ab_l (oracle: polish_guess_slack)
     if (l >= np && l < nx) {
-      const int lx = l < nx ? l : 0;
-      double gv = 0.0, yr = 0.0;
-      int cnt = 0;
-#pragma unroll
-      for (int i = 0; i < ng; ++i) {
-        const double g = G[i * nx + lx];
-        if (g != 0.0) {
-          gv = g;
-          yr = y[nx + i];
-          ++cnt;
-        }
-      }
       const double ql = qv[lx], a = ab[lx];
       if (cnt == 1 && ql != 0.0) {
         const double yb = -(ql + gv * yr) / a;

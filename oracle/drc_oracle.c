@@ -1879,10 +1879,13 @@ static void polish_guess_jacobi(const QPW* w, int* flag) {
     int n = w->n, m = w->m;
     double c[ORC_MAXX], xv[ORC_MAXX], xo[ORC_MAXX];
     int side[ORC_MAXX];
-    for (int j = 0; j < n; ++j) {
-        double s = w->q[j];
-        for (int i = n; i < m; ++i) s += w->A[i * n + j] * w->y[i];
-        c[j] = s;
+    for (int j = 0; j < n; ++j) {  /* two partial sums over the G rows, as the kernel */
+        double s0 = w->q[j], s1 = 0;
+        for (int i = n; i < m; ++i) {
+            if ((i - n) & 1) s1 += w->A[i * n + j] * w->y[i];
+            else s0 += w->A[i * n + j] * w->y[i];
+        }
+        c[j] = s0 + s1;
         xv[j] = w->x[j];
         side[j] = 0;
     }
