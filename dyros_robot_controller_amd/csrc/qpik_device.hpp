@@ -951,11 +951,14 @@ __device__ __forceinline__ void epa_grow_wave(EpaPoly* E, const SV& w, int best)
   int s = l;
   wave_argmin(key, s);
   int d = (own && l != s) ? 1 : 0, p = own ? (l == s ? s : nx) : l;
-#pragma unroll
-  for (int r = 0; r < 6; ++r) {
-    const int dp = __shfl(d, p, 64), pp = __shfl(p, p, 64);
-    d += dp;
-    p = pp;
+  // ceil(log2 H) rounds reach s from every edge of a cycle of H edges (a
+  // pointer at s stays there with d += 0, so more rounds change nothing); the
+  // pair (d, p) travels in one word: one crossbar shuffle per round
+  const int rounds = H > 1 ? 32 - __builtin_clz(H - 1) : 0;
+  for (int r = 0; r < rounds; ++r) {
+    const int dp = __shfl(d * 64 + p, p, 64);
+    d += dp >> 6;
+    p = dp & 63;
   }
   bad = __any(bad || (own && p != s));
   int slot = 0;

@@ -871,6 +871,8 @@ __device__ __forceinline__ void task_instance(const DevModel* __restrict__ M0, c
       atomicAdd(&g_phase_cycles[31], 1ull);
       atomicAdd(&g_phase_cycles[29], dt);
       for (int k_ = 0; k_ < 8; ++k_) atomicAdd(&g_phase_cycles[8 + k_], ph_acc[k_] - ph_snap[k_]);
+    }
+    if (epa_calls) {  // EPA census over every instance
       atomicAdd(&g_phase_cycles[22], epa_calls);
       atomicAdd(&g_phase_cycles[23], epa_steps);
       atomicMax(&g_phase_cycles[28], epa_maxsteps);

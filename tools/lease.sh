@@ -12,6 +12,7 @@
 #   bits:<lib>,<lib>           bit-for-bit comparison of two builds on all five robots (tools/lib_bits.py)
 #   phase:<robot>              DRC_PHASE_TIMING build's phase shares (tools/phase_timing.py)
 #   gpus2                      two-rank rehearsal on the one GPU (gloo), gpurun_out/gpus2_<tag>.json
+#   gpus:<n>[:<args>]          n-rank gloo rehearsal on the one GPU, extra bench.py args (commas become spaces)
 #   final[:<robot>,..]         round-end measurement (tools/final_round.sh)
 #   refcensus                  reference-settings census (tools/reference_census.py)
 set -o pipefail
@@ -75,6 +76,11 @@ for step in "$@"; do
       DRC_DIST_BACKEND=gloo timeout -k 10 300 python3 bench.py --gpus 2 --steps 5 --warmup 2 --no-cpu-baseline \
         > gpurun_out/gpus2_$TAG.json 2> gpurun_out/gpus2_$TAG.err || { tail -5 gpurun_out/gpus2_$TAG.err; exit 1; }
       grep -h '^{' gpurun_out/gpus2_$TAG.json | cut -c1-240 ;;
+    gpus)
+      IFS=: read -r n args <<< "$rest"
+      DRC_DIST_BACKEND=gloo timeout -k 10 600 python3 bench.py --gpus $n --steps 5 --warmup 2 --no-cpu-baseline ${args//,/ } \
+        > gpurun_out/gpus${n}_$TAG.json 2> gpurun_out/gpus${n}_$TAG.err || { tail -5 gpurun_out/gpus${n}_$TAG.err; exit 1; }
+      grep -h '^{' gpurun_out/gpus${n}_$TAG.json | cut -c1-300 ;;
     final)
       timeout -k 10 3000 bash tools/final_round.sh $TAG ${rest//,/ } || exit 1 ;;
     refcensus)
