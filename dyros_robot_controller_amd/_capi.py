@@ -38,7 +38,7 @@ EXPORTED_SYMBOLS = (
     "drc_model_info", "drc_model_limits", "drc_model_find_frame", "drc_model_mobile_fk_jacobian",
     "drc_mobile_fk_jacobian", "drc_mobile_ik_jacobian",
     "drc_default_qpik_params", "drc_qpik_batch", "drc_qpik_stages_batch", "drc_debug_kernel_timing", "drc_debug_lds_plan",
-    "drc_debug_host_timeline", "drc_debug_waves",
+    "drc_debug_host_timeline", "drc_debug_waves", "drc_debug_qpik_stamps",
     "drc_debug_kernel_times", "drc_set_concurrency", "drc_set_fusion", "drc_model_release_stream", "drc_debug_lane_stage", "drc_qpik_host", "drc_qpik_stages_host",
     "drc_dynamics_batch", "drc_dynamics_host", "drc_joint_torque_step_batch", "drc_joint_torque_step_host",
     "drc_default_qpid_params", "drc_qpid_batch", "drc_qpid_stages_batch", "drc_qpid_host",
@@ -145,6 +145,9 @@ def _load():
         lib.drc_debug_waves.argtypes = [vp, C.c_void_p, ip, ip]
     if hasattr(lib, "drc_debug_host_timeline"):
         lib.drc_debug_host_timeline.argtypes = [vp, C.c_int, C.POINTER(C.c_int64), C.c_int64, C.POINTER(C.c_int64)]
+    if hasattr(lib, "drc_debug_qpik_stamps"):
+        lib.drc_debug_qpik_stamps.argtypes = [vp, C.POINTER(QPIKParams), C.c_int64, dp, dp, dp, dp, dp, dp, dp, ip,
+                                              ip, C.POINTER(C.c_uint64)]
     if hasattr(lib, "drc_debug_lds_plan"):  # diagnostic; absent from older A/B builds (tools/ab_bench.sh)
         lib.drc_debug_lds_plan.argtypes = [vp, C.POINTER(QPIKParams), C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]
     lib.drc_debug_kernel_times.argtypes = [vp, dp, dp, dp, ip]
@@ -174,7 +177,8 @@ def _load():
     lib.drc_osf_batch.argtypes = [vp, C.POINTER(QPIKParams), C.c_int64, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     lib.drc_closed_form_host.argtypes = [vp, C.POINTER(QPIKParams), C.c_int, C.c_int64, dp, dp, dp, dp, dp, dp, dp, dp]
     for name in EXPORTED_SYMBOLS:
-        if name in ("drc_debug_lds_plan", "drc_debug_waves", "drc_debug_host_timeline") and not hasattr(lib, name):
+        if name in ("drc_debug_lds_plan", "drc_debug_waves", "drc_debug_host_timeline",
+                    "drc_debug_qpik_stamps") and not hasattr(lib, name):
             continue  # diagnostics an older A/B build may lack
         if name not in ("drc_model_destroy", "drc_error_string", "drc_last_error", "drc_build_id"):
             getattr(lib, name).restype = C.c_int

@@ -1664,7 +1664,7 @@ int drc_qpik_host_timed(drc_model* m, const drc_qpik_params* p, int64_t B, const
   for (int64_t b = 0; b < B; ++b) {
     auto at = [&](int k) { return st[static_cast<size_t>(k * B + b)]; };
     bool ok = at(0) != 0;
-    for (int k = 1; k < drc_amd::kStamps && ok; ++k) ok = at(k) >= at(k - 1);
+    for (int k = 1; k < drc_amd::kTimeStamps && ok; ++k) ok = at(k) >= at(k - 1);
     if (!ok) continue;
     auto dt = [&](int k1, int k0) { return static_cast<double>(at(k1) - at(k0)) * tick; };
     task += dt(drc_amd::ST_TASK1, drc_amd::ST_TASK0);
@@ -1687,6 +1687,19 @@ int drc_qpik_host_timed(drc_model* m, const drc_qpik_params* p, int64_t B, const
   // transfers, synchronisation): getSolution's place in the reference
   ts->solve_qp = store * inv + (wall - span * inv > 0 ? wall - span * inv : 0.0);
   return DRC_OK;
+}
+
+int drc_debug_qpik_stamps(drc_model* m, const drc_qpik_params* p, int64_t B, const double* q, const double* qdot,
+                          const double* xt, const double* xdt, const double* xi, const double* xdi, double* out,
+                          int32_t* status, int32_t* iters, uint64_t* stamps) {
+  if (!m) return drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "null model");
+  if (!out || !status || !stamps) return drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "qdot_out, status and stamps are required");
+  const int64_t n = m->hm.dev.nv, a = m->hm.dev.kind == 1 ? m->hm.dev.n_arm + m->hm.dev.n_wheel : n;
+  HostIO in{{q, qdot, xt, xdt, xi, xdi}, {n, n, 12, 6, 12, 6}};
+  double* outs[1] = {out};
+  const int64_t rows[1] = {a};
+  int32_t* iouts[2] = {status, iters};
+  return host_call(m, p, 0, B, in, outs, rows, 1, iouts, 2, stamps);
 }
 
 int drc_qpik_stages_host(drc_model* m, const drc_qpik_params* p, int64_t B, const double* q, const double* qdot,

@@ -44,6 +44,7 @@ fused_kernel(const DevModel* __restrict__ M0, const KParams kt, const KParams kq
     const int64_t b = seq.at(j);
     if (b >= B) continue;
     stage_stamp(io, ST_TASK0, io.b0 + b);
+    stage_where(io, ST_WTASK, io.b0 + b);
     task_instance<0>(M0, kt, iol, S, b);
     wsync();
     stage_stamp(io, ST_TASK1, io.b0 + b);

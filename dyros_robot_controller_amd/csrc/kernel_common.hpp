@@ -394,8 +394,9 @@ struct IO {
   // (drc_qpik_host_timed -> QP::TimeDuration, include/drc_amd.h)
   uint64_t* stamps;
 };
-constexpr int kStamps = 6;
-enum { ST_TASK0 = 0, ST_TASK1 = 1, ST_QP0 = 2, ST_ASM = 3, ST_SOLVED = 4, ST_OUT = 5 };
+// six clock stamps, then where the task and the QP stage ran (stage_where)
+constexpr int kTimeStamps = 6, kStamps = 8;
+enum { ST_TASK0 = 0, ST_TASK1 = 1, ST_QP0 = 2, ST_ASM = 3, ST_SOLVED = 4, ST_OUT = 5, ST_WTASK = 6, ST_WQP = 7 };
 // Stage stamp k of instance gb (wave-uniform branch; no stamp executes in a
 // call without io.stamps).  The wait keeps the clock read from returning out
 // of order with the LDS reads that follow (cdna_hip_programming.md).
@@ -408,6 +409,17 @@ __device__ __forceinline__ void stage_stamp(const IO& io, int k, int64_t gb) {
     const uint64_t t = __builtin_amdgcn_s_memrealtime();
     __builtin_amdgcn_s_waitcnt(0xC07F);
     if ((__lane_id() & (GS - 1)) == 0) io.stamps[k * io.ld + gb] = t;
+  }
+}
+// Where the stage of instance gb runs: workgroup index << 32 | __smid() (XCC,
+// SE, CU) << 2 | SIMD (HW_ID bits 5:4) -- drc_debug_qpik_stamps, the
+// small-batch makespan study (tools/stamp_study.py)
+template <int GS = 64>
+__device__ __forceinline__ void stage_where(const IO& io, int k, int64_t gb) {
+  if (io.stamps) {
+    const uint64_t w = (static_cast<uint64_t>(blockIdx.x) << 32) | (static_cast<uint64_t>(__smid()) << 2) |
+                       static_cast<uint64_t>(__builtin_amdgcn_s_getreg(GETREG_IMMED(1, 4, 4)));
+    if ((__lane_id() & (GS - 1)) == 0) io.stamps[k * io.ld + gb] = w;
   }
 }
 

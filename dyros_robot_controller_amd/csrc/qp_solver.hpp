@@ -1008,7 +1008,7 @@ __device__ __forceinline__ bool eqp(const KParams& kp, double* S, int actb, int 
 // wrong ADMM active-set guess continue with a primal active-set method
 // (Nocedal & Wright Alg. 16.3) from the first feasible polished point.  Same
 // decisions, in the same row order, as oracle/drc_oracle.c:qp_polish.
-constexpr int kPolishFeasAttempts = 4, kPolishAsIters = 24, kPolishJacobiSweeps = 3;
+constexpr int kPolishFeasAttempts = 5, kPolishAsIters = 24, kPolishJacobiSweeps = 3;
 constexpr double kPolishSlackTol = 0.3;
 template <class QD>
 __device__ DRC_POLISH_ATTR bool polish(const KParams& kp, double* S, bool strict) {
@@ -1281,8 +1281,17 @@ __device__ DRC_POLISH_ATTR bool polish(const KParams& kp, double* S, bool strict
         if (worst < nx) { if (l == worst) actb = 0; }
         else if (l == worst - nx) actg = 0;
       } else if (kp.problem == 0) {
+        // ... and the active row with the worst wrong-signed multiplier
+        // leaves in the same step (a wrong row of the first guess otherwise
+        // stays until the set is feasible; FR3 stragglers never got there in
+        // kPolishFeasAttempts and ran 60 ADMM iterations).  It is an active
+        // row, so never one just added
         if (sb) actb = sb;
         if (sg) actg = sg;
+        if (worst != 0x7fffffff) {
+          if (worst < nx) { if (l == worst) actb = 0; }
+          else if (l == worst - nx) actg = 0;
+        }
       } else {
         GL::argmax(av, add);
         const int row = add >> 2, sd = (add & 3) - 1;
@@ -2274,6 +2283,7 @@ __device__ __forceinline__ void qp_instance(const DevModel* __restrict__ M0, con
   const int64_t gb = io.b0 + b, LD = io.ld;  // position in the caller's [field][B] arrays
   const DevModel* M = opaque_model(M0);
   stage_stamp<QD::gs>(io, ST_QP0, gb);
+  stage_where<QD::gs>(io, ST_WQP, gb);
   qp_assemble<QD>(M, kp, S, io, b);
   stage_stamp<QD::gs>(io, ST_ASM, gb);
   PH(0);

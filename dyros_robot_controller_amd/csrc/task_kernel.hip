@@ -38,6 +38,7 @@ task_kernel(const DevModel* __restrict__ M0, const KParams kp, const IO io) {
     const int64_t b = hard_mode ? int64_t(io.hard_list[j]) : seq.at(j);
     if (b >= B) continue;
     if (PROBLEM == 0) stage_stamp(io, ST_TASK0, io.b0 + b);
+    if (PROBLEM == 0) stage_where(io, ST_WTASK, io.b0 + b);
     task_instance<PROBLEM>(M0, kp, io, S, b);
     if (PROBLEM == 0) stage_stamp(io, ST_TASK1, io.b0 + b);
   }

@@ -289,6 +289,16 @@ int drc_debug_kernel_times(drc_model* model, double* wall_ms, double* task_ms, d
  * LDS plan) and of the QP kernel.  Diagnostic (bench.py latency roof). */
 int drc_debug_waves(drc_model* model, const drc_qpik_params* params, int* task_waves, int* qp_waves);
 
+/* drc_qpik_host that also returns the kernels' per-instance stage stamps,
+ * stamps[8][B]: s_memrealtime ticks (100 MHz) at task start / end, QP start /
+ * assembled / solved / stored, then where the task and the QP stage ran
+ * (workgroup << 32 | CU id (XCC, SE, CU) << 2 | SIMD).  Diagnostic (the
+ * small-batch makespan study, tools/stamp_study.py); no reference counterpart. */
+int drc_debug_qpik_stamps(drc_model* model, const drc_qpik_params* params, int64_t B, const double* q,
+                          const double* qdot, const double* x_target, const double* xdot_target,
+                          const double* x_init, const double* xdot_init, double* qdot_out, int32_t* status,
+                          int32_t* iters, uint64_t* stamps);
+
 /* Concurrency of drc_qpik_batch: the batch is split into up to `chunks`
  * contiguous sub-batches (each >= 4096 instances, >= 16384 when there are 4)
  * that run concurrently: the last on the caller's stream, the others on

@@ -1750,7 +1750,7 @@ static int qp_eqp(const QPW* w, const OracleSettings* s, const int* flag, double
  * decisions as the kernel's kPolishMaxEarly) */
 #define POLISH_MAX_EARLY 4
 #define POLISH_MAX_TOTAL 12   /* then at convergence only the tight ADMM fallback */
-#define POLISH_FEAS_ATTEMPTS 4
+#define POLISH_FEAS_ATTEMPTS 5
 #define POLISH_AS_ITERS 24
 
 /* a working-set row with no weight on the free variables depends on the
@@ -2122,7 +2122,15 @@ static int qp_polish_from(QPW* w, const OracleSettings* s, int strict, int* flag
                 if (worst < 0) return 0;
                 flag[worst] = 0;
             } else if (s->polish_add_all) {
+                /* ... and the active row whose multiplier has the worst wrong
+                 * sign leaves in the same step: otherwise a wrong row of the
+                 * first guess stays until the set is feasible, and on some
+                 * instances never gets there in POLISH_FEAS_ATTEMPTS (FR3
+                 * bench stragglers: three failed polishes, 60 ADMM
+                 * iterations; tools/straggler_study.py).  Dropping every
+                 * wrong-signed row instead measured worse (more EQPs). */
                 for (int i = 0; i < m; ++i) if (add[i]) flag[i] = add[i];
+                if (worst >= 0) flag[worst] = 0;
             } else {
                 flag[best] = bf;
             }

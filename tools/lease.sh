@@ -15,6 +15,7 @@
 #   gpus:<n>[:<args>]          n-rank gloo rehearsal on the one GPU, extra bench.py args (commas become spaces)
 #   final[:<robot>,..]         round-end measurement (tools/final_round.sh)
 #   refcensus                  reference-settings census (tools/reference_census.py)
+#   stamps:<robot>:<batch>[:<fusion>[:<concurrency>]]  small-batch makespan study (tools/stamp_study.py)
 set -o pipefail
 ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 cd $ROOT
@@ -87,6 +88,12 @@ for step in "$@"; do
       timeout -k 10 600 python3 -u tools/reference_census.py > gpurun_out/refcensus_$TAG.log 2>&1 \
         || { tail -20 gpurun_out/refcensus_$TAG.log; exit 1; }
       cut -c1-400 gpurun_out/refcensus_$TAG.log ;;
+    stamps)
+      IFS=: read -r robot batch fz cc <<< "$rest"
+      timeout -k 10 300 python3 tools/stamp_study.py --robot $robot --batch $batch --fusion ${fz:--1} \
+        --concurrency ${cc:-0} >> gpurun_out/stamps_$TAG.jsonl 2> gpurun_out/stamps_$TAG.err \
+        || { tail -5 gpurun_out/stamps_$TAG.err; exit 1; }
+      tail -3 gpurun_out/stamps_$TAG.jsonl | cut -c1-1500 ;;
     *) echo "lease.sh: unknown step $step" >&2; exit 2 ;;
   esac
 done

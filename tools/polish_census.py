@@ -90,6 +90,7 @@ def main():
         row = {"tol": tol, "polish_calls": calls, "certified": ok, "eqp": v[2], "eqp_per_instance": v[2] / a.batch,
                "add_steps": v[3], "drop_steps": v[4], "ratio_blocks": v[5], "certified_on_first_eqp": v[6],
                "eqp_hist": v[8:16], "non_solved": int(np.sum(status != 1)), "iters_mean": float(iters.mean()),
+               "iters_hist": {int(k): int(c) for k, c in zip(*np.unique(iters, return_counts=True))},
                "seconds": dt, "rules": {}}
         for r, name in enumerate(RULES):
             row["rules"][name] = {"match": v[16 + r], "false_neg": v[32 + r], "false_pos": v[48 + r]}
