@@ -1008,7 +1008,7 @@ __device__ __forceinline__ bool eqp(const KParams& kp, double* S, int actb, int 
 // wrong ADMM active-set guess continue with a primal active-set method
 // (Nocedal & Wright Alg. 16.3) from the first feasible polished point.  Same
 // decisions, in the same row order, as oracle/drc_oracle.c:qp_polish.
-constexpr int kPolishFeasAttempts = 5, kPolishAsIters = 24, kPolishJacobiSweeps = 3;
+constexpr int kPolishFeasAttempts = 6, kPolishAsIters = 24, kPolishJacobiSweeps = 3;
 constexpr double kPolishSlackTol = 0.3;
 template <class QD>
 __device__ DRC_POLISH_ATTR bool polish(const KParams& kp, double* S, bool strict) {
@@ -1087,7 +1087,9 @@ __device__ DRC_POLISH_ATTR bool polish(const KParams& kp, double* S, bool strict
   // same polish runs once more from OSQP's guess (oracle: qp_polish): a guess
   // whose ADMM duals settle slowly can fail at every check, and a UR5e bench
   // instance then ran 1 400 ADMM iterations instead of one extra attempt
-  const bool alt = GL::any(actb != ob || actg != og);
+  // (QPIK: the retry also differs in the infeasible phase's drop rule, below,
+  // so it runs whenever the first pass fails)
+  const bool alt = strict && (kp.problem == 0 || GL::any(actb != ob || actg != og));
   double* U = S + kp.oU0;
   double* xx = U + 64;       // [nx]
   double* yy = U + 128;      // [m] (<= 128)
@@ -1281,14 +1283,16 @@ __device__ DRC_POLISH_ATTR bool polish(const KParams& kp, double* S, bool strict
         if (worst < nx) { if (l == worst) actb = 0; }
         else if (l == worst - nx) actg = 0;
       } else if (kp.problem == 0) {
-        // ... and the active row with the worst wrong-signed multiplier
-        // leaves in the same step (a wrong row of the first guess otherwise
-        // stays until the set is feasible; FR3 stragglers never got there in
-        // kPolishFeasAttempts and ran 60 ADMM iterations).  It is an active
-        // row, so never one just added
+        // ... and, in the first pass, the active row with the worst
+        // wrong-signed multiplier leaves in the same step (a wrong row of the
+        // first guess otherwise stays until the set is feasible; FR3
+        // stragglers never got there and ran 60 ADMM iterations).  The retry
+        // pass adds only: an infeasible EQP's multipliers can also point at a
+        // right row (oracle: qp_polish_from).  It is an active row, so never
+        // one just added
         if (sb) actb = sb;
         if (sg) actg = sg;
-        if (worst != 0x7fffffff) {
+        if (pass == 0 && worst != 0x7fffffff) {
           if (worst < nx) { if (l == worst) actb = 0; }
           else if (l == worst - nx) actg = 0;
         }

@@ -1750,7 +1750,7 @@ static int qp_eqp(const QPW* w, const OracleSettings* s, const int* flag, double
  * decisions as the kernel's kPolishMaxEarly) */
 #define POLISH_MAX_EARLY 4
 #define POLISH_MAX_TOTAL 12   /* then at convergence only the tight ADMM fallback */
-#define POLISH_FEAS_ATTEMPTS 5
+#define POLISH_FEAS_ATTEMPTS 6
 #define POLISH_AS_ITERS 24
 
 /* a working-set row with no weight on the free variables depends on the
@@ -1788,6 +1788,12 @@ void oracle_polish_census_rows(long long* out, int reset) {
 }
 static int g_pc_on = 0, g_pc_guess = -1;
 void oracle_polish_guess(int rule) { g_pc_guess = rule; }
+/* study switches of the infeasible phase (tools/polish_census.py --feas-drop / --feas-att):
+ * mode 0 no drop, 1 drop the worst wrong-signed row in both passes, 4 only in the
+ * retry pass, 5 only in the first pass (the product rule); attempts before the
+ * phase gives up (POLISH_FEAS_ATTEMPTS) */
+static int g_feas_drop = 5, g_feas_att = POLISH_FEAS_ATTEMPTS;
+void oracle_polish_feas(int mode, int attempts) { g_feas_drop = mode; g_feas_att = attempts; }
 static double g_pc_tol[PC_RULES];
 void oracle_polish_census(int on, const double* tol, long long* out, int reset) {
     if (out) for (int i = 0; i < PC_N; ++i) out[i] = __atomic_load_n(&g_pc[i], __ATOMIC_RELAXED);
@@ -2006,12 +2012,12 @@ static void polish_guess_slack(const QPW* w, int* flag) {
 static __thread int pcg[PC_RULES][ORC_MAXC];
 /* the polish from one first guess of the active set (flag, modified) */
 static int qp_polish_from(QPW* w, const OracleSettings* s, int strict, int* flag, double pr0, double dr0,
-                          int census) {
+                          int census, int drop) {
     int n = w->n, m = w->m;
     Res tmp;
     double xp[ORC_MAXX], yp[ORC_MAXC], zp[ORC_MAXC], ax[ORC_MAXC], xc[ORC_MAXX];
     int have_feasible = 0, neqp = 0;
-    for (int it = 0; it < (strict ? POLISH_FEAS_ATTEMPTS + POLISH_AS_ITERS : 1); ++it) {
+    for (int it = 0; it < (strict ? g_feas_att + POLISH_AS_ITERS : 1); ++it) {
         polish_drop_fixed_rows(w, flag);
         ++neqp;
         if (census) pc_add(PC_EQP, 1);
@@ -2104,7 +2110,7 @@ static int qp_polish_from(QPW* w, const OracleSettings* s, int strict, int* flag
             memcpy(xc, xp, n * sizeof(double));
         } else {
             if (census) pc_add(PC_ADD, 1);
-            if (it >= POLISH_FEAS_ATTEMPTS - 1) return 0;
+            if (it >= g_feas_att - 1) return 0;
             /* not yet feasible: add every violated inactive row at its
              * violated side (QPIK: the ADMM guess typically misses a
              * couple), or only the most violated one (QPID) */
@@ -2122,15 +2128,18 @@ static int qp_polish_from(QPW* w, const OracleSettings* s, int strict, int* flag
                 if (worst < 0) return 0;
                 flag[worst] = 0;
             } else if (s->polish_add_all) {
-                /* ... and the active row whose multiplier has the worst wrong
-                 * sign leaves in the same step: otherwise a wrong row of the
-                 * first guess stays until the set is feasible, and on some
-                 * instances never gets there in POLISH_FEAS_ATTEMPTS (FR3
-                 * bench stragglers: three failed polishes, 60 ADMM
-                 * iterations; tools/straggler_study.py).  Dropping every
-                 * wrong-signed row instead measured worse (more EQPs). */
+                /* ... and, in the first pass, the active row whose multiplier
+                 * has the worst wrong sign leaves in the same step: otherwise
+                 * a wrong row of the first guess stays until the set is
+                 * feasible, and on some instances never gets there (FR3 bench
+                 * stragglers: three failed polishes, 60 ADMM iterations;
+                 * tools/straggler_study.py).  The multipliers of an
+                 * infeasible EQP can also point at a right row (a Husky-FR3
+                 * instance then cycled to 300 iterations), so the retry pass
+                 * from OSQP's guess adds only.  Dropping every wrong-signed
+                 * row measured worse (more EQPs); census in DESIGN.md. */
                 for (int i = 0; i < m; ++i) if (add[i]) flag[i] = add[i];
-                if (worst >= 0) flag[worst] = 0;
+                if (drop && worst >= 0) flag[worst] = 0;
             } else {
                 flag[best] = bf;
             }
@@ -2163,10 +2172,13 @@ static int qp_polish(QPW* w, const OracleSettings* s, int strict) {
         pc_add(PC_CALLS, 1);
         for (int r = 0; r < PC_RULES; ++r) pc_guess(w, r, pcg[r]);
     }
-    if (qp_polish_from(w, s, strict, flag, pr0, dr0, census)) return 1;
-    if (!strict || !differs) return 0;
+    const int d0 = g_feas_drop == 1 || g_feas_drop == 5, d1 = g_feas_drop == 1 || g_feas_drop == 4;
+    if (qp_polish_from(w, s, strict, flag, pr0, dr0, census, d0)) return 1;
+    /* (QPIK: the retry runs whenever the first pass fails -- it also differs
+     * in the drop rule; QPID only from a different guess) */
+    if (!strict || (!differs && !(s->polish_add_all && d0 != d1))) return 0;
     if (census) pc_add(PC_RETRY, 1);
-    return qp_polish_from(w, s, strict, osqp, pr0, dr0, census);
+    return qp_polish_from(w, s, strict, osqp, pr0, dr0, census, d1);
 }
 
 /* the last termination check's max(pri_res / eps_pri, dua_res / eps_dua) of

@@ -10,7 +10,7 @@
 #   ab:<lib>,<lib>:<robot>,<robot>[:reps]   library A/B (tools/ab_bench.sh)
 #   env:<E=V+E2=V>,base:<robot>,..[:reps]   environment A/B (tools/env_ab.sh; '+' joins variables)
 #   bits:<lib>,<lib>           bit-for-bit comparison of two builds on all five robots (tools/lib_bits.py)
-#   phase:<robot>              DRC_PHASE_TIMING build's phase shares (tools/phase_timing.py)
+#   phase:<robot>[,<batch>]    DRC_PHASE_TIMING build's phase shares (tools/phase_timing.py)
 #   gpus2                      two-rank rehearsal on the one GPU (gloo), gpurun_out/gpus2_<tag>.json
 #   gpus:<n>[:<args>]          n-rank gloo rehearsal on the one GPU, extra bench.py args (commas become spaces)
 #   final[:<robot>,..]         round-end measurement (tools/final_round.sh)
@@ -71,8 +71,8 @@ for step in "$@"; do
       python3 tools/lib_bits.py --compare ${TAG}_a ${TAG}_b >> gpurun_out/bits_$TAG.log 2>&1
       tail -6 gpurun_out/bits_$TAG.log ;;
     phase)
-      timeout -k 10 300 python3 tools/phase_timing.py $rest > gpurun_out/phase_${TAG}_$rest.txt 2>&1 || exit 1
-      cat gpurun_out/phase_${TAG}_$rest.txt ;;
+      timeout -k 10 300 python3 tools/phase_timing.py ${rest//,/ } > gpurun_out/phase_${TAG}_${rest//,/_}.txt 2>&1 || exit 1
+      cat gpurun_out/phase_${TAG}_${rest//,/_}.txt ;;
     gpus2)
       DRC_DIST_BACKEND=gloo timeout -k 10 300 python3 bench.py --gpus 2 --steps 5 --warmup 2 --no-cpu-baseline \
         > gpurun_out/gpus2_$TAG.json 2> gpurun_out/gpus2_$TAG.err || { tail -5 gpurun_out/gpus2_$TAG.err; exit 1; }

@@ -32,7 +32,7 @@ for n, x in zip(names_q, tq): print("  %-16s %6.1f%%  %8.0f cyc/inst" % (n, 100 
 names_a = ["set_rho+factor", "prep+load regs", "admm iterations (+publish)", "admm_check (residuals/polish/refactor)"]
 print("inside rho+factor+admm+checks:")
 for n, x in zip(names_a, ta): print("  %-40s %8.0f cyc/inst" % (n, x / B))
-print("task stragglers: max instance %.0f cycles, %d instances > 2M cycles (%.1f%% of task cycles)" % (v[30], v[31], 100 * v[29] / max(tt.sum(), 1)))
+print("task stragglers: max instance %.0f cycles, %d instances > 400k cycles (%.1f%% of task cycles)" % (v[30], v[31], 100 * v[29] / max(tt.sum(), 1)))
 print("straggler phase split: " + ", ".join("%s %.0f%%" % (n, 100 * x / max(v[8:16].sum(), 1)) for n, x in zip(names_t, v[8:16])))
 print("EPA (all instances): %d calls, %d steps, max %d steps in one call" % (v[22], v[23], v[28]))
 print("EPA step split: scan+support+tests %.0f, grow %.0f cycles/step" % (v[18] / max(v[23], 1), v[20] / max(v[23], 1)))

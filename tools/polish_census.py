@@ -73,6 +73,9 @@ def main():
     ap.add_argument("--tol", type=float, nargs="*", default=[1e-6, 1e-4, 1e-3, 1e-2])
     ap.add_argument("--guess", type=int, default=-1, help="first-guess rule of the polish (-1: OSQP's)")
     ap.add_argument("--check", type=int, default=0, help="check_termination (0: the default 25)")
+    ap.add_argument("--feas-drop", type=int, default=1, help="study: infeasible-phase drop mode (oracle_polish_feas)")
+    ap.add_argument("--feas-att", type=int, default=5, help="study: infeasible-phase attempts")
+    ap.add_argument("--npz", help="inputs from a device dump (tools/dump_batch.py) instead of the CPU generator")
     ap.add_argument("--refine", type=int, default=-1, help="polish_refine_iter (-1: the default 3)")
     a = ap.parse_args()
     _, om, spec = O.load(a.robot)
@@ -81,8 +84,14 @@ def main():
         par.solver.check_termination = a.check
     if a.refine >= 0:
         par.solver.polish_refine_iter = a.refine
-    inputs = workload(om, a.robot, a.batch, a.seed)
+    if a.npz:
+        d = np.load(a.npz)
+        inputs = tuple(np.ascontiguousarray(d[k]) for k in ("q", "qd", "xt", "xdt"))
+        a.batch = inputs[0].shape[1]
+    else:
+        inputs = workload(om, a.robot, a.batch, a.seed)
     O.lib().oracle_polish_guess(C.c_int(a.guess))
+    O.lib().oracle_polish_feas(C.c_int(a.feas_drop), C.c_int(a.feas_att))
     res = {"robot": a.robot, "batch": a.batch, "seed": a.seed, "by_tol": []}
     for tol in a.tol:
         v, status, iters, dt = census(om, par, inputs, [tol] * 16, a.threads)

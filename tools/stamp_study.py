@@ -82,7 +82,7 @@ def analyse(stamps, st, it, slots):
         "waves_used": len(chain), "simds_used": int(len(np.unique(simd))),
         "latest_wave": {"instances": busiest[1][1], "busy_us": round(busiest[1][0], 2),
                         "first_us": round(busiest[1][2], 2), "last_us": round(busiest[1][3], 2)},
-        "slowest_instances": [{"task_us": round(float(task[k]), 2), "qp_us": round(float(qp[k]), 2),
+        "slowest_instances": [{"b": int(np.nonzero(ok)[0][k]), "task_us": round(float(task[k]), 2), "qp_us": round(float(qp[k]), 2),
                                "start_us": round(float(s[0][k]), 2), "iters": int(it[ok][k]),
                                "status": int(st[ok][k])} for k in order],
         "iters": {"mean": round(float(it[ok].mean()), 2), "max": int(it[ok].max())},
@@ -122,6 +122,12 @@ def main():
     fused = a.fusion == 1 or (a.fusion < 0 and a.batch <= 8192 and a.robot != "caster_fr3")
     slots = {"task_waves_per_simd": wt.value, "qp_waves_per_simd": wq.value, "fused": fused}
     r = analyse(stamps, st, it, slots)
+    # the slowest instances' inputs and outputs, for the oracle on the CPU
+    slow = [row["b"] for row in r["slowest_instances"]] + [int(b) for b in np.nonzero(it > 40)[0][:16]]
+    slow = sorted(set(slow))
+    np.savez(os.path.join(ROOT, "gpurun_out", "stamps_slow_%s_%d.npz" % (a.robot, a.batch)), b=np.array(slow),
+             q=sub[0][:, slow], qd=sub[1][:, slow], xt=sub[2][:, slow], xdt=sub[3][:, slow], iters=it[slow],
+             status=st[slow])
     r.update(robot=a.robot, batch=a.batch, fusion=a.fusion, concurrency=a.concurrency)
     print(json.dumps(r), flush=True)
     # isolated instances: B = 1 calls through the two-kernel pipeline and the fused kernel

@@ -40,9 +40,18 @@ def main():
     ap.add_argument("--seed", type=int, default=12345)
     ap.add_argument("--top", type=int, default=8)
     ap.add_argument("--threads", type=int, default=8)
+    ap.add_argument("--npz", help="instances dumped by tools/stamp_study.py (the device's inputs and iterations)")
     a = ap.parse_args()
     _, om, spec = O.load(a.robot)
     par = O.default_params(spec["kind"], exact=True)
+    if a.npz:
+        d = np.load(a.npz)
+        inputs = [np.ascontiguousarray(d[k]) for k in ("q", "qd", "xt", "xdt")]
+        for k, b in enumerate(d["b"]):
+            r = one(O, om, par, inputs, k)
+            r.update(b=int(b), device_iters=int(d["iters"][k]), device_status=int(d["status"][k]))
+            print(json.dumps(r))
+        return
     inputs = workload(om, a.robot, a.batch, a.seed)
     _, st, it = O.qpik_batch(om, par, *inputs, nthreads=a.threads)
     vals, cnt = np.unique(it, return_counts=True)
