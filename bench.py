@@ -559,8 +559,29 @@ def extras(torch, args, rd, mod, robot, link, q, qd, xt, xdt, dq, dqd, dxt, dxdt
     tw, tk, tq, nc = C.c_double(), C.c_double(), C.c_double(), C.c_int()
     _capi.check(lib.drc_debug_kernel_times(h, C.byref(tw), C.byref(tk), C.byref(tq), C.byref(nc)))
     _capi.check(lib.drc_debug_kernel_timing(h, 0))
+    # task / QP latency (seconds) from the kernels' own per-instance stamps
+    # (drc_debug_qpik_stamps: task start -> end, QP start -> stored); HIP events
+    # between two back-to-back kernels on one stream put most of the QP
+    # kernel's time into the task kernel's on this stack (r05 stamp study)
+    from dyros_robot_controller_amd import manipulator as _man
+    p1 = _man.QPIKParamsBuilder(rd.model, exact=(args.solver == "exact")).params(link, _capi.MODE_QPIK_STEP)
+    dpp = lambda a: a.ctypes.data_as(C.POINTER(C.c_double))
+    ipp = lambda a: a.ctypes.data_as(C.POINTER(C.c_int))
+    nout = rd.model.actuated_dof
+    lts, lqs = [], []
+    for one in ones:
+        cols = [np.ascontiguousarray(t.cpu().numpy()) for t in one]
+        o1, s1, i1 = np.zeros((nout, 1)), np.zeros(1, np.int32), np.zeros(1, np.int32)
+        stp = np.zeros((8, 1), np.uint64)
+        for _ in range(2):
+            _capi.check(lib.drc_debug_qpik_stamps(h, C.byref(p1), C.c_int64(1), dpp(cols[0]), dpp(cols[1]),
+                                                  dpp(cols[2]), dpp(cols[3]), dpp(cols[2]), dpp(cols[3]), dpp(o1),
+                                                  ipp(s1), ipp(i1), stp.ctypes.data_as(C.POINTER(C.c_uint64))))
+        t = stp[:6, 0].astype(np.int64)
+        lts.append((t[1] - t[0]) * 1e-8)
+        lqs.append((t[5] - t[2]) * 1e-8)
     _capi.check(lib.drc_set_fusion(h, C.c_int(1)))
-    lt, lq = tk.value / max(nc.value, 1) * 1e-3, tq.value / max(nc.value, 1) * 1e-3   # task / QP latency, seconds
+    lt, lq = float(np.mean(lts)), float(np.mean(lqs))
     # waves per CU of each kernel as the call launches it: the register build's
     # waves per SIMD (drc_debug_waves) x 4, capped by the LDS plan (drc_debug_lds_plan)
     from dyros_robot_controller_amd import manipulator
@@ -579,7 +600,8 @@ def extras(torch, args, rd, mod, robot, link, q, qd, xt, xdt, dq, dqd, dxt, dxdt
         "solves_per_s": roof, "frac": line["value"] / roof,
         "note": "design-relative, not a hardware limit (the hardware roof is valu_issue_roof): task and QP kernel "
                 "latency of one instance alone on the GPU (mean over the batch's first 32 instances, B = 1 calls "
-                "through the two-kernel pipeline, HIP events); with the waves per CU each kernel is launched at (register build x 4 SIMDs, capped "
+                "through the two-kernel pipeline, the kernels' own stage stamps; call_us from HIP events); with the "
+                "waves per CU each kernel is launched at (register build x 4 SIMDs, capped "
                 "by its LDS plan), 256 CUs complete 256 / (t_task / w_task + t_qp / w_qp) instances per second "
                 "if every wave slot stays busy at the isolated latency"}
 

@@ -510,8 +510,8 @@ DRC_HD __forceinline__ int closest_any(SV2 (&S)[4], int n, V3* v, double (&lam)[
 // Support-gap stop tolerances (metres; oracle: GJK_TOL / EPA_TOL).  The
 // winning pair's witnesses are refined to the exact critical point afterwards
 // (refine_witness, D17), so GJK / EPA only decide the argmin and the basin:
-// EPA stops at hpp-fcl's default epa_tolerance, GJK at 1e-9.
-constexpr double kGjkTol = 1e-9, kEpaTol = 1e-6;
+// both stop at hpp-fcl's GJKSolver defaults (gjk_tolerance, epa_tolerance)
+constexpr double kGjkTol = 1e-6, kEpaTol = 1e-6;
 
 // GJK on the cores (same iteration, tolerances and duplicate test as
 // oracle/drc_oracle.c:gjk).  The simplex stays in registers.  ANY: the
@@ -588,6 +588,11 @@ DRC_HD __forceinline__ void gjk_run(const SH& A, const SH& B, GjkState& g, doubl
   g.n = n;
   g.v = v;
 }
+// EPA seed stash (epa_stash, below): the task stage's GJK of a pair that
+// turns out to intersect leaves its final simplex for EPA, which would
+// otherwise rerun the same GJK on one lane
+struct EpaPoly;
+DRC_HD void epa_stash(EpaPoly* E, const GjkState& g, int pair);
 // separation distance and witnesses (valid when !intersect)
 struct GjkDist {
   int intersect, pruned;
@@ -595,9 +600,11 @@ struct GjkDist {
   V3 pA, pB;
 };
 template <class SH>
-DRC_HD inline __noinline__ GjkDist gjk(const SH A, const SH B, double cut = 1e300) {
+DRC_HD inline __noinline__ GjkDist gjk(const SH A, const SH B, double cut = 1e300, EpaPoly* stash = nullptr,
+                                       int pair = 0) {
   GjkState g;
   gjk_run(A, B, g, cut);
+  if (stash && g.intersect) epa_stash(stash, g, pair);
   GjkDist o;
   o.intersect = g.intersect;
   o.pruned = g.pruned;
@@ -657,6 +664,24 @@ DRC_HD __forceinline__ void epa_addv(EpaPoly* E, V3 w, V3 a) {
   st3(E->va[E->nv], a);
   E->nv++;
 }
+// Seed stash: kEpaStash simplices of intersecting pairs in the vertex slots
+// kEpaStashV0.. (only a polytope grown past kEpaStashV0 vertices reaches
+// them), their pair and size in out[] (written only by epa_finish).  The
+// slot comes from an LDS counter in E->nv, zeroed before the candidate GJKs.
+// The GJK of a pair that intersects never took its cut exit, so its final
+// simplex is exactly the one epa_init's rerun would build (same iterations).
+constexpr int kEpaStash = 2, kEpaStashV0 = kEpaMaxV - 4 * kEpaStash;
+DRC_HD __forceinline__ void epa_stash(EpaPoly* E, const GjkState& g, int pair) {
+  const int k = __atomic_fetch_add(&E->nv, 1, __ATOMIC_RELAXED);
+  if (k >= kEpaStash) return;
+  for (int i = 0; i < 4; ++i)
+    if (i < g.n) {
+      st3(E->vw[kEpaStashV0 + 4 * k + i], g.S[i].w);
+      st3(E->va[kEpaStashV0 + 4 * k + i], g.S[i].a);
+    }
+  E->out[2 * k] = pair;
+  E->out[2 * k + 1] = g.n;
+}
 // "face f sees w": the oracle's visibility test (not (n.w - d < -1e-12))
 DRC_HD __forceinline__ bool epa_sees(const EpaPoly* E, int f, V3 w) {
   return !(dot(ld3(E->fn[f]), w) - E->fd[f] < -1e-12);
@@ -702,16 +727,34 @@ DRC_HD __forceinline__ void epa_bind(EpaPoly* E, int f0, int e0, int f1, int e1)
 }
 // rerun GJK and build the initial tetrahedron from its final simplex
 // (lane-serial)
+// (epa_seed: the vertices E->vw / va [0, nv) are GJK's simplex)
+template <class SH>
+DRC_HD __forceinline__ void epa_seed(const SH A, const SH B, EpaPoly* E);
 template <class SH>
 DRC_HD __forceinline__ void epa_init(const SH A, const SH B, EpaPoly* E) {
   GjkState g;
   gjk_run(A, B, g);
   E->nv = 0;
+  for (int i = 0; i < 4; ++i)
+    if (i < g.n) epa_addv(E, g.S[i].w, g.S[i].a);
+  epa_seed(A, B, E);
+}
+// the same from stash slot k (epa_stash)
+template <class SH>
+DRC_HD __forceinline__ void epa_init_stash(const SH A, const SH B, EpaPoly* E, int k, int n) {
+  for (int i = 0; i < 4; ++i)
+    if (i < n) {
+      st3(E->vw[i], epa_vw(E, kEpaStashV0 + 4 * k + i));
+      st3(E->va[i], epa_va(E, kEpaStashV0 + 4 * k + i));
+    }
+  E->nv = n;
+  epa_seed(A, B, E);
+}
+template <class SH>
+DRC_HD __forceinline__ void epa_seed(const SH A, const SH B, EpaPoly* E) {
   E->nf = 0;
   E->fail = 0;
   E->nfree = 0;
-  for (int i = 0; i < 4; ++i)
-    if (i < g.n) epa_addv(E, g.S[i].w, g.S[i].a);
   for (int di = 0; di < 6 && E->nv < 4; ++di) {
     const double sgn = di < 3 ? 1.0 : -1.0;
     const int ax = di % 3;
@@ -868,8 +911,18 @@ DRC_HD __forceinline__ double epa_finish(EpaPoly* E, int best) {
 // Wave form of epa_grow_canon (the task kernel; every lane calls it with the
 // same w and best).  Lane l owns faces l and l + 64 and, after compaction,
 // horizon edge l.  Same slots, adjacency, face data, free list and decisions.
-__device__ __forceinline__ void epa_grow_wave(EpaPoly* E, const SV& w, int best) {
+__device__ __forceinline__ void epa_grow_wave(EpaPoly* E, const SV& w, int best, unsigned long long* gt = nullptr) {
   const int l = threadIdx.x & 63;
+  // (timing builds: gt[0..3] += cycles in visibility + component, horizon +
+  // cycle check, cycle order + new planes, writes)
+  unsigned long long tg = gt ? __builtin_amdgcn_s_memtime() : 0;
+  auto lap = [&](int k) {
+    if (gt) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      gt[k] += t - tg;
+      tg = t;
+    }
+  };
   const int nf = E->nf, wi = E->nv, nfree = E->nfree;
   if (l == 0) {
     st3(E->vw[wi], w.w);
@@ -901,6 +954,7 @@ __device__ __forceinline__ void epa_grow_wave(EpaPoly* E, const SV& w, int best)
     clo = nlo;
     chi = nhi;
   }
+  lap(0);
   // horizon edges (c, e), compacted in (edge slot j, lane) order
   const bool c0 = in(clo, chi, f0), c1 = in(clo, chi, f1);
   bool hz[6];
@@ -946,6 +1000,7 @@ __device__ __forceinline__ void epa_grow_wave(EpaPoly* E, const SV& w, int best)
     bad = E->vout[a] != l || E->vin[b] != l || nx < 0 || pv < 0;
   }
   bad = __any(bad);
+  lap(1);
   // cycle position relative to the edge of smallest key (pointer jumping)
   double key = own ? double(3 * hc + he_) : 1e300;
   int s = l;
@@ -975,6 +1030,7 @@ __device__ __forceinline__ void epa_grow_wave(EpaPoly* E, const SV& w, int best)
     wsync();
     return;
   }
+  lap(2);
   const int snx = __shfl(slot, nx, 64), spv = __shfl(slot, pv, 64);
   const int g = own ? E->adj[hc][he_] : 0;
   // C's faces, ascending, then best: positions in the new free list
@@ -1009,6 +1065,7 @@ __device__ __forceinline__ void epa_grow_wave(EpaPoly* E, const SV& w, int best)
     E->nv = wi + 1;
   }
   wsync();
+  lap(3);
 }
 // EPA on the whole wave for one penetrating pair: lane ln seeds the polytope
 // from GJK's simplex; per step the wave takes the closest alive face, the
@@ -1017,11 +1074,16 @@ __device__ __forceinline__ void epa_grow_wave(EpaPoly* E, const SV& w, int best)
 // E->out.  Same steps and result as epa_serial.  st (timing builds): steps,
 // cycles in face scan, support + tests, growth.
 template <class SH>
-__device__ __forceinline__ double epa_run_wave(const SH& A, const SH& B, EpaPoly* E, int ln,
-                                               unsigned long long* st = nullptr) {
+__device__ __forceinline__ double epa_run_wave(const SH& A, const SH& B, EpaPoly* E, int ln, int sk = -1,
+                                               int sn = 0, unsigned long long* st = nullptr) {
   const int l = threadIdx.x & 63;
-  if (l == ln) epa_init(A, B, E);
+  const unsigned long long ti = st ? __builtin_amdgcn_s_memtime() : 0;
+  if (l == ln) {  // seed from the stashed simplex (sk >= 0) or rerun GJK
+    if (sk >= 0) epa_init_stash(A, B, E, sk, sn);
+    else epa_init(A, B, E);
+  }
   wsync();
+  if (st) st[8] += __builtin_amdgcn_s_memtime() - ti;  // (timing builds: the seed polytope)
   double dres = 0;
   for (int it = 0; it <= 255; ++it) {
     unsigned long long t0 = 0, t1 = 0;
@@ -1061,7 +1123,7 @@ __device__ __forceinline__ double epa_run_wave(const SH& A, const SH& B, EpaPoly
       break;
     }
     if (st) t0 = __builtin_amdgcn_s_memtime(), st[2] += t0 - t1;
-    epa_grow_wave(E, w, fb);
+    epa_grow_wave(E, w, fb, st ? st + 4 : nullptr);
     if (st) st[3] += __builtin_amdgcn_s_memtime() - t0;
   }
   return __shfl(dres, ln, 64);

@@ -393,7 +393,7 @@ __device__ __forceinline__ void task_instance(const DevModel* __restrict__ M0, c
   const int64_t gb = io.b0 + b, LD = io.ld;  // position in the caller's [field][B] arrays
   PH_ONLY(const unsigned long long inst_t0 = __builtin_amdgcn_s_memtime(); unsigned long long ph_snap[8];
           for (int k_ = 0; k_ < 8; ++k_) ph_snap[k_] = ph_acc[k_];
-          unsigned long long epa_calls = 0, epa_steps = 0, epa_maxsteps = 0, epa_t[3] = {0, 0, 0};)
+          unsigned long long epa_calls = 0, epa_steps = 0, epa_maxsteps = 0, epa_t[8] = {0, 0, 0, 0, 0, 0, 0, 0};)
   // re-derive the model pointer each instance: keeps LICM from hoisting
   // model-constant loads out of the instance loop into spilled registers
   const DevModel* M = opaque_model(M0);
@@ -728,6 +728,7 @@ __device__ __forceinline__ void task_instance(const DevModel* __restrict__ M0, c
       if (c) cand[ncand + __popcll(m & ((1ull << l) - 1))] = p;
       ncand += __popcll(m);
     }
+    if (l == 0) ews->nv = 0;  // EPA seed stash counter (epa_stash)
     wsync();
     for (int c = l; c < ncand; c += 64) {
       const int p = cand[c];
@@ -735,7 +736,7 @@ __device__ __forceinline__ void task_instance(const DevModel* __restrict__ M0, c
       ShapeL A{M->gtype[ga], (lds_pose*)(Tg + 12 * ga), M->gparam[ga][0], M->gparam[ga][1], M->gparam[ga][2]};
       ShapeL Bs{M->gtype[gb], (lds_pose*)(Tg + 12 * gb), M->gparam[gb][0], M->gparam[gb][1], M->gparam[gb][2]};
       // early exit once GJK's lower bound shows the pair cannot reach ub
-      const GjkDist g = gjk(A, Bs, ub + 1e-9);
+      const GjkDist g = gjk(A, Bs, ub + 1e-9, ews, p);
       if (g.pruned) {
         pf[p] = 1;
       } else if (g.intersect) {
@@ -763,6 +764,12 @@ __device__ __forceinline__ void task_instance(const DevModel* __restrict__ M0, c
     double gbd = bestd;
     int gbi = besti;
     wave_argmin(gbd, gbi);
+    // stashed GJK simplices of intersecting pairs (epa_stash): pair and size
+    // per slot, valid until a polytope grows into the stash's vertex slots
+    const int nst = ews->nv < kEpaStash ? ews->nv : kEpaStash;
+    int sp0 = nst > 0 ? static_cast<int>(ews->out[0]) : -1, sp1 = nst > 1 ? static_cast<int>(ews->out[2]) : -1;
+    const int sn0 = nst > 0 ? static_cast<int>(ews->out[1]) : 0, sn1 = nst > 1 ? static_cast<int>(ews->out[3]) : 0;
+    wsync();  // stash metadata read before the first EPA overwrites out[]
     for (;;) {
       double cpd = 1.7976931348623157e308;
       int cp = 0x7fffffff;
@@ -776,10 +783,13 @@ __device__ __forceinline__ void task_instance(const DevModel* __restrict__ M0, c
       const int p = cp, ln = p & 63, ga = M->pair_a[p], gb = M->pair_b[p];
       const ShapeL A{M->gtype[ga], (lds_pose*)(Tg + 12 * ga), M->gparam[ga][0], M->gparam[ga][1], M->gparam[ga][2]};
       const ShapeL Bs{M->gtype[gb], (lds_pose*)(Tg + 12 * gb), M->gparam[gb][0], M->gparam[gb][1], M->gparam[gb][2]};
-      PH_ONLY(epa_calls++; unsigned long long est[4] = {0, 0, 0, 0};)
-      const double dall = epa_run_wave(A, Bs, ews, ln PH_ONLY(, est));
+      PH_ONLY(epa_calls++; unsigned long long est[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};)
+      const int sk = p == sp0 ? 0 : (p == sp1 ? 1 : -1);
+      const double dall = epa_run_wave(A, Bs, ews, ln, sk, sk == 0 ? sn0 : sn1 PH_ONLY(, est));
+      if (ews->nv > kEpaStashV0) sp0 = sp1 = -1;  // grown into the stash slots
       PH_ONLY(epa_steps += est[0]; if (est[0] > epa_maxsteps) epa_maxsteps = est[0];
-              epa_t[0] += est[1]; epa_t[1] += est[2]; epa_t[2] += est[3];)
+              epa_t[0] += est[1]; epa_t[1] += est[2]; epa_t[2] += est[3];
+              for (int k_ = 0; k_ < 5; ++k_) epa_t[3 + k_] += est[4 + k_];)
       if (l == ln && (dall < bestd || (dall == bestd && p < besti))) {
         bestd = dall;
         besti = p;
@@ -878,6 +888,12 @@ __device__ __forceinline__ void task_instance(const DevModel* __restrict__ M0, c
       atomicMax(&g_phase_cycles[28], epa_maxsteps);
       atomicAdd(&g_phase_cycles[18], epa_t[0] + epa_t[1]);  // (qp kernel leaves 18, 20 free)
       atomicAdd(&g_phase_cycles[20], epa_t[2]);
+      // growth split (slots no other stage of a QPIK call writes)
+      atomicAdd(&g_phase_cycles[59], epa_t[3]);
+      atomicAdd(&g_phase_cycles[61], epa_t[4]);
+      atomicAdd(&g_phase_cycles[62], epa_t[5]);
+      atomicAdd(&g_phase_cycles[63], epa_t[6]);
+      atomicAdd(&g_phase_cycles[60], epa_t[7]);  // seed polytope (slot 60: the lane stage's, not run here)
     }
   })
   // ---------------- task data out -----------------------------------------

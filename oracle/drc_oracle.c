@@ -487,12 +487,23 @@ static int closest_simplex(SV* S, int n, double* v, double* lam_out) {
 
 /* Stop tolerances (support gaps, metres).  The winning pair's witnesses are
  * refined to the exact critical point afterwards (refine_witness, D17), so
- * GJK / EPA only have to decide the argmin and land in the right basin:
- * EPA stops at hpp-fcl's default epa_tolerance (1e-6), GJK at 1e-9 (the
- * argmin of pairs closer than that is a tie at the reference's own
- * tolerance).  Kernel twins: kGjkTol / kEpaTol in qpik_device.hpp. */
-#define GJK_TOL 1e-9
+ * GJK / EPA only have to decide the argmin and land in the right basin: both
+ * stop at hpp-fcl's defaults, GJKSolver gjk_tolerance and epa_tolerance 1e-6
+ * (pairs whose distances lie closer than that are a tie at the reference's
+ * own tolerance).  r05: GJK from 1e-9 to 1e-6 took 37 % of the GJK
+ * iterations off the UR5e / FR3 bench workloads and moved no q-dot by more
+ * than 7e-12 (16 384 device-dump instances each; the D17 refinement absorbs
+ * the looser estimates).  Kernel twins: kGjkTol / kEpaTol in qpik_device.hpp. */
+#define GJK_TOL g_gjk_tol
 #define EPA_TOL 1e-6
+/* study switch (tolerance census) and a GJK iteration counter */
+static double g_gjk_tol = 1e-6;
+static long long g_gjk_it;
+void oracle_gjk_study(double tol, long long* iters, int reset) {
+    if (tol > 0) g_gjk_tol = tol;
+    if (iters) *iters = __atomic_load_n(&g_gjk_it, __ATOMIC_RELAXED);
+    if (reset) __atomic_store_n(&g_gjk_it, 0, __ATOMIC_RELAXED);
+}
 
 /* GJK on the cores.  Returns 1 when the origin is enclosed (penetration). */
 static int gjk(const Shape* A, const Shape* B, SV* S, int* ns, double* lam, double* v) {
@@ -503,6 +514,7 @@ static int gjk(const Shape* A, const Shape* B, SV* S, int* ns, double* lam, doub
         double nv[3] = {-v[0], -v[1], -v[2]};
         SV w;
         sup_md(A, B, nv, &w);
+        __atomic_fetch_add(&g_gjk_it, 1, __ATOMIC_RELAXED);
         double vv = dot3(v, v);
         if (n > 0 && vv - dot3(v, w.w) <= GJK_TOL * sqrt(vv)) break;
         int dup = 0;
@@ -667,6 +679,19 @@ void oracle_epa_census(long long* out, int reset) {
     if (out) for (int i = 0; i < 8; ++i) out[i] = __atomic_load_n(&g_ec[i], __ATOMIC_RELAXED);
     if (reset) for (int i = 0; i < 8; ++i) __atomic_store_n(&g_ec[i], 0, __ATOMIC_RELAXED);
 }
+/* EPA step histogram (diagnostic): [0..7] calls by steps 0-7, 8-15, 16-23,
+ * 24-31, 32-39, 40-47, 48-59, 60+; [8..11] how they ended: support gap,
+ * vertex cap, duplicate support point, rolled-back growth */
+static long long g_eh[12];
+void oracle_epa_hist(long long* out, int reset) {
+    if (out) for (int i = 0; i < 12; ++i) out[i] = __atomic_load_n(&g_eh[i], __ATOMIC_RELAXED);
+    if (reset) for (int i = 0; i < 12; ++i) __atomic_store_n(&g_eh[i], 0, __ATOMIC_RELAXED);
+}
+static void epa_hist_add(int steps, int why) {
+    const int b = steps < 48 ? steps / 8 : (steps < 60 ? 6 : 7);
+    __atomic_fetch_add(&g_eh[b], 1, __ATOMIC_RELAXED);
+    __atomic_fetch_add(&g_eh[8 + why], 1, __ATOMIC_RELAXED);
+}
 static double epa(const Shape* A, const Shape* B, SV* S, int ns, double* pA, double* pB) {
     static const double dirs[6][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}, {-1, 0, 0}, {0, -1, 0}, {0, 0, -1}};
     static __thread Epa E;
@@ -694,6 +719,7 @@ static double epa(const Shape* A, const Shape* B, SV* S, int ns, double* pA, dou
     if (!E.fail) {
         epa_bind(&E, t0, 0, t1, 0); epa_bind(&E, t0, 1, t2, 0); epa_bind(&E, t0, 2, t3, 0);
         epa_bind(&E, t1, 1, t3, 2); epa_bind(&E, t1, 2, t2, 1); epa_bind(&E, t2, 2, t3, 1);
+        int nst = 0, why = 0;
         for (int it = 0; it < 255; ++it) {
             best = -1;
             double bd = INFINITY;
@@ -701,22 +727,28 @@ static double epa(const Shape* A, const Shape* B, SV* S, int ns, double* pA, dou
                 if (E.alive[f] && E.fd[f] < bd) { bd = E.fd[f]; best = f; }
             SV w;
             sup_md(A, B, E.fn[best], &w);
-            if (dot3(E.fn[best], w.w) - E.fd[best] <= EPA_TOL || E.nv >= EPA_MAXV) break;
+            if (dot3(E.fn[best], w.w) - E.fd[best] <= EPA_TOL || E.nv >= EPA_MAXV) {
+                why = E.nv >= EPA_MAXV && dot3(E.fn[best], w.w) - E.fd[best] > EPA_TOL;
+                break;
+            }
             int dupv = 0;
             for (int i = 0; i < E.nv; ++i) {
                 double d[3];
                 sub3(w.w, E.V[i].w, d);
                 if (fabs(d[0]) <= 1e-14 && fabs(d[1]) <= 1e-14 && fabs(d[2]) <= 1e-14) dupv = 1;
             }
-            if (dupv) break;
+            if (dupv) { why = 2; break; }
             int wi = E.nv;
             E.V[E.nv++] = w;
             ++g_epa_steps;
+            ++nst;
             if (!epa_grow_canon(&E, wi, best)) {  /* rolled back: the last closed polytope */
                 E.nv--;
+                why = 3;
                 break;
             }
         }
+        epa_hist_add(nst, why);
     }
     double bd = INFINITY;
     best = 0;
@@ -1163,6 +1195,7 @@ static int gjk_cut(const Shape* A, const Shape* B, SV* S, int* ns, double* lam, 
         double nv[3] = {-v[0], -v[1], -v[2]};
         SV w;
         sup_md(A, B, nv, &w);
+        __atomic_fetch_add(&g_gjk_it, 1, __ATOMIC_RELAXED);
         const double vv = dot3(v, v), vw = dot3(v, w.w), sv = sqrt(vv);
         if (vw > cut * sv) { *ns = n; return 2; }
         if (n > 0 && vv - vw <= GJK_TOL * sv) break;

@@ -38,10 +38,16 @@ def test_gpu_gjk_epa_match_oracle():
     assert pen.sum() > 800 and (~pen).sum() > 800
     assert np.array_equal(pen, ref[:, 0] < 0)
     err = np.abs(dev[:, 0] - ref[:, 0])
-    # separated: both GJKs stop at a 1e-9 support gap; penetrating: the same
-    # expansion decisions, so depths agree to rounding unless rounding flips a
-    # step, and both stop within the EPA tolerance (1e-6) of the depth
-    assert err[~pen].max() <= 2e-9, err[~pen].max()
+    # separated: both GJKs stop at a 1e-6 support gap (hpp-fcl's default), so
+    # where rounding moves the stop by one iteration they differ up to that
+    # gap; penetrating: the same expansion decisions, so depths agree to
+    # rounding unless rounding flips a step, and both stop within the EPA
+    # tolerance (1e-6) of the depth
+    # (at a 1e-6 gap the stop iteration is more often one rounding away: 95 %
+    # of the separated pairs agree to 1e-9 on the device, r05q; the refined
+    # distances the product uses agree to 1e-12, tests/test_narrow_host.py)
+    assert err[~pen].max() <= 2e-6, err[~pen].max()
+    assert np.mean(err[~pen] <= 1e-9) >= 0.90, np.mean(err[~pen] <= 1e-9)
     assert err[pen].max() <= 2e-6, err[pen].max()
     assert np.mean(err[pen] <= 1e-12) >= 0.95, np.mean(err[pen] <= 1e-12)
     sep = dev[:, 4:7] - dev[:, 1:4]

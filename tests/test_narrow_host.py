@@ -86,20 +86,23 @@ def test_device_narrow_phase_matches_oracle(harness):
     assert 0.2 < pen.mean() < 0.8  # both GJK and EPA exercised
     err = np.abs(dev[:, 0] - ref[:, 0])
     # raw estimates (before the D17 refinement, test below): separated, GJK
-    # stops at a 1e-9 support gap on both sides; penetrating, identical EPA
-    # decisions agree to 1e-9 unless rounding changes a step, and both sides
-    # stop within the EPA tolerance (1e-6, hpp-fcl's default) of the depth
-    assert err[~pen].max() <= 2e-9, err[~pen].max()
+    # stops at a 1e-6 support gap on both sides (hpp-fcl's gjk_tolerance), so
+    # a rounding difference that moves the stop by one iteration shows up to
+    # that gap; penetrating, identical EPA decisions agree to 1e-9 unless
+    # rounding changes a step, and both sides stop within the EPA tolerance
+    # (1e-6, hpp-fcl's default) of the depth
+    assert err[~pen].max() <= 2e-6, err[~pen].max()
+    assert np.mean(err[~pen] <= 1e-9) >= 0.97
     assert err[pen].max() <= 2e-6, err[pen].max()
     assert np.mean(err[pen] <= 1e-9) >= 0.97
     # raw witnesses: flat-flat contacts admit a face of witnesses, so compare
-    # the separation vector pB - pA (unique).  GJK's 1e-9 gap leaves the
+    # the separation vector pB - pA (unique).  GJK's 1e-6 gap leaves the
     # direction accurate to ~sqrt(gap * d); EPA's 1e-6 gap likewise -- the
     # footprint the D17 refinement removes (test_witness_refinement_matches_oracle)
     sep = dev[:, 4:7] - dev[:, 1:4]
     sep_ref = ref[:, 4:7] - ref[:, 1:4]
     serr = np.abs(sep - sep_ref).max(axis=1)
-    assert serr[~pen].max() <= 1e-4, serr[~pen].max()
+    assert serr[~pen].max() <= 3e-3, serr[~pen].max()
     assert np.median(serr[~pen]) <= 1e-12
     assert serr[pen].max() <= 1e-3, serr[pen].max()
     assert np.quantile(serr[pen], 0.9) <= 1e-7

@@ -36,6 +36,9 @@ print("task stragglers: max instance %.0f cycles, %d instances > 400k cycles (%.
 print("straggler phase split: " + ", ".join("%s %.0f%%" % (n, 100 * x / max(v[8:16].sum(), 1)) for n, x in zip(names_t, v[8:16])))
 print("EPA (all instances): %d calls, %d steps, max %d steps in one call" % (v[22], v[23], v[28]))
 print("EPA step split: scan+support+tests %.0f, grow %.0f cycles/step" % (v[18] / max(v[23], 1), v[20] / max(v[23], 1)))
+print("EPA grow split (cycles/step): visibility+component %.0f, horizon+cycle check %.0f, order+planes %.0f, writes %.0f"
+      % tuple(v[k] / max(v[23], 1) for k in (59, 61, 62, 63)))
+print("EPA seed polytope (GJK rerun + tetrahedron, lane-serial): %.0f cycles/call" % (v[60] / max(v[22], 1)))
 print("admm_check: residuals %.0f cyc/inst (%d calls), polish %.0f cyc/inst (%d attempts, %d accepted), refactor after polish %.0f cyc/inst" % (v[32] / B, v[33], v[35] / B, v[36], v[37], v[38] / B))
 print("eqp: %d calls, %.0f cycles/call, mean KKT size %.1f; polish residuals %.0f cycles/call" % (v[41], v[40] / max(v[41], 1), v[42] / max(v[41], 1), v[43] / max(v[41], 1)))
 print("qp record load (inside load+assemble): %.0f cyc/inst" % (v[44] / B))
