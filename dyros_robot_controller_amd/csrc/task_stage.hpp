@@ -718,6 +718,7 @@ __device__ __forceinline__ void task_instance(const DevModel* __restrict__ M0, c
   // exact GJK only where the swept-core bound can still win.  The candidates
   // are compacted into a list first, so a wave runs them in ceil(n / 64)
   // rounds instead of one round per 64 pair slots.
+  bool pen = false;  // some candidate intersects: the EPA search below has work
   {
     int* cand = reinterpret_cast<int*>(S + kp.kCand);
     int ncand = 0;
@@ -741,6 +742,7 @@ __device__ __forceinline__ void task_instance(const DevModel* __restrict__ M0, c
         pf[p] = 1;
       } else if (g.intersect) {
         pf[p] = 2;  // penetrating: EPA below
+        pen = true;
       } else {
         pf[p] = 1;
         if (g.dist < bestd || (g.dist == bestd && p < besti)) {
@@ -760,7 +762,8 @@ __device__ __forceinline__ void task_instance(const DevModel* __restrict__ M0, c
   // the search stops once no remaining pair can undercut the running
   // minimum (same argmin and tie rule as computing every pair).  The owning
   // lane expands the polytope, the whole wave scans for the closest face.
-  {
+  // (Only pairs whose GJK intersected are searched: none, no search.)
+  if (__any(pen)) {
     double gbd = bestd;
     int gbi = besti;
     wave_argmin(gbd, gbi);
