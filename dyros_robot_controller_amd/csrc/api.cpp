@@ -80,6 +80,7 @@ struct drc_model_impl {
   int lane_stage = 0;  // drc_debug_lane_stage: 0 off, 1 lane stage + side-stream hard path, 2 + serial hard path, 3 auto
   // timed calls: {caller-stream start, caller-stream end, per chunk: task start, task end, qp end}
   std::vector<std::vector<hipEvent_t>> events;
+  std::vector<hipEvent_t> evpool;  // timing events returned by drc_debug_kernel_times, reused
   // concurrent sub-batches: the batch is cut into `chunks` contiguous ranges,
   // the last on the caller's stream and the others on internal streams forked
   // from / joined to it, so one range's task kernel overlaps another's QP
@@ -690,8 +691,19 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
       }
   const bool timed = m->timing && !stages;
   std::vector<hipEvent_t> tev;
+  // (timing events come from the model's pool: creating five to fourteen
+  // events per call cost host time inside the bench's timed region)
   auto mkev = [&](hipEvent_t* e) -> int {
-    HIP_TRY(hipEventCreate(e));
+    {
+      std::lock_guard<std::mutex> g(m->mu);
+      if (!m->evpool.empty()) {
+        *e = m->evpool.back();
+        m->evpool.pop_back();
+      } else {
+        *e = nullptr;
+      }
+    }
+    if (!*e) HIP_TRY(hipEventCreate(e));
     tev.push_back(*e);
     return DRC_OK;
   };
@@ -747,7 +759,8 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
           rec ? rec + b0 * stride : nullptr, stride};
     io.stamps = stages ? nullptr : stamps;
     int* qc = cx->d_queue + c * StreamCtx::kSlotInts;  // c < 16 (drc_set_concurrency)
-    HIP_TRY(hipMemsetAsync(qc, 0, 17 * sizeof(int), cs));
+    // the whole slot (128 B, one aligned fill; 17 ints took two fill kernels)
+    HIP_TRY(hipMemsetAsync(qc, 0, StreamCtx::kSlotInts * sizeof(int), cs));
     io.queue = qc;
     hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr;
     if (timed) {
@@ -1094,7 +1107,7 @@ int drc_debug_kernel_times(drc_model* m, double* wall_ms, double* task_ms, doubl
   }
   *calls = static_cast<int>(m->events.size());
   for (auto& ev : m->events)
-    for (hipEvent_t e : ev) (void)hipEventDestroy(e);
+    for (hipEvent_t e : ev) m->evpool.push_back(e);  // completed: reusable
   m->events.clear();
   *wall_ms = tw;
   *task_ms = t0;
@@ -1243,6 +1256,7 @@ void drc_model_destroy(drc_model* m) {
   if (m->hdone) (void)hipEventDestroy(m->hdone);
   for (auto& ev : m->events)
     for (hipEvent_t e : ev) (void)hipEventDestroy(e);
+  for (hipEvent_t e : m->evpool) (void)hipEventDestroy(e);
   delete m;
 }
 
