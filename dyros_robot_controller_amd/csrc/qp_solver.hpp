@@ -1098,6 +1098,10 @@ __device__ DRC_POLISH_ATTR bool polish(const KParams& kp, double* S, bool strict
   double* sc = S + kp.oSc;
   const double pr0 = sc[SC_PRI], dr0 = sc[SC_DUA];
   const int iters = strict ? kPolishFeasAttempts + kPolishAsIters : 1;
+  // QPIK with slacks: G row r is nonzero only in the q-dot columns and its own
+  // slack column np + r (qp_assemble), so the G-row products below take those
+  // np + 1 terms, in the same order (the skipped terms are exact zeros)
+  const bool slk = kp.problem == 0 && np < nx;
   for (int pass = 0; pass < 2; ++pass) {
   if (pass == 1) {
     if (!alt) break;
@@ -1124,6 +1128,14 @@ __device__ DRC_POLISH_ATTR bool polish(const KParams& kp, double* S, bool strict
         double sf = 0, sa = 0, act = 0;
 #pragma unroll
         for (int j = 0; j < nx; ++j) {
+          if (j >= np && slk) break;  // (the slack column below)
+          const double g = G[lg * nx + j];
+          sa = fmax(sa, fabs(g));
+          if (!((fixed >> j) & 1ull)) sf = fmax(sf, fabs(g));
+          else act += g * xx[j];
+        }
+        if (slk) {
+          const int j = np + lg;
           const double g = G[lg * nx + j];
           sa = fmax(sa, fabs(g));
           if (!((fixed >> j) & 1ull)) sf = fmax(sf, fabs(g));
@@ -1160,6 +1172,12 @@ __device__ DRC_POLISH_ATTR bool polish(const KParams& kp, double* S, bool strict
           double axc = 0, ap = 0, a = 2.0;
 #pragma unroll
           for (int j = 0; j < nx; ++j) {
+            if (j >= np && slk) break;
+            axc += G[lg * nx + j] * xc[j];
+            ap += G[lg * nx + j] * (xx[j] - xc[j]);
+          }
+          if (slk) {
+            const int j = np + lg;
             axc += G[lg * nx + j] * xc[j];
             ap += G[lg * nx + j] * (xx[j] - xc[j]);
           }
@@ -1195,7 +1213,11 @@ __device__ DRC_POLISH_ATTR bool polish(const KParams& kp, double* S, bool strict
     if (l < ng) {
       const int lg = l < ng ? l : 0;
 #pragma unroll
-      for (int j = 0; j < nx; ++j) axg += G[lg * nx + j] * xx[j];
+      for (int j = 0; j < nx; ++j) {
+        if (j >= np && slk) break;
+        axg += G[lg * nx + j] * xx[j];
+      }
+      if (slk) axg += G[lg * nx + np + lg] * xx[np + lg];
       zz[nx + lg] = fmin(fmax(axg, lo[nx + lg]), up[nx + lg]);
     }
     wsync();
