@@ -569,8 +569,15 @@ __device__ __forceinline__ bool eqp_regs(const KParams& kp, double* S, int actb,
   if (l < NG && actg != 0) {
     const int lg = l < NG ? l : 0;
     double r = actg < 0 ? lo[NX + lg] : up[NX + lg];
+    // (QPIK with slacks: the q-dot columns and the row's own slack column,
+    // as polish's G-row products)
+    const bool slk = kp.problem == 0 && NP < NX;
 #pragma unroll
-    for (int c = 0; c < NX; ++c) r -= G[lg * NX + c] * xx[c];
+    for (int c = 0; c < NX; ++c) {
+      if (c >= NP && slk) break;
+      r -= G[lg * NX + c] * xx[c];
+    }
+    if (slk) r -= G[lg * NX + NP + lg] * xx[NP + lg];
     rG = r;
   }
   const bool hf = l < nF, hr = l >= nF && l < N;
