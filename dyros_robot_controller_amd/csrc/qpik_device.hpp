@@ -86,6 +86,14 @@ __device__ __forceinline__ double wave_sum(double v) {
   v += dpp_d<kDppMirror>(v);
   return (rd_lane(v, 0) + rd_lane(v, 16)) + (rd_lane(v, 32) + rd_lane(v, 48));
 }
+__device__ __forceinline__ int wave_min_int(int v) {
+  v = min(v, dpp_i<kDppQuad1032>(v));
+  v = min(v, dpp_i<kDppQuad2301>(v));
+  v = min(v, dpp_i<kDppHalfMirror>(v));
+  v = min(v, dpp_i<kDppMirror>(v));
+  return min(min(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 16)),
+             min(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48)));
+}
 // argmin with ties broken toward the smaller index (reference: first strict
 // minimum in pair order, robot_data.cpp:434-442); the (value, index) order
 // is total, so the result does not depend on the reduction tree
@@ -999,12 +1007,17 @@ __device__ __forceinline__ void epa_grow_wave(EpaPoly* E, const SV& w, int best,
     // with no continuation: not one simple cycle
     bad = E->vout[a] != l || E->vin[b] != l || nx < 0 || pv < 0;
   }
+  // the new face's plane (independent of the cycle order below, so its FP64
+  // chain issues before the cross-lane steps; used only when nothing is bad)
+  V3 nn = v3(0, 0, 0);
+  double fd = 0;
+  bool pbad = false;
+  if (own) pbad = !epa_face_plane(E, a, b, wi, E->fd[best], &nn, &fd);
   bad = __any(bad);
   lap(1);
-  // cycle position relative to the edge of smallest key (pointer jumping)
-  double key = own ? double(3 * hc + he_) : 1e300;
-  int s = l;
-  wave_argmin(key, s);
+  // cycle position relative to the edge of smallest key 3 face + edge (unique
+  // per edge, < 2^9): one integer minimum of key << 6 | lane
+  const int s = wave_min_int(own ? ((3 * hc + he_) << 6) | l : 0x7fffffff) & 63;
   int d = (own && l != s) ? 1 : 0, p = own ? (l == s ? s : nx) : l;
   // ceil(log2 H) rounds reach s from every edge of a cycle of H edges (a
   // pointer at s stays there with d += 0, so more rounds change nothing); the
@@ -1018,12 +1031,10 @@ __device__ __forceinline__ void epa_grow_wave(EpaPoly* E, const SV& w, int best,
   bad = __any(bad || (own && p != s));
   int slot = 0;
   bool gbad = bad;
-  V3 nn = v3(0, 0, 0);
-  double fd = 0;
   if (own && !bad) {
     const int k = d == 0 ? 0 : H - d;
     slot = k < nfree ? E->freel[nfree - 1 - k] : nf + (k - nfree);
-    gbad = !epa_face_plane(E, a, b, wi, E->fd[best], &nn, &fd);
+    gbad = pbad;
   }
   if (__any(gbad)) {
     if (l == 0) E->stop = 1;
