@@ -916,10 +916,37 @@ DRC_HD __forceinline__ double epa_finish(EpaPoly* E, int best) {
   st3(E->out + 3, l0 * (aa - aw) + l1 * (ba - bw) + l2 * (ca - cw));
   return -bd;
 }
+// A lane's two faces (l, l + 64) as the step's closest-face scan loads them:
+// alive, offset, normal, adjacency.  epa_run_wave loads them before the scan's
+// reduction and the support point, so the growth's visibility pass starts from
+// registers instead of a second round of LDS reads.
+struct EpaFaces {
+  bool h0, h1, al0, al1;
+  double fd0, fd1;
+  V3 fn0, fn1;
+  int n0[3], n1[3];
+};
+__device__ __forceinline__ void epa_load_faces(const EpaPoly* E, int nf, int l, EpaFaces& F) {
+  const int f0 = l, f1 = l + 64;
+  F.h0 = f0 < nf;
+  F.h1 = f1 < nf;
+  F.al0 = F.h0 && E->alive[f0];
+  F.al1 = F.h1 && E->alive[f1];
+  F.fd0 = F.h0 ? E->fd[f0] : 0.0;
+  F.fd1 = F.h1 ? E->fd[f1] : 0.0;
+  F.fn0 = F.h0 ? ld3(E->fn[f0]) : v3(0, 0, 0);
+  F.fn1 = F.h1 ? ld3(E->fn[f1]) : v3(0, 0, 0);
+#pragma unroll
+  for (int e = 0; e < 3; ++e) {
+    F.n0[e] = F.h0 ? E->adj[f0][e] : 0;
+    F.n1[e] = F.h1 ? E->adj[f1][e] : 0;
+  }
+}
 // Wave form of epa_grow_canon (the task kernel; every lane calls it with the
 // same w and best).  Lane l owns faces l and l + 64 and, after compaction,
 // horizon edge l.  Same slots, adjacency, face data, free list and decisions.
-__device__ __forceinline__ void epa_grow_wave(EpaPoly* E, const SV& w, int best, unsigned long long* gt = nullptr) {
+__device__ __forceinline__ void epa_grow_wave(EpaPoly* E, const SV& w, int best, const EpaFaces& F,
+                                              unsigned long long* gt = nullptr) {
   const int l = threadIdx.x & 63;
   // (timing builds: gt[0..3] += cycles in visibility + component, horizon +
   // cycle check, cycle order + new planes, writes)
@@ -939,15 +966,10 @@ __device__ __forceinline__ void epa_grow_wave(EpaPoly* E, const SV& w, int best,
   E->vout[l] = -1;
   E->vin[l] = -1;
   const int f0 = l, f1 = l + 64;
-  const bool h0 = f0 < nf, h1 = f1 < nf;
-  const bool s0 = h0 && E->alive[f0] && epa_sees(E, f0, w.w);
-  const bool s1 = h1 && E->alive[f1] && epa_sees(E, f1, w.w);
-  int n0[3], n1[3];
-#pragma unroll
-  for (int e = 0; e < 3; ++e) {
-    n0[e] = h0 ? E->adj[f0][e] : 0;
-    n1[e] = h1 ? E->adj[f1][e] : 0;
-  }
+  // "face f sees w" (epa_sees) on the registers of the scan
+  const bool s0 = F.al0 && !(dot(F.fn0, w.w) - F.fd0 < -1e-12);
+  const bool s1 = F.al1 && !(dot(F.fn1, w.w) - F.fd1 < -1e-12);
+  const int *n0 = F.n0, *n1 = F.n1;
   auto in = [](uint64_t lo, uint64_t hi, int f) -> bool {
     return f < 64 ? (lo >> f) & 1ull : (hi >> (f - 64)) & 1ull;
   };
@@ -1105,11 +1127,16 @@ __device__ __forceinline__ double epa_run_wave(const SH& A, const SH& B, EpaPoly
     bool stop = E->stop || it == 255;
     double fdm = 1e300;
     int fb = 0x7fffffff;
-    for (int f = l; f < E->nf; f += 64)
-      if (E->alive[f] && E->fd[f] < fdm) {
-        fdm = E->fd[f];
-        fb = f;
-      }
+    EpaFaces F;
+    epa_load_faces(E, E->nf, l, F);  // (faces l, l + 64: nf <= 128)
+    if (F.al0 && F.fd0 < fdm) {
+      fdm = F.fd0;
+      fb = l;
+    }
+    if (F.al1 && F.fd1 < fdm) {
+      fdm = F.fd1;
+      fb = l + 64;
+    }
     wave_argmin(fdm, fb);
     if (fb == 0x7fffffff) {  // no alive face (failed seed): the oracle takes face 0
       fb = 0;
@@ -1134,7 +1161,7 @@ __device__ __forceinline__ double epa_run_wave(const SH& A, const SH& B, EpaPoly
       break;
     }
     if (st) t0 = __builtin_amdgcn_s_memtime(), st[2] += t0 - t1;
-    epa_grow_wave(E, w, fb, st ? st + 4 : nullptr);
+    epa_grow_wave(E, w, fb, F, st ? st + 4 : nullptr);
     if (st) st[3] += __builtin_amdgcn_s_memtime() - t0;
   }
   return __shfl(dres, ln, 64);
