@@ -496,14 +496,20 @@ static int closest_simplex(SV* S, int n, double* v, double* lam_out) {
  * the looser estimates).  Kernel twins: kGjkTol / kEpaTol in qpik_device.hpp. */
 #define GJK_TOL g_gjk_tol
 #define EPA_TOL 1e-6
-/* study switch (tolerance census) and a GJK iteration counter */
+/* study switch (tolerance census) and a GJK iteration counter,
+ * counted only while a study has it on (reset = 1 zeroes and enables it,
+ * reset = 0 reads and disables it): a shared atomic in the GJK loop would
+ * serialise the multi-threaded CPU baseline */
 static double g_gjk_tol = 1e-6;
 static long long g_gjk_it;
+static int g_diag_on;
 void oracle_gjk_study(double tol, long long* iters, int reset) {
     if (tol > 0) g_gjk_tol = tol;
     if (iters) *iters = __atomic_load_n(&g_gjk_it, __ATOMIC_RELAXED);
     if (reset) __atomic_store_n(&g_gjk_it, 0, __ATOMIC_RELAXED);
+    g_diag_on = reset != 0;
 }
+#define GJK_COUNT() do { if (g_diag_on) __atomic_fetch_add(&g_gjk_it, 1, __ATOMIC_RELAXED); } while (0)
 
 /* GJK on the cores.  Returns 1 when the origin is enclosed (penetration). */
 static int gjk(const Shape* A, const Shape* B, SV* S, int* ns, double* lam, double* v) {
@@ -514,7 +520,7 @@ static int gjk(const Shape* A, const Shape* B, SV* S, int* ns, double* lam, doub
         double nv[3] = {-v[0], -v[1], -v[2]};
         SV w;
         sup_md(A, B, nv, &w);
-        __atomic_fetch_add(&g_gjk_it, 1, __ATOMIC_RELAXED);
+        GJK_COUNT();
         double vv = dot3(v, v);
         if (n > 0 && vv - dot3(v, w.w) <= GJK_TOL * sqrt(vv)) break;
         int dup = 0;
@@ -674,20 +680,25 @@ static int epa_grow_canon(Epa* E, int wi, int best) {
 /* EPA census (diagnostic, tools/polish_census.py --epa): calls, growth steps,
  * calls and steps of pairs that did not end up as the argmin */
 static long long g_ec[8];
+static int g_ec_on;  /* on between oracle_epa_census(.., 1) and (.., 0): no shared atomics otherwise */
 static __thread int g_epa_steps;
 void oracle_epa_census(long long* out, int reset) {
     if (out) for (int i = 0; i < 8; ++i) out[i] = __atomic_load_n(&g_ec[i], __ATOMIC_RELAXED);
     if (reset) for (int i = 0; i < 8; ++i) __atomic_store_n(&g_ec[i], 0, __ATOMIC_RELAXED);
+    g_ec_on = reset != 0;
 }
 /* EPA step histogram (diagnostic): [0..7] calls by steps 0-7, 8-15, 16-23,
  * 24-31, 32-39, 40-47, 48-59, 60+; [8..11] how they ended: support gap,
  * vertex cap, duplicate support point, rolled-back growth */
 static long long g_eh[12];
+static int g_eh_on;  /* on between oracle_epa_hist(.., 1) and oracle_epa_hist(.., 0) */
 void oracle_epa_hist(long long* out, int reset) {
     if (out) for (int i = 0; i < 12; ++i) out[i] = __atomic_load_n(&g_eh[i], __ATOMIC_RELAXED);
     if (reset) for (int i = 0; i < 12; ++i) __atomic_store_n(&g_eh[i], 0, __ATOMIC_RELAXED);
+    g_eh_on = reset != 0;
 }
 static void epa_hist_add(int steps, int why) {
+    if (!g_eh_on) return;
     const int b = steps < 48 ? steps / 8 : (steps < 60 ? 6 : 7);
     __atomic_fetch_add(&g_eh[b], 1, __ATOMIC_RELAXED);
     __atomic_fetch_add(&g_eh[8 + why], 1, __ATOMIC_RELAXED);
@@ -1195,7 +1206,7 @@ static int gjk_cut(const Shape* A, const Shape* B, SV* S, int* ns, double* lam, 
         double nv[3] = {-v[0], -v[1], -v[2]};
         SV w;
         sup_md(A, B, nv, &w);
-        __atomic_fetch_add(&g_gjk_it, 1, __ATOMIC_RELAXED);
+        GJK_COUNT();
         const double vv = dot3(v, v), vw = dot3(v, w.w), sv = sqrt(vv);
         if (vw > cut * sv) { *ns = n; return 2; }
         if (n > 0 && vv - vw <= GJK_TOL * sv) break;
@@ -1271,7 +1282,7 @@ static void min_distance_pruned(const OracleModel* m, const Kin* k, double* dist
         ++ep_calls; ep_steps += g_epa_steps;
         if (d < best || (d == best && cp < bi)) { best = d; bi = cp; bhow = 2; memcpy(bpA, pA, sizeof(pA)); memcpy(bpB, pB, sizeof(pB)); ep_win_steps = g_epa_steps; }
     }
-    if (ep_calls) {
+    if (ep_calls && g_ec_on) {
         __atomic_fetch_add(&g_ec[0], ep_calls, __ATOMIC_RELAXED);
         __atomic_fetch_add(&g_ec[1], ep_steps, __ATOMIC_RELAXED);
         __atomic_fetch_add(&g_ec[2], bhow == 2 ? ep_calls - 1 : ep_calls, __ATOMIC_RELAXED);
