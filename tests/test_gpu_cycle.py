@@ -187,3 +187,36 @@ def test_host_timeline_and_waves(cuda):
     wt, wq = C.c_int(), C.c_int()
     _capi.check(lib.drc_debug_waves(h, C.byref(p), C.byref(wt), C.byref(wq)))
     assert wt.value in (2, 3) and wq.value == 3
+
+
+def test_qpik_stamps_diagnostic(cuda):
+    """drc_debug_qpik_stamps: the same outputs as drc_qpik_host, plus per
+    instance six ordered clock stamps (task start / end, QP start / assembled /
+    solved / stored) and where each stage ran (workgroup << 32 | CU << 2 |
+    SIMD), for the fused kernel and the two-kernel pipeline."""
+    rd = make_manipulator("fr3", cuda)
+    B = 96
+    q, qd, xt, xdt = step_inputs(rd, "fr3", 36, B, cuda)
+    p = manipulator.QPIKParamsBuilder(rd.model, exact=True).params(LINK["fr3"], _capi.MODE_QPIK_STEP)
+    n = rd.model.dof
+    lib, h = _capi.lib(), rd.model.handle
+    o0, s0, i0 = np.zeros((n, B)), np.zeros(B, np.int32), np.zeros(B, np.int32)
+    _capi.check(lib.drc_qpik_host(h, C.byref(p), B, dp(q), dp(qd), dp(xt), dp(xdt), None, None, dp(o0), ip(s0), ip(i0)))
+    try:
+        for fused in (1, 0):
+            _capi.check(lib.drc_set_fusion(h, C.c_int(fused)))
+            o, s, it = np.zeros((n, B)), np.zeros(B, np.int32), np.zeros(B, np.int32)
+            st = np.zeros((8, B), np.uint64)
+            _capi.check(lib.drc_debug_qpik_stamps(h, C.byref(p), B, dp(q), dp(qd), dp(xt), dp(xdt), dp(xt), dp(xdt),
+                                                  dp(o), ip(s), ip(it), st.ctypes.data_as(C.POINTER(C.c_uint64))))
+            assert np.array_equal(o, o0) and np.array_equal(s, s0) and np.array_equal(it, i0)
+            t = st[:6].astype(np.int64)
+            assert np.all(t > 0) and np.all(np.diff(t, axis=0) >= 0)
+            assert np.all((t[5] - t[0]) * 1e-8 < 0.05)        # < 50 ms per instance (100 MHz ticks)
+            for k in (6, 7):                                   # CU id << 2 | SIMD, workgroup in the high word
+                assert np.all(((st[k] & np.uint64(0xFFFFFFFF)) >> np.uint64(2)) < 4096)
+                assert np.all((st[k] >> np.uint64(32)) < 1 << 20)
+            if fused:                                          # one wave runs both stages of an instance
+                assert np.array_equal(st[6] >> np.uint64(32), st[7] >> np.uint64(32))
+    finally:
+        _capi.check(lib.drc_set_fusion(h, C.c_int(1)))
