@@ -361,6 +361,8 @@ def main():
                     help="0 wave-per-instance task kernel (default), 1 lane stage + side-stream hand-backs, "
                          "2 lane stage + serial hand-backs (drc_debug_lane_stage)")
     ap.add_argument("--dry-run", action="store_true", help="launcher and collectives only (no GPU)")
+    ap.add_argument("--no-kernel-events", action="store_true",
+                    help="study: no per-kernel HIP events in the timed region (roofline kernel times then null)")
     args = ap.parse_args()
 
     rc = ddist.launch_if_needed(args.gpus, os.path.abspath(__file__), sys.argv[1:])
@@ -411,7 +413,7 @@ def main():
     torch.cuda.synchronize()
     # per-kernel durations: HIP events recorded by the library on the launch
     # stream around task_kernel and qp_kernel of every timed step
-    _capi.check(_capi.lib().drc_debug_kernel_timing(handle, 1))
+    _capi.check(_capi.lib().drc_debug_kernel_timing(handle, 0 if args.no_kernel_events else 1))
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -435,6 +437,8 @@ def main():
     # kernel_ms: one drc_qpik_batch call on its stream (fork -> join of the
     # concurrent sub-batches); task/qp: summed per-sub-batch kernel durations
     kernel_ms, task_ms, qp_ms = tw.value / ncall, tk.value / ncall, tq.value / ncall
+    if nc.value == 0:   # --no-kernel-events (study): the call's own stream events stand in
+        kernel_ms = step_event_ms
     wall, n_bad, it_mean = ddist.reduce_stats(wall, float((status != 1).sum().item()),
                                               float(iters.double().mean().item()), world, red_dev)
     # per-rank statistics, gathered whole-job: iteration p99 / max (max over

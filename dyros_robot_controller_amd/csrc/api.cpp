@@ -13,6 +13,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <algorithm>
 #include <vector>
 
 #include "../../include/drc_amd.h"
@@ -79,7 +80,9 @@ struct drc_model_impl {
   int timing = 0;  // drc_debug_kernel_timing: HIP events around each launch
   int lane_stage = 0;  // drc_debug_lane_stage: 0 off, 1 lane stage + side-stream hard path, 2 + serial hard path, 3 auto
   // timed calls: {caller-stream start, caller-stream end, per chunk: task start, task end, qp end}
-  std::vector<std::vector<hipEvent_t>> events;
+  // timed calls: {call start, call end, task start, task end, QP end of the
+  // sub-batch on the caller's stream} and the call's sub-batch count
+  std::vector<std::pair<std::vector<hipEvent_t>, int>> events;
   std::vector<hipEvent_t> evpool;  // timing events returned by drc_debug_kernel_times, reused
   // concurrent sub-batches: the batch is cut into `chunks` contiguous ranges,
   // the last on the caller's stream and the others on internal streams forked
@@ -729,8 +732,10 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
     }
     if (!m->ln.fork) HIP_TRY(hipEventCreateWithFlags(&m->ln.fork, hipEventDisableTiming));
   }
-  hipEvent_t e_start = nullptr, e_end = nullptr;
-  if (timed) {
+  // (one sub-batch: its own task-start / last events bracket the call, no
+  // separate call events)
+  hipEvent_t e_start = nullptr, e_end = nullptr, t0e = nullptr, t1e = nullptr, t2e = nullptr;
+  if (timed && S > 1) {
     if (int r = mkev(&e_start)) return r;
     if (int r = mkev(&e_end)) return r;
     HIP_TRY(hipEventRecord(e_start, st));
@@ -763,11 +768,20 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
     HIP_TRY(hipMemsetAsync(qc, 0, StreamCtx::kSlotInts * sizeof(int), cs));
     io.queue = qc;
     hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr;
-    if (timed) {
+    // kernel timing: the sub-batch on the caller's stream only (its task and
+    // QP launches stand for the call's S; every marker is a queue packet
+    // between two kernels: 14 per four-sub-batch call cost 1.5 % of the
+    // FR3 bench, 5 per fused call 6 % at B = 4 096)
+    const bool timed_c = timed && c == S - 1;
+    if (timed_c) {
       if (int r = mkev(&e0)) return r;
       if (int r = mkev(&e1)) return r;
-      if (int r = mkev(&e2)) return r;
+      if (!fuse)  // the fused kernel has no QP launch of its own: its end is e1
+        if (int r = mkev(&e2)) return r;
       HIP_TRY(hipEventRecord(e0, cs));
+      t0e = e0;
+      t1e = e1;
+      t2e = fuse ? e1 : e2;
     }
     const size_t lds_t = static_cast<size_t>(kt_c.lds_doubles) * sizeof(double);
     const size_t lds_q = stages ? 0 : static_cast<size_t>(kq_c.lds_doubles) * sizeof(double);
@@ -792,10 +806,10 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
       io.queue = qc;
       HIP_TRY(static_cast<hipError_t>(
           launch_fused_kernel(static_cast<unsigned>(gf), lds_f, cs, m->d_model, kt_c, kq_c, io)));
-      if (timed) HIP_TRY(hipEventRecord(e1, cs));
+      if (timed_c) HIP_TRY(hipEventRecord(e1, cs));
     } else if (!lane) {  // wave-per-instance task kernel on every instance, then the QP
       if (int r = launch_task(cs)) return r;
-      if (timed) HIP_TRY(hipEventRecord(e1, cs));
+      if (timed_c) HIP_TRY(hipEventRecord(e1, cs));
       if (!stages)
         if (int r = launch_qp()) return r;
     } else {
@@ -806,7 +820,7 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
       io.hard_flag = stages ? nullptr : hard_flag + b0;
       const unsigned gl = static_cast<unsigned>((Bc + 63) / 64);  // one lane per instance
       HIP_TRY(static_cast<hipError_t>(launch_lane_task_kernel(dm.nv, gl, cs, m->d_model, kt_c, io)));
-      if (timed) HIP_TRY(hipEventRecord(e1, cs));
+      if (timed_c) HIP_TRY(hipEventRecord(e1, cs));
       io.hard_mode = 1;
       if (stages || ls != 1) {  // hard task kernel, then one QP pass over every instance
         if (int r = launch_task(cs)) return r;
@@ -829,14 +843,17 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
       }
       io.hard_mode = 0;
     }
-    if (timed) HIP_TRY(hipEventRecord(e2, cs));
+    if (timed_c && !fuse) HIP_TRY(hipEventRecord(e2, cs));
     if (own) HIP_TRY(hipEventRecord(m->ln.joins[c], cs));
   }
   for (int c = 0; c < S - 1; ++c) HIP_TRY(hipStreamWaitEvent(st, m->ln.joins[c], 0));
   if (timed) {
-    HIP_TRY(hipEventRecord(e_end, st));
+    if (S > 1) HIP_TRY(hipEventRecord(e_end, st));
+    std::vector<hipEvent_t> ev = S > 1 ? std::vector<hipEvent_t>{e_start, e_end, t0e, t1e, t2e}
+                                       : std::vector<hipEvent_t>{t0e, t2e, t0e, t1e, t2e};
     std::lock_guard<std::mutex> g(m->mu);
-    m->events.push_back(tev);
+    m->events.push_back({ev, S});
+    (void)tev;
   }
   done_guard.ok = true;
   return DRC_OK;
@@ -1091,7 +1108,8 @@ int drc_debug_kernel_times(drc_model* m, double* wall_ms, double* task_ms, doubl
   if (!m || !wall_ms || !task_ms || !qp_ms || !calls) return drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "null argument");
   std::lock_guard<std::mutex> g(m->mu);
   double tw = 0, t0 = 0, t1 = 0;
-  for (auto& ev : m->events) {  // {start, end, [task start, task end, qp end] per chunk}
+  for (auto& evs : m->events) {  // {start, end, task start, task end, qp end}, sub-batches
+    const std::vector<hipEvent_t>& ev = evs.first;
     float a = 0;
     if (hipEventSynchronize(ev[1]) != hipSuccess) return drc_amd::set_err(DRC_ERR_HIP, "hipEventSynchronize");
     if (hipEventElapsedTime(&a, ev[0], ev[1]) != hipSuccess) return drc_amd::set_err(DRC_ERR_HIP, "hipEventElapsedTime");
@@ -1101,13 +1119,17 @@ int drc_debug_kernel_times(drc_model* m, double* wall_ms, double* task_ms, doubl
       if (hipEventElapsedTime(&x, ev[c], ev[c + 1]) != hipSuccess ||
           hipEventElapsedTime(&y, ev[c + 1], ev[c + 2]) != hipSuccess)
         return drc_amd::set_err(DRC_ERR_HIP, "hipEventElapsedTime");
-      t0 += x;
-      t1 += y;
+      t0 += x * evs.second;  // the timed launch stands for the call's sub-batches
+      t1 += y * evs.second;
     }
   }
   *calls = static_cast<int>(m->events.size());
-  for (auto& ev : m->events)
-    for (hipEvent_t e : ev) m->evpool.push_back(e);  // completed: reusable
+  for (auto& evs : m->events) {  // completed: reusable (each event once: a call's list may name one twice)
+    std::vector<hipEvent_t> u = evs.first;
+    std::sort(u.begin(), u.end());
+    u.erase(std::unique(u.begin(), u.end()), u.end());
+    for (hipEvent_t e : u) m->evpool.push_back(e);
+  }
   m->events.clear();
   *wall_ms = tw;
   *task_ms = t0;
@@ -1254,8 +1276,12 @@ void drc_model_destroy(drc_model* m) {
   if (m->stage) (void)hipFree(m->stage);
   if (m->pinned) (void)hipHostFree(m->pinned);
   if (m->hdone) (void)hipEventDestroy(m->hdone);
-  for (auto& ev : m->events)
-    for (hipEvent_t e : ev) (void)hipEventDestroy(e);
+  for (auto& evs : m->events) {
+    std::vector<hipEvent_t> u = evs.first;
+    std::sort(u.begin(), u.end());
+    u.erase(std::unique(u.begin(), u.end()), u.end());
+    for (hipEvent_t e : u) (void)hipEventDestroy(e);
+  }
   for (hipEvent_t e : m->evpool) (void)hipEventDestroy(e);
   delete m;
 }
