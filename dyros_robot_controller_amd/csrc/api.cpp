@@ -768,11 +768,12 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
     HIP_TRY(hipMemsetAsync(qc, 0, StreamCtx::kSlotInts * sizeof(int), cs));
     io.queue = qc;
     hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr;
-    // kernel timing: the sub-batch on the caller's stream only (its task and
-    // QP launches stand for the call's S; every marker is a queue packet
-    // between two kernels: 14 per four-sub-batch call cost 1.5 % of the
-    // FR3 bench, 5 per fused call 6 % at B = 4 096)
-    const bool timed_c = timed && c == S - 1;
+    // kernel timing: every sub-batch's task and QP launches (each marker is a
+    // queue packet between two kernels; a call of one sub-batch records two or
+    // three: the five of r05 cost 6 % at FR3 B = 4 096.  Timing only the
+    // caller-stream sub-batch of a four-sub-batch call saved 1.5 % but its
+    // events then disagreed with rocprofv3's kernel averages by ~40 %, r05fin)
+    const bool timed_c = timed;
     if (timed_c) {
       if (int r = mkev(&e0)) return r;
       if (int r = mkev(&e1)) return r;
@@ -849,11 +850,9 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
   for (int c = 0; c < S - 1; ++c) HIP_TRY(hipStreamWaitEvent(st, m->ln.joins[c], 0));
   if (timed) {
     if (S > 1) HIP_TRY(hipEventRecord(e_end, st));
-    std::vector<hipEvent_t> ev = S > 1 ? std::vector<hipEvent_t>{e_start, e_end, t0e, t1e, t2e}
-                                       : std::vector<hipEvent_t>{t0e, t2e, t0e, t1e, t2e};
+    std::vector<hipEvent_t> ev = S > 1 ? tev : std::vector<hipEvent_t>{t0e, t2e, t0e, t1e, t2e};
     std::lock_guard<std::mutex> g(m->mu);
     m->events.push_back({ev, S});
-    (void)tev;
   }
   done_guard.ok = true;
   return DRC_OK;
@@ -1119,8 +1118,8 @@ int drc_debug_kernel_times(drc_model* m, double* wall_ms, double* task_ms, doubl
       if (hipEventElapsedTime(&x, ev[c], ev[c + 1]) != hipSuccess ||
           hipEventElapsedTime(&y, ev[c + 1], ev[c + 2]) != hipSuccess)
         return drc_amd::set_err(DRC_ERR_HIP, "hipEventElapsedTime");
-      t0 += x * evs.second;  // the timed launch stands for the call's sub-batches
-      t1 += y * evs.second;
+      t0 += x;
+      t1 += y;
     }
   }
   *calls = static_cast<int>(m->events.size());

@@ -282,10 +282,8 @@ int drc_debug_lds_plan(drc_model* model, const drc_qpik_params* params, int prob
                        int* fused_bytes);
 /* wall_ms: summed caller-stream time of the timed calls (fork to join; a call
  * of one sub-batch: its first kernel's start to its last kernel's end);
- * task_ms / qp_ms: the durations of the task / QP kernel of the sub-batch on
- * the caller's stream (the one timed launch of each per call: every event is
- * a queue packet between two kernels) times the call's sub-batch count,
- * summed over the timed calls (the sub-batches overlap in time). */
+ * task_ms / qp_ms: summed durations of the task / QP kernels of every
+ * sub-batch (they overlap in time when a call runs several sub-batches). */
 int drc_debug_kernel_times(drc_model* model, double* wall_ms, double* task_ms, double* qp_ms, int* calls);
 /* Register-budget occupancy (waves per SIMD) of the QPIK task-kernel build a
  * call with these params launches (two- or three-wave build, chosen from its
