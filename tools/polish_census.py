@@ -73,8 +73,8 @@ def main():
     ap.add_argument("--tol", type=float, nargs="*", default=[1e-6, 1e-4, 1e-3, 1e-2])
     ap.add_argument("--guess", type=int, default=-1, help="first-guess rule of the polish (-1: OSQP's)")
     ap.add_argument("--check", type=int, default=0, help="check_termination (0: the default 25)")
-    ap.add_argument("--feas-drop", type=int, default=1, help="study: infeasible-phase drop mode (oracle_polish_feas)")
-    ap.add_argument("--feas-att", type=int, default=5, help="study: infeasible-phase attempts")
+    ap.add_argument("--feas-drop", type=int, default=5, help="study: infeasible-phase drop mode (oracle_polish_feas)")
+    ap.add_argument("--feas-att", type=int, default=6, help="study: infeasible-phase attempts")
     ap.add_argument("--npz", help="inputs from a device dump (tools/dump_batch.py) instead of the CPU generator")
     ap.add_argument("--refine", type=int, default=-1, help="polish_refine_iter (-1: the default 3)")
     a = ap.parse_args()
