@@ -1390,11 +1390,14 @@ int drc_default_qpik_params(const drc_model* m, int exact, drc_qpik_params* p) {
   s.eps_fallback = 1e-7;
   // exact mode: the ADMM iterate only seeds the certified polish's first
   // active-set guess, so how often it is tried is a speed choice.  With the
-  // projected-Jacobi guess the first polish pays off at iteration 20: +1-2.5 %
-  // on all five robots against 25 (profiles/r05h_envab_check20.jsonl; 15 helps
-  // UR5e and costs FR3, profiles/r05g_envab_check.jsonl).  The oracle's exact
-  // mode uses the same interval.  DRC_EXACT_CHECK overrides (A/B experiments)
-  static const int64_t exact_check = drc_amd::env_int("DRC_EXACT_CHECK", 20, 1);
+  // projected-Jacobi guess the first polish paid off at iteration 20 (+1-2.5 %
+  // against 25, profiles/r05h_envab_check20.jsonl); with the infeasible-phase
+  // drop rule it pays off far earlier: manipulators at 8 (FR3 +7 %, UR5e +4 %;
+  // below 8 UR5e loses), the whole-body QPs at 2 (XLS-FR3 +12 %, Husky-FR3
+  // +6 %; profiles/r05ae-ag_envab_check*.jsonl).  The oracle's exact mode uses
+  // the same intervals.  DRC_EXACT_CHECK overrides both (A/B experiments)
+  static const int64_t exact_check_env = drc_amd::env_int("DRC_EXACT_CHECK", 0, 0);
+  const int64_t exact_check = exact_check_env > 0 ? exact_check_env : (moma ? 2 : 8);
   // OSQP's 3 refinement steps.  2 certify the same attempts at eps_exact
   // (tools/polish_census.py --refine; 1 fails half) and measured UR5e +1.1 %,
   // FR3 +0.1 % (profiles/r05b_envab.jsonl), but leave ~2e-9 in q-dot on some

@@ -2356,8 +2356,9 @@ void oracle_default_params(int kind, OracleParams* p, int exact) {
     s->polish_cap = kind == 0 ? 16 : 0;
     s->polish_add_all = 1;
     s->polish_guess = exact ? 2 : 0;
-    /* parity mode: the first polish at iteration 20 (kernel: drc_default_qpik_params) */
-    if (exact) s->check_termination = 20;
+    /* parity mode: the first polish at iteration 8 (manipulators) / 2 (whole-body)
+     * (kernel: drc_default_qpik_params) */
+    if (exact) s->check_termination = kind == 0 ? 8 : 2;
 }
 
 /* Farkas certificate for the whole-body QP (mobile_manipulator/QP_IK.cpp:
