@@ -247,7 +247,8 @@ def latency_b1(rd, robot, q, qd, xt, xdt, solver, calls=400, warmup=20):
                  "outside_library_slowest_us": float(ts[worst] - (tl[worst, 4] - tl[worst, 0]) / 1e3)
                  if len(ph) == calls else None,
                  "library_max_us": float((tl[:n.value, 4] - tl[:n.value, 0]).max() / 1e3) if n.value else None,
-                 "host_wait": "poll" if int(os.environ.get("DRC_HOST_WAIT", "1")) else "block",
+                 "host_wait": ("poll up to %s us, then block" % os.environ.get("DRC_HOST_WAIT", "300"))
+                 if int(os.environ.get("DRC_HOST_WAIT", "300")) else "block",
                  "calls_over_us": {str(t): int(np.sum(ts > t)) for t in (200, 300, 500)}}
     return {"call": "QPIKCubic, B = 1, drc_qpik_host (host buffers in and out, synchronous)",
             "p50_us": float(np.percentile(ts, 50)), "p99_us": float(np.percentile(ts, 99)),
@@ -551,45 +552,47 @@ def extras(torch, args, rd, mod, robot, link, q, qd, xt, xdt, dq, dqd, dxt, dxdt
     it1 = torch.zeros(1, dtype=torch.int32, device=dq.device)
     ones = [[t[:, k:k + 1].contiguous() for t in (dq, dqd, dxt, dxdt)] for k in range(32)]
     # the two-kernel pipeline (what a full batch runs): task and QP kernel apart
-    _capi.check(lib.drc_set_fusion(h, C.c_int(0)))
-    for one in ones:
-        ctrl.QPIK_step_batch(*one, link, iters=it1)
-    torch.cuda.synchronize()
-    _capi.check(lib.drc_debug_kernel_timing(h, 1))
-    for one in ones:
-        for _ in range(3):
-            ctrl.QPIK_step_batch(*one, link, iters=it1)
-    torch.cuda.synchronize()
-    tw, tk, tq, nc = C.c_double(), C.c_double(), C.c_double(), C.c_int()
-    _capi.check(lib.drc_debug_kernel_times(h, C.byref(tw), C.byref(tk), C.byref(tq), C.byref(nc)))
-    _capi.check(lib.drc_debug_kernel_timing(h, 0))
-    # task / QP latency (seconds) from the kernels' own per-instance stamps
-    # (drc_debug_qpik_stamps: task start -> end, QP start -> stored); HIP events
-    # between two back-to-back kernels on one stream put most of the QP
-    # kernel's time into the task kernel's on this stack (r05 stamp study)
+    # (the params builder fills the model kind's defaults: manipulator or whole-body)
     from dyros_robot_controller_amd import manipulator as _man
     p1 = _man.QPIKParamsBuilder(rd.model, exact=(args.solver == "exact")).params(link, _capi.MODE_QPIK_STEP)
-    dpp = lambda a: a.ctypes.data_as(C.POINTER(C.c_double))
-    ipp = lambda a: a.ctypes.data_as(C.POINTER(C.c_int))
-    nout = rd.model.actuated_dof
-    lts, lqs = [], []
-    for one in ones:
-        cols = [np.ascontiguousarray(t.cpu().numpy()) for t in one]
-        o1, s1, i1 = np.zeros((nout, 1)), np.zeros(1, np.int32), np.zeros(1, np.int32)
-        stp = np.zeros((8, 1), np.uint64)
-        for _ in range(2):
-            _capi.check(lib.drc_debug_qpik_stamps(h, C.byref(p1), C.c_int64(1), dpp(cols[0]), dpp(cols[1]),
-                                                  dpp(cols[2]), dpp(cols[3]), dpp(cols[2]), dpp(cols[3]), dpp(o1),
-                                                  ipp(s1), ipp(i1), stp.ctypes.data_as(C.POINTER(C.c_uint64))))
-        t = stp[:6, 0].astype(np.int64)
-        lts.append((t[1] - t[0]) * 1e-8)
-        lqs.append((t[5] - t[2]) * 1e-8)
-    _capi.check(lib.drc_set_fusion(h, C.c_int(1)))
+    _capi.check(lib.drc_set_fusion(h, C.c_int(0)))
+    try:
+        for one in ones:
+            ctrl.QPIK_step_batch(*one, link, iters=it1)
+        torch.cuda.synchronize()
+        _capi.check(lib.drc_debug_kernel_timing(h, 1))
+        for one in ones:
+            for _ in range(3):
+                ctrl.QPIK_step_batch(*one, link, iters=it1)
+        torch.cuda.synchronize()
+        tw, tk, tq, nc = C.c_double(), C.c_double(), C.c_double(), C.c_int()
+        _capi.check(lib.drc_debug_kernel_times(h, C.byref(tw), C.byref(tk), C.byref(tq), C.byref(nc)))
+        _capi.check(lib.drc_debug_kernel_timing(h, 0))
+        # task / QP latency (seconds) from the kernels' own per-instance stamps
+        # (drc_debug_qpik_stamps: task start -> end, QP start -> stored); HIP events
+        # between two back-to-back kernels on one stream put most of the QP
+        # kernel's time into the task kernel's on this stack (r05 stamp study)
+        dpp = lambda a: a.ctypes.data_as(C.POINTER(C.c_double))
+        ipp = lambda a: a.ctypes.data_as(C.POINTER(C.c_int))
+        nout = rd.model.actuated_dof
+        lts, lqs = [], []
+        for one in ones:
+            cols = [np.ascontiguousarray(t.cpu().numpy()) for t in one]
+            o1, s1, i1 = np.zeros((nout, 1)), np.zeros(1, np.int32), np.zeros(1, np.int32)
+            stp = np.zeros((8, 1), np.uint64)
+            for _ in range(2):
+                _capi.check(lib.drc_debug_qpik_stamps(h, C.byref(p1), C.c_int64(1), dpp(cols[0]), dpp(cols[1]),
+                                                      dpp(cols[2]), dpp(cols[3]), dpp(cols[2]), dpp(cols[3]), dpp(o1),
+                                                      ipp(s1), ipp(i1), stp.ctypes.data_as(C.POINTER(C.c_uint64))))
+            t = stp[:6, 0].astype(np.int64)
+            lts.append((t[1] - t[0]) * 1e-8)
+            lqs.append((t[5] - t[2]) * 1e-8)
+    finally:
+        _capi.check(lib.drc_set_fusion(h, C.c_int(1)))
     lt, lq = float(np.mean(lts)), float(np.mean(lqs))
     # waves per CU of each kernel as the call launches it: the register build's
     # waves per SIMD (drc_debug_waves) x 4, capped by the LDS plan (drc_debug_lds_plan)
-    from dyros_robot_controller_amd import manipulator
-    p = manipulator.QPIKParamsBuilder(rd.model, exact=(args.solver == "exact")).params(link, _capi.MODE_QPIK_STEP)
+    p = p1
     wt, wq, bt, bq, bf = C.c_int(), C.c_int(), C.c_int(), C.c_int(), C.c_int()
     _capi.check(lib.drc_debug_waves(h, C.byref(p), C.byref(wt), C.byref(wq)))
     _capi.check(lib.drc_debug_lds_plan(h, C.byref(p), 0, C.byref(bt), C.byref(bq), C.byref(bf)))

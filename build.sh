@@ -22,7 +22,7 @@ FLAGS="--offload-arch=gfx950 -O3 -fPIC -std=c++17 -Wall -Wno-unused-function -ff
 # profiles/ counter summary can be matched to the build it was measured on
 # (bench.py ignores summaries of another build)
 # (and of the toolchain: the same sources built by another hipcc / ROCm are another build)
-BUILD_ID=$(cat $CSRC/*.hip $CSRC/*.hpp $CSRC/*.cpp include/drc_amd.h build.sh | { cat; echo "$FLAGS"; $HIPCC --version 2>&1; } | sha256sum | cut -c1-16)
+BUILD_ID=$(cat $CSRC/*.hip $CSRC/*.hpp $CSRC/*.cpp include/drc_amd.h include/drc_amd_debug.h build.sh | { cat; echo "$FLAGS"; $HIPCC --version 2>&1; } | sha256sum | cut -c1-16)
 pids=()
 for src in task_kernel.hip qp_kernel.hip fused_kernel.hip qpid_kernel.hip dynamics.hip api.cpp model.cpp; do
   XF=""

@@ -32,7 +32,7 @@ MODE_QPID, MODE_QPID_STEP, MODE_QPID_CUBIC = 0, 1, 2
 DRIVE_DIFFERENTIAL, DRIVE_MECANUM, DRIVE_CASTER = 0, 1, 2
 MAX_WHEELS = 8
 
-# every symbol include/drc_amd.h declares (checked by tests/test_capi_symbols.py)
+# every symbol include/drc_amd.h and include/drc_amd_debug.h declare (checked by tests/test_capi.py)
 EXPORTED_SYMBOLS = (
     "drc_model_create_manipulator", "drc_model_create_mobile_manipulator", "drc_model_destroy",
     "drc_model_info", "drc_model_limits", "drc_model_find_frame", "drc_model_mobile_fk_jacobian",

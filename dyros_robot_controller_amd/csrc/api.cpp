@@ -8,6 +8,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdlib>
+#include <cstddef>
 #include <cstdio>
 #include <cstring>
 #include <memory>
@@ -17,6 +18,7 @@
 #include <vector>
 
 #include "../../include/drc_amd.h"
+#include "../../include/drc_amd_debug.h"
 #include "dynamics.hpp"
 #include "kernel_common.hpp"
 #include "launch.hpp"
@@ -143,16 +145,24 @@ static void free_ctx(StreamCtx* c) {
 
 // Records a stream context's `done` event on every exit of a launch path
 // once the context is in use, so eviction (free_ctx) never frees scratch that
-// kernels of this call still use.  A call that fails after enqueueing part of
-// its work may have left kernels on the internal fork streams that `done` on
-// the caller's stream does not follow: that path drains the device first.
+// kernels of this call still use.  Every launch path enqueues on the caller's
+// stream only, except the QPIK path's concurrent sub-batches: a call that
+// fails after forking may have left kernels on the model's internal fork /
+// side streams that `done` on the caller's stream does not follow, so that
+// path (forks set) waits for those streams -- the model's own, never the
+// device: other streams and models in the process are not stalled, and a
+// failure before anything was forked costs no synchronisation at all.
 struct DoneGuard {
   StreamCtx* const& cx;
   hipStream_t st;
+  const Lanes* forks = nullptr;  // set once a sub-batch may run on a fork stream
   bool ok = false;
   ~DoneGuard() {
     if (!cx || !cx->done) return;
-    if (!ok) (void)hipDeviceSynchronize();
+    if (!ok && forks) {
+      for (hipStream_t s : forks->lanes) (void)hipStreamSynchronize(s);
+      for (hipStream_t s : forks->sides) (void)hipStreamSynchronize(s);
+    }
     (void)hipEventRecord(cx->done, st);
   }
 };
@@ -520,8 +530,21 @@ static int plan_layout(const DevModel& M, KParams* k, bool task_only) {
     k->kEpa = scr0;
     const int ep = scr0 + ((static_cast<int>((sizeof(EpaPoly) + 7) / 8) + 1) & ~1);
     u = u > ep ? u : ep;
-    k->kCand = scr0;  // int list of the GJK candidates
-    const int ce = scr0 + (M.npairs + 1) / 2;
+    // int list of the GJK candidates, in the polytope's face planes (fn, fd):
+    // the candidate GJKs write the EPA seed stash (epa_stash: vertex slots
+    // kEpaStashV0.., out[], nv) while later candidates are still being read,
+    // so the list must not overlap those; the face planes are only written
+    // once EPA starts, after the last candidate is consumed
+    static_assert(offsetof(EpaPoly, fn) % 8 == 0 && offsetof(EpaPoly, fd) == offsetof(EpaPoly, fn) + sizeof(EpaPoly::fn),
+                  "face planes: one contiguous double-aligned region");
+    static_assert(sizeof(EpaPoly::fn) + sizeof(EpaPoly::fd) >= kMaxPairs * sizeof(int),
+                  "the face planes hold a candidate list of kMaxPairs ints");
+    static_assert(offsetof(EpaPoly, fn) >= sizeof(EpaPoly::vw) + sizeof(EpaPoly::va) &&
+                      offsetof(EpaPoly, out) >= offsetof(EpaPoly, fd) + sizeof(EpaPoly::fd) &&
+                      offsetof(EpaPoly, nv) > offsetof(EpaPoly, out),
+                  "stash (vw / va slots, out[], nv) outside the candidate list");
+    k->kCand = scr0 + static_cast<int>(offsetof(EpaPoly, fn) / 8);
+    const int ce = k->kCand + (M.npairs + 1) / 2;
     u = u > ce ? u : ce;
   } else {
     k->kEpa = 0;
@@ -740,6 +763,7 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
     if (int r = mkev(&e_end)) return r;
     HIP_TRY(hipEventRecord(e_start, st));
   }
+  done_guard.forks = &m->ln;  // (launch_mu held: the stream lists do not change under it)
   if (S > 1) HIP_TRY(hipEventRecord(m->ln.fork, st));
   for (int c = 0; c < S; ++c) {
     const int64_t b0 = B * c / S, b1 = B * (c + 1) / S, Bc = b1 - b0;
@@ -1565,19 +1589,23 @@ static inline int64_t now_ns() {
   return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
       .count();
 }
-// How a synchronous entry waits for its copy back (DRC_HOST_WAIT): 1 (default)
-// polls the completion event, 0 blocks in hipEventSynchronize.  Polling keeps
-// the calling thread on its core for the ~100 us of one B = 1 cycle instead of
-// handing it to the scheduler and waking it up again.
+// How a synchronous entry waits for its copy back (DRC_HOST_WAIT, in us): it
+// polls the completion event for up to that long (default 300 us: one B = 1
+// cycle is ~100 us, polling keeps the thread on its core instead of handing
+// it to the scheduler and waking it up again), with a pause between polls,
+// then blocks in hipEventSynchronize -- a long call (large B) does not hold a
+// core busy for its whole GPU time.  0: block at once.
 static int wait_done(drc_model* m) {
-  static const int64_t spin = env_int("DRC_HOST_WAIT", 1, 0);
+  static const int64_t spin_ns = 1000 * env_int("DRC_HOST_WAIT", 300, 0);
   if (hipEventRecord(m->hdone, m->hstream) != hipSuccess) return drc_amd::set_err(DRC_ERR_HIP, "hipEventRecord");
-  if (spin) {
-    for (;;) {
+  if (spin_ns > 0) {
+    const int64_t t_end = now_ns() + spin_ns;
+    do {
       const hipError_t e = hipEventQuery(m->hdone);
       if (e == hipSuccess) return DRC_OK;
       if (e != hipErrorNotReady) return drc_amd::set_err(DRC_ERR_HIP, "hipEventQuery");
-    }
+      for (int k = 0; k < 16; ++k) __builtin_ia32_pause();
+    } while (now_ns() < t_end);
   }
   if (hipEventSynchronize(m->hdone) != hipSuccess) return drc_amd::set_err(DRC_ERR_HIP, "hipEventSynchronize");
   return DRC_OK;

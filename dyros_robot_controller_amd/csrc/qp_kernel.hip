@@ -14,8 +14,11 @@ namespace drc_amd {
 // record written by task_kernel.
 // Occupancy target (waves per SIMD): 3 (168 VGPRs) since the ADMM loop keeps
 // one register set per lane role (core / auxiliary variable) and fits without
-// spills in its iterations; the spills at this budget sit in the per-instance
-// prologue and around the every-25-iterations check
+// spills in its iterations; the spills at this budget (a 320-336 B per-lane
+// scratch frame for the compiled shapes) sit in the per-instance prologue and
+// in the termination check with the certified polish (admm_check, every 8 /
+// 2 ADMM iterations in exact mode, OSQP's 25 in reference mode; DESIGN.md
+// "Traffic")
 #ifndef DRC_QP_WAVES
 #define DRC_QP_WAVES 3
 #endif

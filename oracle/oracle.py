@@ -237,7 +237,12 @@ def load(robot):
     """Returns (pyref Model, OracleModel, spec)."""
     spec = ROBOTS[robot]
     rd = robots_dir()
-    pm = pyref_model.load_urdf(os.path.join(rd, spec["urdf"]), os.path.join(rd, spec["srdf"]))
+    return load_paths(os.path.join(rd, spec["urdf"]), os.path.join(rd, spec["srdf"]), spec)
+
+
+def load_paths(urdf, srdf, spec):
+    """load() for any URDF / SRDF (srdf may be None) with a ROBOTS-style spec."""
+    pm = pyref_model.load_urdf(urdf, srdf)
     om = OracleModel()
     om.nv = pm.nv
     for j in range(1, pm.nv + 1):

@@ -632,6 +632,29 @@ def build_qp_moma(m, q, S, xdot_des, link, mani_start_j, mani_start_a, n_arm, ma
     return P, qv, A, l, u
 
 
+def pose_from12(v12):
+    """[R col-major (9) | p (3)] (the C-ABI pose layout) -> 4 x 4."""
+    T = np.eye(4)
+    T[:3, :3] = np.asarray(v12[:9]).reshape(3, 3).T
+    T[:3, 3] = v12[9:]
+    return T
+
+
+def moma_step_qp(m, q, S, x_target12, xdot_target, link, mani_start_j, mani_start_a, n_arm, dist, kp=400.0):
+    """MobileManipulator::RobotController::QPIKStep's QP for one robot
+    (mobile_manipulator/robot_controller.cpp:170-180: xdot_des = Kp e +
+    xdot_target, Kp = 400 (:15), no Kv term) over build_qp_moma, with the
+    arm-block manipulability computed here and the distance stage (d,
+    grad d[arm]) supplied.  Returns (P, q, A, l, u, xdot_des, (m, grad m))."""
+    arm = np.arange(mani_start_j, mani_start_j + n_arm)
+    x = frame_pose(m, fk(m, q), link)
+    e, _ = task_space_error(pose_from12(x_target12), xdot_target, x, np.zeros(6))
+    xdd = kp * e + xdot_target
+    man = manipulability(m, q, link, arm)
+    P, qv, A, l, u = build_qp_moma(m, q, S, xdd, link, mani_start_j, mani_start_a, n_arm, man=man, dist=dist)
+    return P, qv, A, l, u, xdd, man
+
+
 def build_qp_qpid(m, q, qd, Jt, xdd, jdot_v, M, g, man, dist, arm, arm_col, slacks):
     """QPID's QP (manipulator/QP_ID.cpp:85-192 with slacks; MoMa QP_ID.cpp:
     66-184 without).  Jt: 6 x na task Jacobian over the QP's task variables,

@@ -1,5 +1,6 @@
 """The C-ABI library loads (no GPU needed) and exports every function that
-include/drc_amd.h declares; the Python ctypes layer mirrors the structs."""
+include/drc_amd.h (the drop-in boundary) and include/drc_amd_debug.h (the
+diagnostic entries) declare; the Python ctypes layer mirrors the structs."""
 import ctypes
 import os
 import re
@@ -9,8 +10,8 @@ from dyros_robot_controller_amd import _capi
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _declared():
-    src = open(os.path.join(ROOT, "include", "drc_amd.h")).read()
+def _declared(header="drc_amd.h"):
+    src = open(os.path.join(ROOT, "include", header)).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"\b(drc_[a-z0-9_]+)\s*\(", src)))
 
@@ -18,10 +19,13 @@ def _declared():
 def test_header_symbols_exported():
     lib = ctypes.CDLL(_capi.LIB_PATH)
     names = _declared()
+    debug = _declared("drc_amd_debug.h")
     assert len(names) >= 12
-    for n in names:
+    assert debug and all(n.startswith("drc_debug_") for n in debug)
+    assert not any(n.startswith("drc_debug_") for n in names)   # diagnostics stay out of the boundary
+    for n in names + debug:
         assert hasattr(lib, n), n
-    assert set(names) == set(_capi.EXPORTED_SYMBOLS)
+    assert set(names) | set(debug) == set(_capi.EXPORTED_SYMBOLS)
 
 
 def test_error_strings():

@@ -23,7 +23,7 @@ def test_oracle_reproduces_golden(path):
 
 
 def test_golden_present():
-    assert len(GOLD) == 6
+    assert len(GOLD) == 15   # FR3, UR5e, Husky-FR3, XLS-FR3, Caster-FR3 x seeds 0, 1, 2
 
 
 @pytest.mark.parametrize("path", GOLD, ids=[os.path.basename(p) for p in GOLD])

@@ -102,7 +102,13 @@ def test_device_narrow_phase_matches_oracle(harness):
     sep = dev[:, 4:7] - dev[:, 1:4]
     sep_ref = ref[:, 4:7] - ref[:, 1:4]
     serr = np.abs(sep - sep_ref).max(axis=1)
-    assert serr[~pen].max() <= 3e-3, serr[~pen].max()
+    # per pair: two GJK stops within the gap eps = 1e-6 of the distance d
+    # leave the separation vector (length d) within ~d * sqrt(2 eps / d) =
+    # sqrt(2 eps d) of the exact one on each side; the bound takes twice
+    # that sum (derived, not fitted: the largest observed ratio is below 1)
+    dsep = np.abs(ref[~pen, 0])
+    bound = 2 * 2 * np.sqrt(2e-6 * np.maximum(dsep, 1e-12)) + 1e-9
+    assert np.all(serr[~pen] <= bound), np.max(serr[~pen] / bound)
     assert np.median(serr[~pen]) <= 1e-12
     assert serr[pen].max() <= 1e-3, serr[pen].max()
     assert np.quantile(serr[pen], 0.9) <= 1e-7

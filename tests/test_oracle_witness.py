@@ -78,7 +78,12 @@ def test_refined_witnesses_certified(robot, seed):
     assert refined >= 10
 
 
-@pytest.mark.parametrize("robot,seed", [("ur5e", 1), ("caster_fr3", 2)])
+# seeds whose batch holds a GJK / EPA winner whose raw witness moves under the
+# 1e-13 perturbation (a GJK stop one iteration apart).  Since GJK stops at
+# hpp-fcl's 1e-6 support gap the raw witness can move by up to ~sqrt(gap * d)
+# (~1e-5 here: XLS-FR3 seeds 7 and 10 move 9.4e-6 / 1.2e-5; seed 2 no longer
+# changes path), so each robot is held at a seed that does
+@pytest.mark.parametrize("robot,seed", [("ur5e", 1), ("caster_fr3", 2), ("xls_fr3", 7), ("xls_fr3", 10)])
 def test_refinement_removes_path_dependence(robot, seed):
     pm, om, q = _batch(robot, seed, 160)
     raw_move, ref_move = [], []

@@ -2,12 +2,14 @@
 """Generate the committed golden fixtures under tests/golden/.
 
 Inputs: counter-based synthetic batches (workload.py, fixture seeds 0, 1, 2)
-with targets built from the numpy FK (oracle/pyref.py).  Expected outputs:
+with targets built from the numpy FK (oracle/pyref.py): nominal for the
+manipulators (FR3, UR5e), stress tiers plus PrimalInfeasible instances for
+the whole-body robots (Husky-FR3, XLS-FR3, Caster-FR3).  Expected outputs:
 the C restatement (oracle/drc_oracle.c) in exact mode, each QP solution
 cross-checked against the independent numpy interior-point solver with a
 KKT certificate before it is written.  Run in the build container:
 
-    python tools/gen_golden.py
+    python tools/gen_golden.py [robot ...]
 """
 import os
 import sys
@@ -21,7 +23,8 @@ import oracle as O  # noqa: E402
 import pyref as R  # noqa: E402
 from dyros_robot_controller_amd import workload  # noqa: E402
 
-LINK = {"fr3": "fr3_link8", "ur5e": "tool0"}
+LINK = {"fr3": "fr3_link8", "ur5e": "tool0", "husky_fr3": "fr3_link8", "xls_fr3": "fr3_link8",
+        "caster_fr3": "fr3_link8"}
 
 
 def pose12(T):
@@ -86,7 +89,78 @@ def gen(robot, seed, B):
     print("wrote", path, "B =", B)
 
 
+def moma_selection(pm, spec, q):
+    """S of mobile_manipulator/robot_data.cpp:22-25,115-120 (numpy)."""
+    vs, ms, ws = spec["joint_index"]
+    nw = spec["n_wheel"]
+    Jm = spec["J_mobile"](q[ws:ws + nw]) if spec.get("drive") == 2 else spec["J_mobile"]()
+    return R.selection_matrix(pm.nv, spec["n_arm"], nw, spec["joint_index"], spec["actuator_index"], Jm, q[vs + 2])
+
+
+def gen_moma(robot, seed, B=96, pool=1500, n_infeasible=12):
+    """Whole-body QPIKStep fixture (mobile_manipulator/QP_IK.cpp:59-128): a
+    stress-tier batch -- its first B - k instances plus the first
+    k PrimalInfeasible instances of a pool of ``pool`` -- so the fixture holds
+    the status the whole-body QP's missing slacks make possible.  Each
+    instance is certified independently of the C oracle: the numpy QP
+    (pyref.moma_step_qp) solved by the interior point with a KKT certificate,
+    or found infeasible by HiGHS (pyref.feasible)."""
+    pm, om, spec = O.load(robot)
+    nv = pm.nv
+    lo, hi, v = (np.array(a[:nv]) for a in (om.lower, om.upper, om.vel))
+    vs, ms, ws = spec["joint_index"]
+    n = spec["n_arm"]
+    am = spec["actuator_index"][0]
+    q, qd = workload.mobile_states(lo, hi, v, (vs, ms, ws), n, spec["n_wheel"], seed, pool, 0)
+
+    def ev(qs):
+        m = np.array([O.manipulability(om, qs[:, b])[0] for b in range(qs.shape[1])])
+        d = np.array([O.min_distance(om, qs[:, b])[0] for b in range(qs.shape[1])])
+        return m, d
+    workload.apply_stress(q, lo, hi, list(range(ms, ms + n)), seed, 0, ev)
+    poses = np.stack([pose12(R.frame_pose(pm, R.fk(pm, q[:, b]), LINK[robot])) for b in range(pool)], axis=1)
+    xt, xdt = workload.perturb_targets(poses, seed, pool, 0)
+    par = O.default_params(1, exact=True)
+    _, st_pool, _ = O.qpik_batch(om, par, q, qd, xt, xdt, nthreads=8)
+    inf = [b for b in range(B, pool) if st_pool[b] == O.PRIMAL_INFEASIBLE][:n_infeasible]
+    idx = np.array(list(range(B - len(inf))) + inf)
+    q, qd, xt, xdt, poses = (a[:, idx] for a in (q, qd, xt, xdt, poses))
+    out, status, _ = O.qpik_batch(om, par, q, qd, xt, xdt, nthreads=8)
+    man = np.zeros((1 + n, B))
+    dist = np.zeros((1 + nv, B))
+    pair = np.zeros(B, np.int32)
+    xdd = np.zeros((6, B))
+    for b in range(B):
+        st, o, dg = O.qpik_one(om, par, q[:, b], qd[:, b], xt[:, b], xdt[:, b])
+        assert st == status[b] and np.array_equal(o, out[:, b])
+        man[0, b], man[1:, b] = dg.man, np.array(dg.man_grad[:n])
+        dist[0, b], dist[1:, b] = dg.dist, np.array(dg.dist_grad[:nv])
+        pair[b] = dg.pair
+        xdd[:, b] = np.array(dg.xdot_des)
+        P, qv, A, l, u, xn, mn = R.moma_step_qp(pm, q[:, b], moma_selection(pm, spec, q[:, b]), xt[:, b], xdt[:, b],
+                                                LINK[robot], ms, am, n, (dg.dist, dist[1 + ms:1 + ms + n, b]))
+        assert np.max(np.abs(xn - xdd[:, b])) <= 1e-9 * max(1.0, np.max(np.abs(xn)))
+        assert abs(mn[0] - man[0, b]) <= 1e-12 and np.max(np.abs(mn[1] - man[1:, b])) <= 1e-9
+        x, y, s2 = R.solve_qp_exact(P, qv, A, l, u)
+        if s2 == 3:
+            assert st == O.PRIMAL_INFEASIBLE and np.all(o == 0.0), (robot, seed, b, st)
+        else:
+            assert st == O.SOLVED and s2 == 1, (robot, seed, b, st, s2)
+            assert max(R.kkt_residuals(P, qv, A, l, u, x, y)) < 1e-8
+            # P >= 0.01 I: the oracle's 1e-9-accepted point within ~1e-7 (tests/test_oracle_moma_qp.py)
+            assert np.max(np.abs(x - o)) < 1e-6, (robot, seed, b, np.max(np.abs(x - o)))
+        certify_distance(pm, om, q[:, b])
+    path = os.path.join(ROOT, "tests", "golden", "%s_qpik_step_seed%d.npz" % (robot, seed))
+    np.savez_compressed(path, q=q, qdot=qd, x_target=xt, xdot_target=xdt, poses=poses, qdot_opt=out,
+                        status=status, man=man, dist=dist, pair=pair, xdot_des=xdd)
+    print("wrote", path, "B =", B, "primal infeasible", int(np.sum(status == O.PRIMAL_INFEASIBLE)))
+
+
 if __name__ == "__main__":
-    for robot in ("fr3", "ur5e"):
+    which = sys.argv[1:] or ["fr3", "ur5e", "husky_fr3", "xls_fr3", "caster_fr3"]
+    for robot in which:
         for seed in (0, 1, 2):
-            gen(robot, seed, 96)
+            if O.ROBOTS[robot]["kind"] == 0:
+                gen(robot, seed, 96)
+            else:
+                gen_moma(robot, seed)
