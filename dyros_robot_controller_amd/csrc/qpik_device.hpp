@@ -41,7 +41,13 @@ __device__ __forceinline__ int lane_id() {
 // No vmcnt / lgkmcnt drain of unrelated accesses and no s_barrier
 // (__syncthreads waited for every outstanding global and scratch access at each
 // exchange).  -DDRC_BLOCK_SYNC restores __syncthreads.
-#ifndef DRC_BLOCK_SYNC
+#if defined(DRC_WSYNC_ASM)  // A/B variant: the r04 compiler-barrier form
+__device__ __forceinline__ void wsync() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
+#elif !defined(DRC_BLOCK_SYNC)
 __device__ __forceinline__ void wsync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();

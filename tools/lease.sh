@@ -14,7 +14,7 @@
 #   gpus2                      two-rank rehearsal on the one GPU (gloo), gpurun_out/gpus2_<tag>.json
 #   gpus:<n>[:<args>]          n-rank gloo rehearsal on the one GPU, extra bench.py args (commas become spaces)
 #   final[:<robot>,..]         round-end measurement (tools/final_round.sh)
-#   refcensus                  reference-settings census (tools/reference_census.py)
+#   refcensus[:bench]          reference-settings census (tools/reference_census.py [--bench])
 #   stamps:<robot>:<batch>[:<fusion>[:<concurrency>]]  small-batch makespan study (tools/stamp_study.py)
 set -o pipefail
 ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
@@ -85,9 +85,9 @@ for step in "$@"; do
     final)
       timeout -k 10 3000 bash tools/final_round.sh $TAG ${rest//,/ } || exit 1 ;;
     refcensus)
-      timeout -k 10 600 python3 -u tools/reference_census.py > gpurun_out/refcensus_$TAG.log 2>&1 \
-        || { tail -20 gpurun_out/refcensus_$TAG.log; exit 1; }
-      cut -c1-400 gpurun_out/refcensus_$TAG.log ;;
+      timeout -k 10 600 python3 -u tools/reference_census.py ${rest:+--$rest} > gpurun_out/refcensus_$TAG$rest.log 2>&1 \
+        || { tail -20 gpurun_out/refcensus_$TAG$rest.log; exit 1; }
+      cut -c1-400 gpurun_out/refcensus_$TAG$rest.log ;;
     stamps)
       IFS=: read -r robot batch fz cc <<< "$rest"
       timeout -k 10 300 python3 tools/stamp_study.py --robot $robot --batch $batch --fusion ${fz:--1} \

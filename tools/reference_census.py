@@ -40,7 +40,30 @@ def classify(robot, args, out, status, iters, check=25):
     rows = [{"b": int(b), "iters": [int(iters[b]), int(riters[b])], "status": [int(status[b]), int(rstat[b])],
              "dq": float(dq[b]), "gpu_vs_exact": float(band_g[b]), "oracle_vs_exact": float(band_o[b])}
             for b in np.nonzero(diverged)[0]]
+    # run-length growth of the rounding difference: same status and stopping
+    # iteration, max |d q-dot| per stopping iteration
+    same = (status == rstat) & (iters == riters) & (status == 1)
+    curve = {}
+    for k in np.unique(iters[same]):
+        sel = same & (iters == k)
+        curve[int(k)] = [int(sel.sum()), float(dq[sel].max())]
+    # device non-Solved where the oracle solved: how marginal the oracle's stop
+    # was (res_ratio: max(pri / eps_pri, dua / eps_dua) at its stop) and how
+    # path-dependent the oracle itself is there (8 copies with q moved by 1e-13)
+    nonsolved_rows = []
+    for b in np.nonzero((status != 1) & (rstat == 1))[0]:
+        _, _, dg = O.qpik_one(om, par, *[None if a is None else a[:, b] for a in args])
+        pert = []
+        for k in range(8):
+            a2 = [None if a is None else a[:, b].copy() for a in args]
+            a2[0] = a2[0] + 1e-13 * np.sin(np.arange(len(a2[0])) + 1.0 + k)
+            st2, _, d2 = O.qpik_one(om, par, *a2)
+            pert.append([int(st2), int(d2.iters)])
+        nonsolved_rows.append({"b": int(b), "iters": [int(iters[b]), int(riters[b])],
+                               "status": [int(status[b]), int(rstat[b])], "oracle_res_ratio": float(dg.res_ratio),
+                               "oracle_perturbed": pert})
     return {"B": int(len(status)), "agree": int(agree.sum()), "adjacent": int(adjacent.sum()),
+            "same_iter_curve": curve, "device_only_nonsolved": nonsolved_rows,
             "diverged": int(diverged.sum()), "status_mismatch": int((status != rstat).sum()),
             "nonsolved_gpu": int((status != 1).sum()), "nonsolved_oracle": int((rstat != 1).sum()),
             "band_oracle_max": float(band_o[both].max()) if both.any() else None,
@@ -58,6 +81,9 @@ def main():
     ap.add_argument("--robots", default="fr3,ur5e,husky_fr3,xls_fr3,caster_fr3")
     ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--seed", type=int, default=4)
+    ap.add_argument("--bench", action="store_true",
+                    help="each robot's bench batch (seed 12345, stress tiers): a 1 000-instance spread sample plus "
+                         "every instance the device did not solve")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     res = []
@@ -65,16 +91,26 @@ def main():
         moma = robot in ("husky_fr3", "xls_fr3", "caster_fr3")
         rd = make_moma(robot, dev) if moma else make_manipulator(robot, dev)
         ctrl = (mobile_manipulator if moma else manipulator).RobotController(0.001, rd, solver_mode="osqp_default")
-        for stress in (False, True):
-            args = (moma_step_inputs if moma else step_inputs)(rd, robot, a.seed, a.batch, dev, stress=stress)
-            it = torch.zeros(a.batch, dtype=torch.int32, device=dev)
+        cases = [(a.seed, a.batch, False), (a.seed, a.batch, True)]
+        if a.bench:
+            cases = [(12345, 16384 if robot == "husky_fr3" else 65536, True)]
+        for seed, B, stress in cases:
+            args = (moma_step_inputs if moma else step_inputs)(rd, robot, seed, B, dev, stress=stress)
+            it = torch.zeros(B, dtype=torch.int32, device=dev)
             o, st = ctrl.QPIK_step_batch(*[torch.as_tensor(x, device=dev) for x in args], LINK[robot], iters=it)
             torch.cuda.synchronize()
-            r = classify(robot, args, o.cpu().numpy(), st.cpu().numpy(), it.cpu().numpy())
-            r.update(robot=robot, stress=stress)
+            o, st, it = o.cpu().numpy(), st.cpu().numpy(), it.cpu().numpy()
+            if a.bench:
+                spread = np.unique(np.linspace(0, B - 1, 1000).astype(int))
+                idx = np.unique(np.concatenate([spread, np.nonzero(st != 1)[0]]))
+                args = [np.ascontiguousarray(x[:, idx]) for x in args]
+                o, st, it = np.ascontiguousarray(o[:, idx]), st[idx], it[idx]
+            r = classify(robot, args, o, st, it)
+            r.update(robot=robot, stress=stress, seed=seed, batch=B)
             res.append(r)
             print(json.dumps({k: v for k, v in r.items() if k != "diverged_rows"}), flush=True)
-    json.dump(res, open(os.path.join(ROOT, "gpurun_out", "reference_census.json"), "w"), indent=1)
+    json.dump(res, open(os.path.join(ROOT, "gpurun_out", "reference_census%s.json" % ("_bench" if a.bench else "")),
+                        "w"), indent=1)
 
 
 if __name__ == "__main__":
