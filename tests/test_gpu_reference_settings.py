@@ -5,24 +5,32 @@ every robot, against the oracle's restatement of the same ADMM.
 This mode reproduces what the reference returns, including its zeros when
 OSQP stops at max_iter (QP_IK.cpp:56-61).  Kernel and oracle run the same ADMM
 decisions, but their linear algebra rounds differently (register Schur
-complement vs dense Cholesky).  Measured (tools/reference_census.py, 10 cases
-of 1 024 instances, profiles/r05_reference_census.json): 99.0-99.8 % of the
-instances stop at the same iteration within 1e-7; the rest either stop at the
-same iteration with a rounding-level difference that grows with the run length
-(1e-7 after 75 iterations, up to 2e-3 after 1 275), or -- only on runs of
-1 000+ iterations -- separate into different stopping points (FR3: the device
-at max_iter 4 000 where the oracle stopped at 1 400; UR5e 1 825 vs 1 125).
-Such long runs are OSQP's own path-dependent regime: any two implementations
-(or BLAS builds) of the reference stop at different points there.  The
-contract bounds exactly that, on every instance:
+complement vs dense Cholesky), and an ADMM trajectory amplifies a rounding
+difference with its length.  Measured (tools/reference_census.py: 10 cases of
+1 024 instances plus the five bench batches, profiles/r06_reference_census*.json),
+as max |d q-dot| / max(1, |q-dot|_inf) over the instances that stop at the
+same iteration k: <= 1e-7 up to k = 150 on all robots (the largest, 7e-8, UR5e
+at 150), then growing about tenfold per 250 iterations (6e-6 at 900, 1.4e-5 at
+1 050, 1.7e-3 at 1 275); only runs of 1 000+ iterations separate into
+different stopping points (FR3: the device at max_iter 4 000 where the oracle
+stopped at 1 400-3 725).  There the oracle itself is path-dependent: moving q
+by 1e-13 changes its own stopping point by hundreds of iterations and turns
+some of its Solved runs into MaxIter -- OSQP's own regime, where any two
+implementations (or BLAS builds) of the reference stop at different points.
+The contract, on every instance:
 
   1. non-Solved instances return exact zeros, on both sides;
-  2. an instance either agrees -- same status, same stopping iteration and
-     |q-dot*| within 1e-5 -- or one of the two sides ran at least LONG_RUN
-     ADMM iterations (the trajectories had that long to separate);
-  3. at least 99 % of the instances agree, and statuses agree on at least
+  2. an instance either agrees -- same status, same stopping iteration k and
+     |d q-dot| <= run_length_tol(k) max(1, |q-dot|_inf) (the census envelope
+     above: 1e-7 up to 150 iterations, x10 per 250 beyond) -- or BOTH sides
+     ran at least LONG_RUN ADMM iterations;
+  3. where the statuses differ (one side MaxIter), both ran >= LONG_RUN and
+     the oracle reproduces the device's status on at least one of 16 copies of
+     the instance with q moved by 1e-13 (its outcome there is rounding-
+     dependent, not a different algorithm);
+  4. at least 99 % of the instances agree, and statuses agree on at least
      99.8 % (two instances per 1 024);
-  4. the device's answers lie in the reference's own OSQP band: against the
+  5. the device's answers lie in the reference's own OSQP band: against the
      exact optimum (the oracle's exact mode), every solved device answer is no
      further than the farthest of the oracle's reference-mode answers in the
      same batch (+1e-6), and the 99th percentiles agree within 1e-6.
@@ -30,8 +38,9 @@ contract bounds exactly that, on every instance:
 Cases: all five robots, nominal and stress-tier inputs (B = 1 024), and each
 robot's bench batch (bench.py's workload, seed 12345, B = 65 536 / Husky-FR3
 16 384) through the device at full size, checked on a ~1 000-instance sample
-plus every instance the device did not solve -- for FR3 these include the bench
-line's reference_settings non-solved instances (MaxIter).
+plus every instance the device did not solve: for FR3 the bench line's 14
+reference_settings non-solved (MaxIter) instances, 10 of them MaxIter in the
+oracle as well and 4 under item 3 (DESIGN.md "Exact mode vs reference mode").
 """
 import math
 
@@ -47,9 +56,27 @@ pytestmark = pytest.mark.gpu
 ROBOTS = ["fr3", "ur5e", "husky_fr3", "xls_fr3", "caster_fr3"]
 MOMA = {"husky_fr3", "xls_fr3", "caster_fr3"}
 BENCH_B = {"fr3": 65536, "ur5e": 65536, "husky_fr3": 16384, "xls_fr3": 65536, "caster_fr3": 65536}
-AGREE = 1e-5          # same stopping iteration, rounding-level difference
 LONG_RUN = 500        # ADMM iterations after which the two trajectories may separate
 BAND_TOL = 1e-6
+N_PERTURBED = 16
+
+
+def run_length_tol(k):
+    """Allowed |d q-dot| / max(1, |q-dot|_inf) between device and oracle runs
+    that both stop at ADMM iteration k (the census envelope, module docstring)."""
+    return 1e-7 * 10.0 ** (np.maximum(k - 150, 0) / 250.0)
+
+
+def oracle_status_unstable(om, par, args, b, status_dev):
+    """True when the oracle returns the device's status class (Solved or not)
+    on one of N_PERTURBED copies of instance b with q moved by 1e-13."""
+    for k in range(N_PERTURBED):
+        a2 = [a[:, b].copy() for a in args]
+        a2[0] = a2[0] + 1e-13 * np.sin(np.arange(len(a2[0])) + 1.0 + k)
+        st, _, _ = O.qpik_one(om, par, *a2)
+        if (st == 1) == (status_dev == 1):
+            return True
+    return False
 _rd = {}
 
 
@@ -83,10 +110,13 @@ def check_reference_contract(robot, args, out, status, iters, rated=None):
     assert np.all(np.isfinite(out))
     assert np.all(out[:, status != 1] == 0.0)
     assert np.all(ref[:, rstat != 1] == 0.0)
-    agree = (status == rstat) & (iters == riters) & (np.abs(out - ref).max(axis=0) <= AGREE)
+    scale = np.maximum(1.0, np.abs(ref).max(axis=0))
+    agree = (status == rstat) & (iters == riters) & (np.abs(out - ref).max(axis=0) <= run_length_tol(iters) * scale)
     other = np.nonzero(~agree)[0]
-    long_run = np.maximum(iters, riters) >= LONG_RUN
+    long_run = np.minimum(iters, riters) >= LONG_RUN
     assert np.all(long_run[other]), [(int(b), int(iters[b]), int(riters[b])) for b in other if not long_run[b]]
+    for b in np.nonzero(status != rstat)[0]:
+        assert oracle_status_unstable(om, par, args, b, status[b]), (int(b), int(status[b]), int(rstat[b]))
     rated = np.ones(B, bool) if rated is None else rated
     assert agree[rated].mean() >= 0.99, agree[rated].mean()
     mism = int(np.sum((status != rstat)[rated]))

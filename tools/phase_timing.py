@@ -1,6 +1,7 @@
 """Diagnostic: per-phase cycle shares from the DRC_PHASE_TIMING build."""
 import os, sys, ctypes as C
-os.environ["DRC_AMD_LIB"] = "libdrc_amd_timing.so"
+os.environ["DRC_AMD_LIB"] = os.environ.get("DRC_TIMING_LIB", "libdrc_amd_timing.so")
+SOLVER = os.environ.get("DRC_SOLVER", "exact")   # osqp_default: the reference-settings mode
 sys.path.insert(0, "tests"); sys.path.insert(0, "oracle"); sys.path.insert(0, ".")
 import numpy as np, torch
 import bench
@@ -11,7 +12,7 @@ B = int(sys.argv[2]) if len(sys.argv) > 2 else 65536
 spec = BUNDLED[robot]
 rd = make_robot(robot, dev)
 mod = manipulator if spec["kind"] == "manipulator" else mobile_manipulator
-ctrl = mod.RobotController(0.001, rd, solver_mode="exact")
+ctrl = mod.RobotController(0.001, rd, solver_mode=SOLVER)
 _, args, _ = bench.make_inputs(rd, robot, B, 12345, 0, dev)   # bench.py's workload (stress tiers)
 _capi.lib().drc_set_concurrency(rd.model.handle, 1)  # one sub-batch: per-instance cycles without overlap
 link = spec["link"]
