@@ -39,7 +39,7 @@ EXPORTED_SYMBOLS = (
     "drc_mobile_fk_jacobian", "drc_mobile_ik_jacobian",
     "drc_default_qpik_params", "drc_qpik_batch", "drc_qpik_stages_batch", "drc_debug_kernel_timing", "drc_debug_lds_plan",
     "drc_debug_host_timeline", "drc_debug_waves", "drc_debug_qpik_stamps",
-    "drc_debug_kernel_times", "drc_set_concurrency", "drc_set_fusion", "drc_model_release_stream", "drc_debug_lane_stage", "drc_qpik_host", "drc_qpik_stages_host",
+    "drc_debug_kernel_times", "drc_debug_instance_order", "drc_set_concurrency", "drc_set_fusion", "drc_model_release_stream", "drc_debug_lane_stage", "drc_qpik_host", "drc_qpik_stages_host",
     "drc_dynamics_batch", "drc_dynamics_host", "drc_joint_torque_step_batch", "drc_joint_torque_step_host",
     "drc_default_qpid_params", "drc_qpid_batch", "drc_qpid_stages_batch", "drc_qpid_host",
     "drc_qpid_stages_host", "drc_clik_batch", "drc_osf_batch", "drc_closed_form_host",
@@ -178,7 +178,7 @@ def _load():
     lib.drc_closed_form_host.argtypes = [vp, C.POINTER(QPIKParams), C.c_int, C.c_int64, dp, dp, dp, dp, dp, dp, dp, dp]
     for name in EXPORTED_SYMBOLS:
         if name in ("drc_debug_lds_plan", "drc_debug_waves", "drc_debug_host_timeline",
-                    "drc_debug_qpik_stamps") and not hasattr(lib, name):
+                    "drc_debug_qpik_stamps", "drc_debug_instance_order") and not hasattr(lib, name):
             continue  # diagnostics an older A/B build may lack
         if name not in ("drc_model_destroy", "drc_error_string", "drc_last_error", "drc_build_id"):
             getattr(lib, name).restype = C.c_int

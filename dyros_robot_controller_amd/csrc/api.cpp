@@ -98,6 +98,10 @@ struct drc_model_impl {
   // fused task + QP kernel for the compiled QPIK shapes and small batches
   // (fused_kernel.hip; drc_set_fusion): one launch per call, the record in LDS
   int fused = 1;
+  // drc_debug_instance_order: a scheduling order for calls of exactly
+  // order_n instances (device copy), or none
+  int32_t* d_order = nullptr;
+  int64_t order_n = 0;
   // host-buffer entry points: device staging + an internal stream
   std::mutex host_mu;
   void* stage = nullptr;
@@ -787,6 +791,7 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
     IO io{Bc, b0, B, q, qdot, xt, xdt, xi, xdi, out, status, iters, pose, jac, man, dist, xdd, pair,
           rec ? rec + b0 * stride : nullptr, stride};
     io.stamps = stages ? nullptr : stamps;
+    io.order = (!stages && !lane && m->d_order && m->order_n == B) ? m->d_order : nullptr;
     int* qc = cx->d_queue + c * StreamCtx::kSlotInts;  // c < 16 (drc_set_concurrency)
     // the whole slot (128 B, one aligned fill; 17 ints took two fill kernels)
     HIP_TRY(hipMemsetAsync(qc, 0, StreamCtx::kSlotInts * sizeof(int), cs));
@@ -1181,6 +1186,29 @@ int drc_debug_lane_stage(drc_model* m, int enable) {
   return DRC_OK;
 }
 
+int drc_debug_instance_order(drc_model* m, const int32_t* order, int64_t n) {
+  using drc_amd::set_err;
+  if (!m) return set_err(DRC_ERR_INVALID_ARGUMENT, "null model");
+  std::lock_guard<std::mutex> g(m->launch_mu);
+  HIP_TRY(hipSetDevice(m->device));
+  if (m->d_order) {
+    HIP_TRY(hipDeviceSynchronize());  // calls in flight may still read it
+    HIP_TRY(hipFree(m->d_order));
+  }
+  m->d_order = nullptr;
+  m->order_n = 0;
+  if (!order || n <= 0) return DRC_OK;
+  std::vector<char> seen(n, 0);
+  for (int64_t i = 0; i < n; ++i) {
+    if (order[i] < 0 || order[i] >= n || seen[order[i]]) return drc_amd::set_err(DRC_ERR_INVALID_ARGUMENT, "not a permutation");
+    seen[order[i]] = 1;
+  }
+  HIP_TRY(hipMalloc(&m->d_order, n * sizeof(int32_t)));
+  HIP_TRY(hipMemcpy(m->d_order, order, n * sizeof(int32_t), hipMemcpyHostToDevice));
+  m->order_n = n;
+  return DRC_OK;
+}
+
 #ifdef DRC_PHASE_TIMING
 // diagnostic build only: accumulated per-phase s_memtime cycles (32 slots)
 int drc_debug_phase_cycles(unsigned long long* out, int reset) {
@@ -1295,6 +1323,7 @@ void drc_model_destroy(drc_model* m) {
   for (auto& c : m->ctxs) drc_amd::free_ctx(c.get());
   drc_amd::free_lanes(&m->ln);
   if (m->d_model) (void)hipFree(m->d_model);
+  if (m->d_order) (void)hipFree(m->d_order);
   if (m->hstream) (void)hipStreamSynchronize(m->hstream), (void)hipStreamDestroy(m->hstream);
   if (m->stage) (void)hipFree(m->stage);
   if (m->pinned) (void)hipHostFree(m->pinned);

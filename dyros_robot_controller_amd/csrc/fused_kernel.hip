@@ -41,8 +41,9 @@ fused_kernel(const DevModel* __restrict__ M0, const KParams kt, const KParams kq
   iol.rec_stride = 0;
   const InstSeq seq(B, kq.xcd_map, io.queue);
   for (int64_t j = seq.first(); j < seq.n; j = seq.next(j)) {
-    const int64_t b = seq.at(j);
-    if (b >= B) continue;
+    const int64_t jj = seq.at(j);
+    if (jj >= B) continue;
+    const int64_t b = io.ordered(jj);
     stage_stamp(io, ST_TASK0, io.b0 + b);
     stage_where(io, ST_WTASK, io.b0 + b);
     task_instance<0>(M0, kt, iol, S, b);

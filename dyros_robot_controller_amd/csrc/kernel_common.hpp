@@ -393,6 +393,11 @@ struct IO {
   // task start / end, QP start / assembled / solved / stored
   // (drc_qpik_host_timed -> QP::TimeDuration, include/drc_amd.h)
   uint64_t* stamps;
+  // scheduling order of the instances (task / fused kernels), or NULL: the
+  // instance at queue position j of this launch is order[b0 + j] - b0 (a
+  // permutation of [b0, b0 + B)); results do not depend on it
+  const int32_t* order = nullptr;
+  __device__ __forceinline__ int64_t ordered(int64_t j) const { return order ? int64_t(order[b0 + j]) - b0 : j; }
 };
 // six clock stamps, then where the task and the QP stage ran (stage_where)
 constexpr int kTimeStamps = 6, kStamps = 8;

@@ -63,6 +63,16 @@ int drc_debug_qpik_stamps(drc_model* model, const drc_qpik_params* params, int64
  * tests and benchmarks. */
 int drc_debug_lane_stage(drc_model* model, int enable);
 
+/* Scheduling order of the instances for calls of exactly n instances
+ * (drc_qpik_batch and the host forms; the task / fused kernels take the
+ * instance at queue position j of a sub-batch [b0, b1) as order[b0 + j], so
+ * `order` must map each sub-batch range onto itself -- any permutation when the
+ * call runs as one sub-batch).  Host array, copied; NULL or n <= 0 clears it.
+ * Results do not depend on it (instances are independent); it moves only when
+ * each instance starts.  Diagnostic (the small-batch scheduling study,
+ * tools/stamp_study.py --order); no reference counterpart. */
+int drc_debug_instance_order(drc_model* model, const int32_t* order, int64_t n);
+
 #ifdef __cplusplus
 }
 #endif

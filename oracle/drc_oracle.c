@@ -3023,3 +3023,56 @@ void oracle_manipulability(const OracleModel* m, const double* q, double* man, d
 
 /* DyrosMath::PinvCOD of an m x n matrix (tests) */
 void oracle_pinv_cod(const double* A, int m, int n, double* X) { pinv_qr_trunc_mn(A, m, n, 1e-6, X); }
+
+/* Diagnostic (the small-batch scheduling study, tools/epa_hint_study.py): per
+ * instance, whether the pruned narrow phase runs EPA (some GJK candidate
+ * intersects: *truth) and the cheap predictors a scheduling pass could
+ * evaluate first -- *lb: some non-closed-form pair's pair_lower_bound < 0;
+ * *core: some non-closed-form pair's swept-core bound (segment distance minus
+ * the radii, before the separating-axis raise) < 0. */
+void oracle_epa_predict(const OracleModel* m, const double* q, int* truth, int* lb, int* core) {
+    Kin k;
+    kin_fk(m, q, &k);
+    Shape sh[ORC_MAXG];
+    for (int g = 0; g < m->ngeom; ++g) make_shape(m, &k, g, &sh[g]);
+    double ub = 1e300;
+    *truth = *lb = *core = 0;
+    for (int p = 0; p < m->npairs; ++p) {
+        const Shape *A = &sh[m->pair_a[p]], *B = &sh[m->pair_b[p]];
+        double pA[3], pB[3], d;
+        if (A->type == 0 || B->type == 0) { int how; d = shape_distance(A, B, pA, pB, &how); ub = fmin(ub, d); }
+        else if (A->type == 1 && B->type == 1 && cyl_cyl_side(A, B, &d, pA, pB)) ub = fmin(ub, d);
+    }
+    for (int p = 0; p < m->npairs; ++p) {
+        const Shape *A = &sh[m->pair_a[p]], *B = &sh[m->pair_b[p]];
+        double pA[3], pB[3], d;
+        if (A->type == 0 || B->type == 0) continue;
+        if (A->type == 1 && B->type == 1 && cyl_cyl_side(A, B, &d, pA, pB)) continue;
+        const double pd = pair_lower_bound(A, B);
+        if (pd < 0) *lb = 1;
+        {
+            double a0[3], a1[3], b0[3], b1[3], c1[3], c2[3], rad[2];
+            const Shape* S2[2] = {A, B};
+            double* ends[2][2] = {{a0, a1}, {b0, b1}};
+            for (int kk = 0; kk < 2; ++kk) {
+                const Shape* s = S2[kk];
+                for (int i = 0; i < 3; ++i) { ends[kk][0][i] = s->T[9 + i]; ends[kk][1][i] = s->T[9 + i]; }
+                if (s->type == 1) {
+                    const double ax[3] = {s->T[2], s->T[5], s->T[8]};
+                    for (int i = 0; i < 3; ++i) { ends[kk][0][i] -= s->prm[1] * ax[i]; ends[kk][1][i] += s->prm[1] * ax[i]; }
+                    rad[kk] = s->prm[0];
+                } else if (s->type == 2) {
+                    rad[kk] = sqrt(s->prm[0] * s->prm[0] + s->prm[1] * s->prm[1] + s->prm[2] * s->prm[2]);
+                } else {
+                    rad[kk] = s->prm[0];
+                }
+            }
+            if (seg_seg(a0, a1, b0, b1, c1, c2) - rad[0] - rad[1] < 0) *core = 1;
+        }
+        if (!(pd - 1e-9 <= ub)) continue;
+        SV S[4];
+        int ns;
+        double lam[4], v[3];
+        if (gjk_cut(A, B, S, &ns, lam, v, ub + 1e-9) == 1) *truth = 1;
+    }
+}

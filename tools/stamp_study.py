@@ -101,6 +101,12 @@ def main():
     ap.add_argument("--concurrency", type=int, default=0)
     ap.add_argument("--single", type=int, default=32)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--order", default="",
+                    help="comma list of scheduling orders to compare with the queue order (drc_debug_instance_order): "
+                         "lpt (longest task + QP first, from this run's stamps: the perfect-knowledge bound), "
+                         "task (longest task first), hint (instances a cheap narrow-phase bound flags first: "
+                         "oracle_epa_predict's lower bound, host-side)")
+    ap.add_argument("--subbatches", type=int, default=1, help="sub-batches the call runs as (orders stay inside each)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     rd = make_robot(a.robot, dev)
@@ -130,6 +136,46 @@ def main():
              status=st[slow])
     r.update(robot=a.robot, batch=a.batch, fusion=a.fusion, concurrency=a.concurrency)
     print(json.dumps(r), flush=True)
+    if a.order:
+        s6 = stamps[:6].astype(np.int64)
+        dur_all = (s6[5] - s6[0]).astype(np.float64)
+        dur_task = (s6[1] - s6[0]).astype(np.float64)
+        flags = None
+        S = a.subbatches
+        cuts = [a.batch * c // S for c in range(S + 1)]
+        for name in a.order.split(","):
+            if name == "hint" and flags is None:
+                sys.path.insert(0, os.path.join(ROOT, "oracle"))
+                import oracle as O
+                om = O.load(a.robot)[1]
+                t_, lb_, co_ = C.c_int(), C.c_int(), C.c_int()
+                flags = np.zeros(a.batch, bool)
+                for b in range(a.batch):
+                    O.lib().oracle_epa_predict(C.byref(om), np.ascontiguousarray(sub[0][:, b]).ctypes.data_as(
+                        C.POINTER(C.c_double)), C.byref(t_), C.byref(lb_), C.byref(co_))
+                    flags[b] = lb_.value != 0
+            key = {"lpt": -dur_all, "task": -dur_task, "hint": None}[name]
+            order = np.zeros(a.batch, np.int32)
+            for c in range(S):
+                lo_, hi_ = cuts[c], cuts[c + 1]
+                idx = np.arange(lo_, hi_)
+                if name == "hint":
+                    k = np.argsort(~flags[lo_:hi_], kind="stable")
+                else:
+                    k = np.argsort(key[lo_:hi_], kind="stable")
+                order[lo_:hi_] = idx[k]
+            _capi.check(lib.drc_debug_instance_order(h, order.ctypes.data_as(C.POINTER(C.c_int32)),
+                                                     C.c_int64(a.batch)))
+            for _ in range(a.reps):
+                st2, s2, i2 = run(lib, h, p, sub, a.batch, nrow)
+            assert np.array_equal(s2, st) and np.array_equal(i2, it)
+            r2 = analyse(st2, s2, i2, slots)
+            print(json.dumps({"robot": a.robot, "batch": a.batch, "order": name,
+                              "flagged": float(flags.mean()) if name == "hint" else None,
+                              "span_us": r2["span_us"], "below_half_peak_from_us": r2["below_half_peak_from_us"],
+                              "task_us": r2["task_us"], "qp_us": r2["qp_us"],
+                              "slowest_instances": r2["slowest_instances"][:3]}), flush=True)
+        _capi.check(lib.drc_debug_instance_order(h, None, C.c_int64(0)))
     # isolated instances: B = 1 calls through the two-kernel pipeline and the fused kernel
     for fz in (0, 1):
         _capi.check(lib.drc_set_fusion(h, C.c_int(fz)))
