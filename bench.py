@@ -117,11 +117,14 @@ def make_inputs(rd, robot, B, seed, offset, dev):
     return (q, qd, xt, xdt), (dq, dqd, _batch.as_device(xt, dev), _batch.as_device(xdt, dev)), stats
 
 
-def cpu_baseline(robot, q, qd, xt, xdt, target_s=4.0, warmups=3, runs=5):
+def cpu_baseline(robot, q, qd, xt, xdt, target_s=4.0, warmups=3, runs=5, sequential=10000):
     """Oracle restatement of the reference CPU path (OSQP-default settings,
     fresh setup per solve) on this host's cores: 1 thread and all threads
-    (capped at 16, the box's CPU share), each 3 warm-up + 5 timed runs over a
-    bounded sample of the same batch, median reported (BASELINE.md plan)."""
+    (capped at 16, the box's CPU share), median of 5 timed runs after 3
+    warm-ups (BASELINE.md plan).  1 thread: ``sequential`` (10 000, BASELINE.md's
+    "FR3 single instance, 10 000 sequential solves") solves one after another
+    per timed run, warm-ups on a 256-instance sample; all threads: a bounded
+    sample of about target_s / 8 s per run."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     _, om, spec = O.load(robot)
@@ -135,19 +138,25 @@ def cpu_baseline(robot, q, qd, xt, xdt, target_s=4.0, warmups=3, runs=5):
 
     out = {}
     for threads in (1, cores):
-        n = min(q.shape[1], 256 * threads)
-        per = timed(n, threads) / n                      # calibration run
-        n = int(min(q.shape[1], max(64, target_s / (warmups + runs) / max(per, 1e-9))))
-        for _ in range(warmups):
-            timed(n, threads)
+        if threads == 1:
+            n = min(q.shape[1], sequential)
+            for _ in range(warmups):
+                timed(min(n, 256), 1)
+        else:
+            n = min(q.shape[1], 256 * threads)
+            per = timed(n, threads) / n                      # calibration run
+            n = int(min(q.shape[1], max(64, target_s / (warmups + runs) / max(per, 1e-9))))
+            for _ in range(warmups):
+                timed(n, threads)
         ts = sorted(timed(n, threads) for _ in range(runs))
         out[threads] = (n / ts[len(ts) // 2], n)
     (v1, n1), (vc, nc) = out[1], out[cores]
     return {"value": vc, "unit": "solves/s", "cores": cores, "kind": "port",
-            "single_thread": {"value": v1, "cores": 1, "sample_instances": n1},
-            "sample": "first %d instances of the same batch (1 thread: %d), oracle/drc_oracle.c QPIKStep with the "
-                      "reference OSQP settings (eps 1e-3, no polish, fresh setup per solve), %d pthreads; median of "
-                      "%d timed runs after %d warm-ups" % (nc, n1, cores, runs, warmups)}
+            "single_thread": {"value": v1, "cores": 1, "sample_instances": n1,
+                              "note": "%d sequential solves per timed run (BASELINE.md config 1)" % n1},
+            "sample": "first %d instances of the same batch (1 thread: %d sequential), oracle/drc_oracle.c QPIKStep "
+                      "with the reference OSQP settings (eps 1e-3, no polish, fresh setup per solve), %d pthreads; "
+                      "median of %d timed runs after %d warm-ups" % (nc, n1, cores, runs, warmups)}
 
 
 def load_profile(name, robot, B, build_id):

@@ -24,7 +24,7 @@ FLAGS="--offload-arch=gfx950 -O3 -fPIC -std=c++17 -Wall -Wno-unused-function -ff
 # (and of the toolchain: the same sources built by another hipcc / ROCm are another build)
 BUILD_ID=$(cat $CSRC/*.hip $CSRC/*.hpp $CSRC/*.cpp include/drc_amd.h include/drc_amd_debug.h build.sh | { cat; echo "$FLAGS"; $HIPCC --version 2>&1; } | sha256sum | cut -c1-16)
 pids=()
-for src in task_kernel.hip qp_kernel.hip fused_kernel.hip qpid_kernel.hip dynamics.hip api.cpp model.cpp; do
+for src in task_kernel.hip qp_kernel.hip fused_kernel.hip qpid_kernel.hip dynamics.hip order_kernel.hip api.cpp model.cpp; do
   XF=""
   [ "$src" = api.cpp ] && XF="-DDRC_BUILD_ID=\"$BUILD_ID\""
   $HIPCC $FLAGS $XF -c $CSRC/$src -o "$OBJ/${src%.*}.o" &
@@ -34,7 +34,7 @@ rc=0
 for p in "${pids[@]}"; do wait "$p" || rc=1; done
 [ $rc -eq 0 ] || { echo "build.sh: a HIP translation unit failed to compile" >&2; exit 1; }
 $HIPCC --offload-arch=gfx950 -shared -fPIC "$OBJ"/task_kernel.o "$OBJ"/qp_kernel.o "$OBJ"/fused_kernel.o "$OBJ"/qpid_kernel.o \
-  "$OBJ"/dynamics.o "$OBJ"/api.o "$OBJ"/model.o -o "$OUT" -Wl,-rpath,/opt/rocm/lib
+  "$OBJ"/dynamics.o "$OBJ"/order_kernel.o "$OBJ"/api.o "$OBJ"/model.o -o "$OUT" -Wl,-rpath,/opt/rocm/lib
 [ -n "$DRC_VARIANT" ] && exit 0
 # test-only: the narrow-phase device code on one wave per pair (tests/test_gpu_narrow.py)
 $HIPCC $FLAGS -shared tests/gpu_narrow.hip -o tests/_narrow_gpu.so

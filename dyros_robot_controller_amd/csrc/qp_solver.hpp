@@ -23,23 +23,15 @@ __device__ __forceinline__ void residuals(const KParams& kp, double* S, const do
   // that only adaptive rho reads (SC_PRIS .. SC_NQ keep the ADMM values)
   const int l = GL::lane(), nx = DNX, ng = DNG, np = DNP;
   const double *P = S + kp.oP, *G = S + kp.oG, *q = S + kp.oQ, *ab = S + kp.oAB, *Di = S + kp.oDi, *Ei = S + kp.oEi;
-#ifdef DRC_RESID_DIV  // A/B variant: divide by D / E (the r04 form) instead of multiplying by their inverses
-  const double *Dd = S + kp.oD, *Ed = S + kp.oE;
-#define RS_E(v, i) ((v) / Ed[i])
-#define RS_D(v, i) ((v) / Dd[i])
-#else
-#define RS_E(v, i) ((v) * Ei[i])
-#define RS_D(v, i) ((v) * Di[i])
-#endif
   double pr = 0, prs = 0, nAx = 0, nz = 0, nAxs = 0, nzs = 0;
   double dr = 0, drs = 0, nPx = 0, nAty = 0, nq = 0, nPxs = 0, nAtys = 0, nqs = 0;
   if (l < nx) {  // bound row l and variable l
     const int lx = l < nx ? l : 0;
     double ax = PRE ? axb_pre : ab[lx] * x[lx], r = ax - z[lx];
     prs = fabs(r);
-    pr = fabs(RS_E(r, lx));
-    nAx = fabs(RS_E(ax, lx));
-    nz = fabs(RS_E(z[lx], lx));
+    pr = fabs(r * Ei[lx]);
+    nAx = fabs(ax * Ei[lx]);
+    nz = fabs(z[lx] * Ei[lx]);
     nAxs = fabs(ax);
     nzs = fabs(z[lx]);
     double px = 0;
@@ -53,10 +45,10 @@ __device__ __forceinline__ void residuals(const KParams& kp, double* S, const do
     for (int i = 0; i < ng; ++i) aty += G[i * nx + lx] * y[nx + i];
     double rr = px + q[lx] + aty;
     drs = fabs(rr);
-    dr = fabs(RS_D(rr, lx));
-    nPx = fabs(RS_D(px, lx));
-    nAty = fabs(RS_D(aty, lx));
-    nq = fabs(RS_D(q[lx], lx));
+    dr = fabs(rr * Di[lx]);
+    nPx = fabs(px * Di[lx]);
+    nAty = fabs(aty * Di[lx]);
+    nq = fabs(q[lx] * Di[lx]);
     nPxs = fabs(px);
     nAtys = fabs(aty);
     nqs = fabs(q[lx]);
@@ -73,9 +65,9 @@ __device__ __forceinline__ void residuals(const KParams& kp, double* S, const do
     int row = nx + lg;
     double r = ax - z[row];
     prs = fmax(prs, fabs(r));
-    pr = fmax(pr, fabs(RS_E(r, row)));
-    nAx = fmax(nAx, fabs(RS_E(ax, row)));
-    nz = fmax(nz, fabs(RS_E(z[row], row)));
+    pr = fmax(pr, fabs(r * Ei[row]));
+    nAx = fmax(nAx, fabs(ax * Ei[row]));
+    nz = fmax(nz, fabs(z[row] * Ei[row]));
     nAxs = fmax(nAxs, fabs(ax));
     nzs = fmax(nzs, fabs(z[row]));
   }
@@ -113,8 +105,6 @@ __device__ __forceinline__ void residuals(const KParams& kp, double* S, const do
     sc[SC_EPSD] = eps_abs + eps_rel * fmax(fmax(nPx, nAty), nq) * ci;
   }
   wsync();
-#undef RS_E
-#undef RS_D
 }
 
 // OSQP keeps D^-1, E^-1 and c^-1 beside the Ruiz scaling (scaling.c) and its
