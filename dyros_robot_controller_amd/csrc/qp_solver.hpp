@@ -1953,6 +1953,9 @@ __device__ DRC_ADMM_LOOP_ATTR int admm_loop_schur(const KParams& kpl, double* S,
   PHG(25);
   double ir_v = 1.0 / r_v, irg = 1.0 / rg;  // y / rho as a product in the loop
   double xv = 0, zv = 0, yv = 0, dyv = 0, zg = 0, yg = 0, dyg = 0;
+  // iterations left to the next check / adaptive-rho step (it % every == 0
+  // without an integer division per iteration)
+  int to_check = check_every, to_adapt = adapt_every;
   for (it = 1; it <= max_iter; ++it) {
     // core: r'_c's own term; aux: r_a before the G row's share
     const double tv = hv ? sig * xv - q_v + ab_v * (r_v * zv - yv) : 0.0;
@@ -2025,8 +2028,10 @@ __device__ DRC_ADMM_LOOP_ATTR int admm_loop_schur(const KParams& kpl, double* S,
       yg += dyg;
       zg = zn;
     }
-    const bool check = check_every > 0 && it % check_every == 0;
-    const bool adapt = adapt_every > 0 && it % adapt_every == 0;
+    const bool check = check_every > 0 && --to_check == 0;
+    const bool adapt = adapt_every > 0 && --to_adapt == 0;
+    if (check) to_check = check_every;
+    if (adapt) to_adapt = adapt_every;
     if (!(check || adapt) && it < max_iter) continue;
     {  // publish the iterate for the (LDS) residual / polish / rho code
       const SchurLanes<QD> L(kpl, S);

@@ -764,6 +764,9 @@ __device__ __forceinline__ void task_instance(const DevModel* __restrict__ M0, c
   // lane expands the polytope, the whole wave scans for the closest face.
   // (Only pairs whose GJK intersected are searched: none, no search.)
   if (__any(pen)) {
+#ifdef DRC_EPA_PRIO  // A/B variant: an EPA wave takes issue priority on its SIMD
+    __builtin_amdgcn_s_setprio(DRC_EPA_PRIO);
+#endif
     double gbd = bestd;
     int gbi = besti;
     wave_argmin(gbd, gbi);
@@ -807,6 +810,9 @@ __device__ __forceinline__ void task_instance(const DevModel* __restrict__ M0, c
       if (l == ln) pf[p] = 1;
       wsync();
     }
+#ifdef DRC_EPA_PRIO
+    __builtin_amdgcn_s_setprio(0);
+#endif
   }
   PH(5);
   const double myd = bestd;
