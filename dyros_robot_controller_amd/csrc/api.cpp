@@ -688,11 +688,12 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
   const bool lane = (ls == 1 || ls == 2 || (ls == 3 && stages)) && (dm.nv == 6 || dm.nv == 7) &&
                     dm.ncand_slots <= kMaxCandSlots;
   // penetration-prone instances first (order_kernel.hip) for calls whose
-  // makespan is the EPA tail: up to DRC_ORDER_MAX instances (default 16 Ki:
-  // FR3 B = 4 096's span 329 -> 248 us with an oracle-side hint, Husky-FR3
-  // 16 Ki 1 150 -> 1 080 us, profiles/r06e_stamps_order.jsonl); a caller's
-  // explicit order (drc_debug_instance_order) wins
-  static const int64_t order_max = env_int("DRC_ORDER_MAX", 16384, 0);
+  // makespan is the EPA tail: up to DRC_ORDER_MAX instances (default 8 Ki,
+  // the fused calls: FR3 B = 4 096's span 329 -> 248 us with an oracle-side
+  // hint, profiles/r06e_stamps_order.jsonl; larger calls gain less than the
+  // order kernel costs, profiles/r06f_envab_order_*.jsonl); a caller's explicit
+  // order (drc_debug_instance_order) wins
+  static const int64_t order_max = env_int("DRC_ORDER_MAX", 8192, 0);
   const bool dbg_order = m->d_order && m->order_n == B;
   const bool auto_order = !stages && !lane && !dbg_order && B <= order_max && dm.ncand_slots > 0 &&
                           dm.ncand_slots <= kMaxCandSlots;
@@ -1472,8 +1473,18 @@ int drc_default_qpik_params(const drc_model* m, int exact, drc_qpik_params* p) {
   // FR3 +0.1 % (profiles/r05b_envab.jsonl), but leave ~2e-9 in q-dot on some
   // instances (a golden fixture moved by 2.5e-9): not taken for that
   static const int64_t exact_refine = drc_amd::env_int("DRC_EXACT_REFINE", 3, 0);
-  // Ruiz passes in exact mode (A/B experiments: DRC_EXACT_SCALING; OSQP's 10)
-  static const int64_t exact_scaling = drc_amd::env_int("DRC_EXACT_SCALING", 10, 0);
+  // Ruiz passes in exact mode: 2 instead of OSQP's 10.  The ADMM only seeds
+  // the certified polish there (8 / 2 iterations), and the certified point is
+  // the QP's unique optimum whatever the scaling; two passes equilibrate
+  // enough for the polish to certify at its first attempt, the rest cost
+  // (whole-body QPs run all 10: a balanced row's factor converges
+  // geometrically and never reaches exactly 1).  Measured, one box: FR3 +2.6 %,
+  // UR5e +2.1 %, Husky-FR3 +2.9 %, XLS-FR3 +9.9 %, Caster-FR3 +10.5 %; one pass
+  // is faster on the manipulators but leaves the whole-body polish failing
+  // (3.6 M solves/s), none fails everywhere (profiles/r06f_envab_exact_scaling.jsonl,
+  // r06g_envab_exact_scaling.jsonl).  The oracle's exact mode uses the same
+  // count.  DRC_EXACT_SCALING overrides it (A/B experiments)
+  static const int64_t exact_scaling = drc_amd::env_int("DRC_EXACT_SCALING", 2, 0);
   if (exact) {
     s.check_termination = static_cast<int>(exact_check);
     s.polish_refine_iter = static_cast<int>(exact_refine);
@@ -1512,8 +1523,9 @@ int drc_default_qpid_params(const drc_model* m, int exact, drc_qpik_params* p) {
   // P is singular on null(J); OSQP's polish delta 1e-6 cannot certify at
   // eps_exact there, so parity mode regularises the polish with 1e-10
   if (exact) p->solver.delta = 1e-10;
-  p->solver.check_termination = 25;  // QPID keeps OSQP's check interval and
-  p->solver.polish_refine_iter = 3;   // refinement count in every mode
+  p->solver.check_termination = 25;  // QPID keeps OSQP's check interval,
+  p->solver.polish_refine_iter = 3;   // refinement count and Ruiz passes in every mode
+  p->solver.scaling = 10;             // (its optimum is a face: the scaling picks the point on it)
   return DRC_OK;
 }
 

@@ -13,25 +13,27 @@
 // swept-core lower bound, the broad phase's pair_lower_bound (qpik_device.hpp)
 // -- a superset of the instances with an intersecting GJK candidate
 // (recall 1 in tools/epa_hint_study.py; FR3 bench workload: 6 % flagged).
-// One lane per instance; the joint frames of the 64 lanes in LDS, [frame
-// element][lane] (conflict-free); model indices are wave-uniform scalar loads.
 #include "kernel_common.hpp"
 #include "launch.hpp"
 
 namespace drc_amd {
 
+// One wave per instance: lanes 1..nv form the joints' local transforms, then
+// each lane j composes its joint's world frame along its ancestor chain
+// (M->anc: the ancestors of j, in index order, are a path from the root, each
+// the parent of the next), then one lane per candidate pair (cand_pair slots)
+// evaluates the bound.  (A first version with one lane per instance held 64
+// instances' frames per wave and ran 64 waves at B = 4 096: 75 us against the
+// 80 us the order saves, profiles/r06g_kt_order_b4096.csv.)
 __global__ void __launch_bounds__(64) order_kernel(const DevModel* __restrict__ M, const IO io, int* __restrict__ cnt,
                                                    int32_t* __restrict__ order) {
-  extern __shared__ __attribute__((aligned(16))) double S[];
+  __shared__ double Lq[kMaxJoints + 1][12], Tw[kMaxJoints + 1][12];
   const int l = lane_id();
-  const int64_t b = int64_t(blockIdx.x) * 64 + l;
-  const bool live = b < io.B;
-  const int64_t gb = io.b0 + (live ? b : 0), LD = io.ld;
+  const int64_t b = blockIdx.x;
+  const int64_t gb = io.b0 + b, LD = io.ld;
   const int nv = M->nv;
-  auto TT = [&](int j, int e) -> double& { return S[(j * 12 + e) * 64 + l]; };
-#pragma unroll
-  for (int e = 0; e < 12; ++e) TT(0, e) = (e == 0 || e == 4 || e == 8) ? 1.0 : 0.0;
-  for (int j = 1; j <= nv; ++j) {
+  if (l >= 1 && l <= nv) {  // local transform of joint l: jplace * motion(q_l)
+    const int j = l;
     const double qq = io.q[(j - 1) * LD + gb];
     const double* ax = M->axis[j];
     double Mj[12];
@@ -46,25 +48,29 @@ __global__ void __launch_bounds__(64) order_kernel(const DevModel* __restrict__ 
       Mj[1] = Mj[2] = Mj[3] = Mj[5] = Mj[6] = Mj[7] = 0;
       Mj[9] = ax[0] * qq; Mj[10] = ax[1] * qq; Mj[11] = ax[2] * qq;
     }
-    double Lj[12], Tp[12], Tj[12];
+    double Lj[12];
     tmul(M->jplace[j], Mj, Lj);
-    const int p = M->parent[j];
 #pragma unroll
-    for (int e = 0; e < 12; ++e) Tp[e] = TT(p, e);
-    tmul(Tp, Lj, Tj);
-#pragma unroll
-    for (int e = 0; e < 12; ++e) TT(j, e) = Tj[e];
+    for (int e = 0; e < 12; ++e) Lq[j][e] = Lj[e];
   }
+  wsync();
+  if (l <= nv) {  // world frame of joint l (0: the world)
+    double T[12];
+#pragma unroll
+    for (int e = 0; e < 12; ++e) T[e] = (e == 0 || e == 4 || e == 8) ? 1.0 : 0.0;
+    const uint32_t anc = l > 0 ? M->anc[l] : 0u;
+    for (int k = 1; k <= l; ++k)
+      if (anc & (1u << (k - 1))) tmul(T, Lq[k], T);
+#pragma unroll
+    for (int e = 0; e < 12; ++e) Tw[l][e] = T[e];
+  }
+  wsync();
   bool flag = false;
-  for (int s = 0; s < M->ncand_slots; ++s) {
+  for (int s = l; s < M->ncand_slots; s += 64) {
     const int p = M->cand_pair[s], ga = M->pair_a[p], gb_ = M->pair_b[p];
-    double TA[12], TB[12], Tp[12];
-#pragma unroll
-    for (int e = 0; e < 12; ++e) Tp[e] = TT(M->gparent[ga], e);
-    tmul(Tp, M->gplace[ga], TA);
-#pragma unroll
-    for (int e = 0; e < 12; ++e) Tp[e] = TT(M->gparent[gb_], e);
-    tmul(Tp, M->gplace[gb_], TB);
+    double TA[12], TB[12];
+    tmul(Tw[M->gparent[ga]], M->gplace[ga], TA);
+    tmul(Tw[M->gparent[gb_]], M->gplace[gb_], TB);
     const Shape A{M->gtype[ga], TA, M->gparam[ga][0], M->gparam[ga][1], M->gparam[ga][2]};
     const Shape Bs{M->gtype[gb_], TB, M->gparam[gb_][0], M->gparam[gb_][1], M->gparam[gb_][2]};
     // bounding spheres apart: the pair cannot touch (cheap reject)
@@ -77,25 +83,17 @@ __global__ void __launch_bounds__(64) order_kernel(const DevModel* __restrict__ 
     if (A.type == kCylinder && Bs.type == kCylinder && cyl_cyl_side(A, Bs, &d, &pA, &pB)) continue;  // closed form
     if (pair_lower_bound(A, Bs, M->gbound[ga], M->gbound[gb_]) < 0.0) flag = true;
   }
-  // flagged instances from the front, the others from the back
-  const unsigned long long mf = __ballot(live && flag), mu = __ballot(live && !flag);
-  int bf = 0, bu = 0;
+  // flagged instances from the front of the sub-batch's order, the others from the back
+  const bool hot = __ballot(flag) != 0;
   if (l == 0) {
-    bf = atomicAdd(cnt, __popcll(mf));
-    bu = atomicAdd(cnt + 1, __popcll(mu));
-  }
-  bf = __builtin_amdgcn_readfirstlane(bf);
-  bu = __builtin_amdgcn_readfirstlane(bu);
-  const unsigned long long below = (1ull << l) - 1;
-  if (live) {
-    const int64_t pos = flag ? int64_t(bf + __popcll(mf & below)) : io.B - 1 - (bu + __popcll(mu & below));
-    order[io.b0 + pos] = static_cast<int32_t>(io.b0 + b);
+    const int64_t pos = hot ? int64_t(atomicAdd(cnt, 1)) : io.B - 1 - atomicAdd(cnt + 1, 1);
+    order[io.b0 + pos] = static_cast<int32_t>(gb);
   }
 }
 
 int launch_order_kernel(int64_t B, hipStream_t st, const DevModel* m, int nv, const IO& io, int* cnt, int32_t* order) {
-  const size_t lds = static_cast<size_t>(nv + 1) * 12 * 64 * sizeof(double);
-  hipLaunchKernelGGL(order_kernel, dim3(static_cast<unsigned>((B + 63) / 64)), dim3(64), lds, st, m, io, cnt, order);
+  (void)nv;
+  hipLaunchKernelGGL(order_kernel, dim3(static_cast<unsigned>(B)), dim3(64), 0, st, m, io, cnt, order);
   return hipGetLastError();
 }
 

@@ -2359,6 +2359,8 @@ void oracle_default_params(int kind, OracleParams* p, int exact) {
     /* parity mode: the first polish at iteration 8 (manipulators) / 2 (whole-body)
      * (kernel: drc_default_qpik_params) */
     if (exact) s->check_termination = kind == 0 ? 8 : 2;
+    /* parity mode: two Ruiz passes (kernel: drc_default_qpik_params) */
+    if (exact) s->scaling = 2;
 }
 
 /* Farkas certificate for the whole-body QP (mobile_manipulator/QP_IK.cpp:
@@ -2578,6 +2580,7 @@ void oracle_default_qpid_params(int kind, OracleParams* p, int exact) {
     p->solver.polish_guess = 0;             /* OSQP's first guess (kernel: problem 1)  */
     p->solver.polish_refine_iter = 3;       /* OSQP's refinement count (kernel: QPID)  */
     p->solver.check_termination = 25;       /* OSQP's check interval (kernel: QPID)    */
+    p->solver.scaling = 10;                 /* OSQP's Ruiz passes (kernel: QPID)       */
 }
 
 /* Manipulator::QPID (src/manipulator/QP_ID.cpp:7-193) and MobileManipulator::
