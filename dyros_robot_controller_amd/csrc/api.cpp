@@ -704,7 +704,7 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
     if (!stages || lane) {
       const int64_t rec_bytes = stages ? 0 : stride * B * 8;
       const int64_t ord_off = (rec_bytes + B * 4 + B + 7) & ~int64_t(7);
-      if (int r = ensure_pool(cx, ord_off + (auto_order ? B * 4 : 0))) return r;
+      if (int r = ensure_pool(cx, ord_off + (auto_order ? B * 5 : 0))) return r;
       if (!stages) rec = reinterpret_cast<double*>(cx->pool);
       hard = reinterpret_cast<int*>(static_cast<char*>(cx->pool) + rec_bytes);
       hard_flag = reinterpret_cast<uint8_t*>(static_cast<char*>(cx->pool) + rec_bytes + B * 4);
@@ -839,9 +839,13 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
       HIP_TRY(static_cast<hipError_t>(launch_qp_kernel(static_cast<unsigned>(gq), lds_q, cs, m->d_model, kq_c, io)));
       return DRC_OK;
     };
-    if (order_buf) {  // this sub-batch's order; counters in the (zeroed) queue slot
-      HIP_TRY(static_cast<hipError_t>(launch_order_kernel(Bc, cs, m->d_model, dm.nv, io, qc + 24, order_buf)));
-      io.order = order_buf;
+    if (order_buf) {  // this sub-batch's hot list; its count in the (zeroed) queue slot
+      int32_t* hl = order_buf + b0;
+      uint8_t* hf = reinterpret_cast<uint8_t*>(order_buf + B) + b0;
+      HIP_TRY(static_cast<hipError_t>(launch_order_kernel(Bc, cs, m->d_model, io, qc + 24, hl, hf)));
+      io.hot_n = qc + 24;
+      io.hot_list = hl;
+      io.hot_flag = hf;
     }
     if (fuse) {  // one fused task + QP kernel, the record in LDS
       static const int64_t cap_f = env_int("DRC_GRID_FUSED", 2048, 8) & ~int64_t(7);

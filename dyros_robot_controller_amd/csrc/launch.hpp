@@ -29,9 +29,10 @@ int launch_qpid_kernel(unsigned grid, size_t lds, hipStream_t st, const DevModel
 int launch_fused_kernel(unsigned grid, size_t lds, hipStream_t st, const DevModel* m, const KParams& kt,
                         const KParams& kq, const IO& io);
 
-// scheduling order of one sub-batch (order_kernel.hip): penetration-prone
-// instances first, counters cnt[0..1] zeroed, order[b0 .. b0 + B) written
-int launch_order_kernel(int64_t B, hipStream_t st, const DevModel* m, int nv, const IO& io, int* cnt, int32_t* order);
+// hot list of one sub-batch (order_kernel.hip): penetration-prone instances,
+// *hot_n (zeroed) counts them into hot_list[], hot_flag[B] marks them
+int launch_order_kernel(int64_t B, hipStream_t st, const DevModel* m, const IO& io, int* hot_n, int32_t* hot_list,
+                        uint8_t* hot_flag);
 
 #ifdef DRC_PHASE_TIMING
 // diagnostic build: add each unit's phase slots to out[64]

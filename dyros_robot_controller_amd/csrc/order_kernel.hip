@@ -3,8 +3,9 @@
 // narrow phase runs EPA (tens of serial growth steps, 5-10x a typical
 // instance) and that a wave happened to take as its second or third instance
 // (DESIGN.md "Small batches").  This kernel predicts those instances cheaply
-// and writes a queue order that hands them out first; the task / fused kernels
-// then take the instance at queue position j as order[b0 + j] (IO::ordered).
+// and writes them to a hot list that the task / fused kernels hand out first,
+// before every instance in index order with the hot ones skipped
+// (IO::ordered).
 // Results do not depend on the order (instances are independent): it moves
 // only when each instance starts.
 //
@@ -25,8 +26,8 @@ namespace drc_amd {
 // evaluates the bound.  (A first version with one lane per instance held 64
 // instances' frames per wave and ran 64 waves at B = 4 096: 75 us against the
 // 80 us the order saves, profiles/r06g_kt_order_b4096.csv.)
-__global__ void __launch_bounds__(64) order_kernel(const DevModel* __restrict__ M, const IO io, int* __restrict__ cnt,
-                                                   int32_t* __restrict__ order) {
+__global__ void __launch_bounds__(64) order_kernel(const DevModel* __restrict__ M, const IO io, int* __restrict__ hot_n,
+                                                   int32_t* __restrict__ hot_list, uint8_t* __restrict__ hot_flag) {
   __shared__ double Lq[kMaxJoints + 1][12], Tw[kMaxJoints + 1][12];
   const int l = lane_id();
   const int64_t b = blockIdx.x;
@@ -83,17 +84,19 @@ __global__ void __launch_bounds__(64) order_kernel(const DevModel* __restrict__ 
     if (A.type == kCylinder && Bs.type == kCylinder && cyl_cyl_side(A, Bs, &d, &pA, &pB)) continue;  // closed form
     if (pair_lower_bound(A, Bs, M->gbound[ga], M->gbound[gb_]) < 0.0) flag = true;
   }
-  // flagged instances from the front of the sub-batch's order, the others from the back
+  // a hot instance goes on the hot list (one atomic per hot instance: a few
+  // per cent of them; an atomic per instance on one address serialised 4 096
+  // of them at the L2, 53 us at B = 4 096, profiles/r06h_kt_order_b4096.csv)
   const bool hot = __ballot(flag) != 0;
   if (l == 0) {
-    const int64_t pos = hot ? int64_t(atomicAdd(cnt, 1)) : io.B - 1 - atomicAdd(cnt + 1, 1);
-    order[io.b0 + pos] = static_cast<int32_t>(gb);
+    hot_flag[b] = hot ? 1 : 0;
+    if (hot) hot_list[atomicAdd(hot_n, 1)] = static_cast<int32_t>(b);
   }
 }
 
-int launch_order_kernel(int64_t B, hipStream_t st, const DevModel* m, int nv, const IO& io, int* cnt, int32_t* order) {
-  (void)nv;
-  hipLaunchKernelGGL(order_kernel, dim3(static_cast<unsigned>(B)), dim3(64), 0, st, m, io, cnt, order);
+int launch_order_kernel(int64_t B, hipStream_t st, const DevModel* m, const IO& io, int* hot_n, int32_t* hot_list,
+                        uint8_t* hot_flag) {
+  hipLaunchKernelGGL(order_kernel, dim3(static_cast<unsigned>(B)), dim3(64), 0, st, m, io, hot_n, hot_list, hot_flag);
   return hipGetLastError();
 }
 
