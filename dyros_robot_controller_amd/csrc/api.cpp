@@ -688,15 +688,18 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
   const bool lane = (ls == 1 || ls == 2 || (ls == 3 && stages)) && (dm.nv == 6 || dm.nv == 7) &&
                     dm.ncand_slots <= kMaxCandSlots;
   // penetration-prone instances first (order_kernel.hip) for calls whose
-  // makespan is the EPA tail: up to DRC_ORDER_MAX instances (default 8 Ki,
-  // the fused calls: FR3 B = 4 096's span 329 -> 248 us with an oracle-side
-  // hint, profiles/r06e_stamps_order.jsonl; larger calls gain less than the
-  // order kernel costs, profiles/r06f_envab_order_*.jsonl); a caller's explicit
-  // order (drc_debug_instance_order) wins
+  // makespan is the EPA tail: manipulator calls of 2 049 .. 8 192 instances
+  // (DRC_ORDER_MIN / _MAX).  Fewer: the 2 048-wave fused grid starts every
+  // instance at once anyway.  More: the order gains less than it costs
+  // (profiles/r06f_envab_order_*.jsonl).  Whole-body robots: their predictor
+  // flags ~60 % of the instances, which orders nothing (XLS-FR3 B = 4 096
+  // -2.6 %, profiles/r06j_envab_order_b4096.jsonl; FR3 +15.7 %, UR5e +7.7 %).
+  // A caller's explicit order (drc_debug_instance_order) wins
   static const int64_t order_max = env_int("DRC_ORDER_MAX", 8192, 0);
+  static const int64_t order_min = env_int("DRC_ORDER_MIN", 2049, 0);
   const bool dbg_order = m->d_order && m->order_n == B;
-  const bool auto_order = !stages && !lane && !dbg_order && B <= order_max && dm.ncand_slots > 0 &&
-                          dm.ncand_slots <= kMaxCandSlots;
+  const bool auto_order = !stages && !lane && !dbg_order && B >= order_min && B <= order_max && dm.kind == 0 &&
+                          dm.ncand_slots > 0 && dm.ncand_slots <= kMaxCandSlots;
   int32_t* order_buf = nullptr;
   {
     std::lock_guard<std::mutex> g(m->mu);
@@ -704,7 +707,7 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
     if (!stages || lane) {
       const int64_t rec_bytes = stages ? 0 : stride * B * 8;
       const int64_t ord_off = (rec_bytes + B * 4 + B + 7) & ~int64_t(7);
-      if (int r = ensure_pool(cx, ord_off + (auto_order ? B * 5 : 0))) return r;
+      if (int r = ensure_pool(cx, ord_off + (auto_order ? B * 9 : 0))) return r;
       if (!stages) rec = reinterpret_cast<double*>(cx->pool);
       hard = reinterpret_cast<int*>(static_cast<char*>(cx->pool) + rec_bytes);
       hard_flag = reinterpret_cast<uint8_t*>(static_cast<char*>(cx->pool) + rec_bytes + B * 4);
@@ -839,13 +842,11 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
       HIP_TRY(static_cast<hipError_t>(launch_qp_kernel(static_cast<unsigned>(gq), lds_q, cs, m->d_model, kq_c, io)));
       return DRC_OK;
     };
-    if (order_buf) {  // this sub-batch's hot list; its count in the (zeroed) queue slot
-      int32_t* hl = order_buf + b0;
-      uint8_t* hf = reinterpret_cast<uint8_t*>(order_buf + B) + b0;
-      HIP_TRY(static_cast<hipError_t>(launch_order_kernel(Bc, cs, m->d_model, io, qc + 24, hl, hf)));
-      io.hot_n = qc + 24;
-      io.hot_list = hl;
-      io.hot_flag = hf;
+    if (order_buf) {  // this sub-batch's order (hot count in the zeroed queue slot; hot list / flags after it)
+      int32_t* hl = order_buf + B + b0;
+      uint8_t* hf = reinterpret_cast<uint8_t*>(order_buf + 2 * B) + b0;
+      HIP_TRY(static_cast<hipError_t>(launch_order_kernel(Bc, cs, m->d_model, io, qc + 24, hl, hf, order_buf)));
+      io.order = order_buf;
     }
     if (fuse) {  // one fused task + QP kernel, the record in LDS
       static const int64_t cap_f = env_int("DRC_GRID_FUSED", 2048, 8) & ~int64_t(7);

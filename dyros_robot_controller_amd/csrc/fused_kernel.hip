@@ -39,13 +39,11 @@ fused_kernel(const DevModel* __restrict__ M0, const KParams kt, const KParams kq
   IO iol = io;  // the record lives in LDS: one slot, reused by every instance of the wave
   iol.rec = S + (kt.lds_doubles > kq.lds_doubles ? kt.lds_doubles : kq.lds_doubles);
   iol.rec_stride = 0;
-  const int64_t nq = io.queue_len();
-  const InstSeq seq(nq, kq.xcd_map, io.queue);
+  const InstSeq seq(B, kq.xcd_map, io.queue);
   for (int64_t j = seq.first(); j < seq.n; j = seq.next(j)) {
     const int64_t jj = seq.at(j);
-    if (jj >= nq) continue;
+    if (jj >= B) continue;
     const int64_t b = io.ordered(jj);
-    if (b < 0) continue;
     stage_stamp(io, ST_TASK0, io.b0 + b);
     stage_where(io, ST_WTASK, io.b0 + b);
     task_instance<0>(M0, kt, iol, S, b);

@@ -397,24 +397,7 @@ struct IO {
   // instance at queue position j of this launch is order[b0 + j] - b0 (a
   // permutation of [b0, b0 + B)); results do not depend on it
   const int32_t* order = nullptr;
-  // penetration-prone instances first (order_kernel.hip): hot_n instances
-  // hot_list[0 .. hot_n) (indices in this launch) are handed out first, then
-  // every instance in index order, those with hot_flag set skipped; the queue
-  // is B + hot_n long.  NULL: no hot list
-  const int* hot_n = nullptr;
-  const int32_t* hot_list = nullptr;
-  const uint8_t* hot_flag = nullptr;
-  __device__ __forceinline__ int64_t queue_len() const { return B + (hot_n ? int64_t(*hot_n) : 0); }
-  // instance at queue position j (< queue_len()), or -1: a hot instance's own
-  // index position, already taken from the hot list
-  __device__ __forceinline__ int64_t ordered(int64_t j) const {
-    if (order) return int64_t(order[b0 + j]) - b0;
-    if (!hot_n) return j;
-    const int64_t nh = *hot_n;
-    if (j < nh) return hot_list[j];
-    j -= nh;
-    return hot_flag[j] ? -1 : j;
-  }
+  __device__ __forceinline__ int64_t ordered(int64_t j) const { return order ? int64_t(order[b0 + j]) - b0 : j; }
 };
 // six clock stamps, then where the task and the QP stage ran (stage_where)
 constexpr int kTimeStamps = 6, kStamps = 8;

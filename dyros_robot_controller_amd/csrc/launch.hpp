@@ -29,10 +29,11 @@ int launch_qpid_kernel(unsigned grid, size_t lds, hipStream_t st, const DevModel
 int launch_fused_kernel(unsigned grid, size_t lds, hipStream_t st, const DevModel* m, const KParams& kt,
                         const KParams& kq, const IO& io);
 
-// hot list of one sub-batch (order_kernel.hip): penetration-prone instances,
-// *hot_n (zeroed) counts them into hot_list[], hot_flag[B] marks them
+// queue order of one sub-batch (order_kernel.hip): penetration-prone
+// instances first (*hot_n zeroed; hot_list [B], hot_flag [B] scratch), then the
+// others in index order, into order[b0 .. b0 + B)
 int launch_order_kernel(int64_t B, hipStream_t st, const DevModel* m, const IO& io, int* hot_n, int32_t* hot_list,
-                        uint8_t* hot_flag);
+                        uint8_t* hot_flag, int32_t* order);
 
 #ifdef DRC_PHASE_TIMING
 // diagnostic build: add each unit's phase slots to out[64]

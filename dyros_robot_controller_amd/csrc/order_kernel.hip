@@ -3,9 +3,9 @@
 // narrow phase runs EPA (tens of serial growth steps, 5-10x a typical
 // instance) and that a wave happened to take as its second or third instance
 // (DESIGN.md "Small batches").  This kernel predicts those instances cheaply
-// and writes them to a hot list that the task / fused kernels hand out first,
-// before every instance in index order with the hot ones skipped
-// (IO::ordered).
+// and writes a queue order that hands them out first, then every other
+// instance in index order; the task / fused kernels take queue position j as
+// order[b0 + j] (IO::ordered).
 // Results do not depend on the order (instances are independent): it moves
 // only when each instance starts.
 //
@@ -94,9 +94,39 @@ __global__ void __launch_bounds__(64) order_kernel(const DevModel* __restrict__ 
   }
 }
 
+// The queue order from the flags: the hot list first, then every other
+// instance in index order (one workgroup: a block-wide exclusive scan of the
+// cold flags, in LDS).  Writes order[b0 .. b0 + B) with instance indices
+// b0 + b (IO::ordered).
+__global__ void __launch_bounds__(1024) order_scan_kernel(int64_t B, int64_t b0, const int* __restrict__ hot_n,
+                                                          const int32_t* __restrict__ hot_list,
+                                                          const uint8_t* __restrict__ hot_flag,
+                                                          int32_t* __restrict__ order) {
+  __shared__ int part[1024];
+  const int t = threadIdx.x;
+  const int64_t per = (B + 1023) / 1024, lo = t * per, hi = lo + per < B ? lo + per : B;
+  int cold = 0;
+  for (int64_t i = lo; i < hi; ++i) cold += hot_flag[i] ? 0 : 1;
+  part[t] = cold;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {  // inclusive scan (Hillis-Steele)
+    const int v = t >= off ? part[t - off] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  const int nh = *hot_n;
+  int64_t pos = nh + (part[t] - cold);
+  for (int64_t i = lo; i < hi; ++i)
+    if (!hot_flag[i]) order[b0 + pos++] = static_cast<int32_t>(b0 + i);
+  for (int64_t k = t; k < nh; k += 1024) order[b0 + k] = static_cast<int32_t>(b0 + hot_list[k]);
+}
+
 int launch_order_kernel(int64_t B, hipStream_t st, const DevModel* m, const IO& io, int* hot_n, int32_t* hot_list,
-                        uint8_t* hot_flag) {
+                        uint8_t* hot_flag, int32_t* order) {
   hipLaunchKernelGGL(order_kernel, dim3(static_cast<unsigned>(B)), dim3(64), 0, st, m, io, hot_n, hot_list, hot_flag);
+  if (hipError_t e = hipGetLastError()) return e;
+  hipLaunchKernelGGL(order_scan_kernel, dim3(1), dim3(1024), 0, st, B, io.b0, hot_n, hot_list, hot_flag, order);
   return hipGetLastError();
 }
 

@@ -33,13 +33,11 @@ task_kernel(const DevModel* __restrict__ M0, const KParams kp, const IO io) {
   const int64_t B = io.B;
   // hard mode: the instances the lane-per-instance stage left (grid stride)
   const bool hard_mode = io.hard_mode != 0;
-  const int64_t nq = hard_mode ? B : io.queue_len();
-  const InstSeq seq(hard_mode ? int64_t(*io.hard_n) : nq, hard_mode ? 0 : kp.xcd_map, hard_mode ? nullptr : io.queue);
+  const InstSeq seq(hard_mode ? int64_t(*io.hard_n) : B, hard_mode ? 0 : kp.xcd_map, hard_mode ? nullptr : io.queue);
   for (int64_t j = seq.first(); j < seq.n; j = seq.next(j)) {
     const int64_t jj = hard_mode ? int64_t(io.hard_list[j]) : seq.at(j);
-    if (jj >= nq) continue;
+    if (jj >= B) continue;
     const int64_t b = hard_mode ? jj : io.ordered(jj);
-    if (b < 0) continue;
     if (PROBLEM == 0) stage_stamp(io, ST_TASK0, io.b0 + b);
     if (PROBLEM == 0) stage_where(io, ST_WTASK, io.b0 + b);
     task_instance<PROBLEM>(M0, kp, io, S, b);

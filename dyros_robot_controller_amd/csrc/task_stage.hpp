@@ -417,15 +417,6 @@ __device__ __forceinline__ void task_instance(const DevModel* __restrict__ M0, c
   } else if (l < 36 && kp.mode == DRC_MODE_QPIK_CUBIC) {
     tgt = l < 30 ? io.xi[(l - 18) * LD + gb] : io.xdi[(l - 30) * LD + gb];
   }
-#ifdef DRC_GPLACE_PREFETCH  // A/B variant: this lane's geometry placement loaded before the FK chain
-  double gp0[12];
-  int gpar0 = 0;
-  if (l < M->ngeom) {
-#pragma unroll
-    for (int i = 0; i < 12; ++i) gp0[i] = M->gplace[l][i];
-    gpar0 = M->gparent[l];
-  }
-#endif
   wsync();
   // ---------------- FK: local joint transforms, then the chain ------------
   double* T = S + kp.kT;  // (nv+1) x 12
@@ -474,16 +465,7 @@ __device__ __forceinline__ void task_instance(const DevModel* __restrict__ M0, c
   wsync();
   // geometry poses
   double* Tg = S + kp.kTg;
-#ifdef DRC_GPLACE_PREFETCH
-  if (l < M->ngeom) {
-    double out[12];
-    tmul(T + 12 * gpar0, gp0, out);
-    for (int i = 0; i < 12; ++i) Tg[l * 12 + i] = out[i];
-  }
-  for (int g = l + 64; g < M->ngeom; g += 64) {
-#else
   for (int g = l; g < M->ngeom; g += 64) {
-#endif
     double out[12];
     tmul(T + 12 * M->gparent[g], M->gplace[g], out);
     for (int i = 0; i < 12; ++i) Tg[g * 12 + i] = out[i];
