@@ -1895,11 +1895,15 @@ struct SchurLanes {
   }
 };
 
-// The Schur-complement register ADMM loop (QD::schur shapes), out of line so
-// its register file holds only the loop's state: inlined into the kernel, the
-// values live across it (assembly, scaling, polish) pushed it into VGPR and
-// SGPR spills inside the iteration.  Reads its parameters from the LDS copy
-// kpl.  Returns the iteration count as qp_admm's loop leaves it.
+// The Schur-complement register ADMM iterations (QD::schur shapes): `steps`
+// iterations from the iterate published in LDS, which they publish again.
+// The caller (qp_admm) runs the iterations between two checks / adaptive-rho
+// steps per call and calls admm_check in between, so no call sits inside the
+// iteration loop: with admm_check called from inside it (r03-r06k), the
+// loop's scalar state (counters, lane masks) lived across that call in VGPR
+// lanes, a v_readlane / v_writelane per value and iteration (about 40 of an
+// FR3 iteration's 170 instructions; now about 100, none of them spills).
+// Reads its parameters from the LDS copy kpl.
 // Lane roles: l < NP core variable l (and its bound row); NP + r < NP + NG:
 // G row r together with its auxiliary variable a(r) and that variable's
 // bound row.  R[] holds, on core lanes, row l of S^-1 then column l of
@@ -1908,20 +1912,11 @@ struct SchurLanes {
 //   core: r'_c = sigma x_c - q_c + ab_c w_b + sum_r G_rc u_r   (NG broadcasts)
 //   core: x~_c = S^-1 r';  rows: v_r = G_r,c x~_c = (G_c S^-1)_r r'   (NP broadcasts)
 //   rows: x~_a = t_a - coef_r v_r,  (G x~)_r = v_r + g_r x~_a
-#ifdef DRC_INLINE_ADMM_LOOP  // experiment: the loop in the QP kernel's own frame
-#define DRC_ADMM_LOOP_ATTR __forceinline__
-#else
-#define DRC_ADMM_LOOP_ATTR __noinline__
-#endif
 template <class QD>
-__device__ DRC_ADMM_LOOP_ATTR int admm_loop_schur(const KParams& kpl, double* S, int* status_out) {
+__device__ __forceinline__ void admm_iters_schur(const KParams& kpl, double* S, int steps) {
   using GL = Grp<QD::gs>;
   const KParams& kp = kpl;
   const double sig = kp.s.sigma, al = kp.s.alpha;
-  const int max_iter = kp.s.max_iter, check_every = kp.s.check_termination;
-  const int adapt_every = kp.s.adaptive_rho && kp.s.adaptive_rho_interval > 0 ? kp.s.adaptive_rho_interval : 0;
-  int status = *status_out;
-  int it;
   PHG_DECL
   constexpr int NX = QD::nx, NG = QD::ng, NP = QD::np;
   (void)NX;
@@ -1933,10 +1928,11 @@ __device__ DRC_ADMM_LOOP_ATTR int admm_loop_schur(const KParams& kpl, double* S,
   // registers live across the loop and one code path instead of two)
   bool hc, hr, ha, hv;
   double ab_v, q_v, lo_v, up_v, g_r, lo_g, up_g, d_r, c_r, r_v, rg;
+  double xv, zv, yv, dyv = 0, zg, yg, dyg = 0;
 #ifndef DRC_ADMM_READLANE_BCAST
   int rr_l = 0, lc_l = 0;
 #endif
-  {
+  {  // S^-1 / rho and the iterate as the setup or the last check left them
     const SchurLanes<QD> L(kpl, S);
     L.load(R);
     hc = L.hc; hr = L.hr; ha = L.ha; hv = L.hv;
@@ -1945,138 +1941,117 @@ __device__ DRC_ADMM_LOOP_ATTR int admm_loop_schur(const KParams& kpl, double* S,
     lo_g = L.lo[L.ig]; up_g = L.up[L.ig];
     d_r = L.dv[L.rr]; c_r = L.cf[L.rr];
     r_v = L.rv[L.iv]; rg = L.rv[L.ig];
+    xv = L.x[L.iv]; zv = L.z[L.iv]; yv = L.y[L.iv];
+    zg = L.z[L.ig]; yg = L.y[L.ig];
 #ifndef DRC_ADMM_READLANE_BCAST
     rr_l = L.rr;
     lc_l = L.lc;
 #endif
   }
   PHG(25);
-  double ir_v = 1.0 / r_v, irg = 1.0 / rg;  // y / rho as a product in the loop
-  double xv = 0, zv = 0, yv = 0, dyv = 0, zg = 0, yg = 0, dyg = 0;
-  // iterations left to the next check / adaptive-rho step (it % every == 0
-  // without an integer division per iteration)
-  int to_check = check_every, to_adapt = adapt_every;
-  for (it = 1; it <= max_iter; ++it) {
-    // core: r'_c's own term; aux: r_a before the G row's share
-    const double tv = hv ? sig * xv - q_v + ab_v * (r_v * zv - yv) : 0.0;
-    double u = 0, ta = 0;
-    if (hr) {
-      const double wg = rg * zg - yg;
-      if (ha) {
-        const double r_a = tv + g_r * wg;
-        ta = r_a * d_r;  // d_r holds 1 / d_a
-        u = wg - rg * g_r * ta;
-      } else {
-        u = wg;
-      }
-    }
-    const double loc = hc ? tv : 0.0;
-    double r0 = 0, r1 = 0;
-#ifndef DRC_ADMM_READLANE_BCAST  // the two passes' vectors broadcast through LDS (r04: +1-3 %)
-    lds_double* wb = (lds_double*)(S + kpl.oBc);
-    if (hr) wb[rr_l] = u;
-    asm volatile("" ::: "memory");
-    static_for<NG>([&](auto I) {
-      constexpr int i = decltype(I)::value;
-      const double ui = wb[i];
-      if constexpr (i & 1) r1 += R[NP + i] * ui;
-      else r0 += R[NP + i] * ui;
-    });
-    const double rp = loc + (r0 + r1);
-    if (hc) wb[NG + lc_l] = rp;
-    asm volatile("" ::: "memory");
-    double s0 = 0, s1 = 0;
-    static_for<NP>([&](auto C) {
-      constexpr int c = decltype(C)::value;
-      const double rpc = wb[NG + c];
-      if constexpr (c & 1) s1 += R[c] * rpc;
-      else s0 += R[c] * rpc;
-    });
-#else
-    static_for<NG>([&](auto I) {
-      constexpr int i = decltype(I)::value;
-      const double ui = GL::template bcastc<NP + i>(u);
-      if constexpr (i & 1) r1 += R[NP + i] * ui;
-      else r0 += R[NP + i] * ui;
-    });
-    const double rp = loc + (r0 + r1);
-    double s0 = 0, s1 = 0;
-    static_for<NP>([&](auto C) {
-      constexpr int c = decltype(C)::value;
-      const double rpc = GL::template bcastc<c>(rp);
-      if constexpr (c & 1) s1 += R[c] * rpc;
-      else s0 += R[c] * rpc;
-    });
+  const double ir_v = 1.0 / r_v, irg = 1.0 / rg;  // y / rho as a product in the loop
+#ifndef DRC_ADMM_READLANE_BCAST
+  // (formed once: the compiler barriers below would re-read kpl.oBc per iteration)
+  lds_double* const wb = (lds_double*)(S + kpl.oBc);
 #endif
-    const double sv = s0 + s1;  // core: x~_c; row: v_r = G_r,c x~_c
-    const double xta = ha ? ta - c_r * sv : 0.0;  // aux: x~_a
-    if (hv) {  // the variable's bound row: z~ = ab x~, relaxation, projection, dual update
-      const double xin = hc ? sv : xta;
-      const double zr = al * ab_v * xin + (1 - al) * zv;
-      double zn = zr + yv * ir_v;
-      zn = fmin(fmax(zn, lo_v), up_v);
-      dyv = r_v * (zr - zn);
-      yv += dyv;
-      zv = zn;
-      xv = al * xin + (1 - al) * xv;
-    }
-    if (hr) {  // G row
-      const double zr = al * (sv + g_r * xta) + (1 - al) * zg;
-      double zn = zr + yg * irg;
-      zn = fmin(fmax(zn, lo_g), up_g);
-      dyg = rg * (zr - zn);
-      yg += dyg;
-      zg = zn;
-    }
-    const bool check = check_every > 0 && --to_check == 0;
-    const bool adapt = adapt_every > 0 && --to_adapt == 0;
-    if (check) to_check = check_every;
-    if (adapt) to_adapt = adapt_every;
-    if (!(check || adapt) && it < max_iter) continue;
-    {  // publish the iterate for the (LDS) residual / polish / rho code
-      const SchurLanes<QD> L(kpl, S);
-      if (hv) {
-        L.x[L.iv] = xv;
-        L.z[L.iv] = zv;
-        L.y[L.iv] = yv;
-        L.dy[L.iv] = dyv;
-      }
+  const int n = __builtin_amdgcn_readfirstlane(steps);  // wave-uniform trip count
+  for (int k = 0; k < n; ++k) {
+      // core: r'_c's own term; aux: r_a before the G row's share
+      const double tv = hv ? sig * xv - q_v + ab_v * (r_v * zv - yv) : 0.0;
+      double u = 0, ta = 0;
       if (hr) {
-        L.z[L.ig] = zg;
-        L.y[L.ig] = yg;
-        L.dy[L.ig] = dyg;
+        const double wg = rg * zg - yg;
+        if (ha) {
+          const double r_a = tv + g_r * wg;
+          ta = r_a * d_r;  // d_r holds 1 / d_a
+          u = wg - rg * g_r * ta;
+        } else {
+          u = wg;
+        }
       }
+      const double loc = hc ? tv : 0.0;
+      double r0 = 0, r1 = 0;
+#ifndef DRC_ADMM_READLANE_BCAST  // the two passes' vectors broadcast through LDS (r04: +1-3 %)
+      if (hr) wb[rr_l] = u;
+      asm volatile("" ::: "memory");
+      static_for<NG>([&](auto I) {
+        constexpr int i = decltype(I)::value;
+        const double ui = wb[i];
+        if constexpr (i & 1) r1 += R[NP + i] * ui;
+        else r0 += R[NP + i] * ui;
+      });
+      const double rp = loc + (r0 + r1);
+      if (hc) wb[NG + lc_l] = rp;
+      asm volatile("" ::: "memory");
+      double s0 = 0, s1 = 0;
+      static_for<NP>([&](auto C) {
+        constexpr int c = decltype(C)::value;
+        const double rpc = wb[NG + c];
+        if constexpr (c & 1) s1 += R[c] * rpc;
+        else s0 += R[c] * rpc;
+      });
+#else
+      static_for<NG>([&](auto I) {
+        constexpr int i = decltype(I)::value;
+        const double ui = GL::template bcastc<NP + i>(u);
+        if constexpr (i & 1) r1 += R[NP + i] * ui;
+        else r0 += R[NP + i] * ui;
+      });
+      const double rp = loc + (r0 + r1);
+      double s0 = 0, s1 = 0;
+      static_for<NP>([&](auto C) {
+        constexpr int c = decltype(C)::value;
+        const double rpc = GL::template bcastc<c>(rp);
+        if constexpr (c & 1) s1 += R[c] * rpc;
+        else s0 += R[c] * rpc;
+      });
+#endif
+      const double sv = s0 + s1;  // core: x~_c; row: v_r = G_r,c x~_c
+      const double xta = ha ? ta - c_r * sv : 0.0;  // aux: x~_a
+      if (hv) {  // the variable's bound row: z~ = ab x~, relaxation, projection, dual update
+        const double xin = hc ? sv : xta;
+        const double zr = al * ab_v * xin + (1 - al) * zv;
+        double zn = zr + yv * ir_v;
+        zn = fmin(fmax(zn, lo_v), up_v);
+        dyv = r_v * (zr - zn);
+        yv += dyv;
+        zv = zn;
+        xv = al * xin + (1 - al) * xv;
+      }
+      if (hr) {  // G row
+        const double zr = al * (sv + g_r * xta) + (1 - al) * zg;
+        double zn = zr + yg * irg;
+        zn = fmin(fmax(zn, lo_g), up_g);
+        dyg = rg * (zr - zn);
+        yg += dyg;
+        zg = zn;
+      }
+  }
+  {  // publish the iterate for the (LDS) residual / polish / rho code
+    const SchurLanes<QD> L(kpl, S);
+    if (hv) {
+      L.x[L.iv] = xv;
+      L.z[L.iv] = zv;
+      L.y[L.iv] = yv;
+      L.dy[L.iv] = dyv;
     }
-    wsync();
-    if (!(check || adapt)) continue;  // last iteration: published for the output
-    PH_STAMP(tc0);
-    const int act = admm_check<QD>(kpl, S, it, check, adapt, &status);
-    PH_ONLY(const unsigned long long dchk = __builtin_amdgcn_s_memtime() - tc0; PH_ADD(27, dchk); PH_ADD(26, 0ull - dchk));  // checks out of the loop's slot
-    if (act == 2) break;
-    {  // S^-1 / rho may have changed, the iterate may be polished
-      const SchurLanes<QD> L(kpl, S);
-      L.load(R);
-      // every loop constant re-read too, so none is live across the call
-      hc = L.hc; hr = L.hr; ha = L.ha; hv = L.hv;
-      ab_v = L.ab[L.iv]; q_v = L.qq[L.iv]; lo_v = L.lo[L.iv]; up_v = L.up[L.iv];
-      g_r = ha ? L.G[L.rr * NX + L.ia] : 0.0;
-      lo_g = L.lo[L.ig]; up_g = L.up[L.ig];
-      d_r = L.dv[L.rr];
-      c_r = L.cf[L.rr];
-      r_v = L.rv[L.iv];
-      rg = L.rv[L.ig];
-      ir_v = 1.0 / r_v;
-      irg = 1.0 / rg;
-      xv = L.x[L.iv];
-      zv = L.z[L.iv];
-      yv = L.y[L.iv];
-      zg = L.z[L.ig];
-      yg = L.y[L.ig];
+    if (hr) {
+      L.z[L.ig] = zg;
+      L.y[L.ig] = yg;
+      L.dy[L.ig] = dyg;
     }
   }
+  wsync();
   PHG(26);
-  *status_out = status;
-  return it;
+}
+
+// The same iterations out of line (the reference-settings mode: about 120
+// iterations in five calls per instance ran faster in a leaf function of their
+// own than inlined into the QP kernel, exact mode's single call of 8
+// iterations slower -- profiles/r06l_ab_admm_iters_*.jsonl, r06m_ab_*)
+template <class QD>
+__device__ __noinline__ void admm_iters_schur_call(const KParams& kpl, double* S, int steps) {
+  admm_iters_schur<QD>(kpl, S, steps);
 }
 
 // rho, K^-1 and the ADMM iterations (+ polish); returns the status
@@ -2109,7 +2084,37 @@ __device__ __forceinline__ int qp_admm(const KParams& kp, const KParams& kpl, do
   const double sig = kp.s.sigma, al = kp.s.alpha;
   int it;
   if constexpr (QD::schur) {
-    it = admm_loop_schur<QD>(kpl, S, &status);
+    // the iterations between two checks / adaptive-rho steps (or the last)
+    // per call; wave-uniform control in SGPRs (the LDS parameter copy reads
+    // into VGPRs, and admm_check's verdict is uniform by construction)
+    const int max_iter = __builtin_amdgcn_readfirstlane(kp.s.max_iter);
+    const int check_every = __builtin_amdgcn_readfirstlane(kp.s.check_termination);
+    const int adapt_every = __builtin_amdgcn_readfirstlane(
+        kp.s.adaptive_rho && kp.s.adaptive_rho_interval > 0 ? kp.s.adaptive_rho_interval : 0);
+    constexpr int kNever = 0x7fffffff;
+    int to_check = check_every > 0 ? check_every : kNever, to_adapt = adapt_every > 0 ? adapt_every : kNever;
+    bool stopped = false;
+    it = 0;
+    while (it < max_iter) {
+      const int steps = min(min(to_check, to_adapt), max_iter - it);
+      if (kp.s.exact) admm_iters_schur<QD>(kpl, S, steps);
+      else admm_iters_schur_call<QD>(kpl, S, steps);
+      it += steps;
+      to_check -= steps;
+      to_adapt -= steps;
+      const bool check = to_check == 0, adapt = to_adapt == 0;
+      if (check) to_check = check_every;
+      if (adapt) to_adapt = adapt_every;
+      if (!(check || adapt)) continue;  // last iteration: published for the output
+      PH_STAMP(tc0);
+      const int act = __builtin_amdgcn_readfirstlane(admm_check<QD>(kpl, S, it, check, adapt, &status));
+      PH_ONLY(const unsigned long long dchk = __builtin_amdgcn_s_memtime() - tc0; PH_ADD(27, dchk));
+      if (act == 2) {
+        stopped = true;
+        break;
+      }
+    }
+    if (!stopped) it = (max_iter > 0 ? max_iter : 0) + 1;  // as a counted loop 1..max_iter leaves it
   } else if constexpr (QD::reg) {
     constexpr int NX = QD::nx, NG = QD::ng;
     double Gc[NG], Kr[NX], GKr[NX];

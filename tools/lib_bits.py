@@ -2,7 +2,7 @@
 (stress tiers, seed 12345) through the library DRC_AMD_LIB names and saves
 q-dot*, status and ADMM iterations per robot; with --compare, reports how
 many instances differ from a previous dump.
-    DRC_AMD_LIB=<lib> python tools/lib_bits.py <tag> [robot ...]
+    DRC_AMD_LIB=<lib> [DRC_SOLVER=osqp_default] python tools/lib_bits.py <tag> [robot ...]
     python tools/lib_bits.py --compare <tagA> <tagB> [robot ...]"""
 import os
 import sys
@@ -10,7 +10,7 @@ import sys
 sys.path.insert(0, "tests"); sys.path.insert(0, "oracle"); sys.path.insert(0, ".")
 import numpy as np
 
-OUT = "gpurun_out"
+OUT = os.environ.get("DRC_BITS_DIR", "gpurun_out")
 ROBOTS = ["fr3", "ur5e", "husky_fr3", "xls_fr3", "caster_fr3"]
 BATCH = {"husky_fr3": 16384}
 
@@ -23,7 +23,7 @@ def dump(tag, robots):
     for robot in robots:
         moma = robot in ("husky_fr3", "xls_fr3", "caster_fr3")
         rd = make_moma(robot, dev) if moma else make_manipulator(robot, dev)
-        ctrl = (mobile_manipulator if moma else manipulator).RobotController(0.001, rd, solver_mode="exact")
+        ctrl = (mobile_manipulator if moma else manipulator).RobotController(0.001, rd, solver_mode=os.environ.get("DRC_SOLVER", "exact"))
         B = BATCH.get(robot, 65536)
         q, qd, xt, xdt = (moma_step_inputs if moma else step_inputs)(rd, robot, 12345, B, dev, stress=True)
         args = [torch.as_tensor(a, device=dev) for a in (q, qd, xt, xdt)]
