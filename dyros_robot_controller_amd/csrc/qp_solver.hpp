@@ -588,15 +588,17 @@ __device__ __forceinline__ bool eqp_regs(const KParams& kp, double* S, int actb,
   double K0[NK], Ki[NK];
   {
     unsigned long long fm = freeMask, rm = rowMask;
+    // (entries j >= N are never read: every loop below stops at N)
 #pragma unroll
     for (int j = 0; j < NK; ++j) {
+      if (j >= N) break;
       double v = 0.0;
       if (j < nF) {
         const int fj = __builtin_ctzll(fm);
         fm &= fm - 1;
         if (hf) v = (fi < NP && fj < NP) ? P[fi * NP + fj] : 0.0;
         else if (hr) v = G[gi * NX + fj];
-      } else if (j < N) {
+      } else {
         const int gj = __builtin_ctzll(rm);
         rm &= rm - 1;
         if (hf) v = G[gj * NX + fi];
@@ -623,7 +625,10 @@ __device__ __forceinline__ bool eqp_regs(const KParams& kp, double* S, int actb,
       const double p = 1.0 / Ki[k];
       Ki[k] = 1.0;
 #pragma unroll
-      for (int j = 0; j < NK; ++j) Ki[j] *= p;
+      for (int j = 0; j < NK; ++j) {
+        if (j >= N) break;
+        Ki[j] *= p;
+      }
       if constexpr (kLds) {
 #pragma unroll
         for (int j = 0; j < NK; ++j) {
