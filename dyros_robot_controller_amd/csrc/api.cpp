@@ -719,11 +719,27 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
   // kernel waits for the whole task kernel, with several they overlap
   // (Husky-FR3's 16 Ki batch)
   static const int64_t min_sub = env_int("DRC_MIN_SUBBATCH", 4096, 1);
-  // fused for small batches only: it wins where a call is one or two
-  // instances per wave (B <= 8 Ki: FR3 +10-20 %, XLS-FR3 +20-30 %) and loses
-  // to the overlapped sub-batch pipeline above (FR3 B = 65 536: 14.3 M vs
-  // 17.6 M solves/s; tools/fusion_sweep.py)
-  static const int64_t fuse_max = env_int("DRC_FUSE_MAX", 8192, 0);
+  // fused for small batches only: it wins where a call is a few instances per
+  // wave and loses to the overlapped sub-batch pipeline at full batch (B =
+  // 65 536: FR3 -6 %, UR5e -18 %, XLS-FR3 -13 %, profiles/r06t_envab_fuse_*.jsonl).
+  // Up to 8 Ki instances always; up to 16 Ki where the fused kernel (two waves
+  // per SIMD, its LDS plan) holds at most two waves per CU fewer than the
+  // pipeline's task kernel: B = 16 384 FR3 +10.5 %, XLS-FR3 +4.3 %, Husky-FR3
+  // +5.9 %, but UR5e -4.1 % (its three-wave task build holds 11 waves per CU
+  // against the fused kernel's 8).  DRC_FUSE_MAX overrides (>= 0)
+  static const int64_t fuse_env = env_int("DRC_FUSE_MAX", -1, -1);
+  int64_t fuse_max = 8192;
+  if (fuse_env >= 0) {
+    fuse_max = fuse_env;
+  } else {
+    const size_t lt = static_cast<size_t>(kt.lds_doubles) * sizeof(double);
+    const size_t lf = static_cast<size_t>((kt.lds_doubles > kq.lds_doubles ? kt.lds_doubles : kq.lds_doubles) +
+                                          ((kt.rLen + 1) & ~1)) * sizeof(double);
+    const int64_t cu_lds = 160 * 1024;
+    auto cap = [&](int64_t w, size_t lds) { return lds ? std::min<int64_t>(w, cu_lds / int64_t(lds)) : w; };
+    const int64_t w_task = cap(4 * task_waves_per_simd(0, lt), lt), w_fused = cap(4 * fused_waves_per_simd(), lf);
+    if (w_fused + 2 >= w_task) fuse_max = 16384;
+  }
   const bool fuse =
       m->fused && !stages && !lane && B <= fuse_max && kQpGroup == 64 && qp_compiled(kq.nx, kq.ng, kq.np);
   int S = 1;

@@ -16,10 +16,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("robot,per_rank,mode", [("fr3", 384, "weak"), ("xls_fr3", 257, "strong"),
-                                                 ("fr3", 4500, "weak")])
+                                                 ("fr3", 8500, "weak")])
 def test_two_ranks_match_single_process(tmp_path, robot, per_rank, mode):
-    """(fr3, 4500): each rank's shard runs the fused kernel (B <= 8 192), the
-    single-process run of the whole 9 000 the sub-batch pipeline; the
+    """(fr3, 8500): each rank's shard runs the fused kernel (FR3: B <= 16 384),
+    the single-process run of the whole 17 000 the sub-batch pipeline; the
     bit-identity contract holds across that threshold."""
     sys.path.insert(0, ROOT)
     from dyros_robot_controller_amd import dist as ddist

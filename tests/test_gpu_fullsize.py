@@ -3,7 +3,8 @@
 the code the bench times -- four concurrent sub-batches, the XCD-aware
 instance order for sub-batches of >= 16 Ki, the compile-time QP shapes
 Dims<23,16,7> / <20,14,6> / <9,16,9> / <11,16,11>, the fused kernel at
-B <= 8 192 -- is the code the oracle checks:
+B <= 8 192 (16 384 except UR5e: Husky-FR3's bench batch) -- is the code the
+oracle checks:
 
   config                                   robot        B        offset
   FR3 QPIKStep (the metric)                fr3          65 536   0
@@ -18,8 +19,8 @@ Properties checked on every instance:
   * sub-batch invariance: the call split into 1, 3 or 4 (the default) concurrent
     sub-batches (drc_set_concurrency) returns bit-identical q-dot, status and
     iterations;
-    at B = 4 096 the fused kernel against the two-kernel pipeline
-    (drc_set_fusion), bit for bit;
+    at B = 4 096 and Husky-FR3's 16 384 the fused kernel against the
+    two-kernel pipeline (drc_set_fusion), bit for bit;
   * feasibility: every output finite; non-solved instances exactly zero
     (QP_IK.cpp:56-61); manipulators: |q-dot| <= the velocity limit (the QP's
     bound rows, QP_IK.cpp:89-97) within 1e-6; whole-body QPs (no bounds, no
@@ -63,7 +64,7 @@ def _run(cfg, cuda):
     h = rd.model.handle
     runs = {}
     # (label, concurrency, fusion): the bench's default call last
-    variants = [("one", 1, 1), ("three", 3, 1), ("four", 4, 1)] if B > 8192 else [("pipeline", 4, 0), ("fused", 4, 1)]
+    variants = [("one", 1, 1), ("three", 3, 1), ("four", 4, 1)] if B > 16384 else [("pipeline", 4, 0), ("fused", 4, 1)]
     for label, chunks, fused in variants:
         _capi.check(_capi.lib().drc_set_concurrency(h, chunks))
         _capi.check(_capi.lib().drc_set_fusion(h, C.c_int(fused)))
