@@ -687,10 +687,23 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
   const int ls = m->lane_stage;
   const bool lane = (ls == 1 || ls == 2 || (ls == 3 && stages)) && (dm.nv == 6 || dm.nv == 7) &&
                     dm.ncand_slots <= kMaxCandSlots;
+  // fused up to 16 Ki instances: there a call is a few instances per wave, its
+  // makespan the tail the fused kernel and the EPA-first order below shorten;
+  // at full batch the overlapped sub-batch pipeline wins.  Measured at
+  // B = 16 384 (fused / pipeline): FR3 +10.5 % (+33 % with the order), UR5e
+  // +10 % with the order (-4.1 % without), XLS-FR3 +4.3 %, Husky-FR3 +5.9 %;
+  // B = 32 768: FR3 +3.7 %, UR5e -13 %, XLS-FR3 -12 %; B = 65 536: FR3 -13 %,
+  // UR5e -21 % (profiles/r06t_envab_fuse_*.jsonl, r06x_*, r06y_*).
+  // DRC_FUSE_MAX overrides
+  static const int64_t fuse_max = env_int("DRC_FUSE_MAX", 16384, 0);
+  const bool fuse =
+      m->fused && !stages && !lane && B <= fuse_max && kQpGroup == 64 && qp_compiled(kq.nx, kq.ng, kq.np);
   // penetration-prone instances first (order_kernel.hip) for calls whose
   // makespan is the EPA tail: manipulator calls of 2 049 .. 8 192 instances
-  // (DRC_ORDER_MIN / _MAX).  Fewer: the 2 048-wave fused grid starts every
-  // instance at once anyway.  More: the order gains less than it costs
+  // (DRC_ORDER_MIN / _MAX), and every fused manipulator call above that (FR3
+  // fused at B = 12 288 +38 %, 16 384 +20 %, profiles/r06v_envab_order*.jsonl).
+  // Fewer: the 2 048-wave fused grid starts every instance at once anyway.
+  // Pipeline calls above 8 192: the order gains less than it costs
   // (profiles/r06f_envab_order_*.jsonl).  Whole-body robots: their predictor
   // flags ~60 % of the instances, which orders nothing (XLS-FR3 B = 4 096
   // -2.6 %, profiles/r06j_envab_order_b4096.jsonl; FR3 +15.7 %, UR5e +7.7 %).
@@ -698,8 +711,8 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
   static const int64_t order_max = env_int("DRC_ORDER_MAX", 8192, 0);
   static const int64_t order_min = env_int("DRC_ORDER_MIN", 2049, 0);
   const bool dbg_order = m->d_order && m->order_n == B;
-  const bool auto_order = !stages && !lane && !dbg_order && B >= order_min && B <= order_max && dm.kind == 0 &&
-                          dm.ncand_slots > 0 && dm.ncand_slots <= kMaxCandSlots;
+  const bool auto_order = !stages && !lane && !dbg_order && B >= order_min && (B <= order_max || fuse) &&
+                          dm.kind == 0 && dm.ncand_slots > 0 && dm.ncand_slots <= kMaxCandSlots;
   int32_t* order_buf = nullptr;
   {
     std::lock_guard<std::mutex> g(m->mu);
@@ -719,29 +732,6 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
   // kernel waits for the whole task kernel, with several they overlap
   // (Husky-FR3's 16 Ki batch)
   static const int64_t min_sub = env_int("DRC_MIN_SUBBATCH", 4096, 1);
-  // fused for small batches only: it wins where a call is a few instances per
-  // wave and loses to the overlapped sub-batch pipeline at full batch (B =
-  // 65 536: FR3 -6 %, UR5e -18 %, XLS-FR3 -13 %, profiles/r06t_envab_fuse_*.jsonl).
-  // Up to 8 Ki instances always; up to 16 Ki where the fused kernel (two waves
-  // per SIMD, its LDS plan) holds at most two waves per CU fewer than the
-  // pipeline's task kernel: B = 16 384 FR3 +10.5 %, XLS-FR3 +4.3 %, Husky-FR3
-  // +5.9 %, but UR5e -4.1 % (its three-wave task build holds 11 waves per CU
-  // against the fused kernel's 8).  DRC_FUSE_MAX overrides (>= 0)
-  static const int64_t fuse_env = env_int("DRC_FUSE_MAX", -1, -1);
-  int64_t fuse_max = 8192;
-  if (fuse_env >= 0) {
-    fuse_max = fuse_env;
-  } else {
-    const size_t lt = static_cast<size_t>(kt.lds_doubles) * sizeof(double);
-    const size_t lf = static_cast<size_t>((kt.lds_doubles > kq.lds_doubles ? kt.lds_doubles : kq.lds_doubles) +
-                                          ((kt.rLen + 1) & ~1)) * sizeof(double);
-    const int64_t cu_lds = 160 * 1024;
-    auto cap = [&](int64_t w, size_t lds) { return lds ? std::min<int64_t>(w, cu_lds / int64_t(lds)) : w; };
-    const int64_t w_task = cap(4 * task_waves_per_simd(0, lt), lt), w_fused = cap(4 * fused_waves_per_simd(), lf);
-    if (w_fused + 2 >= w_task) fuse_max = 16384;
-  }
-  const bool fuse =
-      m->fused && !stages && !lane && B <= fuse_max && kQpGroup == 64 && qp_compiled(kq.nx, kq.ng, kq.np);
   int S = 1;
   if (!stages && !fuse)
     for (int c = m->chunks; c > 1; --c)

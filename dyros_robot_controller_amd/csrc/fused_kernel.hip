@@ -53,8 +53,6 @@ fused_kernel(const DevModel* __restrict__ M0, const KParams kt, const KParams kq
   }
 }
 
-int fused_waves_per_simd() { return DRC_FUSED_WAVES; }
-
 int launch_fused_kernel(unsigned grid, size_t lds, hipStream_t st, const DevModel* m, const KParams& kt,
                         const KParams& kq, const IO& io) {
   const dim3 g(grid), blk(64);

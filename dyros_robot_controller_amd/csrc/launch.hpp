@@ -16,7 +16,6 @@ int launch_task_kernel(int problem, unsigned grid, size_t lds, hipStream_t st, c
 // for a plan of `lds` bytes per wave, and of the QP kernel
 int task_waves_per_simd(int problem, size_t lds);
 int qp_waves_per_simd();
-int fused_waves_per_simd();
 // lane-per-instance task stage (nv = 6 or 7)
 int launch_lane_task_kernel(int nv, unsigned grid, hipStream_t st, const DevModel* m, const KParams& kp,
                             const IO& io);

@@ -274,11 +274,9 @@ int drc_state_host(drc_model* model, int frame_id, int64_t B, const double* q, c
 int drc_set_concurrency(drc_model* model, int chunks);
 
 /* Fused task + QP kernel for the QP shapes the library compiles (the bundled
- * FR3, UR5e, Husky-FR3, XLS-FR3 layouts) and batches of up to 8 192
- * instances (16 384 where the fused kernel holds at most two waves per CU
- * fewer than the pipeline's task kernel: all bundled models but UR5e; the
- * DRC_FUSE_MAX environment variable overrides): 1 (default) runs such a
- * drc_qpik_batch call as one kernel whose
+ * FR3, UR5e, Husky-FR3, XLS-FR3 layouts) and batches of up to 16 384
+ * instances (the DRC_FUSE_MAX environment variable overrides): 1 (default)
+ * runs such a drc_qpik_batch call as one kernel whose
  * waves take an instance through the task stage and the QP before the next,
  * the task record kept in LDS; 0 always runs the task-kernel -> QP-kernel
  * pipeline (drc_set_concurrency sub-batches), as larger batches do.  Results

@@ -3,7 +3,7 @@
 the code the bench times -- four concurrent sub-batches, the XCD-aware
 instance order for sub-batches of >= 16 Ki, the compile-time QP shapes
 Dims<23,16,7> / <20,14,6> / <9,16,9> / <11,16,11>, the fused kernel at
-B <= 8 192 (16 384 except UR5e: Husky-FR3's bench batch) -- is the code the
+B <= 16 384 (FR3 B = 4 096 and Husky-FR3's bench batch) -- is the code the
 oracle checks:
 
   config                                   robot        B        offset

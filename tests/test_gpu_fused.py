@@ -1,5 +1,5 @@
 """The fused task + QP kernel (fused_kernel.hip, the default for the compiled
-QP shapes and B <= 8 192) against the two-kernel pipeline
+QP shapes and B <= 16 384) against the two-kernel pipeline
 (drc_set_fusion(model, 0)): the same device functions on the same
 task-record values, built with -ffp-contract=on (build.sh) so that every
 multiply-add rounds the same in both kernels.  The contract is bit-identical

@@ -4,7 +4,7 @@ move only when each instance starts, never what it returns: the automatic
 order (calls of up to DRC_ORDER_MAX instances), the identity order and a
 reversed order (drc_debug_instance_order, which replaces the automatic one)
 give bit-identical q-dot*, statuses and ADMM iteration counts -- fused
-(B <= 8 192) and two-kernel pipeline (several sub-batches, each ordered
+(B <= 16 384) and two-kernel pipeline (several sub-batches, each ordered
 within its own range)."""
 import ctypes as C
 
@@ -36,7 +36,11 @@ def _set_order(rd, order):
                                                  C.c_int64(len(o))))
 
 
-@pytest.mark.parametrize("robot,B,subs", [("fr3", 4096, 1), ("ur5e", 3000, 1), ("husky_fr3", 16384, 3)])
+# fused: fr3 4 096, ur5e 3 000, fr3 12 000 and husky_fr3 16 384 (its ranges of
+# three are still a permutation of the one fused range); fr3 20 000: the
+# pipeline's three sub-batches, each ordered within its own range
+@pytest.mark.parametrize("robot,B,subs", [("fr3", 4096, 1), ("ur5e", 3000, 1), ("fr3", 12000, 1),
+                                          ("husky_fr3", 16384, 3), ("fr3", 20000, 3)])
 def test_order_does_not_change_results(cuda, robot, B, subs):
     moma = robot in ("husky_fr3", "xls_fr3", "caster_fr3")
     rd = make_moma(robot, cuda) if moma else make_manipulator(robot, cuda)
