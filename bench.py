@@ -469,6 +469,10 @@ def main():
         ms_per_step = 1e3 * wall / args.steps
         bps = algorithmic_bytes(dof, act)
         per_launch_bytes = bps * B
+        # the library runs calls of up to DRC_FUSE_MAX (default 16 384) instances
+        # of the compiled (bundled) shapes as one fused task + QP launch
+        fuse_max = int(os.environ.get("DRC_FUSE_MAX", "16384"))
+        fused = B <= fuse_max
         achieved = per_launch_bytes / (kernel_ms * 1e-3) / 1e9
         # counter summaries are used only when measured on this very build
         traffic = load_profile("pmc_traffic_%s.json" % robot, robot, B, build)
@@ -478,8 +482,10 @@ def main():
                 "frac": achieved / HBM_PEAK_GBS, "traffic": traffic.get("hbm_bytes_per_step") if traffic else None,
                 "traffic_source": ("profiles/pmc_traffic_%s.json (build %s)" % (robot, build)) if traffic else
                                   "no PMC summary of this build (%s) for this robot and batch" % build,
-                "kernel": "drc_qpik_batch call (task_kernel + qp_kernel per sub-batch, %d concurrent sub-batches)"
-                          % args.chunks,
+                "kernel": ("drc_qpik_batch call (one fused_kernel launch: B <= DRC_FUSE_MAX = %d; "
+                           "task_kernel_ms_sum is its duration)" % fuse_max) if fused else
+                          ("drc_qpik_batch call (task_kernel + qp_kernel per sub-batch, %d concurrent sub-batches)"
+                           % args.chunks),
                 "bytes_per_solve": bps, "bytes_per_launch": per_launch_bytes,
                 "kernel_ms": kernel_ms, "task_kernel_ms_sum": task_ms, "qp_kernel_ms_sum": qp_ms,
                 "step_event_ms": step_event_ms,

@@ -25,7 +25,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def short(name):
-    for k in ("task_kernel", "qp_kernel"):
+    for k in ("task_kernel", "qp_kernel", "fused_kernel"):
         if k in name:
             return k
     return None
@@ -40,8 +40,9 @@ def bench_rows(rows, grid_key, grid=MAIN_GRID):
     bench's first task dispatch immediately precedes it."""
     rows = [r for r in rows if short(r.get("Kernel_Name", "")) and int(r.get(grid_key, grid)) == grid]
     ids = [int(r["Dispatch_Id"]) for r in rows if short(r["Kernel_Name"]) == "qp_kernel" and "Dispatch_Id" in r]
-    if not ids:
-        return rows
+    if not ids:   # a fused call (B <= 16 384): its own dispatches only
+        fid = [int(r["Dispatch_Id"]) for r in rows if short(r["Kernel_Name"]) == "fused_kernel" and "Dispatch_Id" in r]
+        return [r for r in rows if short(r["Kernel_Name"]) == "fused_kernel"] if fid else rows
     first = min(ids) - 1
     return [r for r in rows if int(r.get("Dispatch_Id", first)) >= first]
 

@@ -18,7 +18,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def short(name):
-    for k in ("task_kernel", "qpid_kernel", "qp_kernel", "dyn_kernel"):
+    for k in ("task_kernel", "qpid_kernel", "qp_kernel", "dyn_kernel", "fused_kernel"):
         if k in name:
             return k
     return name[:40]

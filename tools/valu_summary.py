@@ -24,7 +24,7 @@ from pmc_summary import bench_rows  # noqa: E402
 
 
 def short(name):
-    for k in ("task_kernel", "qpid_kernel", "qp_kernel", "dyn_kernel"):
+    for k in ("task_kernel", "qpid_kernel", "qp_kernel", "dyn_kernel", "fused_kernel"):
         if k in name:
             return k
     return None
@@ -53,7 +53,7 @@ def main():
                    "fp64_share_of_valu": (a.get("SQ_INSTS_VALU_FMA_F64", 0) + a.get("SQ_INSTS_VALU_ADD_F64", 0)
                                           + a.get("SQ_INSTS_VALU_MUL_F64", 0) + a.get("SQ_INSTS_VALU_TRANS_F64", 0))
                    / max(a.get("SQ_INSTS_VALU", 0), 1)}
-    qp = [k for k in ("task_kernel", "qp_kernel") if k in kern]
+    qp = [k for k in ("task_kernel", "qp_kernel", "fused_kernel") if k in kern]
     step = chunks * sum(kern[k]["fp64_flops_per_dispatch"] for k in qp)
     step_hw = chunks * sum(kern[k]["fp64_flops_hw_per_dispatch"] or 0 for k in qp)
     tc = sum(kern[k]["per_dispatch"].get("SQ_THREAD_CYCLES_VALU", 0) for k in qp)
