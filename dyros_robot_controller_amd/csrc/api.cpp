@@ -800,15 +800,16 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
     if (own) HIP_TRY(hipStreamWaitEvent(cs, m->ln.fork, 0));
     KParams kt_c = kt, kq_c = kq;
     kt_c.xcd_map = kq_c.xcd_map = Bc >= 16384 ? 1 : 0;
-    // persistent grids (work queues hand out the instances): 2048 waves per
-    // kernel and sub-batch keep every SIMD fed while each wave's prologue
-    // (kernel-argument spills, written once per wave) stays a small share of
-    // the HBM writes -- measured sweep in DESIGN.md; DRC_GRID_TASK / _QP
-    // override for such experiments
+    // persistent grids (work queues hand out the instances): 1 024 task and
+    // 4 096 QP waves per sub-batch.  Re-swept on the r06 kernels (the QP
+    // kernel's instances are now cheaper than the task kernel's): against
+    // 2 048 / 2 048, FR3 +2.8 %, UR5e +2.0 %, XLS-FR3 +1.4 %
+    // (profiles/r06ae_envab_grid.jsonl, r06af_envab_grid2.jsonl); DRC_GRID_TASK
+    // / _QP override for such experiments
     // (clamped to >= 8 and a multiple of 8: with the XCD-aware order every
     // residue class blockIdx & 7 needs waves to drain its queue)
-    static const int64_t cap_t = env_int("DRC_GRID_TASK", 2048, 8) & ~int64_t(7);
-    static const int64_t cap_q = env_int("DRC_GRID_QP", 2048, 8) & ~int64_t(7);
+    static const int64_t cap_t = env_int("DRC_GRID_TASK", 1024, 8) & ~int64_t(7);
+    static const int64_t cap_q = env_int("DRC_GRID_QP", 4096, 8) & ~int64_t(7);
     const int64_t gq = Bc < cap_q ? Bc : cap_q, gt = Bc < cap_t ? Bc : cap_t;
     IO io{Bc, b0, B, q, qdot, xt, xdt, xi, xdi, out, status, iters, pose, jac, man, dist, xdd, pair,
           rec ? rec + b0 * stride : nullptr, stride};

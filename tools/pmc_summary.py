@@ -31,14 +31,16 @@ def short(name):
     return None
 
 
-MAIN_GRID = 2048 * 64   # work-items of the bench's task/QP dispatches (persistent grid: 2048 waves)
+MAIN_GRID = None   # (r06: the task / QP / fused grids differ; the dispatch order selects the bench's rows)
 
 
 def bench_rows(rows, grid_key, grid=MAIN_GRID):
     """The bench's own task/QP dispatches: the workload generator's stage
     launches (task kernel only) all precede the first QP dispatch, and the
-    bench's first task dispatch immediately precedes it."""
-    rows = [r for r in rows if short(r.get("Kernel_Name", "")) and int(r.get(grid_key, grid)) == grid]
+    bench's first task dispatch immediately precedes it (a call enqueues task,
+    QP, task, QP, ... for its sub-batches).  `grid` (work-items) additionally
+    keeps only dispatches of that size when given."""
+    rows = [r for r in rows if short(r.get("Kernel_Name", "")) and (grid is None or int(r.get(grid_key, grid)) == grid)]
     ids = [int(r["Dispatch_Id"]) for r in rows if short(r["Kernel_Name"]) == "qp_kernel" and "Dispatch_Id" in r]
     if not ids:   # a fused call (B <= 16 384): its own dispatches only
         fid = [int(r["Dispatch_Id"]) for r in rows if short(r["Kernel_Name"]) == "fused_kernel" and "Dispatch_Id" in r]
@@ -108,8 +110,8 @@ def main():
            "hbm_bytes_per_instance": chunks * per_dispatch / batch,
            "corrections": "FETCH_SIZE KiB x1024 x2 (gfx950 half-count), WRITE_SIZE KiB x1024",
            "main_dispatch_avg_ns": avg, "main_dispatches_traced": ndisp,
-           "note": "averages over the bench's own dispatches (grid %d work-items); the kernel_stats csv "
-                   "also counts the workload generator's stage launches" % MAIN_GRID}
+           "note": "averages over the bench's own dispatches (grid %s work-items); the kernel_stats csv "
+                   "also counts the workload generator's stage launches" % "task 1024 x 64, QP 4096 x 64 / fused 2048 x 64"}
     for name in (tag + "_pmc.json", "pmc_traffic_%s.json" % robot):
         with open(os.path.join(dst, name), "w") as fh:
             json.dump(out, fh, indent=1)
