@@ -123,12 +123,21 @@ def shard_global(rank, world, global_batch):
     return lo, hi - lo
 
 
+def _group(world):
+    """True when the collectives run: several ranks, or a process group that
+    exists (a one-rank RCCL group runs the same code path: tests/test_gpu_rccl.py)."""
+    if world > 1:
+        return True
+    import torch.distributed as dist
+    return dist.is_available() and dist.is_initialized()
+
+
 def gather_outputs(local, counts, world):
     """Optional epilogue: all-gather every rank's [F][B_r] output
     block into one [F][sum B_r] tensor on each rank (instance order = rank
     order).  Blocks are padded to the largest shard for the collective."""
     import torch
-    if world == 1:
+    if not _group(world):
         return local
     import torch.distributed as dist
     F, Bmax = local.shape[0], max(counts)
@@ -145,7 +154,7 @@ def reduce_stats(wall_s, n_bad, iters_mean, world, device="cpu"):
     mean ADMM iterations.  Returns plain floats."""
     import torch
     t = torch.tensor([float(wall_s), float(n_bad), float(iters_mean)], dtype=torch.float64, device=device)
-    if world > 1:
+    if _group(world):
         import torch.distributed as dist
         mx = t[:1].clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
@@ -163,7 +172,7 @@ def gather_stats(values, world, device="cpu"):
     import numpy as np
     import torch
     t = torch.tensor([float(v) for v in values], dtype=torch.float64, device=device)
-    if world == 1:
+    if not _group(world):
         return t.cpu().numpy()[None, :]
     import torch.distributed as dist
     parts = [torch.empty_like(t) for _ in range(world)]
