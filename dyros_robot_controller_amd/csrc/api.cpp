@@ -1485,18 +1485,21 @@ int drc_default_qpik_params(const drc_model* m, int exact, drc_qpik_params* p) {
   // FR3 +0.1 % (profiles/r05b_envab.jsonl), but leave ~2e-9 in q-dot on some
   // instances (a golden fixture moved by 2.5e-9): not taken for that
   static const int64_t exact_refine = drc_amd::env_int("DRC_EXACT_REFINE", 3, 0);
-  // Ruiz passes in exact mode: 2 instead of OSQP's 10.  The ADMM only seeds
-  // the certified polish there (8 / 2 iterations), and the certified point is
-  // the QP's unique optimum whatever the scaling; two passes equilibrate
-  // enough for the polish to certify at its first attempt, the rest cost
-  // (whole-body QPs run all 10: a balanced row's factor converges
-  // geometrically and never reaches exactly 1).  Measured, one box: FR3 +2.6 %,
-  // UR5e +2.1 %, Husky-FR3 +2.9 %, XLS-FR3 +9.9 %, Caster-FR3 +10.5 %; one pass
-  // is faster on the manipulators but leaves the whole-body polish failing
-  // (3.6 M solves/s), none fails everywhere (profiles/r06f_envab_exact_scaling.jsonl,
-  // r06g_envab_exact_scaling.jsonl).  The oracle's exact mode uses the same
-  // count.  DRC_EXACT_SCALING overrides it (A/B experiments)
-  static const int64_t exact_scaling = drc_amd::env_int("DRC_EXACT_SCALING", 2, 0);
+  // Ruiz passes in exact mode: 1 (manipulators) / 2 (whole-body) instead of
+  // OSQP's 10.  The ADMM only seeds the certified polish there (8 / 2
+  // iterations), and the certified point is the QP's unique optimum whatever
+  // the scaling; a pass or two equilibrate enough for the polish to certify at
+  // its first attempt, the rest cost (whole-body QPs run all 10: a balanced
+  // row's factor converges geometrically and never reaches exactly 1).
+  // Measured, one box, 2 against 10: FR3 +2.6 %, UR5e +2.1 %, Husky-FR3
+  // +2.9 %, XLS-FR3 +9.9 %, Caster-FR3 +10.5 %; one pass leaves the whole-body
+  // polish failing (3.6 M solves/s), none fails everywhere
+  // (profiles/r06f_envab_exact_scaling.jsonl, r06g_envab_exact_scaling.jsonl);
+  // 1 against 2 on the manipulators: FR3 +0.6 %, UR5e +1.8 %, FR3 B = 4 096
+  // +1.2 % (profiles/r06al_envab_scal1*.jsonl).  The oracle's exact mode uses
+  // the same counts.  DRC_EXACT_SCALING overrides both kinds (A/B experiments)
+  static const int64_t exact_scaling_env = drc_amd::env_int("DRC_EXACT_SCALING", 0, 0);
+  const int64_t exact_scaling = exact_scaling_env > 0 ? exact_scaling_env : (moma ? 2 : 1);
   if (exact) {
     s.check_termination = static_cast<int>(exact_check);
     s.polish_refine_iter = static_cast<int>(exact_refine);

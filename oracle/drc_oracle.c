@@ -2359,8 +2359,9 @@ void oracle_default_params(int kind, OracleParams* p, int exact) {
     /* parity mode: the first polish at iteration 8 (manipulators) / 2 (whole-body)
      * (kernel: drc_default_qpik_params) */
     if (exact) s->check_termination = kind == 0 ? 8 : 2;
-    /* parity mode: two Ruiz passes (kernel: drc_default_qpik_params) */
-    if (exact) s->scaling = 2;
+    /* parity mode: one (manipulators) / two (whole-body) Ruiz passes
+     * (kernel: drc_default_qpik_params) */
+    if (exact) s->scaling = kind == 0 ? 1 : 2;
 }
 
 /* Farkas certificate for the whole-body QP (mobile_manipulator/QP_IK.cpp:
