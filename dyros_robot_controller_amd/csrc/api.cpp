@@ -858,9 +858,8 @@ static int launch(const drc_model_impl* cm, const drc_qpik_params* params, int s
     if (fuse) {  // one fused task + QP kernel, the record in LDS
       static const int64_t cap_f = env_int("DRC_GRID_FUSED", 2048, 8) & ~int64_t(7);
       const int64_t gf = Bc < cap_f ? Bc : cap_f;
-      const int rec_doubles = (kt_c.rLen + 1) & ~1;
       const size_t lds_f =
-          static_cast<size_t>((kt_c.lds_doubles > kq_c.lds_doubles ? kt_c.lds_doubles : kq_c.lds_doubles) + rec_doubles) *
+          static_cast<size_t>(fused_lds_doubles(kt_c, kq_c)) *
           sizeof(double);
       io.queue = qc;
       HIP_TRY(static_cast<hipError_t>(
@@ -1130,7 +1129,7 @@ int drc_debug_lds_plan(drc_model* m, const drc_qpik_params* params, int problem,
   *task_bytes = kt.lds_doubles * 8;
   *qp_bytes = kq.lds_doubles * 8;
   // the fused kernel (QPIK only): the larger plan plus the task record
-  *fused_bytes = problem == 0 ? ((kt.lds_doubles > kq.lds_doubles ? kt.lds_doubles : kq.lds_doubles) + ((kt.rLen + 1) & ~1)) * 8 : 0;
+  *fused_bytes = problem == 0 ? drc_amd::fused_lds_doubles(kt, kq) * 8 : 0;
   return DRC_OK;
 }
 

@@ -37,7 +37,7 @@ fused_kernel(const DevModel* __restrict__ M0, const KParams kt, const KParams kq
   static_assert(QD::gs == 64, "the fused kernel runs one instance per wave");
   const int64_t B = io.B;
   IO iol = io;  // the record lives in LDS: one slot, reused by every instance of the wave
-  iol.rec = S + (kt.lds_doubles > kq.lds_doubles ? kt.lds_doubles : kq.lds_doubles);
+  iol.rec = S + fused_rec_offset(kt, kq);  // (kernel_common.hpp: past the QP plan, in the task plan's dead overlay)
   iol.rec_stride = 0;
   const InstSeq seq(B, kq.xcd_map, io.queue);
   for (int64_t j = seq.first(); j < seq.n; j = seq.next(j)) {

@@ -346,6 +346,26 @@ struct InstSeqG {
 // LDS (address space 3) views: an opaque copy of an LDS address must keep its
 // address space, or every access through it becomes a flat access (vector
 // memory path and its waits) instead of a ds_read / ds_write
+// The fused kernel's LDS: the task plan (kt) and the QP plan (kq) overlay each
+// other from offset 0, and the task record sits where neither stage touches it
+// while the other reads it: in the task plan's overlay region (kEpa: EPA
+// polytope, GJK candidates, manipulability scratch -- dead once the record is
+// written, task_stage.hpp "task data out") when that region lies past the QP
+// plan and holds the record, else past both plans.  Whole-body plans then need
+// no extra space for the record: 8 instead of 7 fused waves per CU (r06).
+// Offsets in doubles; same function on the host (launch size) and the device.
+__host__ __device__ __forceinline__ int fused_rec_offset(const KParams& kt, const KParams& kq) {
+  const int rec = (kt.rLen + 1) & ~1;
+  const int plans = kt.lds_doubles > kq.lds_doubles ? kt.lds_doubles : kq.lds_doubles;
+  const int inside = kt.kEpa > kq.lds_doubles ? kt.kEpa : kq.lds_doubles;
+  return kt.kEpa > 0 && inside + rec <= kt.lds_doubles ? inside : plans;
+}
+__host__ __device__ __forceinline__ int fused_lds_doubles(const KParams& kt, const KParams& kq) {
+  const int plans = kt.lds_doubles > kq.lds_doubles ? kt.lds_doubles : kq.lds_doubles;
+  const int end = fused_rec_offset(kt, kq) + ((kt.rLen + 1) & ~1);
+  return end > plans ? end : plans;
+}
+
 typedef __attribute__((address_space(3))) double lds_double;
 typedef __attribute__((address_space(3))) const double lds_cdouble;
 typedef __attribute__((address_space(3))) const int lds_cint;

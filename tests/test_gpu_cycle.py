@@ -149,7 +149,9 @@ def test_lds_plan(cuda, robot):
     """Per-wave LDS of the three QPIK kernels (drc_debug_lds_plan): the QP
     kernel's plan fits three waves per SIMD (12 per CU in 160 KB), the task
     kernel's at least one (its VGPRs allow two; DESIGN.md "Occupancy"), and the
-    fused plan holds the larger of the two plus the record."""
+    fused plan holds the larger of the two and the task record -- inside the
+    task plan's dead overlay region where it fits there (kernel_common.hpp
+    fused_rec_offset: the whole-body plans), else past both plans."""
     moma = robot in ("husky_fr3", "xls_fr3", "caster_fr3")
     rd = make_moma(robot, cuda) if moma else make_manipulator(robot, cuda)
     p = manipulator.QPIKParamsBuilder(rd.model, exact=True).params(LINK[robot], _capi.MODE_QPIK_STEP)
@@ -158,7 +160,9 @@ def test_lds_plan(cuda, robot):
     print(robot, "task", t.value, "qp", q.value, "fused", f.value)
     assert 0 < q.value <= 160 * 1024 // 12
     assert 0 < t.value <= 160 * 1024 // 4
-    assert f.value > max(t.value, q.value)
+    assert max(t.value, q.value) <= f.value <= max(t.value, q.value) + 8 * 128
+    if moma:   # the whole-body record fits in the task plan's overlay region
+        assert f.value == t.value
 
 
 def test_host_timeline_and_waves(cuda):
